@@ -1,0 +1,111 @@
+"""ctypes access to the CPU oracle (TEST INFRASTRUCTURE ONLY).
+
+oracle/_build/libstarch_oracle.so : the C restatement (oracle/starch_oracle.c)
+oracle/_ref/libbz2ref.so          : the reference's vendored libbz2 (optional;
+                                    built here from /root/reference, travels
+                                    to the GPU box as a prebuilt binary)
+"""
+import ctypes
+import os
+import subprocess
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+ORACLE_SO = os.path.join(ROOT, "oracle", "_build", "libstarch_oracle.so")
+REF_SO = os.path.join(ROOT, "oracle", "_ref", "libbz2ref.so")
+
+
+class Seg(ctypes.Structure):
+    _fields_ = [("name_off", ctypes.c_uint64), ("name_len", ctypes.c_uint64),
+                ("line_count", ctypes.c_uint64), ("text_off", ctypes.c_uint64),
+                ("text_len", ctypes.c_uint64)]
+
+
+_lib = None
+_ref = None
+
+
+def lib():
+    global _lib
+    if _lib is None:
+        if not os.path.exists(ORACLE_SO):
+            subprocess.check_call(["make", "-s", "-C", os.path.join(ROOT, "oracle"),
+                                   os.path.join(ROOT, "oracle", "_build", "libstarch_oracle.so")])
+        L = ctypes.CDLL(ORACLE_SO)
+        L.oracle_transform.restype = ctypes.c_size_t
+        L.oracle_bz2_compress.restype = ctypes.c_size_t
+        L.oracle_crc32_bzip2.restype = ctypes.c_uint32
+        L.oracle_block_sort.restype = ctypes.c_int32
+        _lib = L
+    return _lib
+
+
+def ref():
+    """The reference's libbz2 (None when oracle/_ref was not built)."""
+    global _ref
+    if _ref is None and os.path.exists(REF_SO):
+        R = ctypes.CDLL(REF_SO)
+        R.ref_bz2_compress.restype = ctypes.c_int
+        R.ref_bz2_script.restype = ctypes.c_int
+        R.ref_bz2_version.restype = ctypes.c_char_p
+        _ref = R
+    return _ref
+
+
+def transform(data: bytes):
+    """-> (text bytes, [(chr bytes, line_count, text bytes)])"""
+    L = lib()
+    cap = 2 * len(data) + 64 * (data.count(b"\n") + 1) + 1024
+    seg_cap = data.count(b"\n") + 2
+    out = ctypes.create_string_buffer(cap)
+    segs = (Seg * seg_cap)()
+    nseg = ctypes.c_size_t(0)
+    n = L.oracle_transform(data, ctypes.c_size_t(len(data)), out, ctypes.c_size_t(cap),
+                           segs, ctypes.c_size_t(seg_cap), ctypes.byref(nseg))
+    assert n != ctypes.c_size_t(-1).value
+    text = out.raw[:n]
+    res = []
+    for s in segs[:nseg.value]:
+        res.append((data[s.name_off:s.name_off + s.name_len], s.line_count,
+                    text[s.text_off:s.text_off + s.text_len]))
+    return text, res
+
+
+def bz2(data: bytes, bs: int = 9) -> bytes:
+    L = lib()
+    cap = len(data) + len(data) // 50 + 1024
+    out = ctypes.create_string_buffer(cap)
+    n = L.oracle_bz2_compress(data, ctypes.c_size_t(len(data)), bs, out, ctypes.c_size_t(cap))
+    assert n != ctypes.c_size_t(-1).value
+    return out.raw[:n]
+
+
+def ref_bz2(data: bytes, bs: int = 9, wf: int = 30) -> bytes:
+    R = ref()
+    cap = len(data) + len(data) // 50 + 1024
+    out = ctypes.create_string_buffer(cap)
+    n = ctypes.c_size_t(0)
+    rc = R.ref_bz2_compress(data, ctypes.c_size_t(len(data)), bs, wf, out, ctypes.c_size_t(cap),
+                            ctypes.byref(n))
+    assert rc == 0, rc
+    return out.raw[:n.value]
+
+
+def ref_bz2_script(data: bytes, ops, bs=9, wf=30, out_chunk=0):
+    """ops: [(action, nbytes)] -> (stream bytes, [rc per op])"""
+    R = ref()
+    arr = (ctypes.c_int32 * (2 * len(ops)))(*[v for op in ops for v in op])
+    rcs = (ctypes.c_int32 * len(ops))()
+    cap = len(data) + len(data) // 50 + 4096 + 64 * len(ops)
+    out = ctypes.create_string_buffer(cap)
+    n = ctypes.c_size_t(0)
+    rc = R.ref_bz2_script(data, arr, len(ops), bs, wf, ctypes.c_size_t(out_chunk), out,
+                          ctypes.c_size_t(cap), ctypes.byref(n), rcs)
+    assert rc == 0, rc
+    return out.raw[:n.value], list(rcs)
+
+
+def block_sort(block: bytes):
+    L = lib()
+    fmap = (ctypes.c_uint32 * max(1, len(block)))()
+    op = L.oracle_block_sort(block, ctypes.c_int32(len(block)), fmap)
+    return op, list(fmap[:len(block)])
