@@ -1,0 +1,129 @@
+/*
+ * include/starch_amd.h -- C ABI of the MI355X Starch compressor
+ * (libstarch_amd.so, built from starch_amd/csrc/ for gfx950).
+ *
+ * Plain pointers and sizes only; no C++ or torch types cross this boundary.
+ * Every entry point returns an int status: STARCH_OK (0) or a negative code
+ * (starch_strerror()).  Device pointers are HIP device pointers on the
+ * context's device; host pointers are ordinary memory.  One context per
+ * thread (a context owns its HIP stream and HBM workspace); contexts on
+ * different devices are independent.
+ *
+ * What each entry point replaces in the reference (alexpreynolds/starch3):
+ *   starch_encode_*      the whole starch3 pipeline: produce_line/consume_line
+ *                        (include/starch3api.hpp:158-345), update_transformation_
+ *                        state (hpp:428-504), per-chromosome flush
+ *                        process_tf_buffer (hpp:393-407), and the libbz2
+ *                        compressor the reference links for it (hpp:819-888,
+ *                        initialize_bz_stream_ptr: BZ2_bzCompressInit(s, 9, .., 30))
+ *   starch_transform_*   hpp:158-504 alone (the stderr "Content" text)
+ *   starch_bz2_compress_* one BZ2_bzCompressInit + BZ2_bzCompress(BZ_FINISH)
+ *                        stream (bz:bzlib.c:148-474), byte-identical
+ *   the archive layout   magic bytes ca 5c ad 1a (hpp:765-769, 907-910), then
+ *                        one bzip2 stream per chromosome segment, then a JSON
+ *                        index and a 32-byte footer (DESIGN.md "Archive")
+ * The patched-libbz2 streaming ABI (BZ2_bzCompress*) lives in
+ * include/starch_bzlib.h.
+ */
+#ifndef STARCH_AMD_H_
+#define STARCH_AMD_H_
+
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define STARCH_OK 0
+#define STARCH_ERR_ARG (-2)        /* bad argument (bz: BZ_PARAM_ERROR) */
+#define STARCH_ERR_MEM (-3)        /* allocation / capacity (bz: BZ_MEM_ERROR) */
+#define STARCH_ERR_STATE (-4)      /* no result yet */
+#define STARCH_ERR_DEVICE (-10)    /* HIP runtime error or no MI355X */
+#define STARCH_ERR_INTERNAL (-11)
+
+typedef struct starch_ctx starch_ctx;
+
+typedef struct {
+    int block_size_100k;     /* bzip2 level, 1..9 (reference uses 9, hpp:837) */
+    int emit_index;          /* 1: append JSON index + footer after the streams */
+    int reference_compat;    /* 1: archive is exactly the reference's stdout (magic only) */
+    const char* note;        /* --note text for the index (may be NULL) */
+} starch_options;
+
+typedef struct {
+    uint64_t line_count;     /* transform_state_t.line_count at flush (hpp:395) */
+    uint64_t text_bytes;     /* transformed bytes of this segment */
+    uint64_t stream_offset;  /* byte offset of its bzip2 stream in the archive */
+    uint64_t stream_bytes;
+    uint64_t name_len;       /* chromosome name length (starch_segment_name) */
+    uint32_t n_blocks;       /* bzip2 blocks in the stream */
+    uint32_t combined_crc;   /* bzip2 combined stream CRC */
+} starch_segment;
+
+typedef struct {
+    uint64_t input_bytes, n_lines, n_segments, text_bytes, archive_bytes;
+    uint64_t n_blocks, rle_bytes, bwt_rounds, periodic_blocks;
+    float ms_transform, ms_rle, ms_bwt, ms_mtf, ms_tables, ms_emit, ms_total;
+} starch_stats;
+
+int starch_version(void);                         /* 0x000100 = 0.1.0 */
+const char* starch_strerror(int code);
+const char* starch_last_error(starch_ctx* ctx);   /* detail text of the last failure */
+
+int starch_create(int device, starch_ctx** out);
+void starch_destroy(starch_ctx* ctx);
+/* Use an external hipStream_t (e.g. torch.cuda.current_stream().cuda_stream);
+ * NULL restores the context's own stream. */
+int starch_set_stream(starch_ctx* ctx, void* hip_stream);
+void starch_options_init(starch_options* opt);
+
+/* Whole pipeline.  Input BED bytes already in HBM (d_bed, n bytes).  The
+ * archive stays in context-owned HBM until the next call. */
+int starch_encode_device(starch_ctx* ctx, const void* d_bed, uint64_t n, const starch_options* opt);
+/* Same, from host memory (copied to HBM first; the copy is not in ms_total). */
+int starch_encode_host(starch_ctx* ctx, const void* bed, uint64_t n, const starch_options* opt);
+
+int starch_archive_size(starch_ctx* ctx, uint64_t* n);
+int starch_archive_device(starch_ctx* ctx, const void** d_ptr);
+int starch_archive_copy(starch_ctx* ctx, void* dst, uint64_t cap);
+int starch_segment_count(starch_ctx* ctx, uint64_t* n);
+int starch_segments(starch_ctx* ctx, starch_segment* out, uint64_t cap);
+int starch_segment_name(starch_ctx* ctx, uint64_t i, char* buf, uint64_t cap, uint64_t* len);
+int starch_get_stats(starch_ctx* ctx, starch_stats* out);
+
+/* Transform stage only: afterwards starch_text_size/starch_text_copy give the
+ * concatenated segment texts and starch_segments the per-segment counts. */
+int starch_transform_host(starch_ctx* ctx, const void* bed, uint64_t n);
+int starch_text_size(starch_ctx* ctx, uint64_t* n);
+int starch_text_copy(starch_ctx* ctx, void* dst, uint64_t cap);
+
+/* One bzip2 stream (BZ_FINISH semantics) of n bytes; result to host. */
+int starch_bz2_compress_host(starch_ctx* ctx, const void* in, uint64_t n, int block_size_100k, void* out,
+                             uint64_t cap, uint64_t* out_len);
+
+/* Several independent bzip2 streams in one launch sequence (device memory):
+ * stream k = d_in[offs[k] .. offs[k]+lens[k]); results packed back to back in
+ * d_out (4-byte aligned), out_offs[k]/out_lens[k] filled. */
+int starch_bz2_compress_many_device(starch_ctx* ctx, const void* d_in, const uint64_t* offs, const uint64_t* lens,
+                                    uint64_t nstreams, int block_size_100k, void* d_out, uint64_t cap,
+                                    uint64_t* out_offs, uint64_t* out_lens);
+
+/* Synthetic hg38 BED generator (bench/tests): writes the lines of the given
+ * chromosomes (indices into the 24 hg38 chromosomes in sort-bed order) into
+ * dst; kind 0 = BED3 (cfg2), 1 = narrowPeak BED6+4 (cfg4), 2 = per-position
+ * (cfg5).  total_lines is the whole-genome line count the per-chromosome
+ * counts are derived from.  Returns bytes written via *len; pass dst = NULL to
+ * size. */
+int starch_gen_bed(int kind, uint64_t seed, uint64_t total_lines, const int32_t* chroms, int nchroms, void* dst,
+                   uint64_t cap, uint64_t* len);
+
+/* Archive index writer: the JSON index + footer for a set of segments
+ * (used by the multi-GPU gather to assemble rank 0's archive). */
+int starch_build_index(const starch_segment* segs, const char* const* names, const uint64_t* name_lens,
+                       uint64_t nseg, uint64_t index_offset, const char* note, int block_size_100k, char* dst,
+                       uint64_t cap, uint64_t* len);
+
+#ifdef __cplusplus
+}
+#endif
+#endif

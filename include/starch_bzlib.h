@@ -1,0 +1,75 @@
+/*
+ * include/starch_bzlib.h -- drop-in replacement for the compression half of
+ * the PATCHED libbz2 the reference builds against
+ * (third-party/bzip2-1.0.6.tar.gz: bzlib.h:48-69 layout, bzlib.h:103-117
+ * prototypes), implemented on MI355X by libstarch_amd.so.
+ *
+ * Code written against the reference's include/starch3api.hpp (which calls
+ * BZ2_bzCompressInit(s, 9, 0|4, 30) at hpp:835/837, installs handler and
+ * block_close_functor at hpp:857-862 and calls BZ2_bzCompressEnd at hpp:868)
+ * compiles unchanged against this header and links with -lstarch_amd.
+ *
+ * Differences from the patched library (documented in INTEGRATION.md):
+ *  - a NULL block_close_functor is allowed (the patched library calls it
+ *    unconditionally at BZ_STREAM_END, bz:bzlib.c:470, and crashes);
+ *  - the compressed bytes are produced on the GPU when the stream is
+ *    finished; BZ_RUN and BZ_FLUSH consume input and return at once.  The
+ *    final bytes are identical to the patched library for the same call
+ *    sequence (including BZ_FLUSH block boundaries).
+ */
+#ifndef STARCH_BZLIB_H_
+#define STARCH_BZLIB_H_
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define BZ_RUN 0
+#define BZ_FLUSH 1
+#define BZ_FINISH 2
+
+#define BZ_OK 0
+#define BZ_RUN_OK 1
+#define BZ_FLUSH_OK 2
+#define BZ_FINISH_OK 3
+#define BZ_STREAM_END 4
+#define BZ_SEQUENCE_ERROR (-1)
+#define BZ_PARAM_ERROR (-2)
+#define BZ_MEM_ERROR (-3)
+#define BZ_DATA_ERROR (-4)
+#define BZ_DATA_ERROR_MAGIC (-5)
+#define BZ_IO_ERROR (-6)
+#define BZ_UNEXPECTED_EOF (-7)
+#define BZ_OUTBUFF_FULL (-8)
+#define BZ_CONFIG_ERROR (-9)
+
+typedef struct {
+    char* next_in;
+    unsigned int avail_in;
+    unsigned int total_in_lo32;
+    unsigned int total_in_hi32;
+
+    char* next_out;
+    unsigned int avail_out;
+    unsigned int total_out_lo32;
+    unsigned int total_out_hi32;
+
+    void* state;
+
+    void* (*bzalloc)(void*, int, int);
+    void (*bzfree)(void*, void*);
+    void* opaque;
+
+    void* handler;                      /* patched fields (bz:bzlib.h:66-67) */
+    void (*block_close_functor)(void*);
+} bz_stream;
+
+int BZ2_bzCompressInit(bz_stream* strm, int blockSize100k, int verbosity, int workFactor);
+int BZ2_bzCompress(bz_stream* strm, int action);
+int BZ2_bzCompressEnd(bz_stream* strm);
+const char* BZ2_bzlibVersion(void);
+
+#ifdef __cplusplus
+}
+#endif
+#endif

@@ -1,0 +1,296 @@
+"""starch_amd -- host-side (Python) mirror of the Starch operator interface.
+
+The compute lives in ``starch_amd/_build/libstarch_amd.so`` (HIP kernels for
+gfx950 behind the C ABI of ``include/starch_amd.h``).  This module only loads
+that library with ctypes and marshals arguments; there is no Python or CPU
+fallback: if the library or an MI355X is missing, every call raises.
+
+Names follow the reference (alexpreynolds/starch3): ``Starch`` mirrors
+``starch3::Starch`` (include/starch3api.hpp:21-584) -- ``set_note``,
+``set_compression_method``, ``initialize_header_magic_bytes`` -- and
+``Starch.compress(bed)`` is the whole produce_line -> consume_line ->
+update_transformation_state -> process_tf_buffer -> bzip2 path.
+"""
+import ctypes
+import json
+import os
+
+__all__ = ["Starch", "StarchError", "load", "gen_bed", "build_index", "parse_archive", "MAGIC", "HG38"]
+
+_HERE = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.path.join(_HERE, "_build", "libstarch_amd.so")
+MAGIC = b"\xca\x5c\xad\x1a"          # hpp:907-910
+HG38 = [  # sort-bed order; index = chromosome id used by gen_bed
+    "chr1", "chr10", "chr11", "chr12", "chr13", "chr14", "chr15", "chr16", "chr17", "chr18", "chr19",
+    "chr2", "chr20", "chr21", "chr22", "chr3", "chr4", "chr5", "chr6", "chr7", "chr8", "chr9", "chrX", "chrY",
+]
+
+# compression methods (hpp:23-27)
+K_BZIP2, K_GZIP, K_UNDEFINED = 0, 1, 2
+
+
+class StarchError(RuntimeError):
+    def __init__(self, code, msg):
+        super().__init__("starch error %d: %s" % (code, msg))
+        self.code = code
+
+
+class Segment(ctypes.Structure):
+    _fields_ = [("line_count", ctypes.c_uint64), ("text_bytes", ctypes.c_uint64),
+                ("stream_offset", ctypes.c_uint64), ("stream_bytes", ctypes.c_uint64),
+                ("name_len", ctypes.c_uint64), ("n_blocks", ctypes.c_uint32),
+                ("combined_crc", ctypes.c_uint32)]
+
+
+class Options(ctypes.Structure):
+    _fields_ = [("block_size_100k", ctypes.c_int), ("emit_index", ctypes.c_int),
+                ("reference_compat", ctypes.c_int), ("note", ctypes.c_char_p)]
+
+
+class Stats(ctypes.Structure):
+    _fields_ = [(n, ctypes.c_uint64) for n in ("input_bytes", "n_lines", "n_segments", "text_bytes",
+                                               "archive_bytes", "n_blocks", "rle_bytes", "bwt_rounds",
+                                               "periodic_blocks")] + \
+               [(n, ctypes.c_float) for n in ("ms_transform", "ms_rle", "ms_bwt", "ms_mtf", "ms_tables",
+                                              "ms_emit", "ms_total")]
+
+
+_lib = None
+
+
+def load():
+    """Load libstarch_amd.so (raises if it was not built)."""
+    global _lib
+    if _lib is not None:
+        return _lib
+    if not os.path.exists(LIB_PATH):
+        raise StarchError(-10, "native library missing: %s (run __graft_entry__.build())" % LIB_PATH)
+    L = ctypes.CDLL(LIB_PATH)
+    vp, u64, pu64 = ctypes.c_void_p, ctypes.c_uint64, ctypes.POINTER(ctypes.c_uint64)
+    sig = {
+        "starch_version": ([], ctypes.c_int),
+        "starch_strerror": ([ctypes.c_int], ctypes.c_char_p),
+        "starch_last_error": ([vp], ctypes.c_char_p),
+        "starch_create": ([ctypes.c_int, ctypes.POINTER(vp)], ctypes.c_int),
+        "starch_destroy": ([vp], None),
+        "starch_set_stream": ([vp, vp], ctypes.c_int),
+        "starch_options_init": ([ctypes.POINTER(Options)], None),
+        "starch_encode_device": ([vp, vp, u64, ctypes.POINTER(Options)], ctypes.c_int),
+        "starch_encode_host": ([vp, ctypes.c_char_p, u64, ctypes.POINTER(Options)], ctypes.c_int),
+        "starch_archive_size": ([vp, pu64], ctypes.c_int),
+        "starch_archive_device": ([vp, ctypes.POINTER(vp)], ctypes.c_int),
+        "starch_archive_copy": ([vp, vp, u64], ctypes.c_int),
+        "starch_segment_count": ([vp, pu64], ctypes.c_int),
+        "starch_segments": ([vp, ctypes.POINTER(Segment), u64], ctypes.c_int),
+        "starch_segment_name": ([vp, u64, vp, u64, pu64], ctypes.c_int),
+        "starch_get_stats": ([vp, ctypes.POINTER(Stats)], ctypes.c_int),
+        "starch_transform_host": ([vp, ctypes.c_char_p, u64], ctypes.c_int),
+        "starch_text_size": ([vp, pu64], ctypes.c_int),
+        "starch_text_copy": ([vp, vp, u64], ctypes.c_int),
+        "starch_bz2_compress_host": ([vp, ctypes.c_char_p, u64, ctypes.c_int, vp, u64, pu64], ctypes.c_int),
+        "starch_bz2_compress_many_device": ([vp, vp, pu64, pu64, u64, ctypes.c_int, vp, u64, pu64, pu64],
+                                            ctypes.c_int),
+        "starch_gen_bed": ([ctypes.c_int, u64, u64, ctypes.POINTER(ctypes.c_int32), ctypes.c_int, vp, u64, pu64],
+                           ctypes.c_int),
+        "starch_build_index": ([ctypes.POINTER(Segment), ctypes.POINTER(ctypes.c_char_p), pu64, u64, u64,
+                                ctypes.c_char_p, ctypes.c_int, vp, u64, pu64], ctypes.c_int),
+    }
+    for name, (args, res) in sig.items():
+        f = getattr(L, name)
+        f.argtypes = args
+        f.restype = res
+    _lib = L
+    return L
+
+
+def _check(rc, ctx=None):
+    if rc != 0:
+        L = load()
+        detail = L.starch_last_error(ctx).decode(errors="replace") if ctx else ""
+        raise StarchError(rc, (L.starch_strerror(rc) or b"").decode() + (": " + detail if detail else ""))
+
+
+class Starch:
+    """One compression context on one MI355X (``starch3::Starch``, hpp:21-584)."""
+
+    client_name = "starch3"
+    client_version = "0.1"
+
+    def __init__(self, device=0):
+        L = load()
+        h = ctypes.c_void_p()
+        _check(L.starch_create(device, ctypes.byref(h)))
+        self._h = h
+        self._L = L
+        self._note = ""
+        self._method = K_BZIP2
+        self.block_size_100k = 9
+        self._magic = MAGIC
+
+    def close(self):
+        if getattr(self, "_h", None):
+            self._L.starch_destroy(self._h)
+            self._h = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+    # -- starch3::Starch configuration surface -------------------------------
+    def set_note(self, s):                      # hpp:807-809
+        self._note = s
+
+    def get_note(self):
+        return self._note
+
+    def set_compression_method(self, m):        # hpp:815-817
+        if m not in (K_BZIP2, K_GZIP, K_UNDEFINED):
+            raise StarchError(-2, "unknown compression method")
+        self._method = m
+
+    def get_compression_method(self):
+        return self._method
+
+    def initialize_header_magic_bytes(self):    # hpp:907-910
+        self._magic = MAGIC
+        return self._magic
+
+    def set_stream(self, hip_stream_ptr):
+        _check(self._L.starch_set_stream(self._h, ctypes.c_void_p(hip_stream_ptr)), self._h)
+
+    # -- the hot path ----------------------------------------------------------
+    def _opts(self, emit_index=True, reference_compat=False):
+        if self._method == K_GZIP:
+            raise StarchError(-38, "This method is unsupported at this time")      # hpp:777-779
+        if self._method == K_UNDEFINED:
+            raise StarchError(-38, "This method is undefined")                      # hpp:780-782
+        o = Options()
+        self._L.starch_options_init(ctypes.byref(o))
+        o.block_size_100k = self.block_size_100k
+        o.emit_index = 1 if emit_index else 0
+        o.reference_compat = 1 if reference_compat else 0
+        self._note_b = self._note.encode() if self._note else None
+        o.note = self._note_b
+        return o
+
+    def compress(self, bed: bytes, emit_index=True, reference_compat=False) -> bytes:
+        """BED bytes (host) -> Starch archive bytes."""
+        o = self._opts(emit_index, reference_compat)
+        _check(self._L.starch_encode_host(self._h, bed, len(bed), ctypes.byref(o)), self._h)
+        return self.archive()
+
+    def compress_device(self, d_ptr: int, n: int, emit_index=True):
+        """BED bytes already in HBM (device pointer) -> archive stays in HBM."""
+        o = self._opts(emit_index)
+        _check(self._L.starch_encode_device(self._h, ctypes.c_void_p(d_ptr), n, ctypes.byref(o)), self._h)
+
+    def archive_size(self):
+        n = ctypes.c_uint64()
+        _check(self._L.starch_archive_size(self._h, ctypes.byref(n)), self._h)
+        return n.value
+
+    def archive_device_ptr(self):
+        p = ctypes.c_void_p()
+        _check(self._L.starch_archive_device(self._h, ctypes.byref(p)), self._h)
+        return p.value
+
+    def archive(self) -> bytes:
+        n = self.archive_size()
+        buf = ctypes.create_string_buffer(max(1, n))
+        _check(self._L.starch_archive_copy(self._h, buf, n), self._h)
+        return buf.raw[:n]
+
+    def segments(self):
+        """[(chromosome bytes, Segment)] of the last call."""
+        n = ctypes.c_uint64()
+        _check(self._L.starch_segment_count(self._h, ctypes.byref(n)), self._h)
+        arr = (Segment * max(1, n.value))()
+        _check(self._L.starch_segments(self._h, arr, n.value), self._h)
+        out = []
+        for i in range(n.value):
+            ln = ctypes.c_uint64()
+            buf = ctypes.create_string_buffer(max(1, arr[i].name_len))
+            _check(self._L.starch_segment_name(self._h, i, buf, arr[i].name_len, ctypes.byref(ln)), self._h)
+            out.append((buf.raw[:ln.value], arr[i]))
+        return out
+
+    def stats(self):
+        s = Stats()
+        _check(self._L.starch_get_stats(self._h, ctypes.byref(s)), self._h)
+        return {k: getattr(s, k) for k, _ in Stats._fields_}
+
+    def transform(self, bed: bytes):
+        """Transform stage only -> (text, [(chr, line_count, segment text)])."""
+        _check(self._L.starch_transform_host(self._h, bed, len(bed)), self._h)
+        n = ctypes.c_uint64()
+        _check(self._L.starch_text_size(self._h, ctypes.byref(n)), self._h)
+        buf = ctypes.create_string_buffer(max(1, n.value))
+        _check(self._L.starch_text_copy(self._h, buf, n.value), self._h)
+        text = buf.raw[:n.value]
+        segs = []
+        for name, s in self.segments():
+            segs.append((name, s.line_count, text[s.stream_offset:s.stream_offset + s.text_bytes]))
+        return text, segs
+
+    def bz2_compress(self, data: bytes, level: int = 9) -> bytes:
+        """One bzip2 stream, byte-identical to libbz2 BZ2_bzCompress(BZ_FINISH)."""
+        cap = len(data) + len(data) // 50 + 4096
+        buf = ctypes.create_string_buffer(cap)
+        n = ctypes.c_uint64()
+        _check(self._L.starch_bz2_compress_host(self._h, data, len(data), level, buf, cap, ctypes.byref(n)),
+               self._h)
+        return buf.raw[:n.value]
+
+    def bz2_compress_many_device(self, d_in, offs, lens, level, d_out, cap):
+        k = len(offs)
+        O = (ctypes.c_uint64 * max(1, k))(*offs)
+        N = (ctypes.c_uint64 * max(1, k))(*lens)
+        oo = (ctypes.c_uint64 * max(1, k))()
+        ol = (ctypes.c_uint64 * max(1, k))()
+        _check(self._L.starch_bz2_compress_many_device(self._h, ctypes.c_void_p(d_in), O, N, k, level,
+                                                       ctypes.c_void_p(d_out), cap, oo, ol), self._h)
+        return list(oo[:k]), list(ol[:k])
+
+
+def gen_bed(kind, total_lines, chroms=None, seed=20261015, into=None):
+    """Synthetic hg38 BED (kind 0 BED3 / 1 narrowPeak / 2 per-position) for the
+    given chromosome ids; returns bytes, or writes into a ctypes buffer."""
+    L = load()
+    chroms = list(range(24)) if chroms is None else list(chroms)
+    C = (ctypes.c_int32 * max(1, len(chroms)))(*chroms)
+    n = ctypes.c_uint64()
+    _check(L.starch_gen_bed(kind, seed, total_lines, C, len(chroms), None, 0, ctypes.byref(n)))
+    if into is not None:
+        _check(L.starch_gen_bed(kind, seed, total_lines, C, len(chroms), into, n.value, ctypes.byref(n)))
+        return n.value
+    buf = ctypes.create_string_buffer(max(1, n.value))
+    _check(L.starch_gen_bed(kind, seed, total_lines, C, len(chroms), buf, n.value, ctypes.byref(n)))
+    return buf.raw[:n.value]
+
+
+def build_index(segs, names, index_offset, note=None, level=9):
+    """JSON index + 32-byte footer for already-placed streams (multi-GPU gather)."""
+    L = load()
+    k = len(segs)
+    arr = (Segment * max(1, k))(*segs)
+    nm = (ctypes.c_char_p * max(1, k))(*names)
+    nl = (ctypes.c_uint64 * max(1, k))(*[len(x) for x in names])
+    n = ctypes.c_uint64()
+    note_b = note.encode() if note else None
+    _check(L.starch_build_index(arr, nm, nl, k, index_offset, note_b, level, None, 0, ctypes.byref(n)))
+    buf = ctypes.create_string_buffer(max(1, n.value))
+    _check(L.starch_build_index(arr, nm, nl, k, index_offset, note_b, level, buf, n.value, ctypes.byref(n)))
+    return buf.raw[:n.value]
+
+
+def parse_archive(blob: bytes):
+    """Split an archive into (index dict, [stream bytes]) using its footer."""
+    if blob[:4] != MAGIC:
+        raise ValueError("bad magic")
+    foot = blob[-32:]
+    off = int(foot[:20])
+    idx = json.loads(blob[off:-32].decode("latin-1"))
+    streams = [blob[s["offset"]:s["offset"] + s["size"]] for s in idx["streams"]]
+    return idx, streams

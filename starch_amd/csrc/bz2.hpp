@@ -1,0 +1,81 @@
+// starch_amd/csrc/bz2.hpp -- host interface of the GPU bzip2 block pipeline.
+//
+// One bzip2 stream per input segment (a chromosome's transformed text, or a
+// raw byte range for the bzlib ABI).  Byte-exact with bzip2-1.0.6
+// BZ2_bzCompress(..., BZ_FINISH) at blockSize100k = 1..9 (the reference's
+// vendored libbz2, third-party/bzip2-1.0.6.tar.gz).
+#pragma once
+#include "common.hpp"
+#include <vector>
+
+namespace bz {
+
+constexpr int kMaxSelectors = 18002 + 8;   // BZ_MAX_SELECTORS (bz:bzlib_private.h:125)
+
+struct StreamIn {          // one RLE1 piece: a stream, or the part of a stream between BZ_FLUSHes
+    uint64_t text_off;     // offset of its bytes in the device text buffer
+    uint64_t text_len;
+    uint32_t final_run_joins;  // 1: its last byte arrived with the FLUSH/FINISH call (bz:bzlib.c:393-397)
+    uint32_t group;        // output stream it belongs to (pieces of a stream are consecutive)
+};
+
+struct BlockDesc {         // one bzip2 block (bz:compress.c:602-667)
+    uint64_t in_beg, in_end;   // text bytes covered (pre-RLE1)
+    uint64_t w_beg;            // stream-relative RLE1 size before in_beg
+    uint64_t bits;             // bits this block contributes (header + tables + data)
+    uint64_t bit_off;          // absolute bit offset of the block in the output buffer
+    uint32_t stream;           // index into StreamIn
+    uint32_t n;                // nblock (RLE1 bytes)
+    uint32_t crc;              // finalised blockCRC
+    uint32_t orig_ptr;
+    uint32_t n_in_use;
+    uint32_t n_mtf;
+    uint32_t flags;            // bit0: periodic (tie order from exact fallbackSort)
+    uint32_t n_groups, n_sel;
+    uint32_t in_use[8];        // 256-bit inUse map
+    uint32_t hdr_bits;         // bits before the coded data (block header, map, selectors, tables)
+    uint32_t pad;
+};
+
+struct StreamOut {
+    uint64_t out_off;          // byte offset of the stream in the output buffer
+    uint64_t bytes;            // stream length in bytes
+    uint32_t first_block, n_blocks;
+    uint32_t combined_crc;
+    uint32_t pad;
+};
+
+struct Stats {                 // per-stage device timings (ms) from HIP events
+    float rle = 0, bwt = 0, mtf = 0, tables = 0, emit = 0;
+    uint64_t n_blocks = 0, rle_bytes = 0, bwt_rounds = 0, periodic_blocks = 0;
+};
+
+class Encoder {
+public:
+    // Compress `streams` whose bytes live in d_text (device).  The result is
+    // written to d_out (device) at out_base: stream k at out_base +
+    // outs[k].out_off, streams back to back.  Capacity is checked.  Returns
+    // the total number of bytes written after out_base.
+    uint64_t plan_and_encode(const uint8_t* d_text, const std::vector<StreamIn>& streams, int bs100k,
+                             uint8_t* d_out, uint64_t out_cap, uint64_t out_base, std::vector<StreamOut>& outs,
+                             hipStream_t st, Stats* stats = nullptr);
+    // Two-phase form used by the archive writer: plan() computes stream sizes;
+    // emit() writes the bits once the caller has chosen out_base.
+    void plan(const uint8_t* d_text, const std::vector<StreamIn>& streams, int bs100k, hipStream_t st,
+              std::vector<StreamOut>& outs, Stats* stats = nullptr);
+    void emit(uint8_t* d_out, uint64_t out_cap, uint64_t out_base, std::vector<StreamOut>& outs, hipStream_t st,
+              Stats* stats = nullptr);
+
+private:
+    DevBuf b_streams, b_tiles, b_tile_sum, b_tile_carry, b_tile_w, b_tile_wpre, b_tpos, b_seg_tile0, b_seg_nblk,
+        b_blk_tmp, b_blk, b_blkbytes, b_scal, b_tmp, b_bwt, b_mtfv, b_freq, b_sel, b_tabs, b_gbits, b_souts,
+        b_fallback;
+    const uint8_t* text_ = nullptr;
+    int bs100k_ = 9;
+    uint32_t nblocks_ = 0, nstreams_ = 0, ngroups_ = 0;
+    uint64_t blk_stride_ = 0;
+    std::vector<StreamIn> streams_;
+    std::vector<BlockDesc> host_blocks_;
+};
+
+}  // namespace bz

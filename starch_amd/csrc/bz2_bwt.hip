@@ -1,0 +1,486 @@
+// starch_amd/csrc/bz2_bwt.hip -- Burrows-Wheeler block sort on MI355X.
+//
+// Replaces BZ2_blockSort (bz:blocksort.c:1031-1089).  For a non-periodic
+// block every rotation is distinct, so the sorted order -- and hence origPtr
+// and the last column -- is unique: any exact cyclic-rotation sort reproduces
+// bzip2's bytes.  We sort with prefix doubling, one 1024-thread
+// workgroup per block, all state in HBM:
+//   round 0: key = first D symbols of the rotation, packed with
+//            B = ceil(log2(nInUse)) bits each (D = 64/B: 16 symbols for the
+//            <=16-symbol alphabets of BED3 transforms), stable LSD radix sort
+//            (8-bit digits, histogram + wave-ballot ranking in LDS);
+//   round r: only rotations in unresolved groups are re-sorted by
+//            (group head, rank of rotation + h), h = D*2^(r-1).
+// A round that splits no group proves the remaining groups are true ties, i.e.
+// the block is periodic.  For those blocks bzip2's origPtr is
+// fallbackSort's tie order, so k_fallback_exact re-runs a restatement of
+// fallbackSort (bz:blocksort.c:30-329) for that block only, with the
+// all-equal-key buckets (whose 3-way partition is the identity) skipped.
+#include "bz2_int.hpp"
+#include "bz2_bwt.hpp"
+
+namespace bz {
+
+constexpr int BT = 1024;          // threads per block-sort workgroup
+constexpr int NWV = BT / 64;      // waves
+
+struct RadixSmem {
+    uint32_t hist[256];
+    uint32_t base[256];
+    uint32_t wcnt[NWV][256];
+    uint32_t scan[NWV + 1];
+    uint32_t flag;
+};
+
+__device__ __forceinline__ uint64_t lanemask_lt()
+{
+    const int lane = threadIdx.x & 63;
+    return lane ? (~0ull >> (64 - lane)) : 0ull;
+}
+
+// One stable LSD pass by digit (key >> shift) & 255 over [0, m).
+// Returns false (and writes nothing) when every key has the same digit.
+template <class V>
+__device__ bool radix_pass(const uint64_t* Ks, const V* Vs, uint64_t* Kd, V* Vd, uint32_t m, int shift,
+                           RadixSmem& sm)
+{
+    const int tid = threadIdx.x, wid = tid >> 6;
+    for (int i = tid; i < 256; i += BT) sm.hist[i] = 0;
+    for (int i = tid; i < NWV * 256; i += BT) (&sm.wcnt[0][0])[i] = 0;
+    __syncthreads();
+    for (uint32_t i = tid; i < m; i += BT) atomicAdd(&sm.hist[(Ks[i] >> shift) & 255u], 1u);
+    __syncthreads();
+    if (tid < 64) {   // exclusive scan of 256 bins, 4 per lane
+        uint32_t a0 = sm.hist[4 * tid], a1 = sm.hist[4 * tid + 1], a2 = sm.hist[4 * tid + 2],
+                 a3 = sm.hist[4 * tid + 3];
+        uint32_t s = a0 + a1 + a2 + a3;
+        uint32_t inc = wave_incl_scan_add(s);
+        uint32_t e = inc - s;
+        sm.base[4 * tid] = e;
+        sm.base[4 * tid + 1] = e + a0;
+        sm.base[4 * tid + 2] = e + a0 + a1;
+        sm.base[4 * tid + 3] = e + a0 + a1 + a2;
+        bool single = (a0 == m) || (a1 == m) || (a2 == m) || (a3 == m);
+        uint64_t any = __ballot(single);
+        if (tid == 0) sm.flag = any ? 1u : 0u;
+    }
+    __syncthreads();
+    if (sm.flag) return false;
+    for (uint32_t t0 = 0; t0 < m; t0 += BT) {
+        const uint32_t i = t0 + tid;
+        const bool valid = i < m;
+        uint64_t k = 0;
+        V v = V(0);
+        uint32_t d = 0;
+        if (valid) { k = Ks[i]; v = Vs[i]; d = (uint32_t)(k >> shift) & 255u; }
+        uint64_t mask = __ballot(valid);
+#pragma unroll
+        for (int b = 0; b < 8; ++b) {
+            uint64_t bal = __ballot((d >> b) & 1u);
+            mask &= ((d >> b) & 1u) ? bal : ~bal;
+        }
+        const uint32_t rank = __popcll(mask & lanemask_lt());
+        if (valid && rank == 0) sm.wcnt[wid][d] = __popcll(mask);
+        __syncthreads();
+        if (tid < 256) {
+            uint32_t run = sm.base[tid];
+#pragma unroll
+            for (int w = 0; w < NWV; ++w) { uint32_t c = sm.wcnt[w][tid]; sm.wcnt[w][tid] = run; run += c; }
+            sm.base[tid] = run;
+        }
+        __syncthreads();
+        if (valid) {
+            uint32_t dst = sm.wcnt[wid][d] + rank;
+            Kd[dst] = k;
+            Vd[dst] = v;
+        }
+        __syncthreads();
+        for (int j = tid; j < NWV * 256; j += BT) (&sm.wcnt[0][0])[j] = 0;
+        __syncthreads();
+    }
+    return true;
+}
+
+// Sort (K,V)[0,m) by the low `bits` bits; result may end in either buffer.
+template <class V>
+__device__ void radix_sort(uint64_t*& K, V*& Vv, uint64_t*& K2, V*& V2, uint32_t m, int bits, RadixSmem& sm)
+{
+    for (int sh = 0; sh < bits; sh += 8) {
+        if (radix_pass<V>(K, Vv, K2, V2, m, sh, sm)) {
+            uint64_t* tk = K; K = K2; K2 = tk;
+            V* tv = Vv; Vv = V2; V2 = tv;
+        }
+    }
+}
+
+__device__ __forceinline__ int bits_for(uint32_t x) { return x ? 32 - __clz(x) : 0; }
+
+__global__ void __launch_bounds__(BT) k_bwt(BlockDesc* __restrict__ blocks, uint32_t b0,
+                                             const uint8_t* __restrict__ blkbytes, uint64_t stride,
+                                             BwtScratch scr, unsigned long long* __restrict__ stats)
+{
+    __shared__ RadixSmem sm;
+    __shared__ uint8_t sym[256];
+    __shared__ uint32_t carry[4];
+    const int tid = threadIdx.x;
+    const uint32_t b = b0 + blockIdx.x;
+    const uint32_t n = blocks[b].n;
+    const uint8_t* blk = blkbytes + (uint64_t)b * stride;
+    const uint64_t so = (uint64_t)blockIdx.x * scr.stride;
+    uint64_t* K = scr.K + so;
+    uint64_t* K2 = scr.K2 + so;
+    uint32_t* Vv = scr.V + so;
+    uint32_t* V2 = scr.V2 + so;
+    uint32_t* SA = scr.SA + so;
+    uint32_t* RK = scr.RK + so;
+    uint32_t* U = scr.U + so;
+    uint32_t* U2 = scr.U2 + so;
+
+    // alphabet -> dense order-preserving symbols
+    if (tid < 256) {
+        uint32_t c = tid;
+        uint32_t w = blocks[b].in_use[c >> 5];
+        uint32_t below = 0;
+        for (uint32_t j = 0; j < (c >> 5); ++j) below += __popc(blocks[b].in_use[j]);
+        below += __popc(w & ((1u << (c & 31)) - 1u));
+        sym[c] = (uint8_t)below;
+    }
+    if (tid == 0) {
+        uint32_t nu = 0;
+        for (int j = 0; j < 8; ++j) nu += __popc(blocks[b].in_use[j]);
+        carry[0] = nu;
+    }
+    __syncthreads();
+    const uint32_t n_in_use = carry[0];
+    const int B = n_in_use > 1 ? bits_for(n_in_use - 1) : 1;
+    const int D = 64 / B;
+    __syncthreads();
+
+    if (n <= 1) {
+        if (tid == 0) { blocks[b].orig_ptr = 0; SA[0] = 0; blocks[b].flags = 0; blocks[b].n_in_use = n_in_use; }
+        return;
+    }
+    // ---- round 0: sort by D-symbol packed prefix ----
+    for (uint32_t i = tid; i < n; i += BT) {
+        uint64_t key = 0;
+        uint32_t j = i;
+        for (int k = 0; k < D; ++k) {
+            key = (key << B) | sym[blk[j]];
+            if (++j == n) j = 0;
+        }
+        K[i] = key;
+        Vv[i] = i;
+    }
+    __syncthreads();
+    radix_sort<uint32_t>(K, Vv, K2, V2, n, D * B, sm);
+    // heads, ranks, unresolved list
+    if (tid == 0) { carry[0] = 0; carry[1] = 0; carry[2] = 0; }
+    __syncthreads();
+    for (uint32_t t0 = 0; t0 < n; t0 += BT) {
+        const uint32_t j = t0 + tid;
+        const bool valid = j < n;
+        uint64_t kj = valid ? K[j] : 0;
+        bool head = valid && (j == 0 || K[j - 1] != kj);
+        bool nexth = !valid || (j + 1 >= n) || K[j + 1] != kj;
+        uint32_t hp = block_incl_scan_max<uint32_t>(head ? j : 0u, sm.scan);
+        uint32_t cm = carry[0];
+        hp = hp > cm ? hp : cm;
+        uint32_t sa = valid ? Vv[j] : 0;
+        if (valid) { SA[j] = sa; RK[sa] = hp; }
+        bool unres = valid && !(head && nexth);
+        uint32_t tot, gtot;
+        uint32_t pre = block_excl_scan_add<uint32_t>(unres ? 1u : 0u, sm.scan, &tot);
+        if (unres) U[carry[1] + pre] = j;
+        (void)block_excl_scan_add<uint32_t>((unres && head) ? 1u : 0u, sm.scan, &gtot);
+        if (tid == BT - 1) { carry[0] = hp; carry[1] += tot; carry[2] += gtot; }
+        __syncthreads();
+    }
+    uint32_t m = carry[1];
+    uint32_t groups = carry[2];
+    const int rbits = bits_for(n - 1);
+    uint64_t h = (uint64_t)D;
+    uint32_t rounds = 0;
+    bool periodic = false;
+    while (m > 0) {
+        ++rounds;
+        for (uint32_t k = tid; k < m; k += BT) {
+            uint32_t j = U[k];
+            uint32_t sa = SA[j];
+            uint32_t nx = (uint32_t)(((uint64_t)sa + h) % n);
+            K[k] = ((uint64_t)RK[sa] << rbits) | RK[nx];
+            Vv[k] = sa;
+        }
+        __syncthreads();
+        radix_sort<uint32_t>(K, Vv, K2, V2, m, 2 * rbits, sm);
+        if (tid == 0) { carry[0] = 0; carry[1] = 0; carry[2] = 0; }
+        __syncthreads();
+        for (uint32_t t0 = 0; t0 < m; t0 += BT) {
+            const uint32_t k = t0 + tid;
+            const bool valid = k < m;
+            uint64_t key = valid ? K[k] : 0;
+            bool nh = valid && (k == 0 || K[k - 1] != key);
+            bool nexth = !valid || (k + 1 >= m) || K[k + 1] != key;
+            uint32_t j = valid ? U[k] : 0;
+            uint32_t hp = block_incl_scan_max<uint32_t>(nh ? j : 0u, sm.scan);
+            uint32_t cm = carry[0];
+            hp = hp > cm ? hp : cm;
+            if (valid) {
+                uint32_t sa = Vv[k];
+                SA[j] = sa;
+                RK[sa] = hp;
+            }
+            bool keep = valid && !(nh && nexth);
+            uint32_t tot, gtot;
+            uint32_t pre = block_excl_scan_add<uint32_t>(keep ? 1u : 0u, sm.scan, &tot);
+            if (keep) U2[carry[1] + pre] = j;
+            (void)block_excl_scan_add<uint32_t>(nh ? 1u : 0u, sm.scan, &gtot);
+            if (tid == BT - 1) { carry[0] = hp; carry[1] += tot; carry[2] += gtot; }
+            __syncthreads();
+        }
+        uint32_t new_groups = carry[2];
+        uint32_t nm = carry[1];
+        __syncthreads();
+        if (new_groups == groups) { periodic = true; break; }   // nothing split: true ties
+        // groups still unresolved for the next round
+        groups = 0;
+        {
+            uint32_t* t = U; U = U2; U2 = t;
+        }
+        m = nm;
+        // count heads among the remaining unresolved positions
+        if (tid == 0) carry[3] = 0;
+        __syncthreads();
+        uint32_t local = 0;
+        for (uint32_t k = tid; k < m; k += BT) {
+            uint32_t j = U[k];
+            uint32_t r = RK[SA[j]];
+            local += (r == j) ? 1u : 0u;
+        }
+        local = wave_reduce_add(local);
+        if ((tid & 63) == 0) atomicAdd(&carry[3], local);
+        __syncthreads();
+        groups = carry[3];
+        __syncthreads();
+        h *= 2;
+        if (h >= 2ull * n + (uint64_t)D) { periodic = (m > 0); break; }
+    }
+    __syncthreads();
+    for (uint32_t j = tid; j < n; j += BT)
+        if (SA[j] == 0) blocks[b].orig_ptr = j;
+    if (tid == 0) {
+        blocks[b].flags = periodic ? 1u : 0u;
+        blocks[b].n_in_use = n_in_use;
+        atomicAdd(stats, (unsigned long long)rounds);
+        if (periodic) atomicAdd(stats + 1, 1ull);
+    }
+}
+
+// ---------------------------------------------------------------------------
+// Exact fallbackSort restatement for periodic blocks (bz:blocksort.c:30-329).
+// ---------------------------------------------------------------------------
+__device__ void fb_simple(uint32_t* fmap, const uint32_t* ecls, int32_t lo, int32_t hi)
+{
+    if (lo == hi) return;
+    if (hi - lo > 3) {
+        for (int32_t a = hi - 4; a >= lo; --a) {
+            uint32_t x = fmap[a], kx = ecls[x];
+            int32_t q = a + 4;
+            while (q <= hi && kx > ecls[fmap[q]]) { fmap[q - 4] = fmap[q]; q += 4; }
+            fmap[q - 4] = x;
+        }
+    }
+    for (int32_t a = hi - 1; a >= lo; --a) {
+        uint32_t x = fmap[a], kx = ecls[x];
+        int32_t q = a + 1;
+        while (q <= hi && kx > ecls[fmap[q]]) { fmap[q - 1] = fmap[q]; ++q; }
+        fmap[q - 1] = x;
+    }
+}
+
+__device__ void fb_qsort3(uint32_t* fmap, const uint32_t* ecls, int32_t lo0, int32_t hi0)
+{
+    int32_t slo[100], shi[100];
+    int32_t sp = 0;
+    uint32_t r = 0;
+    slo[sp] = lo0; shi[sp] = hi0; ++sp;
+    while (sp > 0) {
+        --sp;
+        int32_t lo = slo[sp], hi = shi[sp];
+        if (hi - lo < 10) { fb_simple(fmap, ecls, lo, hi); continue; }
+        r = (r * 7621u + 1u) % 32768u;
+        uint32_t pv;
+        uint32_t r3 = r % 3u;
+        if (r3 == 0) pv = ecls[fmap[lo]]; else if (r3 == 1) pv = ecls[fmap[(lo + hi) >> 1]]; else pv = ecls[fmap[hi]];
+        int32_t ulo = lo, lt = lo, uhi = hi, gt = hi;
+        for (;;) {
+            while (ulo <= uhi) {
+                int64_t dd = (int64_t)ecls[fmap[ulo]] - (int64_t)pv;
+                if (dd == 0) { uint32_t t = fmap[ulo]; fmap[ulo] = fmap[lt]; fmap[lt] = t; ++lt; ++ulo; continue; }
+                if (dd > 0) break;
+                ++ulo;
+            }
+            while (ulo <= uhi) {
+                int64_t dd = (int64_t)ecls[fmap[uhi]] - (int64_t)pv;
+                if (dd == 0) { uint32_t t = fmap[uhi]; fmap[uhi] = fmap[gt]; fmap[gt] = t; --gt; --uhi; continue; }
+                if (dd < 0) break;
+                --uhi;
+            }
+            if (ulo > uhi) break;
+            uint32_t t = fmap[ulo]; fmap[ulo] = fmap[uhi]; fmap[uhi] = t;
+            ++ulo; --uhi;
+        }
+        if (gt < lt) continue;
+        int32_t k = (lt - lo < ulo - lt) ? lt - lo : ulo - lt;
+        for (int32_t a = lo, bb = ulo - k; k > 0; --k, ++a, ++bb) { uint32_t t = fmap[a]; fmap[a] = fmap[bb]; fmap[bb] = t; }
+        int32_t mm = (hi - gt < gt - uhi) ? hi - gt : gt - uhi;
+        for (int32_t a = ulo, bb = hi - mm + 1; mm > 0; --mm, ++a, ++bb) { uint32_t t = fmap[a]; fmap[a] = fmap[bb]; fmap[bb] = t; }
+        int32_t ahi = lo + ulo - lt - 1;
+        int32_t blo = hi - (gt - uhi) + 1;
+        if (ahi - lo > hi - blo) {
+            slo[sp] = lo; shi[sp] = ahi; ++sp;
+            slo[sp] = blo; shi[sp] = hi; ++sp;
+        } else {
+            slo[sp] = blo; shi[sp] = hi; ++sp;
+            slo[sp] = lo; shi[sp] = ahi; ++sp;
+        }
+    }
+}
+
+// One workgroup per periodic block.  fmap <- V, eclass <- RK (as scratch),
+// head flags <- U (u32 0/1), mixed flags <- U2.
+__global__ void __launch_bounds__(BT) k_fallback_exact(BlockDesc* __restrict__ blocks, uint32_t b0,
+                                                        const uint32_t* __restrict__ which, uint32_t nwhich,
+                                                        const uint8_t* __restrict__ blkbytes, uint64_t stride,
+                                                        BwtScratch scr)
+{
+    __shared__ RadixSmem sm;
+    __shared__ uint32_t carry[4];
+    const int tid = threadIdx.x;
+    if (blockIdx.x >= nwhich) return;
+    const uint32_t slot = which[blockIdx.x];        // batch-relative block index
+    const uint32_t b = b0 + slot;
+    const uint32_t n = blocks[b].n;
+    const uint8_t* blk = blkbytes + (uint64_t)b * stride;
+    const uint64_t so = (uint64_t)slot * scr.stride;
+    uint64_t* K = scr.K + so;
+    uint64_t* K2 = scr.K2 + so;
+    uint32_t* fmap = scr.V + so;
+    uint32_t* V2 = scr.V2 + so;
+    uint32_t* SA = scr.SA + so;
+    uint32_t* ecls = scr.RK + so;
+    uint32_t* head = scr.U + so;
+    uint32_t* mixed = scr.U2 + so;
+
+    // initial 1-byte bucket sort: within a bucket, indices DESCENDING (bz:blocksort.c:245-249)
+    for (uint32_t i = tid; i < n; i += BT) { K[i] = blk[i]; fmap[i] = i; }
+    __syncthreads();
+    uint64_t* Kp = K; uint64_t* K2p = K2; uint32_t* Vp = fmap; uint32_t* V2p = V2;
+    radix_sort<uint32_t>(Kp, Vp, K2p, V2p, n, 8, sm);
+    // bucket bounds: reuse hist via a fresh count
+    for (int i = tid; i < 256; i += BT) { sm.hist[i] = 0; }
+    __syncthreads();
+    for (uint32_t i = tid; i < n; i += BT) atomicAdd(&sm.hist[blk[i]], 1u);
+    __syncthreads();
+    if (tid == 0) { uint32_t a = 0; for (int c = 0; c < 256; ++c) { sm.base[c] = a; a += sm.hist[c]; } }
+    __syncthreads();
+    for (uint32_t j = tid; j < n; j += BT) {
+        uint32_t c = (uint32_t)Kp[j];
+        uint32_t bs = sm.base[c], be = bs + sm.hist[c];
+        SA[bs + be - 1 - j] = Vp[j];
+        head[j] = 0;
+    }
+    __syncthreads();
+    for (int c = tid; c < 256; c += BT) if (sm.hist[c]) head[sm.base[c]] = 1;
+    __syncthreads();
+    fmap = SA;   // fmap now lives in SA
+    for (uint64_t H = 1;; H *= 2) {
+        // eclass[fmap[i]-H] = last head at or before i
+        if (tid == 0) carry[0] = 0;
+        __syncthreads();
+        for (uint32_t t0 = 0; t0 < n; t0 += BT) {
+            uint32_t i = t0 + tid;
+            bool valid = i < n;
+            uint32_t hv = (valid && head[i]) ? i : 0u;
+            uint32_t j = block_incl_scan_max<uint32_t>(hv, sm.scan);
+            uint32_t cm = carry[0];
+            j = j > cm ? j : cm;
+            if (valid) {
+                int64_t k = (int64_t)fmap[i] - (int64_t)H;
+                k %= (int64_t)n;
+                if (k < 0) k += n;
+                ecls[k] = j;
+                mixed[i] = 0;
+            }
+            if (tid == BT - 1) carry[0] = j;
+            __syncthreads();
+        }
+        // mark buckets whose keys are not all equal (group head l = max-scan of heads)
+        if (tid == 0) { carry[0] = 0; carry[1] = 0; }
+        __syncthreads();
+        for (uint32_t t0 = 0; t0 < n; t0 += BT) {
+            uint32_t i = t0 + tid;
+            bool valid = i < n;
+            uint32_t hv = (valid && head[i]) ? i : 0u;
+            uint32_t l = block_incl_scan_max<uint32_t>(hv, sm.scan);
+            uint32_t cm = carry[0];
+            l = l > cm ? l : cm;
+            bool nd = valid && !(head[i] && (i + 1 >= n || head[i + 1]));
+            if (valid && !head[i] && ecls[fmap[i]] != ecls[fmap[l]]) mixed[l] = 1;
+            uint32_t c = 0;
+            c = nd ? 1u : 0u;
+            uint32_t tot;
+            (void)block_excl_scan_add<uint32_t>(c, sm.scan, &tot);
+            if (tid == BT - 1) { carry[0] = l; carry[1] += tot; }
+            __syncthreads();
+        }
+        uint32_t not_done = carry[1];
+        __syncthreads();
+        // mixed buckets: exact fallbackQSort3, one thread per bucket, in any order
+        // (buckets are disjoint and r restarts per call, bz:blocksort.c:104)
+        for (uint32_t l = tid; l < n; l += BT) {
+            if (head[l] && mixed[l]) {
+                uint32_t r = l + 1;
+                while (r < n && !head[r]) ++r;
+                fb_qsort3(fmap, ecls, (int32_t)l, (int32_t)(r - 1));
+            }
+        }
+        __syncthreads();
+        // new heads where eclass changes inside mixed buckets
+        for (uint32_t t0 = 0; t0 < n; t0 += BT) {
+            uint32_t i = t0 + tid;
+            bool valid = i < n;
+            uint32_t hv = (valid && head[i]) ? i : 0u;
+            uint32_t l = block_incl_scan_max<uint32_t>(hv, sm.scan);
+            if (tid == 0 && t0 == 0) carry[0] = 0;
+            uint32_t cm = (t0 == 0) ? 0u : carry[0];
+            l = l > cm ? l : cm;
+            bool set = valid && !head[i] && mixed[l] && ecls[fmap[i]] != ecls[fmap[i - 1]];
+            __syncthreads();
+            if (set) head[i] = 1;
+            if (tid == BT - 1) carry[0] = l;
+            __syncthreads();
+        }
+        if (2 * H > n || not_done == 0) break;
+    }
+    __syncthreads();
+    for (uint32_t j = tid; j < n; j += BT)
+        if (SA[j] == 0) blocks[b].orig_ptr = j;
+}
+
+void launch_bwt(BlockDesc* blocks, uint32_t b0, uint32_t nb, const uint8_t* blkbytes, uint64_t stride,
+                const BwtScratch& scr, unsigned long long* stats, hipStream_t st)
+{
+    hipLaunchKernelGGL(k_bwt, dim3(nb), dim3(BT), 0, st, blocks, b0, blkbytes, stride, scr, stats);
+    HIP_CHECK(hipGetLastError());
+}
+
+void launch_fallback(BlockDesc* blocks, uint32_t b0, const uint32_t* which, uint32_t nwhich,
+                     const uint8_t* blkbytes, uint64_t stride, const BwtScratch& scr, hipStream_t st)
+{
+    if (!nwhich) return;
+    hipLaunchKernelGGL(k_fallback_exact, dim3(nwhich), dim3(BT), 0, st, blocks, b0, which, nwhich, blkbytes, stride,
+                       scr);
+    HIP_CHECK(hipGetLastError());
+}
+
+}  // namespace bz

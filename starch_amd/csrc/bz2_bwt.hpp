@@ -1,0 +1,33 @@
+// starch_amd/csrc/bz2_bwt.hpp -- block-sort scratch (per batch slot, HBM).
+#pragma once
+#include "bz2_int.hpp"
+
+namespace bz {
+
+struct BwtScratch {            // 40 bytes per rotation per batch slot
+    uint64_t* K;
+    uint64_t* K2;
+    uint32_t* V;
+    uint32_t* V2;
+    uint32_t* SA;              // sorted rotation order (ptr[] of bz:blocksort.c)
+    uint32_t* RK;
+    uint32_t* U;
+    uint32_t* U2;
+    uint64_t stride;           // elements per slot
+};
+
+void launch_bwt(BlockDesc* blocks, uint32_t b0, uint32_t nb, const uint8_t* blkbytes, uint64_t stride,
+                const BwtScratch& scr, unsigned long long* stats, hipStream_t st);
+void launch_fallback(BlockDesc* blocks, uint32_t b0, const uint32_t* which, uint32_t nwhich,
+                     const uint8_t* blkbytes, uint64_t stride, const BwtScratch& scr, hipStream_t st);
+void launch_mtf(BlockDesc* blocks, uint32_t b0, uint32_t nb, const uint8_t* blkbytes, uint64_t stride,
+                const BwtScratch& scr, uint16_t* mtfv, uint64_t mtf_stride, Tables* tabs, hipStream_t st);
+void launch_tables(BlockDesc* blocks, uint32_t b0, uint32_t nb, const uint16_t* mtfv, uint64_t mtf_stride,
+                   Tables* tabs, uint8_t* sel, uint32_t* gbits, hipStream_t st);
+void launch_emit_blocks(const BlockDesc* blocks, uint32_t nb, const uint16_t* mtfv, uint64_t mtf_stride,
+                        const Tables* tabs, const uint8_t* sel, const uint32_t* gbits, uint32_t* out32,
+                        hipStream_t st);
+void launch_stream_frame(const StreamOut* souts, const BlockDesc* blocks, uint32_t nstreams, int bs100k,
+                         uint64_t out_base, uint32_t* out32, hipStream_t st);
+
+}  // namespace bz

@@ -1,0 +1,192 @@
+// starch_amd/csrc/bz2_emit.hip -- bit emission straight into the archive.
+//
+// Restates the writing half of sendMTFValues / BZ2_compressBlock
+// (bz:compress.c:494-598, 602-667) and the MSB-first bit writer
+// (bz:compress.c:37-97).  Every block already knows its absolute bit offset
+// (blocks are bit-concatenated inside a stream, bz:compress.c:609), so all
+// 50-symbol groups of all blocks are written in parallel: a lane owns a bit
+// range, plain-stores the 32-bit big-endian words fully inside it and ORs
+// (atomically) the two words it may share with its neighbours.  The output
+// buffer is zeroed beforehand.
+#include "bz2_bwt.hpp"
+
+namespace bz {
+
+struct BitOut {
+    uint32_t* w;
+    uint64_t word;
+    uint64_t acc;
+    int nb;
+    bool first;
+    __device__ void init(uint32_t* out, uint64_t pos)
+    {
+        w = out;
+        word = pos >> 5;
+        nb = (int)(pos & 31);
+        acc = 0;
+        first = nb != 0;
+    }
+    __device__ __forceinline__ void flush_word(uint32_t v)
+    {
+        uint32_t be = __builtin_bswap32(v);
+        if (first) atomicOr(&w[word], be); else w[word] = be;
+        first = false;
+        ++word;
+    }
+    __device__ __forceinline__ void put(int len, uint32_t code)
+    {
+        acc = (acc << len) | (uint64_t)code;
+        nb += len;
+        if (nb >= 32) {
+            nb -= 32;
+            flush_word((uint32_t)(acc >> nb));
+            acc &= nb ? ((1ull << nb) - 1ull) : 0ull;
+        }
+    }
+    __device__ void finish()
+    {
+        if (nb > 0) atomicOr(&w[word], __builtin_bswap32((uint32_t)(acc << (32 - nb))));
+        nb = 0;
+    }
+};
+
+constexpr int ET = 256;
+
+__global__ void __launch_bounds__(ET) k_emit_block(const BlockDesc* __restrict__ blocks,
+                                                    const uint16_t* __restrict__ mtfv_all, uint64_t mtf_stride,
+                                                    const Tables* __restrict__ tabs, const uint8_t* __restrict__ sel_all,
+                                                    const uint32_t* __restrict__ gbits_all, uint32_t* __restrict__ out32)
+{
+    __shared__ uint8_t len[6][258];
+    __shared__ uint32_t code[6][258];
+    __shared__ uint32_t scan_sh[ET / 64 + 1];
+    __shared__ unsigned long long carry;
+    const int tid = threadIdx.x;
+    const uint32_t b = blockIdx.x;
+    const BlockDesc bd = blocks[b];
+    const int alpha = (int)bd.n_in_use + 2;
+    const int ng = (int)bd.n_groups;
+    for (int i = tid; i < 6 * 258; i += ET) {
+        int t = i / 258, v = i % 258;
+        if (t < ng && v < alpha) { len[t][v] = tabs[b].len[t][v]; code[t][v] = tabs[b].code[t][v]; }
+    }
+    if (tid == 0) carry = 0;
+    __syncthreads();
+    const uint16_t* mtfv = mtfv_all + (uint64_t)b * mtf_stride;
+    const uint8_t* sel = sel_all + (uint64_t)b * (2 * kMaxSelectors);
+    const uint8_t* selmtf = sel + kMaxSelectors;
+    const uint32_t* gbits = gbits_all + (uint64_t)b * kMaxSelectors;
+
+    if (tid == 0) {   // block header, mapping table, selectors, code lengths
+        BitOut o;
+        o.init(out32, bd.bit_off);
+        o.put(24, 0x314159u);
+        o.put(24, 0x265359u);
+        o.put(32, bd.crc);
+        o.put(1, 0);
+        o.put(24, bd.orig_ptr);
+        uint32_t u16 = 0;
+        for (int i = 0; i < 16; ++i) {
+            uint32_t w = bd.in_use[i >> 1];
+            uint32_t half = (i & 1) ? (w >> 16) : (w & 0xffffu);
+            if (half) u16 |= 1u << (15 - i);
+        }
+        o.put(16, u16);
+        for (int i = 0; i < 16; ++i) {
+            if (!(u16 & (1u << (15 - i)))) continue;
+            uint32_t w = bd.in_use[i >> 1];
+            uint32_t half = (i & 1) ? (w >> 16) : (w & 0xffffu);
+            uint32_t bits = 0;
+            for (int j = 0; j < 16; ++j) if (half & (1u << j)) bits |= 1u << (15 - j);
+            o.put(16, bits);
+        }
+        o.put(3, (uint32_t)ng);
+        o.put(15, bd.n_sel);
+        for (uint32_t i = 0; i < bd.n_sel; ++i) {
+            uint32_t j = selmtf[i];
+            o.put((int)j + 1, ((1u << j) - 1u) << 1);
+        }
+        for (int t = 0; t < ng; ++t) {
+            int cur = len[t][0];
+            o.put(5, (uint32_t)cur);
+            for (int i = 0; i < alpha; ++i) {
+                while (cur < len[t][i]) { o.put(2, 2); ++cur; }
+                while (cur > len[t][i]) { o.put(2, 3); --cur; }
+                o.put(1, 0);
+            }
+        }
+        o.finish();
+    }
+    // coded data, one 50-symbol group per lane
+    const uint64_t data0 = bd.bit_off + bd.hdr_bits;
+    for (uint32_t g0 = 0; g0 < bd.n_sel; g0 += ET) {
+        uint32_t g = g0 + tid;
+        uint32_t gb = (g < bd.n_sel) ? gbits[g] : 0u;
+        uint32_t tot;
+        uint32_t pre = block_excl_scan_add<uint32_t>(gb, scan_sh, &tot);
+        if (g < bd.n_sel) {
+            BitOut o;
+            o.init(out32, data0 + carry + pre);
+            uint32_t gs = g * 50, ge = gs + 50;
+            if (ge > bd.n_mtf) ge = bd.n_mtf;
+            const int t = sel[g];
+            for (uint32_t i = gs; i < ge; ++i) {
+                uint32_t v = mtfv[i];
+                o.put(len[t][v], code[t][v]);
+            }
+            o.finish();
+        }
+        __syncthreads();
+        if (tid == 0) carry += tot;
+        __syncthreads();
+    }
+}
+
+// stream header "BZh"+level and trailer (end magic, combined CRC, byte pad)
+__global__ void k_stream_frame(const StreamOut* __restrict__ souts, const BlockDesc* __restrict__ blocks,
+                               uint32_t nstreams, int bs100k, uint64_t out_base, uint32_t* __restrict__ out32)
+{
+    uint32_t s = blockIdx.x * blockDim.x + threadIdx.x;
+    if (s >= nstreams) return;
+    const StreamOut so = souts[s];
+    uint64_t pos = (out_base + so.out_off) * 8;
+    BitOut o;
+    o.init(out32, pos);
+    o.put(8, 'B');
+    o.put(8, 'Z');
+    o.put(8, 'h');
+    o.put(8, (uint32_t)('0' + bs100k));
+    o.finish();
+    uint32_t comb = 0;
+    uint64_t end = pos + 32;
+    for (uint32_t k = 0; k < so.n_blocks; ++k) {
+        const BlockDesc& bd = blocks[so.first_block + k];
+        comb = ((comb << 1) | (comb >> 31)) ^ bd.crc;                   // bz:compress.c:606-608
+        end += bd.bits;
+    }
+    o.init(out32, end);
+    o.put(24, 0x177245u);
+    o.put(24, 0x385090u);
+    o.put(32, comb);
+    o.finish();
+}
+
+void launch_emit_blocks(const BlockDesc* blocks, uint32_t nb, const uint16_t* mtfv, uint64_t mtf_stride,
+                        const Tables* tabs, const uint8_t* sel, const uint32_t* gbits, uint32_t* out32,
+                        hipStream_t st)
+{
+    if (!nb) return;
+    hipLaunchKernelGGL(k_emit_block, dim3(nb), dim3(ET), 0, st, blocks, mtfv, mtf_stride, tabs, sel, gbits, out32);
+    HIP_CHECK(hipGetLastError());
+}
+
+void launch_stream_frame(const StreamOut* souts, const BlockDesc* blocks, uint32_t nstreams, int bs100k,
+                         uint64_t out_base, uint32_t* out32, hipStream_t st)
+{
+    if (!nstreams) return;
+    hipLaunchKernelGGL(k_stream_frame, dim3((nstreams + 63) / 64), dim3(64), 0, st, souts, blocks, nstreams, bs100k,
+                       out_base, out32);
+    HIP_CHECK(hipGetLastError());
+}
+
+}  // namespace bz

@@ -1,0 +1,272 @@
+// starch_amd/csrc/bz2_encoder.hip -- host orchestration of the GPU bzip2
+// pipeline (the work bzip2's handle_compress / BZ2_compressBlock loop does
+// serially, bz:bzlib.c:369-412, bz:compress.c:602-667).  All byte work runs
+// in the kernels of bz2_rle / bz2_bwt / bz2_mtf / bz2_tables / bz2_emit; the
+// host only sizes buffers, reads back per-stream / per-block counters and
+// lays out offsets.
+#include "bz2_bwt.hpp"
+
+#include <algorithm>
+
+namespace bz {
+
+struct EvTimer {
+    hipEvent_t a = nullptr, b = nullptr;
+    hipStream_t st;
+    float* out;
+    EvTimer(hipStream_t s, float* o) : st(s), out(o)
+    {
+        if (!out) return;
+        HIP_CHECK(hipEventCreate(&a));
+        HIP_CHECK(hipEventCreate(&b));
+        HIP_CHECK(hipEventRecord(a, st));
+    }
+    void stop()
+    {
+        if (!out || !a) return;
+        HIP_CHECK(hipEventRecord(b, st));
+        HIP_CHECK(hipEventSynchronize(b));
+        float ms = 0;
+        HIP_CHECK(hipEventElapsedTime(&ms, a, b));
+        *out += ms;
+        (void)hipEventDestroy(a);
+        (void)hipEventDestroy(b);
+        a = b = nullptr;
+    }
+    ~EvTimer() { if (a) stop(); }
+};
+
+static uint64_t round_up(uint64_t x, uint64_t m) { return (x + m - 1) / m * m; }
+
+void Encoder::plan(const uint8_t* d_text, const std::vector<StreamIn>& streams, int bs100k, hipStream_t st,
+                   std::vector<StreamOut>& outs, Stats* stats)
+{
+    if (bs100k < 1 || bs100k > 9) throw StarchError(-2, "blockSize100k must be 1..9");
+    upload_crc_constants();
+    text_ = d_text;
+    bs100k_ = bs100k;
+    streams_ = streams;
+    nstreams_ = (uint32_t)streams.size();
+    const uint32_t nblock_max = 100000u * (uint32_t)bs100k - 19u;     // bz:bzlib.c:194
+    blk_stride_ = round_up(100000ull * bs100k + 64, 256);
+    ngroups_ = 0;
+    for (uint32_t s = 0; s < nstreams_; ++s) {
+        if (streams[s].group < ngroups_ - (ngroups_ ? 1u : 0u) || streams[s].group > ngroups_)
+            throw StarchError(-2, "stream pieces must be grouped consecutively");
+        ngroups_ = std::max(ngroups_, streams[s].group + 1);
+    }
+    outs.assign(ngroups_, StreamOut());
+    nblocks_ = 0;
+    if (nstreams_ == 0) return;
+
+    EvTimer t_rle(st, stats ? &stats->rle : nullptr);
+    StreamIn* d_streams = b_streams.as<StreamIn>(nstreams_);
+    HIP_CHECK(hipMemcpyAsync(d_streams, streams.data(), nstreams_ * sizeof(StreamIn), hipMemcpyHostToDevice, st));
+    std::vector<uint64_t> tile0(nstreams_ + 1, 0);
+    uint64_t text_end = 0;
+    for (uint32_t s = 0; s < nstreams_; ++s) {
+        tile0[s + 1] = tile0[s] + ceil_div(streams[s].text_len, kTB);
+        text_end = std::max(text_end, streams[s].text_off + streams[s].text_len);
+    }
+    const uint64_t ntiles = tile0[nstreams_];
+    uint64_t* d_tile0 = b_seg_tile0.as<uint64_t>(nstreams_ + 1);
+    HIP_CHECK(hipMemcpyAsync(d_tile0, tile0.data(), (nstreams_ + 1) * sizeof(uint64_t), hipMemcpyHostToDevice, st));
+
+    TileDesc* d_tiles = b_tiles.as<TileDesc>(ntiles + 1);
+    TileSum* d_sums = b_tile_sum.as<TileSum>(ntiles + 1);
+    uint32_t* d_carry = b_tile_carry.as<uint32_t>(ntiles + 1);
+    uint32_t* d_tw = b_tile_w.as<uint32_t>(ntiles + 1);
+    uint64_t* d_twpre = b_tile_wpre.as<uint64_t>(ntiles + 1);
+    uint8_t* d_tpos = b_tpos.as<uint8_t>(text_end + 16);
+    uint64_t* d_scal = b_scal.as<uint64_t>(nstreams_ + 16);
+    HIP_CHECK(hipMemsetAsync(d_twpre, 0, (ntiles + 1) * sizeof(uint64_t), st));
+    if (ntiles) {
+        rle_tiles(d_tile0, d_streams, nstreams_, ntiles, d_tiles, st);
+        rle_sum(d_text, d_tiles, ntiles, d_sums, st);
+        rle_carry(d_tile0, nstreams_, d_sums, d_carry, st);
+        rle_pos(d_text, d_tiles, ntiles, d_carry, d_tpos, d_tw, st);
+        scan::excl_sum_u32_to_u64(d_tw, d_twpre, ntiles, d_twpre + ntiles, b_tmp, st);
+    }
+    rle_stream_w(d_tile0, d_twpre, nstreams_, d_scal, st);
+    HIP_CHECK(hipGetLastError());
+    std::vector<uint64_t> wtot(nstreams_);
+    HIP_CHECK(hipMemcpyAsync(wtot.data(), d_scal, nstreams_ * sizeof(uint64_t), hipMemcpyDeviceToHost, st));
+    HIP_CHECK(hipStreamSynchronize(st));
+
+    std::vector<uint64_t> slot0(nstreams_ + 1, 0);
+    for (uint32_t s = 0; s < nstreams_; ++s) slot0[s + 1] = slot0[s] + wtot[s] / nblock_max + 2;
+    uint64_t* d_slot0 = b_seg_nblk.as<uint64_t>(2 * nstreams_ + 2);
+    uint32_t* d_nblk = reinterpret_cast<uint32_t*>(d_slot0 + nstreams_ + 1);
+    HIP_CHECK(hipMemcpyAsync(d_slot0, slot0.data(), (nstreams_ + 1) * sizeof(uint64_t), hipMemcpyHostToDevice, st));
+    BlockDesc* d_btmp = b_blk_tmp.as<BlockDesc>(slot0[nstreams_] + 1);
+    rle_cut(d_streams, d_tile0, d_twpre, d_tpos, nstreams_, nblock_max, d_slot0, d_btmp, d_nblk, st);
+    HIP_CHECK(hipGetLastError());
+    std::vector<uint32_t> nblk(nstreams_);
+    HIP_CHECK(hipMemcpyAsync(nblk.data(), d_nblk, nstreams_ * sizeof(uint32_t), hipMemcpyDeviceToHost, st));
+    HIP_CHECK(hipStreamSynchronize(st));
+    std::vector<uint32_t> first(nstreams_, 0);
+    uint32_t nb = 0;
+    for (uint32_t s = 0; s < nstreams_; ++s) {
+        first[s] = nb;
+        StreamOut& g = outs[streams[s].group];
+        if (g.n_blocks == 0) g.first_block = nb;
+        g.n_blocks += nblk[s];
+        nb += nblk[s];
+    }
+    nblocks_ = nb;
+    uint32_t* d_first = reinterpret_cast<uint32_t*>(b_souts.as<uint64_t>(nstreams_ + 1));
+    HIP_CHECK(hipMemcpyAsync(d_first, first.data(), nstreams_ * sizeof(uint32_t), hipMemcpyHostToDevice, st));
+    BlockDesc* d_blocks = b_blk.as<BlockDesc>(nb + 1);
+    rle_compact(d_btmp, d_slot0, d_nblk, d_first, nstreams_, d_blocks, st);
+    uint8_t* d_blkbytes = b_blkbytes.as<uint8_t>((uint64_t)nb * blk_stride_ + 64);
+    if (ntiles) {
+        rle_emit(d_text, d_tiles, ntiles, d_twpre, d_tile0, d_tpos, d_streams, d_first, d_nblk, d_blocks, d_blkbytes,
+                     blk_stride_, st);
+    }
+    rle_crc(d_text, d_blocks, nb, st);
+    HIP_CHECK(hipGetLastError());
+    t_rle.stop();
+    if (stats) stats->n_blocks += nb;
+    if (nb == 0) {
+        for (uint32_t g = 0; g < ngroups_; ++g) outs[g].bytes = 14;   // header + trailer (bz:compress.c:622-666)
+        uint64_t off = 0;
+        for (uint32_t g = 0; g < ngroups_; ++g) { outs[g].out_off = off; off += outs[g].bytes; }
+        return;
+    }
+
+    // ---- per-batch: block sort, MTF, tables ---------------------------------
+    size_t free_b = 0, total_b = 0;
+    HIP_CHECK(hipMemGetInfo(&free_b, &total_b));
+    const uint64_t mtf_stride = blk_stride_ + 16;
+    uint16_t* d_mtfv = b_mtfv.as<uint16_t>((uint64_t)nb * mtf_stride);
+    Tables* d_tabs = b_tabs.as<Tables>(nb);
+    uint8_t* d_sel = b_sel.as<uint8_t>((uint64_t)nb * 2 * kMaxSelectors);
+    uint32_t* d_gbits = b_gbits.as<uint32_t>((uint64_t)nb * kMaxSelectors);
+    HIP_CHECK(hipMemGetInfo(&free_b, &total_b));
+    const uint64_t per_slot = blk_stride_ * 40ull;
+    uint64_t max_batch = std::max<uint64_t>(1, (uint64_t)(free_b * 0.45) / per_slot);
+    uint32_t batch = (uint32_t)std::min<uint64_t>({(uint64_t)nb, max_batch, 2048ull});
+    if (b_bwt.cap < batch * per_slot) {
+        // allocate the whole batch scratch once
+        b_bwt.get(batch * per_slot);
+    }
+    BwtScratch scr;
+    {
+        uint8_t* base = static_cast<uint8_t*>(b_bwt.get(batch * per_slot));
+        uint64_t S = blk_stride_;
+        scr.stride = S;
+        scr.K = reinterpret_cast<uint64_t*>(base);
+        scr.K2 = scr.K + S * batch;
+        scr.V = reinterpret_cast<uint32_t*>(scr.K2 + S * batch);
+        scr.V2 = scr.V + S * batch;
+        scr.SA = scr.V2 + S * batch;
+        scr.RK = scr.SA + S * batch;
+        scr.U = scr.RK + S * batch;
+        scr.U2 = scr.U + S * batch;
+    }
+    unsigned long long* d_stats = reinterpret_cast<unsigned long long*>(d_scal);
+    HIP_CHECK(hipMemsetAsync(d_stats, 0, 4 * sizeof(uint64_t), st));
+    std::vector<BlockDesc> hb(nb);
+    uint32_t* d_which = reinterpret_cast<uint32_t*>(b_fallback.as<uint32_t>(batch + 1));
+    for (uint32_t b0 = 0; b0 < nb; b0 += batch) {
+        uint32_t cnt = std::min(batch, nb - b0);
+        {
+            EvTimer tb(st, stats ? &stats->bwt : nullptr);
+            launch_bwt(d_blocks, b0, cnt, d_blkbytes, blk_stride_, scr, d_stats, st);
+            HIP_CHECK(hipMemcpyAsync(hb.data() + b0, d_blocks + b0, cnt * sizeof(BlockDesc), hipMemcpyDeviceToHost,
+                                     st));
+            HIP_CHECK(hipStreamSynchronize(st));
+            std::vector<uint32_t> which;
+            for (uint32_t k = 0; k < cnt; ++k)
+                if (hb[b0 + k].flags & 1u) which.push_back(k);
+            if (!which.empty()) {
+                HIP_CHECK(hipMemcpyAsync(d_which, which.data(), which.size() * sizeof(uint32_t),
+                                         hipMemcpyHostToDevice, st));
+                launch_fallback(d_blocks, b0, d_which, (uint32_t)which.size(), d_blkbytes, blk_stride_, scr, st);
+                if (stats) stats->periodic_blocks += which.size();
+            }
+        }
+        {
+            EvTimer tm(st, stats ? &stats->mtf : nullptr);
+            launch_mtf(d_blocks, b0, cnt, d_blkbytes, blk_stride_, scr, d_mtfv, mtf_stride, d_tabs, st);
+        }
+        {
+            EvTimer tt(st, stats ? &stats->tables : nullptr);
+            launch_tables(d_blocks, b0, cnt, d_mtfv, mtf_stride, d_tabs, d_sel, d_gbits, st);
+        }
+    }
+    HIP_CHECK(hipMemcpyAsync(hb.data(), d_blocks, nb * sizeof(BlockDesc), hipMemcpyDeviceToHost, st));
+    uint64_t hstats[4] = {0, 0, 0, 0};
+    HIP_CHECK(hipMemcpyAsync(hstats, d_stats, sizeof(hstats), hipMemcpyDeviceToHost, st));
+    HIP_CHECK(hipStreamSynchronize(st));
+    if (stats) {
+        stats->bwt_rounds += hstats[0];
+        for (auto& b : hb) stats->rle_bytes += b.n;
+    }
+    // stream sizes: 32 header bits + blocks + 80 trailer bits, padded to a byte
+    uint64_t off = 0;
+    for (uint32_t s = 0; s < ngroups_; ++s) {
+        uint64_t bits = 32 + 80;
+        for (uint32_t k = 0; k < outs[s].n_blocks; ++k) bits += hb[outs[s].first_block + k].bits;
+        outs[s].bytes = (bits + 7) / 8;
+        outs[s].out_off = off;
+        off += outs[s].bytes;
+    }
+    host_blocks_.swap(hb);
+}
+
+void Encoder::emit(uint8_t* d_out, uint64_t out_cap, uint64_t out_base, std::vector<StreamOut>& outs,
+                   hipStream_t st, Stats* stats)
+{
+    EvTimer te(st, stats ? &stats->emit : nullptr);
+    uint64_t total = 0;
+    for (auto& o : outs) total = std::max(total, o.out_off + o.bytes);
+    if (((uintptr_t)d_out & 3u) != 0) throw StarchError(-2, "output buffer must be 4-byte aligned");
+    if (out_base + total + 4 > out_cap) throw StarchError(-3, "output buffer too small");
+    if (total == 0) return;
+    HIP_CHECK(hipMemsetAsync(d_out + out_base, 0, total, st));
+    // absolute bit offsets of every block
+    for (uint32_t s = 0; s < ngroups_; ++s) {
+        uint64_t pos = (out_base + outs[s].out_off) * 8 + 32;
+        for (uint32_t k = 0; k < outs[s].n_blocks; ++k) {
+            BlockDesc& b = host_blocks_[outs[s].first_block + k];
+            b.bit_off = pos;
+            pos += b.bits;
+        }
+    }
+    BlockDesc* d_blocks = static_cast<BlockDesc*>(b_blk.p);
+    if (nblocks_) {
+        HIP_CHECK(hipMemcpyAsync(d_blocks, host_blocks_.data(), nblocks_ * sizeof(BlockDesc), hipMemcpyHostToDevice,
+                                 st));
+    }
+    StreamOut* d_souts = b_souts.as<StreamOut>(ngroups_ + 1);
+    HIP_CHECK(hipMemcpyAsync(d_souts, outs.data(), ngroups_ * sizeof(StreamOut), hipMemcpyHostToDevice, st));
+    uint32_t* out32 = reinterpret_cast<uint32_t*>(d_out);
+    const uint64_t mtf_stride = blk_stride_ + 16;
+    launch_emit_blocks(d_blocks, nblocks_, static_cast<uint16_t*>(b_mtfv.p), mtf_stride,
+                       static_cast<Tables*>(b_tabs.p), static_cast<uint8_t*>(b_sel.p),
+                       static_cast<uint32_t*>(b_gbits.p), out32, st);
+    launch_stream_frame(d_souts, d_blocks, ngroups_, bs100k_, out_base, out32, st);
+    for (uint32_t s = 0; s < ngroups_; ++s) {
+        uint32_t comb = 0;
+        for (uint32_t k = 0; k < outs[s].n_blocks; ++k) {
+            uint32_t c = host_blocks_[outs[s].first_block + k].crc;
+            comb = ((comb << 1) | (comb >> 31)) ^ c;
+        }
+        outs[s].combined_crc = comb;
+    }
+    te.stop();
+}
+
+uint64_t Encoder::plan_and_encode(const uint8_t* d_text, const std::vector<StreamIn>& streams, int bs100k,
+                                  uint8_t* d_out, uint64_t out_cap, uint64_t out_base, std::vector<StreamOut>& outs,
+                                  hipStream_t st, Stats* stats)
+{
+    plan(d_text, streams, bs100k, st, outs, stats);
+    emit(d_out, out_cap, out_base, outs, st, stats);
+    uint64_t total = 0;
+    for (auto& o : outs) total = std::max(total, o.out_off + o.bytes);
+    return total;
+}
+
+}  // namespace bz

@@ -1,0 +1,59 @@
+// starch_amd/csrc/bz2_int.hpp -- internal types shared by the bzip2 stage files.
+#pragma once
+#include "bz2.hpp"
+
+namespace bz {
+
+constexpr int kTB = 4096;             // tile bytes for the RLE1 passes
+
+struct TileDesc {                     // a <= 4 KiB slice of one stream
+    uint64_t beg;
+    uint32_t len;
+    uint32_t stream;
+    uint32_t first;
+    uint32_t pad;
+};
+
+struct TileSum {                      // run summary of a tile
+    uint32_t len, trail;
+    uint8_t first, last, uni, pad;
+};
+
+struct Tables {                       // per-block Huffman state (bz:compress.c:238-598)
+    uint8_t len[6][258];
+    uint8_t pad[4];
+    uint32_t code[6][258];
+    uint32_t freq[258];               // mtfFreq
+    uint32_t pad2[2];
+};
+
+static inline uint32_t host_mulmod(uint32_t a, uint32_t b)
+{
+    uint32_t r = 0;
+    for (int i = 31; i >= 0; --i) {
+        r = (r & 0x80000000u) ? ((r << 1) ^ 0x04c11db7u) : (r << 1);
+        if ((b >> i) & 1u) r ^= a;
+    }
+    return r;
+}
+
+void upload_crc_constants();
+
+// bz2_rle.hip launch wrappers
+void rle_tiles(const uint64_t* tile0, const StreamIn* streams, uint32_t ns, uint64_t ntiles, TileDesc* tiles,
+               hipStream_t st);
+void rle_sum(const uint8_t* text, const TileDesc* tiles, uint64_t ntiles, TileSum* sums, hipStream_t st);
+void rle_carry(const uint64_t* tile0, uint32_t ns, const TileSum* sums, uint32_t* carry, hipStream_t st);
+void rle_pos(const uint8_t* text, const TileDesc* tiles, uint64_t ntiles, const uint32_t* carry, uint8_t* tpos,
+             uint32_t* tile_w, hipStream_t st);
+void rle_stream_w(const uint64_t* tile0, const uint64_t* wpre, uint32_t ns, uint64_t* out, hipStream_t st);
+void rle_cut(const StreamIn* streams, const uint64_t* tile0, const uint64_t* wpre, const uint8_t* tpos, uint32_t ns,
+             uint32_t nblock_max, const uint64_t* slot0, BlockDesc* tmp, uint32_t* nblk, hipStream_t st);
+void rle_compact(const BlockDesc* tmp, const uint64_t* slot0, const uint32_t* nblk, const uint32_t* first, uint32_t ns,
+                 BlockDesc* out, hipStream_t st);
+void rle_emit(const uint8_t* text, const TileDesc* tiles, uint64_t ntiles, const uint64_t* wpre, const uint64_t* tile0,
+              const uint8_t* tpos, const StreamIn* streams, const uint32_t* first, const uint32_t* nblk,
+              BlockDesc* blocks, uint8_t* blk, uint64_t stride, hipStream_t st);
+void rle_crc(const uint8_t* text, BlockDesc* blocks, uint32_t nb, hipStream_t st);
+
+}  // namespace bz

@@ -1,0 +1,218 @@
+// starch_amd/csrc/bz2_tables.hip -- coding-table selection and Huffman code
+// lengths on MI355X (restates sendMTFValues' table part, bz:compress.c:266-
+// 489, and BZ2_hbMakeCodeLengths / BZ2_hbAssignCodes, bz:huffman.c:63-166).
+//
+// One 1024-thread workgroup per block.  Per refinement pass the 50-symbol
+// groups are costed against every table in parallel (lengths in LDS, first
+// minimum wins as in bz:compress.c:399-401) and the chosen table's symbol
+// frequencies are accumulated with LDS atomics; then one lane per table
+// rebuilds that table's lengths with the exact heap algorithm (weights carry
+// depth in the low byte, maxLen 17, halving retry).  The block's exact bit
+// length (header + selectors + tables + data) is produced here, so stream
+// offsets are known before any bit is written.
+#include "bz2_bwt.hpp"
+
+namespace bz {
+
+constexpr int TT = 1024;
+
+struct HuffSmem {
+    int32_t heap[6][262];
+    int32_t weight[6][516];
+    int32_t parent[6][516];
+};
+
+__device__ void hb_make_lengths(uint8_t* len, const uint32_t* freq, int32_t alpha, int32_t max_len, int32_t* heap,
+                                int32_t* weight, int32_t* parent)
+{
+    for (int32_t i = 0; i < alpha; ++i) weight[i + 1] = (int32_t)((freq[i] == 0 ? 1u : freq[i]) << 8);
+    for (;;) {
+        int32_t nodes = alpha, nheap = 0;
+        heap[0] = 0; weight[0] = 0; parent[0] = -2;
+        for (int32_t i = 1; i <= alpha; ++i) {
+            parent[i] = -1;
+            heap[++nheap] = i;
+            int32_t zz = nheap, t = heap[zz];                       // UPHEAP
+            while (weight[t] < weight[heap[zz >> 1]]) { heap[zz] = heap[zz >> 1]; zz >>= 1; }
+            heap[zz] = t;
+        }
+        while (nheap > 1) {
+            int32_t pick[2];
+            for (int q = 0; q < 2; ++q) {
+                pick[q] = heap[1];
+                heap[1] = heap[nheap--];
+                int32_t zz = 1, t = heap[zz];                       // DOWNHEAP
+                for (;;) {
+                    int32_t yy = zz << 1;
+                    if (yy > nheap) break;
+                    if (yy < nheap && weight[heap[yy + 1]] < weight[heap[yy]]) ++yy;
+                    if (weight[t] < weight[heap[yy]]) break;
+                    heap[zz] = heap[yy];
+                    zz = yy;
+                }
+                heap[zz] = t;
+            }
+            ++nodes;
+            parent[pick[0]] = parent[pick[1]] = nodes;
+            int32_t wa = weight[pick[0]], wb = weight[pick[1]];
+            int32_t da = wa & 0xff, db = wb & 0xff;
+            weight[nodes] = (int32_t)(((uint32_t)wa & 0xffffff00u) + ((uint32_t)wb & 0xffffff00u)) |
+                            (1 + (da > db ? da : db));
+            parent[nodes] = -1;
+            heap[++nheap] = nodes;
+            int32_t zz = nheap, t = heap[zz];
+            while (weight[t] < weight[heap[zz >> 1]]) { heap[zz] = heap[zz >> 1]; zz >>= 1; }
+            heap[zz] = t;
+        }
+        bool too_long = false;
+        for (int32_t i = 1; i <= alpha; ++i) {
+            int32_t d = 0, k = i;
+            while (parent[k] >= 0) { k = parent[k]; ++d; }
+            len[i - 1] = (uint8_t)d;
+            if (d > max_len) too_long = true;
+        }
+        if (!too_long) break;
+        for (int32_t i = 1; i <= alpha; ++i) weight[i] = (1 + ((weight[i] >> 8) / 2)) << 8;
+    }
+}
+
+__global__ void __launch_bounds__(TT) k_tables(BlockDesc* __restrict__ blocks, uint32_t b0,
+                                                const uint16_t* __restrict__ mtfv_all, uint64_t mtf_stride,
+                                                Tables* __restrict__ tabs, uint8_t* __restrict__ sel_all,
+                                                uint32_t* __restrict__ gbits_all)
+{
+    __shared__ HuffSmem hs;
+    __shared__ uint8_t len[6][258];
+    __shared__ uint32_t rfreq[6][258];
+    __shared__ uint32_t freq[258];
+    __shared__ uint32_t scan_sh[TT / 64 + 1];
+    __shared__ uint32_t info[4];
+    __shared__ unsigned long long hdr_bits;
+
+    const int tid = threadIdx.x;
+    const uint32_t b = b0 + blockIdx.x;
+    const uint16_t* mtfv = mtfv_all + (uint64_t)b * mtf_stride;
+    uint8_t* sel = sel_all + (uint64_t)b * (2 * kMaxSelectors);
+    uint8_t* selmtf = sel + kMaxSelectors;
+    uint32_t* gbits = gbits_all + (uint64_t)b * kMaxSelectors;
+    const uint32_t n_mtf = blocks[b].n_mtf;
+    const int32_t alpha = (int32_t)blocks[b].n_in_use + 2;
+    const int ng = n_mtf < 200 ? 2 : n_mtf < 600 ? 3 : n_mtf < 1200 ? 4 : n_mtf < 2400 ? 5 : 6;
+    const uint32_t nsel = (n_mtf + 49) / 50;
+
+    if (tid < 258) freq[tid] = tabs[b].freq[tid];
+    for (int i = tid; i < 6 * 258; i += TT) (&len[0][0])[i] = 15;   // BZ_GREATER_ICOST
+    __syncthreads();
+    if (tid == 0) {   // initial equal-frequency bands (bz:compress.c:280-317)
+        int32_t parts = ng, rem = (int32_t)n_mtf, gs = 0;
+        while (parts > 0) {
+            int32_t target = rem / parts, ge = gs - 1, acc = 0;
+            while (acc < target && ge < alpha - 1) { ++ge; acc += (int32_t)freq[ge]; }
+            if (ge > gs && parts != ng && parts != 1 && ((ng - parts) % 2 == 1)) { acc -= (int32_t)freq[ge]; --ge; }
+            for (int32_t v = 0; v < alpha; ++v) len[parts - 1][v] = (v >= gs && v <= ge) ? 0 : 15;
+            --parts;
+            gs = ge + 1;
+            rem -= acc;
+        }
+    }
+    __syncthreads();
+    for (int iter = 0; iter < 4; ++iter) {                         // BZ_N_ITERS
+        for (int i = tid; i < 6 * 258; i += TT) (&rfreq[0][0])[i] = 0;
+        __syncthreads();
+        for (uint32_t g = tid; g < nsel; g += TT) {
+            uint32_t gs = g * 50, ge = gs + 50;
+            if (ge > n_mtf) ge = n_mtf;
+            uint32_t cost[6] = {0, 0, 0, 0, 0, 0};
+            for (uint32_t i = gs; i < ge; ++i) {
+                uint32_t v = mtfv[i];
+#pragma unroll
+                for (int t = 0; t < 6; ++t) cost[t] += len[t][v];
+            }
+            int bt = 0;
+            uint32_t bc = cost[0];
+            for (int t = 1; t < ng; ++t) if (cost[t] < bc) { bc = cost[t]; bt = t; }
+            sel[g] = (uint8_t)bt;
+            for (uint32_t i = gs; i < ge; ++i) atomicAdd(&rfreq[bt][mtfv[i]], 1u);
+        }
+        __syncthreads();
+        if (tid < ng) hb_make_lengths(len[tid], rfreq[tid], alpha, 17, hs.heap[tid], hs.weight[tid], hs.parent[tid]);
+        __syncthreads();
+    }
+    // selector MTF (bz:compress.c:461-478) and header size
+    if (tid == 0) {
+        uint8_t pos[6];
+        for (int i = 0; i < ng; ++i) pos[i] = (uint8_t)i;
+        uint64_t sbits = 0;
+        for (uint32_t i = 0; i < nsel; ++i) {
+            uint8_t want = sel[i];
+            int j = 0;
+            uint8_t carry_v = pos[0];
+            while (carry_v != want && j < 5) { ++j; uint8_t t = pos[j]; pos[j] = carry_v; carry_v = t; }
+            pos[0] = carry_v;
+            selmtf[i] = (uint8_t)j;
+            sbits += (uint64_t)j + 1;
+        }
+        uint32_t used16 = 0;
+        for (int i = 0; i < 16; ++i) {
+            uint32_t w = blocks[b].in_use[i >> 1];
+            uint32_t half = (i & 1) ? (w >> 16) : (w & 0xffffu);
+            if (half) ++used16;
+        }
+        uint64_t tbits = 0;
+        for (int t = 0; t < ng; ++t) {
+            int32_t cur = len[t][0];
+            tbits += 5;
+            for (int32_t i = 0; i < alpha; ++i) {
+                int32_t d = (int32_t)len[t][i] - cur;
+                tbits += 1 + 2 * (uint64_t)(d < 0 ? -d : d);
+                cur = len[t][i];
+            }
+        }
+        hdr_bits = 48 + 32 + 1 + 24 + 16 + 16ull * used16 + 3 + 15 + sbits + tbits;
+        blocks[b].hdr_bits = (uint32_t)hdr_bits;
+    }
+    // canonical codes (bz:huffman.c:152-166)
+    if (tid < ng) {
+        int32_t mn = 32, mx = 0;
+        for (int32_t i = 0; i < alpha; ++i) {
+            int32_t l = len[tid][i];
+            if (l > mx) mx = l;
+            if (l < mn) mn = l;
+        }
+        int32_t v = 0;
+        for (int32_t L = mn; L <= mx; ++L) {
+            for (int32_t i = 0; i < alpha; ++i) if (len[tid][i] == L) tabs[b].code[tid][i] = (uint32_t)v++;
+            v <<= 1;
+        }
+        for (int32_t i = 0; i < alpha; ++i) tabs[b].len[tid][i] = len[tid][i];
+    }
+    __syncthreads();
+    // data bits per group
+    uint64_t local = 0;
+    for (uint32_t g = tid; g < nsel; g += TT) {
+        uint32_t gs = g * 50, ge = gs + 50;
+        if (ge > n_mtf) ge = n_mtf;
+        const uint8_t* L = len[sel[g]];
+        uint32_t bits = 0;
+        for (uint32_t i = gs; i < ge; ++i) bits += L[mtfv[i]];
+        gbits[g] = bits;
+        local += bits;
+    }
+    local = wave_reduce_add(local);
+    if ((tid & 63) == 0) atomicAdd(&hdr_bits, (unsigned long long)local);
+    __syncthreads();
+    if (tid == 0) {
+        blocks[b].bits = hdr_bits;
+        blocks[b].n_groups = (uint32_t)ng;
+        blocks[b].n_sel = nsel;
+    }
+}
+
+void launch_tables(BlockDesc* blocks, uint32_t b0, uint32_t nb, const uint16_t* mtfv, uint64_t mtf_stride,
+                   Tables* tabs, uint8_t* sel, uint32_t* gbits, hipStream_t st)
+{
+    hipLaunchKernelGGL(k_tables, dim3(nb), dim3(TT), 0, st, blocks, b0, mtfv, mtf_stride, tabs, sel, gbits);
+    HIP_CHECK(hipGetLastError());
+}
+
+}  // namespace bz

@@ -1,0 +1,142 @@
+// starch_amd/csrc/common.hpp -- shared device/host helpers for the MI355X
+// (gfx950, CDNA4) Starch pipeline.  wave64 throughout; all arithmetic integer.
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+#include <stdio.h>
+#include <stdlib.h>
+#include <string>
+#include <stdexcept>
+
+#define ST_WAVE 64
+
+struct StarchError : std::runtime_error {
+    int code;
+    StarchError(int c, const std::string& m) : std::runtime_error(m), code(c) {}
+};
+
+#define HIP_CHECK(expr)                                                                 \
+    do {                                                                                \
+        hipError_t _e = (expr);                                                         \
+        if (_e != hipSuccess)                                                           \
+            throw StarchError(-10, std::string("HIP error ") + hipGetErrorString(_e) + \
+                                       " at " __FILE__ ":" + std::to_string(__LINE__)); \
+    } while (0)
+
+static inline uint64_t ceil_div(uint64_t a, uint64_t b) { return (a + b - 1) / b; }
+
+// ---------------------------------------------------------------------------
+// Device workspace: grow-only buffers owned by the context.
+// ---------------------------------------------------------------------------
+struct DevBuf {
+    void* p = nullptr;
+    size_t cap = 0;
+    void* get(size_t bytes) {
+        if (bytes == 0) bytes = 16;
+        if (bytes > cap) {
+            if (p) HIP_CHECK(hipFree(p));
+            p = nullptr;
+            size_t want = bytes + bytes / 8 + 256;
+            HIP_CHECK(hipMalloc(&p, want));
+            cap = want;
+        }
+        return p;
+    }
+    template <class T> T* as(size_t count) { return static_cast<T*>(get(count * sizeof(T))); }
+    void release() { if (p) (void)hipFree(p); p = nullptr; cap = 0; }
+    ~DevBuf() { release(); }
+};
+
+// ---------------------------------------------------------------------------
+// Wave / workgroup scan helpers (wave64).
+// ---------------------------------------------------------------------------
+template <class T>
+__device__ __forceinline__ T wave_incl_scan_add(T v)
+{
+    const int lane = threadIdx.x & 63;
+#pragma unroll
+    for (int d = 1; d < 64; d <<= 1) {
+        T o = __shfl_up(v, d, 64);
+        if (lane >= d) v += o;
+    }
+    return v;
+}
+
+template <class T>
+__device__ __forceinline__ T wave_incl_scan_max(T v)
+{
+    const int lane = threadIdx.x & 63;
+#pragma unroll
+    for (int d = 1; d < 64; d <<= 1) {
+        T o = __shfl_up(v, d, 64);
+        if (lane >= d) v = (o > v) ? o : v;
+    }
+    return v;
+}
+
+template <class T>
+__device__ __forceinline__ T wave_reduce_add(T v)
+{
+#pragma unroll
+    for (int d = 32; d >= 1; d >>= 1) v += __shfl_xor(v, d, 64);
+    return v;
+}
+
+// Block-wide exclusive sum; `sh` must hold blockDim.x/64 + 1 elements.
+// Returns the exclusive prefix for this thread; *total gets the block sum.
+template <class T>
+__device__ __forceinline__ T block_excl_scan_add(T v, T* sh, T* total)
+{
+    const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6, nw = blockDim.x >> 6;
+    T inc = wave_incl_scan_add(v);
+    if (lane == 63) sh[wid] = inc;
+    __syncthreads();
+    if (wid == 0) {
+        T s = (lane < nw) ? sh[lane] : T(0);
+        T si = wave_incl_scan_add(s);
+        if (lane < nw) sh[lane] = si - s;
+        if (lane == nw - 1) sh[nw] = si;
+    }
+    __syncthreads();
+    T res = sh[wid] + inc - v;
+    if (total) *total = sh[nw];
+    __syncthreads();
+    return res;
+}
+
+template <class T>
+__device__ __forceinline__ T block_incl_scan_max(T v, T* sh)
+{
+    const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6, nw = blockDim.x >> 6;
+    T inc = wave_incl_scan_max(v);
+    if (lane == 63) sh[wid] = inc;
+    __syncthreads();
+    if (wid == 0) {
+        T s = (lane < nw) ? sh[lane] : T(0);
+        T si = wave_incl_scan_max(s);
+        if (lane < nw) sh[lane] = si;   // inclusive max up to wave lane
+    }
+    __syncthreads();
+    T prev = (wid > 0) ? sh[wid - 1] : T(0);
+    T res = (prev > inc) ? prev : inc;
+    __syncthreads();
+    return res;
+}
+
+// ---------------------------------------------------------------------------
+// Device-wide exclusive scans (reduce -> scan partials -> downsweep).
+// ---------------------------------------------------------------------------
+namespace scan {
+constexpr int kThreads = 256;
+constexpr int kItems = 16;                   // elements per thread
+constexpr int kTile = kThreads * kItems;     // 4096 per tile
+
+// Exclusive prefix sum of in[0..n) into out (may alias), 64-bit accumulation.
+// Returns nothing; *total_dev (optional) receives the grand total.
+void excl_sum_u64(const uint64_t* in, uint64_t* out, uint64_t n, uint64_t* total_dev,
+                  DevBuf& tmp, hipStream_t st);
+void excl_sum_u32_to_u64(const uint32_t* in, uint64_t* out, uint64_t n, uint64_t* total_dev,
+                         DevBuf& tmp, hipStream_t st);
+// In-place inclusive max-scan of u64 (used for "index of last valid" propagation).
+void incl_max_u64(uint64_t* data, uint64_t n, DevBuf& tmp, hipStream_t st);
+}  // namespace scan

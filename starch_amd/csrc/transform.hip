@@ -1,0 +1,428 @@
+// starch_amd/csrc/transform.hip -- Starch coordinate transform on MI355X.
+//
+// Restates, as data-parallel kernels, the per-line pipeline of the reference
+// (include/starch3api.hpp): line framing (produce_line, hpp:158-199),
+// tokenizing + sscanf (consume_line, hpp:201-345), chromosome segmentation
+// (hpp:325-342, 347-407) and update_transformation_state (hpp:428-504).
+// Normative semantics, including the reference's quirks, are SURVEY.md
+// Appendix A; tests/test_transform_gpu.py checks byte equality against the
+// oracle and the reference goldens.
+//
+// Layout in HBM (all per-line arrays are struct-of-arrays, indexed by line):
+//   bed      u8[n]          input bytes
+//   line_end u64[L]         offset one past each line's '\n'
+//   start/stop i64[L]       parsed integers (stale values propagated)
+//   rem_beg u64[L], rem_len u32[L], chr_len u32[L], flags u8[L]
+//   out_off u64[L]          exclusive scan of per-line output lengths
+//   text     u8[T]          transformed text, segments back to back
+#include "common.hpp"
+#include "transform.hpp"
+
+namespace tf {
+
+constexpr int kTileBytes = 16384;   // 256 threads x 64 B
+constexpr int kThreads = 256;
+
+enum : uint8_t { F_START_OK = 1, F_STOP_OK = 2, F_NEW_SEG = 4 };
+
+// --- framing -------------------------------------------------------------
+__global__ void __launch_bounds__(kThreads)
+k_count_nl(const uint8_t* __restrict__ bed, uint64_t n, uint32_t* __restrict__ tile_cnt,
+           unsigned long long* __restrict__ ff_pos)
+{
+    const uint64_t base = (uint64_t)blockIdx.x * kTileBytes + (uint64_t)threadIdx.x * 64;
+    uint32_t c = 0;
+    uint64_t ff = ~0ull;
+    if (base + 64 <= n) {
+        const uint4* p = reinterpret_cast<const uint4*>(bed + base);
+#pragma unroll
+        for (int k = 0; k < 4; ++k) {
+            uint4 v = p[k];
+            uint32_t w[4] = {v.x, v.y, v.z, v.w};
+#pragma unroll
+            for (int j = 0; j < 4; ++j) {
+#pragma unroll
+                for (int b = 0; b < 4; ++b) {
+                    uint32_t by = (w[j] >> (8 * b)) & 0xff;
+                    c += (by == '\n');
+                    if (by == 0xff && ff == ~0ull) ff = base + k * 16 + j * 4 + b;
+                }
+            }
+        }
+    } else {
+        for (uint64_t i = base; i < n && i < base + 64; ++i) {
+            uint8_t by = bed[i];
+            c += (by == '\n');
+            if (by == 0xff && ff == ~0ull) ff = i;
+        }
+    }
+    if (ff != ~0ull) atomicMin(ff_pos, (unsigned long long)ff);
+    __shared__ uint32_t sh[kThreads / 64 + 1];
+    uint32_t tot;
+    (void)block_excl_scan_add<uint32_t>(c, sh, &tot);
+    if (threadIdx.x == 0) tile_cnt[blockIdx.x] = tot;
+}
+
+__global__ void __launch_bounds__(kThreads)
+k_index_nl(const uint8_t* __restrict__ bed, uint64_t n, const uint64_t* __restrict__ tile_off,
+           uint64_t* __restrict__ line_end)
+{
+    const uint64_t base = (uint64_t)blockIdx.x * kTileBytes + (uint64_t)threadIdx.x * 64;
+    uint8_t loc[64];
+    uint32_t c = 0;
+#pragma unroll 8
+    for (int k = 0; k < 64; ++k) {
+        uint64_t i = base + k;
+        uint8_t by = (i < n) ? bed[i] : 0;
+        loc[k] = by;
+        c += (by == '\n');
+    }
+    __shared__ uint32_t sh[kThreads / 64 + 1];
+    uint32_t pre = block_excl_scan_add<uint32_t>(c, sh, (uint32_t*)nullptr);
+    uint64_t o = tile_off[blockIdx.x] + pre;
+    for (int k = 0; k < 64; ++k)
+        if (loc[k] == '\n') line_end[o++] = base + k + 1;
+}
+
+// number of lines whose '\n' precedes the first 0xFF (hpp:181: 0xFF reads as EOF)
+__global__ void k_lines_before(const uint64_t* __restrict__ line_end, uint64_t nl, const unsigned long long* ff_pos,
+                               uint64_t* __restrict__ out)
+{
+    uint64_t lim = *ff_pos;
+    uint64_t lo = 0, hi = nl;     // first index with line_end > lim
+    while (lo < hi) {
+        uint64_t mid = (lo + hi) >> 1;
+        if (line_end[mid] <= lim) lo = mid + 1; else hi = mid;
+    }
+    *out = lo;
+}
+
+// --- parsing ---------------------------------------------------------------
+__device__ __forceinline__ bool is_c_space(uint8_t c)
+{
+    return c == ' ' || c == '\t' || c == '\n' || c == '\v' || c == '\f' || c == '\r';
+}
+
+// sscanf "%" SCNd64 on the C-string s[0..len) (hpp:306-307); glibc clamps on overflow.
+__device__ __forceinline__ bool scan_i64(const uint8_t* s, uint64_t len, int64_t& v)
+{
+    uint64_t i = 0;
+    while (i < len && is_c_space(s[i])) ++i;
+    bool neg = false;
+    if (i < len && (s[i] == '+' || s[i] == '-')) { neg = (s[i] == '-'); ++i; }
+    if (i >= len || s[i] < '0' || s[i] > '9') return false;
+    const uint64_t lim = neg ? 0x8000000000000000ull : 0x7fffffffffffffffull;
+    uint64_t acc = 0;
+    bool over = false;
+    for (; i < len; ++i) {
+        uint8_t c = s[i];
+        if (c < '0' || c > '9') break;
+        uint64_t d = c - '0';
+        if (!over && acc <= (lim - d) / 10u) acc = acc * 10u + d; else over = true;
+    }
+    if (over) acc = lim;
+    v = neg ? (int64_t)(0ull - acc) : (int64_t)acc;
+    return true;
+}
+
+// effective C-string length (first NUL ends a token: strcmp/strlen/sscanf)
+__device__ __forceinline__ uint64_t cstr_len(const uint8_t* p, uint64_t n)
+{
+    for (uint64_t i = 0; i < n; ++i) if (p[i] == 0) return i;
+    return n;
+}
+
+// Tokenize one line [ls, le) (le-1 is '\n'): fields per hpp:220-305.
+struct Fields { uint64_t b[4], e[4]; int tok; };
+
+__device__ __forceinline__ Fields tokenize(const uint8_t* bed, uint64_t ls, uint64_t le)
+{
+    Fields f;
+    f.tok = 0;
+    f.b[0] = ls;
+    uint64_t p = ls;
+    for (;;) {
+        if (bed[p] == '\t' && f.tok != 3) { f.e[f.tok] = p; ++f.tok; ++p; f.b[f.tok] = p; }
+        ++p;
+        if (bed[p - 1] == '\n') break;
+    }
+    f.e[f.tok] = p;
+    for (int t = f.tok + 1; t < 4; ++t) f.b[t] = f.e[t] = p;
+    if (f.tok >= 2) f.e[f.tok] -= 1;                // strip '\n' from stop or rem
+    return f;
+}
+
+// chromosome token only (bytes before the first tab; '\n' kept if no tab)
+__device__ __forceinline__ uint64_t chr_end(const uint8_t* bed, uint64_t ls)
+{
+    uint64_t p = ls;
+    for (;;) {
+        uint8_t c = bed[p];
+        if (c == '\t') return p;
+        ++p;
+        if (c == '\n') return p;
+    }
+}
+
+__global__ void __launch_bounds__(kThreads)
+k_parse(const uint8_t* __restrict__ bed, const uint64_t* __restrict__ line_end, uint64_t nl,
+        int64_t* __restrict__ start, int64_t* __restrict__ stop, uint8_t* __restrict__ flags,
+        uint64_t* __restrict__ rem_beg, uint32_t* __restrict__ rem_len, uint32_t* __restrict__ chr_len,
+        uint32_t* __restrict__ any_fail)
+{
+    uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= nl) return;
+    uint64_t ls = i ? line_end[i - 1] : 0, le = line_end[i];
+    Fields f = tokenize(bed, ls, le);
+    uint64_t len[4];
+#pragma unroll
+    for (int t = 0; t < 4; ++t) len[t] = cstr_len(bed + f.b[t], f.e[t] - f.b[t]);
+    int64_t a = 0, b = 0;
+    bool aok = scan_i64(bed + f.b[1], len[1], a);
+    bool bok = scan_i64(bed + f.b[2], len[2], b);
+    bool newseg = true;
+    if (i > 0) {
+        uint64_t ps = (i > 1) ? line_end[i - 2] : 0;
+        uint64_t pe = chr_end(bed, ps);
+        uint64_t plen = cstr_len(bed + ps, pe - ps);
+        if (plen == len[0]) {
+            newseg = false;
+            for (uint64_t k = 0; k < plen; ++k)
+                if (bed[ps + k] != bed[ls + k]) { newseg = true; break; }
+        }
+    }
+    start[i] = a;
+    stop[i] = b;
+    flags[i] = (aok ? F_START_OK : 0) | (bok ? F_STOP_OK : 0) | (newseg ? F_NEW_SEG : 0);
+    rem_beg[i] = f.b[3];
+    rem_len[i] = (uint32_t)len[3];
+    chr_len[i] = (uint32_t)len[0];
+    if (!aok || !bok) atomicOr(any_fail, 1u);
+}
+
+// stale-value propagation: idx[i] = ok ? i+1 : 0  -> inclusive max-scan -> gather
+__global__ void k_ok_index(const uint8_t* __restrict__ flags, uint64_t nl, uint8_t bit, uint64_t* __restrict__ idx)
+{
+    uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (i < nl) idx[i] = (flags[i] & bit) ? i + 1 : 0;
+}
+__global__ void k_gather_stale(const int64_t* __restrict__ cp, const uint64_t* __restrict__ idx, uint64_t nl,
+                               int64_t* __restrict__ v)
+{
+    uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (i < nl) {
+        uint64_t j = idx[i];
+        v[i] = j ? cp[j - 1] : 0;   // uninitialised malloc memory was observed as 0
+    }
+}
+
+// --- per-line output length ----------------------------------------------------
+__device__ __forceinline__ int ndig_u64(uint64_t u)
+{
+    int d = 1;
+    while (u >= 10u) { u /= 10u; ++d; }
+    return d;
+}
+// n_digits (hpp:559-581): |i| digits, INT64_MIN -> 1
+__device__ __forceinline__ int n_digits_ref(int64_t i)
+{
+    uint64_t u = (i < 0) ? 0ull - (uint64_t)i : (uint64_t)i;
+    if ((int64_t)u < 0) return 1;
+    int d = ndig_u64(u);
+    return d > 19 ? 19 : d;
+}
+__device__ __forceinline__ int dec_len(int64_t v)
+{
+    uint64_t u = (v < 0) ? 0ull - (uint64_t)v : (uint64_t)v;
+    return ndig_u64(u) + (v < 0 ? 1 : 0);
+}
+
+struct LineState { int64_t cd, last_cd, v; bool emit_p; };
+
+__device__ __forceinline__ LineState line_state(const int64_t* start, const int64_t* stop, const uint8_t* flags,
+                                                uint64_t i)
+{
+    LineState s;
+    int64_t a = start[i], b = stop[i];
+    s.cd = (int64_t)((uint64_t)b - (uint64_t)a);
+    int64_t last_stop = 0;
+    s.last_cd = 0;
+    if (!(flags[i] & F_NEW_SEG)) {
+        int64_t pa = start[i - 1], pb = stop[i - 1];
+        s.last_cd = (int64_t)((uint64_t)pb - (uint64_t)pa);
+        last_stop = pb;
+    }
+    s.emit_p = (s.cd != s.last_cd);
+    s.v = (last_stop != 0) ? (int64_t)((uint64_t)a - (uint64_t)last_stop) : a;
+    return s;
+}
+
+__global__ void __launch_bounds__(kThreads)
+k_line_len(const int64_t* __restrict__ start, const int64_t* __restrict__ stop, const uint8_t* __restrict__ flags,
+           const uint32_t* __restrict__ rem_len, uint64_t nl, uint32_t* __restrict__ out_len,
+           uint32_t* __restrict__ seg_flag)
+{
+    uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= nl) return;
+    LineState s = line_state(start, stop, flags, i);
+    uint32_t L = 0;
+    if (s.emit_p) L += 2 + n_digits_ref(s.cd);          // "p%ld\n" truncated (hpp:440,452)
+    L += dec_len(s.v) + 1;
+    if (rem_len[i]) L += 1 + rem_len[i];
+    out_len[i] = L;
+    seg_flag[i] = (flags[i] & F_NEW_SEG) ? 1u : 0u;
+}
+
+__device__ __forceinline__ uint64_t put_dec(uint8_t* o, int64_t v)
+{
+    uint64_t u = (v < 0) ? 0ull - (uint64_t)v : (uint64_t)v;
+    int nd = ndig_u64(u);
+    uint64_t k = 0;
+    if (v < 0) o[k++] = '-';
+    for (int d = nd - 1; d >= 0; --d) { o[k + d] = (uint8_t)('0' + (u % 10u)); u /= 10u; }
+    return k + nd;
+}
+
+__global__ void __launch_bounds__(kThreads)
+k_emit(const uint8_t* __restrict__ bed, const int64_t* __restrict__ start, const int64_t* __restrict__ stop,
+       const uint8_t* __restrict__ flags, const uint64_t* __restrict__ rem_beg, const uint32_t* __restrict__ rem_len,
+       const uint64_t* __restrict__ out_off, uint64_t nl, uint8_t* __restrict__ text)
+{
+    uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= nl) return;
+    LineState s = line_state(start, stop, flags, i);
+    uint8_t* o = text + out_off[i];
+    if (s.emit_p) {
+        int keep = 2 + n_digits_ref(s.cd);
+        uint8_t tmp[24];
+        tmp[0] = 'p';
+        uint64_t k = 1 + put_dec(tmp + 1, s.cd);
+        tmp[k++] = '\n';
+        for (int j = 0; j < keep; ++j) o[j] = tmp[j];
+        o += keep;
+    }
+    o += put_dec(o, s.v);
+    uint32_t rl = rem_len[i];
+    if (rl) {
+        *o++ = '\t';
+        const uint8_t* r = bed + rem_beg[i];
+        for (uint32_t j = 0; j < rl; ++j) o[j] = r[j];
+        o += rl;
+    }
+    *o = '\n';
+}
+
+// segment table: for each new-segment line, its ordinal -> first line
+__global__ void k_seg_first(const uint32_t* __restrict__ seg_flag, const uint64_t* __restrict__ seg_ord, uint64_t nl,
+                            uint64_t* __restrict__ seg_first)
+{
+    uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (i < nl && seg_flag[i]) seg_first[seg_ord[i]] = i;
+}
+
+__global__ void k_seg_info(const uint64_t* __restrict__ seg_first, uint64_t nseg, uint64_t nl,
+                           const uint64_t* __restrict__ line_end, const uint32_t* __restrict__ chr_len,
+                           const uint64_t* __restrict__ out_off, uint64_t text_total, SegInfo* __restrict__ info)
+{
+    uint64_t s = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (s >= nseg) return;
+    uint64_t f = seg_first[s], g = (s + 1 < nseg) ? seg_first[s + 1] : nl;
+    SegInfo r;
+    r.first_line = f;
+    r.line_count = g - f;
+    r.name_off = f ? line_end[f - 1] : 0;
+    r.name_len = chr_len[f];
+    r.text_off = out_off[f];
+    r.text_len = ((g < nl) ? out_off[g] : text_total) - r.text_off;
+    info[s] = r;
+}
+
+}  // namespace tf
+
+// ---------------------------------------------------------------------------
+// Host driver
+// ---------------------------------------------------------------------------
+using namespace tf;
+
+void TransformWorkspace::run(const uint8_t* d_bed, uint64_t n, hipStream_t st, TransformResult& res)
+{
+    res = TransformResult();
+    uint64_t ntile = ceil_div(n, kTileBytes);
+    uint32_t* tile_cnt = b_tile_cnt.as<uint32_t>(ntile + 1);
+    uint64_t* tile_off = b_tile_off.as<uint64_t>(ntile + 1);
+    uint64_t* scal = b_scal.as<uint64_t>(16);      // [0]=nl_total [1]=ff_pos [2]=nl_eff [3]=nseg [4]=text_total [5]=any_fail
+    HIP_CHECK(hipMemsetAsync(scal, 0, 16 * sizeof(uint64_t), st));
+    HIP_CHECK(hipMemsetAsync(scal + 1, 0xff, sizeof(uint64_t), st));
+    if (n > 0) {
+        hipLaunchKernelGGL(k_count_nl, dim3((unsigned)ntile), dim3(kThreads), 0, st, d_bed, n, tile_cnt,
+                           (unsigned long long*)(scal + 1));
+        scan::excl_sum_u32_to_u64(tile_cnt, tile_off, ntile, scal + 0, b_tmp, st);
+    }
+    uint64_t h[2];
+    HIP_CHECK(hipMemcpyAsync(h, scal, 2 * sizeof(uint64_t), hipMemcpyDeviceToHost, st));
+    HIP_CHECK(hipStreamSynchronize(st));
+    uint64_t nl = h[0];
+    uint64_t* line_end = b_line_end.as<uint64_t>(nl + 1);
+    if (nl) {
+        hipLaunchKernelGGL(k_index_nl, dim3((unsigned)ntile), dim3(kThreads), 0, st, d_bed, n, tile_off, line_end);
+        if (h[1] != ~0ull) {
+            hipLaunchKernelGGL(k_lines_before, dim3(1), dim3(1), 0, st, line_end, nl,
+                               (const unsigned long long*)(scal + 1), scal + 2);
+            HIP_CHECK(hipMemcpyAsync(&nl, scal + 2, sizeof(uint64_t), hipMemcpyDeviceToHost, st));
+            HIP_CHECK(hipStreamSynchronize(st));
+        }
+    }
+    res.n_lines = nl;
+    res.ff_pos = h[1];
+    if (nl == 0) { res.n_segments = 0; res.text_bytes = 0; return; }
+
+    int64_t* start = b_start.as<int64_t>(nl);
+    int64_t* stop = b_stop.as<int64_t>(nl);
+    uint8_t* flags = b_flags.as<uint8_t>(nl);
+    uint64_t* rem_beg = b_rem_beg.as<uint64_t>(nl);
+    uint32_t* rem_len = b_rem_len.as<uint32_t>(nl);
+    uint32_t* chr_len = b_chr_len.as<uint32_t>(nl);
+    uint32_t* any_fail = reinterpret_cast<uint32_t*>(scal + 5);
+    unsigned nb = (unsigned)ceil_div(nl, kThreads);
+    hipLaunchKernelGGL(k_parse, dim3(nb), dim3(kThreads), 0, st, d_bed, line_end, nl, start, stop, flags, rem_beg,
+                       rem_len, chr_len, any_fail);
+    uint32_t fail = 0;
+    HIP_CHECK(hipMemcpyAsync(&fail, any_fail, sizeof(uint32_t), hipMemcpyDeviceToHost, st));
+    HIP_CHECK(hipStreamSynchronize(st));
+    if (fail) {
+        uint64_t* idx = b_idx.as<uint64_t>(nl);
+        for (int w = 0; w < 2; ++w) {
+            hipLaunchKernelGGL(k_ok_index, dim3(nb), dim3(kThreads), 0, st, flags, nl,
+                               (uint8_t)(w == 0 ? F_START_OK : F_STOP_OK), idx);
+            scan::incl_max_u64(idx, nl, b_tmp, st);
+            // gather into a copy to avoid read/write races across blocks
+            int64_t* v = (w == 0) ? start : stop;
+            int64_t* cp = b_vcopy.as<int64_t>(nl);
+            HIP_CHECK(hipMemcpyAsync(cp, v, nl * sizeof(int64_t), hipMemcpyDeviceToDevice, st));
+            hipLaunchKernelGGL(k_gather_stale, dim3(nb), dim3(kThreads), 0, st, cp, idx, nl, v);
+        }
+    }
+    uint32_t* out_len = b_out_len.as<uint32_t>(nl);
+    uint32_t* seg_flag = b_seg_flag.as<uint32_t>(nl);
+    hipLaunchKernelGGL(k_line_len, dim3(nb), dim3(kThreads), 0, st, start, stop, flags, rem_len, nl, out_len,
+                       seg_flag);
+    uint64_t* out_off = b_out_off.as<uint64_t>(nl);
+    uint64_t* seg_ord = b_seg_ord.as<uint64_t>(nl);
+    scan::excl_sum_u32_to_u64(out_len, out_off, nl, scal + 4, b_tmp, st);
+    scan::excl_sum_u32_to_u64(seg_flag, seg_ord, nl, scal + 3, b_tmp, st);
+    HIP_CHECK(hipMemcpyAsync(h, scal + 3, 2 * sizeof(uint64_t), hipMemcpyDeviceToHost, st));
+    HIP_CHECK(hipStreamSynchronize(st));
+    uint64_t nseg = h[0], ttot = h[1];
+    uint64_t* seg_first = b_seg_first.as<uint64_t>(nseg + 1);
+    hipLaunchKernelGGL(k_seg_first, dim3(nb), dim3(kThreads), 0, st, seg_flag, seg_ord, nl, seg_first);
+    SegInfo* info = b_seg_info.as<SegInfo>(nseg + 1);
+    hipLaunchKernelGGL(k_seg_info, dim3((unsigned)ceil_div(nseg, 256)), dim3(256), 0, st, seg_first, nseg, nl,
+                       line_end, chr_len, out_off, ttot, info);
+    text = b_text.as<uint8_t>(ttot + 64);
+    hipLaunchKernelGGL(k_emit, dim3(nb), dim3(kThreads), 0, st, d_bed, start, stop, flags, rem_beg, rem_len, out_off,
+                       nl, text);
+    HIP_CHECK(hipGetLastError());
+    res.n_segments = nseg;
+    res.text_bytes = ttot;
+    seg_info_dev = info;
+}

@@ -1,0 +1,24 @@
+// starch_amd/csrc/transform.hpp -- host interface of the transform stage.
+#pragma once
+#include "common.hpp"
+
+struct SegInfo {            // one chromosome segment (hpp:393-407 flush unit)
+    uint64_t first_line;
+    uint64_t line_count;    // transform_state_t.line_count (hpp:503)
+    uint64_t name_off;      // chr token offset in the input
+    uint64_t name_len;      // strlen() of the chr token
+    uint64_t text_off;      // offset of the segment's text in the text buffer
+    uint64_t text_len;
+};
+
+struct TransformResult {
+    uint64_t n_lines = 0, n_segments = 0, text_bytes = 0, ff_pos = ~0ull;
+};
+
+struct TransformWorkspace {
+    DevBuf b_tile_cnt, b_tile_off, b_scal, b_tmp, b_line_end, b_start, b_stop, b_flags, b_rem_beg, b_rem_len,
+        b_chr_len, b_idx, b_vcopy, b_out_len, b_seg_flag, b_out_off, b_seg_ord, b_seg_first, b_seg_info, b_text;
+    uint8_t* text = nullptr;          // device: transformed text (valid after run)
+    SegInfo* seg_info_dev = nullptr;  // device: n_segments entries
+    void run(const uint8_t* d_bed, uint64_t n, hipStream_t st, TransformResult& res);
+};

@@ -1,0 +1,159 @@
+// tools/starch3_cli.cpp -- the `starch3` command line on MI355X.
+//
+// Keeps the reference CLI surface (src/starch3.cpp:72-167): getopt_long with
+// "n:bghv?", long options --note/--bzip2/--gzip/--help/--version, an optional
+// input filename (extra names warned and ignored, cpp:147-157), stdin checked
+// for a redirect (hpp:890-905), and the same exit codes: 61 (ENODATA) no input
+// / missing file, 38 (ENOSYS) gzip, 1 two methods, 22 (EINVAL) codec init.
+// The archive goes to stdout: magic ca5cad1a, one bzip2 stream per chromosome,
+// JSON index + footer.  Build-only flags: --level N, --no-index,
+// --reference-compat (stdout exactly as the reference: the 4 magic bytes),
+// --device N, --stats.
+#include <errno.h>
+#include <getopt.h>
+#include <stdio.h>
+#include <stdlib.h>
+#include <string.h>
+#include <sys/stat.h>
+#include <unistd.h>
+
+#include <string>
+#include <vector>
+
+#include "../include/starch_amd.h"
+
+static const char* kName = "starch3";
+static const char* kVersion = "0.1 (mi355x)";
+
+static void usage(FILE* f)
+{
+    fprintf(f,
+            "%s\n  version: %s\n\n"
+            "  Compress sorted BED data to a Starch archive (bzip2 streams per chromosome) on AMD MI355X.\n\n"
+            "  Usage:  %s [options] < input > output\n"
+            "     or:  %s [options] input > output\n\n"
+            "  --note=\"text\"        note stored in the archive index\n"
+            "  --bzip2 | -b          bzip2 streams (default)\n"
+            "  --gzip | -g           gzip streams (not supported)\n"
+            "  --level N             bzip2 block size 1..9 (default 9)\n"
+            "  --no-index            streams only, no JSON index/footer\n"
+            "  --reference-compat    write exactly what the reference writes (magic bytes only)\n"
+            "  --device N            GPU ordinal (default 0)\n"
+            "  --stats               print per-stage timings to stderr\n"
+            "  --help | -h           this message\n"
+            "  --version | -v        version\n",
+            kName, kVersion, kName, kName);
+}
+
+int main(int argc, char** argv)
+{
+    std::string note, input;
+    int methods = 0, gzip = 0, level = 9, emit_index = 1, compat = 0, device = 0, stats = 0;
+    static struct option longs[] = {
+        {"note", required_argument, nullptr, 'n'}, {"bzip2", no_argument, nullptr, 'b'},
+        {"gzip", no_argument, nullptr, 'g'},       {"help", no_argument, nullptr, 'h'},
+        {"version", no_argument, nullptr, 'v'},    {"level", required_argument, nullptr, 'L'},
+        {"no-index", no_argument, nullptr, 'I'},   {"reference-compat", no_argument, nullptr, 'R'},
+        {"device", required_argument, nullptr, 'D'}, {"stats", no_argument, nullptr, 'S'},
+        {nullptr, 0, nullptr, 0}};
+    opterr = 0;
+    int c, li;
+    while ((c = getopt_long(argc, argv, "n:bghv?", longs, &li)) != -1) {
+        switch (c) {
+            case 'n': note = optarg; break;
+            case 'b': ++methods; gzip = 0; break;
+            case 'g': ++methods; gzip = 1; break;
+            case 'h': usage(stdout); return 0;
+            case 'v': printf("%s\n  version: %s\n", kName, kVersion); return 0;
+            case '?': usage(stdout); return 0;
+            case 'L': level = atoi(optarg); break;
+            case 'I': emit_index = 0; break;
+            case 'R': compat = 1; break;
+            case 'D': device = atoi(optarg); break;
+            case 'S': stats = 1; break;
+            default: break;
+        }
+    }
+    for (; optind < argc; ++optind) {
+        if (input.empty()) {
+            struct stat sb;
+            if (stat(argv[optind], &sb) != 0) {
+                fprintf(stderr, "Error: Input file does not exist (%s)\n", argv[optind]);
+                return ENODATA;
+            }
+            input = argv[optind];
+        } else {
+            fprintf(stderr, "Warning: Ignoring additional input file [%s]\n", argv[optind]);
+        }
+    }
+    if (methods > 1) {
+        fprintf(stderr, "Error: Only one compression method may be set\n");
+        usage(stderr);
+        return EXIT_FAILURE;
+    }
+    if (level < 1 || level > 9) {
+        fprintf(stderr, "Error: --level must be 1..9\n");
+        return EINVAL;
+    }
+    struct stat st;
+    if (input.empty() && fstat(STDIN_FILENO, &st) == 0 && S_ISCHR(st.st_mode)) {
+        fprintf(stderr, "Error: No input is specified; please redirect or pipe in formatted data, or specify filename\n");
+        usage(stderr);
+        return ENODATA;
+    }
+    FILE* in = input.empty() ? stdin : fopen(input.c_str(), "rb");
+    if (!in) {
+        fprintf(stderr, "Error: Input file handle could not be created\n");
+        return ENODATA;
+    }
+    static const unsigned char magic[4] = {0xca, 0x5c, 0xad, 0x1a};
+    if (gzip) {   // the reference writes the magic, then fails (hpp:765-769, 777-779)
+        fwrite(magic, 1, 4, stdout);
+        fprintf(stderr, "Error: This method is unsupported at this time\n");
+        return ENOSYS;
+    }
+    std::vector<char> data;
+    {
+        std::vector<char> buf(1 << 24);
+        size_t k;
+        while ((k = fread(buf.data(), 1, buf.size(), in)) > 0) data.insert(data.end(), buf.begin(), buf.begin() + k);
+        if (in != stdin) fclose(in);
+    }
+    starch_ctx* ctx = nullptr;
+    int rc = starch_create(device, &ctx);
+    if (rc != STARCH_OK) {
+        fprintf(stderr, "Error: could not open MI355X device %d (%s)\n", device, starch_strerror(rc));
+        return EINVAL;
+    }
+    starch_options opt;
+    starch_options_init(&opt);
+    opt.block_size_100k = level;
+    opt.emit_index = emit_index;
+    opt.reference_compat = compat;
+    opt.note = note.empty() ? nullptr : note.c_str();
+    rc = starch_encode_host(ctx, data.data(), data.size(), &opt);
+    if (rc != STARCH_OK) {
+        fprintf(stderr, "Error: encode failed (%s: %s)\n", starch_strerror(rc), starch_last_error(ctx));
+        starch_destroy(ctx);
+        return rc == STARCH_ERR_MEM ? ENOMEM : EINVAL;
+    }
+    uint64_t n = 0;
+    starch_archive_size(ctx, &n);
+    std::vector<char> out(n);
+    starch_archive_copy(ctx, out.data(), n);
+    fwrite(out.data(), 1, n, stdout);
+    fflush(stdout);
+    if (stats) {
+        starch_stats s;
+        starch_get_stats(ctx, &s);
+        fprintf(stderr,
+                "{\"input_bytes\": %llu, \"lines\": %llu, \"segments\": %llu, \"text_bytes\": %llu, "
+                "\"archive_bytes\": %llu, \"blocks\": %llu, \"ms_total\": %.3f, \"ms_transform\": %.3f, "
+                "\"ms_rle\": %.3f, \"ms_bwt\": %.3f, \"ms_mtf\": %.3f, \"ms_tables\": %.3f, \"ms_emit\": %.3f}\n",
+                (unsigned long long)s.input_bytes, (unsigned long long)s.n_lines, (unsigned long long)s.n_segments,
+                (unsigned long long)s.text_bytes, (unsigned long long)s.archive_bytes, (unsigned long long)s.n_blocks,
+                s.ms_total, s.ms_transform, s.ms_rle, s.ms_bwt, s.ms_mtf, s.ms_tables, s.ms_emit);
+    }
+    starch_destroy(ctx);
+    return 0;
+}
