@@ -291,6 +291,6 @@ def parse_archive(blob: bytes):
         raise ValueError("bad magic")
     foot = blob[-32:]
     off = int(foot[:20])
-    idx = json.loads(blob[off:-32].decode("latin-1"))
+    idx = json.loads(blob[off:-32].decode("utf-8"))
     streams = [blob[s["offset"]:s["offset"] + s["size"]] for s in idx["streams"]]
     return idx, streams

@@ -41,14 +41,31 @@ struct Ctx {   // device guard
     ~Ctx() { if (prev >= 0) (void)hipSetDevice(prev); }
 };
 
-void json_str(std::string& o, const char* p, size_t n)
+bool valid_utf8(const unsigned char* s, size_t n)
+{
+    for (size_t i = 0; i < n;) {
+        unsigned char c = s[i];
+        int k = c < 0x80 ? 0 : (c >> 5) == 6 ? 1 : (c >> 4) == 14 ? 2 : (c >> 3) == 30 ? 3 : -1;
+        if (k < 0 || i + k >= n + (k == 0 ? 1 : 0)) return false;
+        for (int j = 1; j <= k; ++j) if (i + j >= n || (s[i + j] & 0xc0) != 0x80) return false;
+        i += 1 + k;
+    }
+    return true;
+}
+
+// Chromosome names are arbitrary bytes: escaped byte-wise as \u00XX so the
+// original bytes are recovered as latin-1 code points.  Free text (the note)
+// that is valid UTF-8 is kept as UTF-8.
+void json_str(std::string& o, const char* p, size_t n, bool keep_utf8 = false)
 {
     static const char* hx = "0123456789abcdef";
+    const bool raw_hi = keep_utf8 && valid_utf8(reinterpret_cast<const unsigned char*>(p), n);
     o += '"';
     for (size_t i = 0; i < n; ++i) {
         unsigned char c = (unsigned char)p[i];
         if (c == '"') o += "\\\"";
         else if (c == '\\') o += "\\\\";
+        else if (c >= 0x80 && raw_hi) o += (char)c;
         else if (c < 0x20 || c >= 0x7f) {   // control and non-ASCII bytes as latin-1 code points
             o += "\\u00";
             o += hx[c >> 4];
@@ -66,7 +83,7 @@ std::string build_index(const starch_segment* segs, const char* const* names, co
          "\"revision\":0},\"compressionFormat\":\"bzip2\",\"blockSize100k\":";
     j += std::to_string(bs);
     j += ",\"note\":";
-    json_str(j, note ? note : "", note ? strlen(note) : 0);
+    json_str(j, note ? note : "", note ? strlen(note) : 0, true);
     j += "},\"streams\":[";
     for (uint64_t s = 0; s < nseg; ++s) {
         if (s) j += ',';

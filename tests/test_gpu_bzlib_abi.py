@@ -1,0 +1,137 @@
+"""The patched-libbz2 ABI (include/starch_bzlib.h) exported by
+libstarch_amd.so, driven with the same call sequences as the reference's
+vendored libbz2 (oracle/_ref/libbz2ref.so): identical bytes and return codes."""
+import ctypes
+import random
+
+import pytest
+
+from tests import oracle_lib
+
+pytestmark = pytest.mark.gpu
+
+BZ_RUN, BZ_FLUSH, BZ_FINISH = 0, 1, 2
+BZ_RUN_OK, BZ_FINISH_OK, BZ_STREAM_END = 1, 3, 4
+
+
+class BzStream(ctypes.Structure):
+    _fields_ = [("next_in", ctypes.c_void_p), ("avail_in", ctypes.c_uint), ("total_in_lo32", ctypes.c_uint),
+                ("total_in_hi32", ctypes.c_uint), ("next_out", ctypes.c_void_p), ("avail_out", ctypes.c_uint),
+                ("total_out_lo32", ctypes.c_uint), ("total_out_hi32", ctypes.c_uint), ("state", ctypes.c_void_p),
+                ("bzalloc", ctypes.c_void_p), ("bzfree", ctypes.c_void_p), ("opaque", ctypes.c_void_p),
+                ("handler", ctypes.c_void_p), ("block_close_functor", ctypes.c_void_p)]
+
+
+def _lib():
+    import starch_amd
+    L = starch_amd.load()
+    for n in ("BZ2_bzCompressInit", "BZ2_bzCompress", "BZ2_bzCompressEnd"):
+        getattr(L, n).restype = ctypes.c_int
+    return L
+
+
+def run_script(data, ops, bs=9, out_chunk=0):
+    """Drive the GPU bzlib ABI like ref_bz2_script does."""
+    L = _lib()
+    s = BzStream()
+    assert L.BZ2_bzCompressInit(ctypes.byref(s), bs, 0, 30) == 0
+    called = []
+    CB = ctypes.CFUNCTYPE(None, ctypes.c_void_p)
+    cb = CB(lambda h: called.append(h))
+    s.block_close_functor = ctypes.cast(cb, ctypes.c_void_p)
+    src = ctypes.create_string_buffer(data, len(data) + 1)
+    cap = len(data) + len(data) // 50 + 4096 + 64 * len(ops)
+    out = ctypes.create_string_buffer(cap)
+    used = produced = 0
+    rcs = []
+    for act, nbytes in ops:
+        s.next_in = ctypes.addressof(src) + used
+        s.avail_in = nbytes
+        used += nbytes
+        while True:
+            room = cap - produced
+            if out_chunk:
+                room = min(room, out_chunk)
+            s.next_out = ctypes.addressof(out) + produced
+            s.avail_out = room
+            rc = L.BZ2_bzCompress(ctypes.byref(s), act)
+            produced += room - s.avail_out
+            if rc < 0:
+                raise AssertionError("rc %d" % rc)
+            if act == BZ_RUN and s.avail_in == 0:
+                break
+            if act == BZ_FLUSH and rc == BZ_RUN_OK:
+                break
+            if act == BZ_FINISH and rc == BZ_STREAM_END:
+                break
+        rcs.append(rc)
+    assert (s.total_in_hi32 << 32 | s.total_in_lo32) == used
+    assert (s.total_out_hi32 << 32 | s.total_out_lo32) == produced
+    assert L.BZ2_bzCompressEnd(ctypes.byref(s)) == 0
+    assert called, "block_close_functor not called at BZ_STREAM_END"
+    return out.raw[:produced], rcs
+
+
+def test_single_finish_matches_reference():
+    r = random.Random(5)
+    for n in (0, 1, 100, 5000, 250000):
+        data = bytes(r.choice(b"0123\np-") for _ in range(n))
+        got, rcs = run_script(data, [(BZ_FINISH, n)])
+        assert got == oracle_lib.bz2(data, 9)
+        assert rcs == [BZ_STREAM_END]
+
+
+@pytest.mark.skipif(oracle_lib.ref() is None, reason="oracle/_ref not built")
+def test_call_sequences_match_reference_lib():
+    r = random.Random(17)
+    for trial in range(12):
+        n = r.randint(1000, 300000)
+        if trial % 3 == 0:
+            data = b"ab" * (n // 2)
+        elif trial % 3 == 1:
+            data = b"".join(bytes([r.randrange(3) + 48]) * r.choice([1, 2, 5, 255, 300]) for _ in range(n // 60))
+        else:
+            data = bytes(r.choice(b"0123456789\n") for _ in range(n))
+        # random split into RUN / FLUSH pieces, then FINISH with the tail (maybe empty)
+        ops, left = [], len(data)
+        while left > 0 and len(ops) < 6:
+            k = r.randint(0, left)
+            ops.append((r.choice([BZ_RUN, BZ_RUN, BZ_FLUSH]), k))
+            left -= k
+        ops.append((BZ_FINISH, left))
+        bs = r.choice([1, 9])
+        want, _ = oracle_lib.ref_bz2_script(data, ops, bs=bs)
+        got, _ = run_script(data, ops, bs=bs, out_chunk=r.choice([0, 997]))
+        assert got == want, (trial, ops, bs)
+
+
+@pytest.mark.skipif(oracle_lib.ref() is None, reason="oracle/_ref not built")
+def test_full_block_then_empty_finish_final_run_rule():
+    # RUN all input so that the last byte leaves a full block behind, then an
+    # empty FINISH: the final single-byte run must start a new block
+    # (bz:bzlib.c:399-402 in RUN mode) -- unlike a FINISH that carries it.
+    base = bytes((i * 7919) % 251 for i in range(99981))   # fills a level-1 block exactly
+    for data in (base + b"Z", base + b"ZZ", base[:-1] + b"QZ"):
+        for ops in ([(BZ_RUN, len(data)), (BZ_FINISH, 0)], [(BZ_FINISH, len(data))],
+                    [(BZ_RUN, len(data) - 1), (BZ_FINISH, 1)]):
+            want, _ = oracle_lib.ref_bz2_script(data, ops, bs=1)
+            got, _ = run_script(data, ops, bs=1)
+            assert got == want, ops
+
+
+def test_param_and_sequence_errors():
+    L = _lib()
+    s = BzStream()
+    assert L.BZ2_bzCompressInit(ctypes.byref(s), 0, 0, 30) == -2
+    assert L.BZ2_bzCompressInit(ctypes.byref(s), 9, 0, 251) == -2
+    assert L.BZ2_bzCompressInit(ctypes.byref(s), 9, 0, 0) == 0
+    # BZ_RUN without input makes no progress -> BZ_PARAM_ERROR (bz:bzlib.c:432-434)
+    s.avail_in = 0
+    assert L.BZ2_bzCompress(ctypes.byref(s), BZ_RUN) == -2
+    out = ctypes.create_string_buffer(64)
+    s.next_out = ctypes.addressof(out)
+    s.avail_out = 64
+    assert L.BZ2_bzCompress(ctypes.byref(s), BZ_FINISH) == BZ_STREAM_END   # functor NULL: allowed
+    assert L.BZ2_bzCompress(ctypes.byref(s), BZ_FINISH) == -1              # IDLE -> sequence error
+    assert L.BZ2_bzCompressEnd(ctypes.byref(s)) == 0
+    assert L.BZ2_bzCompressEnd(ctypes.byref(s)) == -2
