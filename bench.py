@@ -118,7 +118,7 @@ def main():
     ap.add_argument("--lines", type=int, default=TOTAL_LINES)
     ap.add_argument("--kind", type=int, default=0, help="0 BED3 (cfg2), 1 narrowPeak (cfg4)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
-    ap.add_argument("--cpu-sample-lines", type=int, default=250_000)
+    ap.add_argument("--cpu-sample-lines", type=int, default=1_000_000)
     ap.add_argument("--cpu-threads", type=int, default=16)
     ap.add_argument("--verify", action="store_true", help="check 2 chromosome streams vs the CPU path")
     args = ap.parse_args()
@@ -220,6 +220,11 @@ def main():
                 w.wait()
             return None
 
+    def log(msg):
+        if rank == 0:
+            print("[bench] %s" % msg, file=sys.stderr, flush=True)
+
+    log("input %.1f MB generated + copied to HBM in %.1f s; warmup %d" % (my_bytes / 1e6, t_gen, args.warmup))
     for _ in range(args.warmup):
         step()
     torch.cuda.synchronize()
@@ -231,6 +236,7 @@ def main():
     for _ in range(args.steps):
         step()
         stats_acc.append(ctx.stats())
+        log("step: %.1f ms (device %.1f ms)" % ((time.perf_counter() - t0) * 1e3, stats_acc[-1]["ms_total"]))
     torch.cuda.synchronize()
     if dist is not None:
         dist.barrier()

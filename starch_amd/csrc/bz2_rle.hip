@@ -146,21 +146,56 @@ __global__ void __launch_bounds__(256) k_rle_sum(const uint8_t* __restrict__ tex
     }
 }
 
-// one thread per stream: run length entering each tile
-__global__ void k_rle_carry(const uint64_t* __restrict__ seg_tile0, uint32_t nstreams, const TileSum* __restrict__ sums,
-                            uint32_t* __restrict__ carry)
+// one 256-thread workgroup per stream: run length entering each tile, via an
+// inclusive scan of tile run summaries (the run-summary combine is associative)
+struct RunSum64 {
+    uint64_t len, trail;
+    int first, last, uni, pad;
+};
+__device__ __forceinline__ RunSum64 rs64_combine(const RunSum64& A, const RunSum64& B)
 {
-    uint32_t s = blockIdx.x * blockDim.x + threadIdx.x;
-    if (s >= nstreams) return;
-    uint64_t t0 = seg_tile0[s], t1 = seg_tile0[s + 1];
-    int prev_last = -1;
-    uint64_t prev_trail = 0;
-    for (uint64_t t = t0; t < t1; ++t) {
-        TileSum S = sums[t];
-        uint64_t c = (t > t0 && prev_last == (int)S.first) ? prev_trail : 0;
-        carry[t] = (uint32_t)(c % 255u);   // only the RLE1 chunk position (run mod 255) matters
-        prev_trail = S.uni ? c + S.len : S.trail;
-        prev_last = S.last;
+    if (A.len == 0) return B;
+    if (B.len == 0) return A;
+    RunSum64 R;
+    R.first = A.first;
+    R.last = B.last;
+    R.len = A.len + B.len;
+    R.uni = A.uni && B.uni && A.last == B.first;
+    R.trail = (B.uni && B.first == A.last) ? B.len + A.trail : B.trail;
+    R.pad = 0;
+    return R;
+}
+
+__global__ void __launch_bounds__(256) k_rle_carry(const uint64_t* __restrict__ seg_tile0, uint32_t nstreams,
+                                                    const TileSum* __restrict__ sums, uint32_t* __restrict__ carry)
+{
+    __shared__ RunSum64 sh[256];
+    const uint32_t s = blockIdx.x;
+    const int tid = threadIdx.x;
+    const uint64_t t0 = seg_tile0[s], t1 = seg_tile0[s + 1];
+    RunSum64 acc;
+    acc.len = 0; acc.trail = 0; acc.first = acc.last = -1; acc.uni = 1; acc.pad = 0;
+    for (uint64_t c0 = t0; c0 < t1; c0 += 256) {
+        const uint64_t t = c0 + tid;
+        RunSum64 S;
+        S.len = 0; S.trail = 0; S.first = S.last = -1; S.uni = 1; S.pad = 0;
+        if (t < t1) {
+            TileSum x = sums[t];
+            S.len = x.len; S.trail = x.trail; S.first = x.first; S.last = x.last; S.uni = x.uni;
+        }
+        sh[tid] = S;
+        __syncthreads();
+        for (int d = 1; d < 256; d <<= 1) {
+            RunSum64 v = (tid >= d) ? rs64_combine(sh[tid - d], sh[tid]) : sh[tid];
+            __syncthreads();
+            sh[tid] = v;
+            __syncthreads();
+        }
+        RunSum64 P = tid ? rs64_combine(acc, sh[tid - 1]) : acc;
+        if (t < t1)
+            carry[t] = (t > t0 && P.len > 0 && P.last == S.first) ? (uint32_t)(P.trail % 255u) : 0u;
+        acc = rs64_combine(acc, sh[255]);
+        __syncthreads();
     }
 }
 
@@ -223,14 +258,17 @@ __global__ void k_stream_w(const uint64_t* __restrict__ seg_tile0, const uint64_
     if (s < nstreams) out[s] = tile_wpre[seg_tile0[s + 1]] - tile_wpre[seg_tile0[s]];
 }
 
-// one thread per stream: greedy cut (see file header)
-__global__ void k_cut(const StreamIn* __restrict__ streams, const uint64_t* __restrict__ seg_tile0,
-                      const uint64_t* __restrict__ tile_wpre, const uint8_t* __restrict__ tpos, uint32_t nstreams,
-                      uint32_t nblock_max, const uint64_t* __restrict__ slot0, BlockDesc* __restrict__ tmp,
-                      uint32_t* __restrict__ nblk)
+// one wave per stream: greedy cut (see file header).  Per block: binary search
+// of the tile where the RLE1 size crosses nblockMAX, a 64-lane scan of that
+// tile's byte weights for the crossing byte q, then a ballot over the next 256
+// bytes for the first chunk start p >= q (chunks are at most 255 bytes).
+__global__ void __launch_bounds__(64) k_cut(const StreamIn* __restrict__ streams, const uint64_t* __restrict__ seg_tile0,
+                                             const uint64_t* __restrict__ tile_wpre, const uint8_t* __restrict__ tpos,
+                                             uint32_t nstreams, uint32_t nblock_max, const uint64_t* __restrict__ slot0,
+                                             BlockDesc* __restrict__ tmp, uint32_t* __restrict__ nblk)
 {
-    uint32_t s = blockIdx.x * blockDim.x + threadIdx.x;
-    if (s >= nstreams) return;
+    const uint32_t s = blockIdx.x;
+    const int lane = threadIdx.x;
     const uint64_t beg = streams[s].text_off, end = beg + streams[s].text_len;
     const uint64_t t0 = seg_tile0[s], t1 = seg_tile0[s + 1];
     const uint64_t w0 = tile_wpre[t0], wend = tile_wpre[t1] - w0;
@@ -238,42 +276,65 @@ __global__ void k_cut(const StreamIn* __restrict__ streams, const uint64_t* __re
     uint64_t bs = beg, wbs = 0;
     uint32_t k = 0;
     while (bs < end) {
-        uint64_t target = wbs + nblock_max;
-        uint64_t block_end = end;
+        const uint64_t target = wbs + nblock_max;
+        uint64_t block_end = end, wblock_end = wend;
         if (wend >= target) {
-            // tile holding the crossing: last tile t with Wstart(t) < target
-            uint64_t lo = t0 + (bs - beg) / kTB, hi = t1;   // Wstart(lo) <= wbs < target
+            uint64_t lo = t0 + (bs - beg) / kTB, hi = t1;   // Wstart(lo) <= wbs < target <= Wstart(hi)
             while (hi - lo > 1) {
                 uint64_t mid = (lo + hi) >> 1;
                 if (tile_wpre[mid] - w0 < target) lo = mid; else hi = mid;
             }
-            uint64_t y = beg + (lo - t0) * kTB;
-            uint64_t W = tile_wpre[lo] - w0;
-            if (y < bs) {  // start inside the block's first tile: W(bs) is known
-                y = bs;
-                W = wbs;
+            uint64_t q = 0, Wq = 0;
+            for (;;) {   // normally one iteration
+                const uint64_t tstart = beg + (lo - t0) * kTB;
+                uint64_t tend = tstart + kTB;
+                if (tend > end) tend = end;
+                const uint64_t y0 = tstart < bs ? bs : tstart;
+                const uint64_t W0 = tstart < bs ? wbs : tile_wpre[lo] - w0;
+                const uint64_t a = y0 + (uint64_t)lane * 64;
+                const uint64_t e = (a + 64 < tend) ? a + 64 : tend;
+                uint32_t ssum = 0;
+                for (uint64_t y = a; y < e; ++y) ssum += rle_w(tpos[y]);
+                const uint32_t incl = wave_incl_scan_add(ssum);
+                const uint64_t ball = __ballot(a < tend && W0 + incl >= target);
+                if (ball) {
+                    const int L = __ffsll((unsigned long long)ball) - 1;
+                    uint64_t x = a, Wx = W0 + incl - ssum;
+                    if (lane == L) {
+                        while (Wx < target) { Wx += rle_w(tpos[x]); ++x; }
+                    }
+                    q = __shfl(x, L, 64);
+                    Wq = __shfl(Wx, L, 64);
+                    break;
+                }
+                ++lo;   // cannot happen when the tile search is exact; stay safe
+                if (lo >= t1) { q = end; Wq = wend; break; }
             }
-            while (W < target) { W += rle_w(tpos[y]); ++y; }   // q = y: first x with W(x) >= target
-            uint64_t p = y;
-            while (p < end && tpos[p] != 0) { W += rle_w(tpos[p]); ++p; }
-            if (p < end && !(frj && p == end - 1)) block_end = p;
-            if (block_end != end) {
-                BlockDesc b;
-                b.in_beg = bs; b.in_end = block_end; b.w_beg = wbs; b.n = (uint32_t)(W - wbs); b.stream = s;
-                tmp[slot0[s] + k] = b;
-                ++k;
-                bs = block_end;
-                wbs = W;
-                continue;
+            uint64_t p = end;
+            for (int r = 0; r < 4; ++r) {
+                const uint64_t pos = q + (uint64_t)r * 64 + lane;
+                const uint64_t hit = __ballot(pos < end && tpos[pos] == 0);
+                if (hit) { p = q + (uint64_t)r * 64 + (__ffsll((unsigned long long)hit) - 1); break; }
+                if (q + (uint64_t)(r + 1) * 64 >= end) break;
             }
+            uint32_t part = 0;
+            for (int r = 0; r < 4; ++r) {
+                const uint64_t pos = q + (uint64_t)r * 64 + lane;
+                if (pos < p) part += rle_w(tpos[pos]);
+            }
+            const uint64_t Wp = Wq + wave_reduce_add(part);
+            if (p < end && !(frj && p == end - 1)) { block_end = p; wblock_end = Wp; }
         }
-        BlockDesc b;
-        b.in_beg = bs; b.in_end = end; b.w_beg = wbs; b.n = (uint32_t)(wend - wbs); b.stream = s;
-        tmp[slot0[s] + k] = b;
+        if (lane == 0) {
+            BlockDesc b;
+            b.in_beg = bs; b.in_end = block_end; b.w_beg = wbs; b.n = (uint32_t)(wblock_end - wbs); b.stream = s;
+            tmp[slot0[s] + k] = b;
+        }
         ++k;
-        break;
+        bs = block_end;
+        wbs = wblock_end;
     }
-    nblk[s] = k;
+    if (lane == 0) nblk[s] = k;
 }
 
 __global__ void k_compact_blocks(const BlockDesc* __restrict__ tmp, const uint64_t* __restrict__ slot0,
@@ -417,7 +478,7 @@ void rle_sum(const uint8_t* text, const TileDesc* tiles, uint64_t ntiles, TileSu
 }
 void rle_carry(const uint64_t* tile0, uint32_t ns, const TileSum* sums, uint32_t* carry, hipStream_t st)
 {
-    hipLaunchKernelGGL(k_rle_carry, dim3(g1(ns, 64)), dim3(64), 0, st, tile0, ns, sums, carry);
+    hipLaunchKernelGGL(k_rle_carry, dim3(ns), dim3(256), 0, st, tile0, ns, sums, carry);
 }
 void rle_pos(const uint8_t* text, const TileDesc* tiles, uint64_t ntiles, const uint32_t* carry, uint8_t* tpos,
              uint32_t* tile_w, hipStream_t st)
@@ -431,7 +492,7 @@ void rle_stream_w(const uint64_t* tile0, const uint64_t* wpre, uint32_t ns, uint
 void rle_cut(const StreamIn* streams, const uint64_t* tile0, const uint64_t* wpre, const uint8_t* tpos, uint32_t ns,
              uint32_t nblock_max, const uint64_t* slot0, BlockDesc* tmp, uint32_t* nblk, hipStream_t st)
 {
-    hipLaunchKernelGGL(k_cut, dim3(g1(ns, 64)), dim3(64), 0, st, streams, tile0, wpre, tpos, ns, nblock_max, slot0, tmp,
+    hipLaunchKernelGGL(k_cut, dim3(ns), dim3(64), 0, st, streams, tile0, wpre, tpos, ns, nblock_max, slot0, tmp,
                        nblk);
 }
 void rle_compact(const BlockDesc* tmp, const uint64_t* slot0, const uint32_t* nblk, const uint32_t* first, uint32_t ns,

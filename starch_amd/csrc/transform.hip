@@ -33,7 +33,7 @@ k_count_nl(const uint8_t* __restrict__ bed, uint64_t n, uint32_t* __restrict__ t
     const uint64_t base = (uint64_t)blockIdx.x * kTileBytes + (uint64_t)threadIdx.x * 64;
     uint32_t c = 0;
     uint64_t ff = ~0ull;
-    if (base + 64 <= n) {
+    if (base + 64 <= n && ((reinterpret_cast<uintptr_t>(bed) & 15u) == 0)) {
         const uint4* p = reinterpret_cast<const uint4*>(bed + base);
 #pragma unroll
         for (int k = 0; k < 4; ++k) {
@@ -41,12 +41,11 @@ k_count_nl(const uint8_t* __restrict__ bed, uint64_t n, uint32_t* __restrict__ t
             uint32_t w[4] = {v.x, v.y, v.z, v.w};
 #pragma unroll
             for (int j = 0; j < 4; ++j) {
-#pragma unroll
-                for (int b = 0; b < 4; ++b) {
-                    uint32_t by = (w[j] >> (8 * b)) & 0xff;
-                    c += (by == '\n');
-                    if (by == 0xff && ff == ~0ull) ff = base + k * 16 + j * 4 + b;
-                }
+                uint32_t x = w[j];
+                uint32_t t = ((x ^ 0x0a0a0a0au) & 0x7f7f7f7fu) + 0x7f7f7f7fu;
+                c += __popc(~(t | (x ^ 0x0a0a0a0au)) & 0x80808080u);
+                uint32_t f = ~(((~x & 0x7f7f7f7fu) + 0x7f7f7f7fu) | ~x) & 0x80808080u;   // bytes == 0xff
+                if (f && ff == ~0ull) ff = base + k * 16 + j * 4 + ((uint32_t)__builtin_ctz(f) >> 3);
             }
         }
     } else {
@@ -63,25 +62,62 @@ k_count_nl(const uint8_t* __restrict__ bed, uint64_t n, uint32_t* __restrict__ t
     if (threadIdx.x == 0) tile_cnt[blockIdx.x] = tot;
 }
 
+// exact per-byte '\n' flags of a little-endian word (bit 7 of each byte)
+__device__ __forceinline__ uint32_t nl_flags(uint32_t w)
+{
+    uint32_t x = w ^ 0x0a0a0a0au;
+    uint32_t t = ((x & 0x7f7f7f7fu) + 0x7f7f7f7fu) | x;
+    return ~t & 0x80808080u;
+}
+
 __global__ void __launch_bounds__(kThreads)
 k_index_nl(const uint8_t* __restrict__ bed, uint64_t n, const uint64_t* __restrict__ tile_off,
            uint64_t* __restrict__ line_end)
 {
     const uint64_t base = (uint64_t)blockIdx.x * kTileBytes + (uint64_t)threadIdx.x * 64;
-    uint8_t loc[64];
+    uint32_t fl[16];
     uint32_t c = 0;
-#pragma unroll 8
-    for (int k = 0; k < 64; ++k) {
-        uint64_t i = base + k;
-        uint8_t by = (i < n) ? bed[i] : 0;
-        loc[k] = by;
-        c += (by == '\n');
+    if (base + 64 <= n && ((reinterpret_cast<uintptr_t>(bed) & 15u) == 0)) {
+        const uint4* p = reinterpret_cast<const uint4*>(bed + base);
+#pragma unroll
+        for (int k = 0; k < 4; ++k) {
+            uint4 v = p[k];
+            fl[4 * k + 0] = nl_flags(v.x);
+            fl[4 * k + 1] = nl_flags(v.y);
+            fl[4 * k + 2] = nl_flags(v.z);
+            fl[4 * k + 3] = nl_flags(v.w);
+        }
+    } else {
+#pragma unroll
+        for (int j = 0; j < 16; ++j) {
+            uint32_t w = 0;
+#pragma unroll
+            for (int b = 0; b < 4; ++b) {
+                uint64_t i = base + 4 * j + b;
+                uint32_t by = (i < n) ? bed[i] : 0u;
+                w |= by << (8 * b);
+            }
+            uint32_t f = nl_flags(w);
+#pragma unroll
+            for (int b = 0; b < 4; ++b)
+                if (base + 4 * j + b >= n) f &= ~(0x80u << (8 * b));
+            fl[j] = f;
+        }
     }
+#pragma unroll
+    for (int j = 0; j < 16; ++j) c += __popc(fl[j]);
     __shared__ uint32_t sh[kThreads / 64 + 1];
     uint32_t pre = block_excl_scan_add<uint32_t>(c, sh, (uint32_t*)nullptr);
     uint64_t o = tile_off[blockIdx.x] + pre;
-    for (int k = 0; k < 64; ++k)
-        if (loc[k] == '\n') line_end[o++] = base + k + 1;
+#pragma unroll
+    for (int j = 0; j < 16; ++j) {
+        uint32_t m = fl[j];
+        while (m) {
+            uint32_t bpos = (uint32_t)__builtin_ctz(m) >> 3;
+            line_end[o++] = base + 4 * j + bpos + 1;
+            m &= m - 1;
+        }
+    }
 }
 
 // number of lines whose '\n' precedes the first 0xFF (hpp:181: 0xFF reads as EOF)

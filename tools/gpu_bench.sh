@@ -1,0 +1,13 @@
+#!/usr/bin/env bash
+# GPU box: bench line + rocprofv3 kernel-trace summary of the same command.
+set -o pipefail
+mkdir -p gpurun_out
+export PYTHONUNBUFFERED=1
+timeout -k 10 ${TB:-900} python bench.py ${BENCH_ARGS:-} > gpurun_out/bench.json 2> gpurun_out/bench.err || { tail -30 gpurun_out/bench.err; exit 1; }
+cat gpurun_out/bench.json
+tail -5 gpurun_out/bench.err
+if [ -n "${PROF:-}" ]; then
+  cd /tmp && export TMPDIR=/tmp
+  timeout -k 10 ${TP:-900} rocprofv3 --kernel-trace --stats -d $GRAFT_REPO_ROOT/gpurun_out/prof -o run --output-format csv -- python3 $GRAFT_REPO_ROOT/bench.py --steps 2 --warmup 1 --no-cpu-baseline > $GRAFT_REPO_ROOT/gpurun_out/prof.log 2>&1 || { tail -20 $GRAFT_REPO_ROOT/gpurun_out/prof.log; exit 1; }
+  find $GRAFT_REPO_ROOT/gpurun_out/prof -name '*stats*' | head
+fi
