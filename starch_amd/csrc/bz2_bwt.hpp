@@ -23,7 +23,7 @@ void launch_fallback(BlockDesc* blocks, uint32_t b0, const uint32_t* which, uint
 void launch_mtf(BlockDesc* blocks, uint32_t b0, uint32_t nb, const uint8_t* blkbytes, uint64_t stride,
                 const BwtScratch& scr, uint16_t* mtfv, uint64_t mtf_stride, Tables* tabs, hipStream_t st);
 void launch_tables(BlockDesc* blocks, uint32_t b0, uint32_t nb, const uint16_t* mtfv, uint64_t mtf_stride,
-                   Tables* tabs, uint8_t* sel, uint32_t* gbits, hipStream_t st);
+                   Tables* tabs, uint8_t* sel, uint32_t* gbits, const BwtScratch& scr, hipStream_t st);
 void launch_emit_blocks(const BlockDesc* blocks, uint32_t nb, const uint16_t* mtfv, uint64_t mtf_stride,
                         const Tables* tabs, const uint8_t* sel, const uint32_t* gbits, uint32_t* out32,
                         hipStream_t st);

@@ -192,7 +192,7 @@ void Encoder::plan(const uint8_t* d_text, const std::vector<StreamIn>& streams, 
         }
         {
             EvTimer tt(st, stats ? &stats->tables : nullptr);
-            launch_tables(d_blocks, b0, cnt, d_mtfv, mtf_stride, d_tabs, d_sel, d_gbits, st);
+            launch_tables(d_blocks, b0, cnt, d_mtfv, mtf_stride, d_tabs, d_sel, d_gbits, scr, st);
         }
     }
     HIP_CHECK(hipMemcpyAsync(hb.data(), d_blocks, nb * sizeof(BlockDesc), hipMemcpyDeviceToHost, st));

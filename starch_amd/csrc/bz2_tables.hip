@@ -79,7 +79,8 @@ __device__ void hb_make_lengths(uint8_t* len, const uint32_t* freq, int32_t alph
 __global__ void __launch_bounds__(TT) k_tables(BlockDesc* __restrict__ blocks, uint32_t b0,
                                                 const uint16_t* __restrict__ mtfv_all, uint64_t mtf_stride,
                                                 Tables* __restrict__ tabs, uint8_t* __restrict__ sel_all,
-                                                uint32_t* __restrict__ gbits_all)
+                                                uint32_t* __restrict__ gbits_all, uint8_t* __restrict__ hist_all,
+                                                uint64_t hist_stride)
 {
     __shared__ HuffSmem hs;
     __shared__ uint8_t len[6][258];
@@ -116,23 +117,70 @@ __global__ void __launch_bounds__(TT) k_tables(BlockDesc* __restrict__ blocks, u
         }
     }
     __syncthreads();
+    // Small alphabets: per-group symbol histograms (u8, <= 50) built once, so a
+    // group's cost against a table is alpha multiply-adds and the per-table
+    // frequencies are a reduction over groups by (symbol, group chunk) lanes
+    // instead of 50 contended LDS atomics per group.
+    const bool use_hist = alpha <= 64;
+    uint8_t* hist = hist_all + (uint64_t)blockIdx.x * hist_stride;
+    if (use_hist) {
+        for (uint32_t g = tid; g < nsel; g += TT) {
+            uint8_t* h = hist + (uint64_t)g * alpha;
+            for (int32_t v = 0; v < alpha; ++v) h[v] = 0;
+            uint32_t gs = g * 50, ge = gs + 50;
+            if (ge > n_mtf) ge = n_mtf;
+            for (uint32_t i = gs; i < ge; ++i) h[mtfv[i]]++;
+        }
+    }
+    __syncthreads();
     for (int iter = 0; iter < 4; ++iter) {                         // BZ_N_ITERS
         for (int i = tid; i < 6 * 258; i += TT) (&rfreq[0][0])[i] = 0;
         __syncthreads();
         for (uint32_t g = tid; g < nsel; g += TT) {
-            uint32_t gs = g * 50, ge = gs + 50;
-            if (ge > n_mtf) ge = n_mtf;
             uint32_t cost[6] = {0, 0, 0, 0, 0, 0};
-            for (uint32_t i = gs; i < ge; ++i) {
-                uint32_t v = mtfv[i];
+            if (use_hist) {
+                const uint8_t* h = hist + (uint64_t)g * alpha;
+                for (int32_t v = 0; v < alpha; ++v) {
+                    uint32_t c = h[v];
+                    if (!c) continue;
 #pragma unroll
-                for (int t = 0; t < 6; ++t) cost[t] += len[t][v];
+                    for (int t = 0; t < 6; ++t) cost[t] += c * len[t][v];
+                }
+            } else {
+                uint32_t gs = g * 50, ge = gs + 50;
+                if (ge > n_mtf) ge = n_mtf;
+                for (uint32_t i = gs; i < ge; ++i) {
+                    uint32_t v = mtfv[i];
+#pragma unroll
+                    for (int t = 0; t < 6; ++t) cost[t] += len[t][v];
+                }
             }
             int bt = 0;
             uint32_t bc = cost[0];
             for (int t = 1; t < ng; ++t) if (cost[t] < bc) { bc = cost[t]; bt = t; }
             sel[g] = (uint8_t)bt;
-            for (uint32_t i = gs; i < ge; ++i) atomicAdd(&rfreq[bt][mtfv[i]], 1u);
+            if (!use_hist) {
+                uint32_t gs = g * 50, ge = gs + 50;
+                if (ge > n_mtf) ge = n_mtf;
+                for (uint32_t i = gs; i < ge; ++i) atomicAdd(&rfreq[bt][mtfv[i]], 1u);
+            }
+        }
+        __syncthreads();
+        if (use_hist) {
+            const uint32_t nchunk = TT / (uint32_t)alpha;
+            const uint32_t v = tid % alpha, c = tid / alpha;
+            if (c < nchunk) {
+                const uint32_t per = (nsel + nchunk - 1) / nchunk;
+                uint32_t acc[6] = {0, 0, 0, 0, 0, 0};
+                const uint32_t g1 = (c + 1) * per < nsel ? (c + 1) * per : nsel;
+                for (uint32_t g = c * per; g < g1; ++g) {
+                    uint32_t cnt = hist[(uint64_t)g * alpha + v];
+                    uint32_t t = sel[g];
+#pragma unroll
+                    for (int q = 0; q < 6; ++q) acc[q] += (t == (uint32_t)q) ? cnt : 0u;
+                }
+                for (int q = 0; q < ng; ++q) if (acc[q]) atomicAdd(&rfreq[q][v], acc[q]);
+            }
         }
         __syncthreads();
         if (tid < ng) hb_make_lengths(len[tid], rfreq[tid], alpha, 17, hs.heap[tid], hs.weight[tid], hs.parent[tid]);
@@ -190,11 +238,16 @@ __global__ void __launch_bounds__(TT) k_tables(BlockDesc* __restrict__ blocks, u
     // data bits per group
     uint64_t local = 0;
     for (uint32_t g = tid; g < nsel; g += TT) {
-        uint32_t gs = g * 50, ge = gs + 50;
-        if (ge > n_mtf) ge = n_mtf;
         const uint8_t* L = len[sel[g]];
         uint32_t bits = 0;
-        for (uint32_t i = gs; i < ge; ++i) bits += L[mtfv[i]];
+        if (use_hist) {
+            const uint8_t* h = hist + (uint64_t)g * alpha;
+            for (int32_t v = 0; v < alpha; ++v) bits += (uint32_t)h[v] * L[v];
+        } else {
+            uint32_t gs = g * 50, ge = gs + 50;
+            if (ge > n_mtf) ge = n_mtf;
+            for (uint32_t i = gs; i < ge; ++i) bits += L[mtfv[i]];
+        }
         gbits[g] = bits;
         local += bits;
     }
@@ -209,9 +262,13 @@ __global__ void __launch_bounds__(TT) k_tables(BlockDesc* __restrict__ blocks, u
 }
 
 void launch_tables(BlockDesc* blocks, uint32_t b0, uint32_t nb, const uint16_t* mtfv, uint64_t mtf_stride,
-                   Tables* tabs, uint8_t* sel, uint32_t* gbits, hipStream_t st)
+                   Tables* tabs, uint8_t* sel, uint32_t* gbits, const BwtScratch& scr, hipStream_t st)
 {
-    hipLaunchKernelGGL(k_tables, dim3(nb), dim3(TT), 0, st, blocks, b0, mtfv, mtf_stride, tabs, sel, gbits);
+    // per-group histograms live in the (now free) block-sort key scratch
+    uint8_t* hist = reinterpret_cast<uint8_t*>(scr.K);
+    const uint64_t hist_stride = scr.stride * sizeof(uint64_t);
+    hipLaunchKernelGGL(k_tables, dim3(nb), dim3(TT), 0, st, blocks, b0, mtfv, mtf_stride, tabs, sel, gbits, hist,
+                       hist_stride);
     HIP_CHECK(hipGetLastError());
 }
 
