@@ -18,6 +18,8 @@ struct BwtScratch {            // 40 bytes per rotation per batch slot
 
 void launch_bwt(BlockDesc* blocks, uint32_t b0, uint32_t nb, const uint8_t* blkbytes, uint64_t stride,
                 const BwtScratch& scr, unsigned long long* stats, hipStream_t st);
+void launch_bwt2(BlockDesc* blocks, uint32_t b0, uint32_t nb, const uint8_t* blkbytes, uint64_t stride,
+                 const BwtScratch& scr, unsigned long long* stats, hipStream_t st);
 void launch_fallback(BlockDesc* blocks, uint32_t b0, const uint32_t* which, uint32_t nwhich,
                      const uint8_t* blkbytes, uint64_t stride, const BwtScratch& scr, hipStream_t st);
 void launch_mtf(BlockDesc* blocks, uint32_t b0, uint32_t nb, const uint8_t* blkbytes, uint64_t stride,

@@ -6,6 +6,8 @@
 // lays out offsets.
 #include "bz2_bwt.hpp"
 
+#include <string.h>
+
 #include <algorithm>
 
 namespace bz {
@@ -172,7 +174,9 @@ void Encoder::plan(const uint8_t* d_text, const std::vector<StreamIn>& streams, 
         uint32_t cnt = std::min(batch, nb - b0);
         {
             EvTimer tb(st, stats ? &stats->bwt : nullptr);
-            launch_bwt(d_blocks, b0, cnt, d_blkbytes, blk_stride_, scr, d_stats, st);
+            static const bool lsd = [] { const char* e = getenv("STARCH_BWT"); return e && !strcmp(e, "lsd"); }();
+            if (lsd) launch_bwt(d_blocks, b0, cnt, d_blkbytes, blk_stride_, scr, d_stats, st);
+            else launch_bwt2(d_blocks, b0, cnt, d_blkbytes, blk_stride_, scr, d_stats, st);
             HIP_CHECK(hipMemcpyAsync(hb.data() + b0, d_blocks + b0, cnt * sizeof(BlockDesc), hipMemcpyDeviceToHost,
                                      st));
             HIP_CHECK(hipStreamSynchronize(st));

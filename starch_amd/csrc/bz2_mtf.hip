@@ -103,7 +103,8 @@ __global__ void __launch_bounds__(MT) k_mtf(BlockDesc* __restrict__ blocks, uint
     }
     __syncthreads();
 
-    const uint32_t csz = (n + C - 1) / C;
+    // chunks are 16-byte aligned so every lane moves its bytes with 16-B loads
+    const uint32_t csz = ((n + C - 1) / C + 15u) & ~15u;
     const uint32_t a = tid * csz;
     uint32_t e = a + csz;
     if (e > n) e = n;
@@ -115,9 +116,21 @@ __global__ void __launch_bounds__(MT) k_mtf(BlockDesc* __restrict__ blocks, uint
         NibState loc;
         loc.list = 0; loc.set = 0; loc.cnt = 0;
         if (mine) {
-            for (uint32_t j = e; j > a; --j) {
-                uint32_t s = ll[j - 1];
-                if (!((loc.set >> s) & 1u)) { loc.set |= 1u << s; loc.list |= (uint64_t)s << (4 * loc.cnt); ++loc.cnt; }
+            for (uint32_t j0 = a + ((e - a - 1) & ~15u);; j0 -= 16) {
+                const uint4 v = *reinterpret_cast<const uint4*>(ll + j0);
+                const uint32_t w[4] = {v.x, v.y, v.z, v.w};
+#pragma unroll
+                for (int k = 15; k >= 0; --k) {
+                    if (j0 + k < e) {
+                        uint32_t s = (w[k >> 2] >> (8 * (k & 3))) & 0xffu;
+                        if (!((loc.set >> s) & 1u)) {
+                            loc.set |= 1u << s;
+                            loc.list |= (uint64_t)s << (4 * loc.cnt);
+                            ++loc.cnt;
+                        }
+                    }
+                }
+                if (j0 == a) break;
             }
         }
         nst[tid] = loc;
@@ -140,17 +153,29 @@ __global__ void __launch_bounds__(MT) k_mtf(BlockDesc* __restrict__ blocks, uint
         cs.lz = 0; cs.tz = 0; cs.len = e > a ? e - a : 0; cs.inner = 0; cs.has_nz = 0; cs.zin = 0; cs.out = 0;
         if (mine) {
             uint32_t z = 0;
-            for (uint32_t j = a; j < e; ++j) {
-                uint32_t s = ll[j];
-                uint64_t x = L ^ (0x1111111111111111ull * s);
-                uint64_t t = x | (x >> 1) | (x >> 2) | (x >> 3);
-                uint64_t zn = ~t & 0x1111111111111111ull;
-                uint32_t k = (uint32_t)__builtin_ctzll(zn) >> 2;
-                L = (L & ~lowmask4(k + 1)) | ((L & lowmask4(k)) << 4) | (uint64_t)s;
-                idx[j] = (uint8_t)k;
-                if (k == 0) { ++z; continue; }
-                if (!cs.has_nz) { cs.lz = z; cs.has_nz = 1; } else { cs.inner += 1 + nsym_run(z); }
-                z = 0;
+            for (uint32_t j0 = a; j0 < e; j0 += 16) {
+                const uint4 v = *reinterpret_cast<const uint4*>(ll + j0);
+                const uint32_t w[4] = {v.x, v.y, v.z, v.w};
+                uint32_t o[4] = {0, 0, 0, 0};
+#pragma unroll
+                for (int q = 0; q < 16; ++q) {
+                    if (j0 + q < e) {
+                        const uint32_t s = (w[q >> 2] >> (8 * (q & 3))) & 0xffu;
+                        const uint64_t x = L ^ (0x1111111111111111ull * s);
+                        const uint64_t t = x | (x >> 1) | (x >> 2) | (x >> 3);
+                        const uint64_t zn = ~t & 0x1111111111111111ull;
+                        const uint32_t k = (uint32_t)__builtin_ctzll(zn) >> 2;
+                        L = (L & ~lowmask4(k + 1)) | ((L & lowmask4(k)) << 4) | (uint64_t)s;
+                        o[q >> 2] |= k << (8 * (q & 3));
+                        if (k == 0) {
+                            ++z;
+                        } else {
+                            if (!cs.has_nz) { cs.lz = z; cs.has_nz = 1; } else { cs.inner += 1 + nsym_run(z); }
+                            z = 0;
+                        }
+                    }
+                }
+                *reinterpret_cast<uint4*>(idx + j0) = make_uint4(o[0], o[1], o[2], o[3]);
             }
             if (!cs.has_nz) cs.lz = z;
             cs.tz = z;
@@ -246,17 +271,22 @@ __global__ void __launch_bounds__(MT) k_mtf(BlockDesc* __restrict__ blocks, uint
         const ChunkSum cs = cs_sh[tid];
         uint32_t o = cs.out;
         uint32_t z = cs.zin;
-        for (uint32_t j = a; j < e; ++j) {
-            uint32_t v = idx[j];
-            if (v == 0) { ++z; continue; }
-            while (z) {
-                uint32_t d = ((z - 1) & 1u) ? 1u : 0u;       // RUNB : RUNA
-                mtfv[o++] = (uint16_t)d;
-                atomicAdd(&freq[wv][d], 1u);
-                z = (z - (d + 1)) >> 1;
+        for (uint32_t j0 = a; j0 < e; j0 += 16) {
+            const uint4 vv = *reinterpret_cast<const uint4*>(idx + j0);
+            const uint64_t lo = ((uint64_t)vv.y << 32) | vv.x, hi = ((uint64_t)vv.w << 32) | vv.z;
+            const uint32_t qn = (e - j0) < 16u ? (e - j0) : 16u;
+            for (uint32_t q = 0; q < qn; ++q) {
+                const uint32_t v = (uint32_t)((q < 8 ? (lo >> (8 * q)) : (hi >> (8 * (q - 8)))) & 0xffu);
+                if (v == 0) { ++z; continue; }
+                while (z) {
+                    uint32_t d = ((z - 1) & 1u) ? 1u : 0u;       // RUNB : RUNA
+                    mtfv[o++] = (uint16_t)d;
+                    atomicAdd(&freq[wv][d], 1u);
+                    z = (z - (d + 1)) >> 1;
+                }
+                mtfv[o++] = (uint16_t)(v + 1);
+                atomicAdd(&freq[wv][v + 1], 1u);
             }
-            mtfv[o++] = (uint16_t)(v + 1);
-            atomicAdd(&freq[wv][v + 1], 1u);
         }
     }
     __syncthreads();

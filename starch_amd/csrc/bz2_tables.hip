@@ -124,12 +124,17 @@ __global__ void __launch_bounds__(TT) k_tables(BlockDesc* __restrict__ blocks, u
     const bool use_hist = alpha <= 64;
     uint8_t* hist = hist_all + (uint64_t)blockIdx.x * hist_stride;
     if (use_hist) {
+        // layout [symbol][group]: lanes of a wave touch consecutive bytes
         for (uint32_t g = tid; g < nsel; g += TT) {
-            uint8_t* h = hist + (uint64_t)g * alpha;
-            for (int32_t v = 0; v < alpha; ++v) h[v] = 0;
+            for (int32_t v = 0; v < alpha; ++v) hist[(uint64_t)v * nsel + g] = 0;
             uint32_t gs = g * 50, ge = gs + 50;
             if (ge > n_mtf) ge = n_mtf;
-            for (uint32_t i = gs; i < ge; ++i) h[mtfv[i]]++;
+            const uint32_t* m32 = reinterpret_cast<const uint32_t*>(mtfv + gs);   // gs even: 4-B aligned
+            for (uint32_t i = gs; i < ge; i += 2) {
+                uint32_t w = m32[(i - gs) >> 1];
+                hist[(uint64_t)(w & 0xffffu) * nsel + g]++;
+                if (i + 1 < ge) hist[(uint64_t)(w >> 16) * nsel + g]++;
+            }
         }
     }
     __syncthreads();
@@ -139,9 +144,8 @@ __global__ void __launch_bounds__(TT) k_tables(BlockDesc* __restrict__ blocks, u
         for (uint32_t g = tid; g < nsel; g += TT) {
             uint32_t cost[6] = {0, 0, 0, 0, 0, 0};
             if (use_hist) {
-                const uint8_t* h = hist + (uint64_t)g * alpha;
                 for (int32_t v = 0; v < alpha; ++v) {
-                    uint32_t c = h[v];
+                    uint32_t c = hist[(uint64_t)v * nsel + g];
                     if (!c) continue;
 #pragma unroll
                     for (int t = 0; t < 6; ++t) cost[t] += c * len[t][v];
@@ -174,7 +178,7 @@ __global__ void __launch_bounds__(TT) k_tables(BlockDesc* __restrict__ blocks, u
                 uint32_t acc[6] = {0, 0, 0, 0, 0, 0};
                 const uint32_t g1 = (c + 1) * per < nsel ? (c + 1) * per : nsel;
                 for (uint32_t g = c * per; g < g1; ++g) {
-                    uint32_t cnt = hist[(uint64_t)g * alpha + v];
+                    uint32_t cnt = hist[(uint64_t)v * nsel + g];
                     uint32_t t = sel[g];
 #pragma unroll
                     for (int q = 0; q < 6; ++q) acc[q] += (t == (uint32_t)q) ? cnt : 0u;
@@ -241,8 +245,7 @@ __global__ void __launch_bounds__(TT) k_tables(BlockDesc* __restrict__ blocks, u
         const uint8_t* L = len[sel[g]];
         uint32_t bits = 0;
         if (use_hist) {
-            const uint8_t* h = hist + (uint64_t)g * alpha;
-            for (int32_t v = 0; v < alpha; ++v) bits += (uint32_t)h[v] * L[v];
+            for (int32_t v = 0; v < alpha; ++v) bits += (uint32_t)hist[(uint64_t)v * nsel + g] * L[v];
         } else {
             uint32_t gs = g * 50, ge = gs + 50;
             if (ge > n_mtf) ge = n_mtf;
