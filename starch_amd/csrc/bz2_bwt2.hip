@@ -49,7 +49,8 @@ struct Bwt2Smem {
             uint32_t flag;
         } rad;
     } u;
-    uint32_t large[LCAP][2];
+    uint32_t stk[LCAP][3];                // MSD refinement stack: (start, size, remaining bits)
+    uint32_t rh[256], rs[256], rc[256];   // refinement histogram, sub-bucket starts, cursors
     uint32_t scan[B2W + 1];
     uint32_t ctr[8];
     uint8_t sym[256];
@@ -191,64 +192,115 @@ __device__ void wg_radix_group(uint64_t* K, uint32_t* V, uint64_t* K2, uint32_t*
     __syncthreads();
 }
 
-// Sort every listed group [s, s+m) of (K, V) by key: lanes take groups of <=
-// TCAP elements, waves groups of <= WCAP, the workgroup the rest.
+// Sort one sub-bucket ladder step: lanes for <= TCAP, waves for <= WCAP.
+__device__ __forceinline__ void sort_small(uint64_t* K, uint32_t* V, uint32_t s, uint32_t m, Bwt2Smem& sm, int wid)
+{
+    if (m <= 64) wave_rank_sort(K, V, s, m);
+    else wave_bitonic_sort(K, V, s, m, sm.u.wave.key[wid], sm.u.wave.val[wid]);
+    wave_sync_lds();
+}
+
+__device__ void push_large(Bwt2Smem& sm, uint32_t s, uint32_t m, uint32_t bits)
+{
+    uint32_t slot = atomicAdd(&sm.ctr[4], 1u);
+    if (slot < (uint32_t)LCAP) { sm.stk[slot][0] = s; sm.stk[slot][1] = m; sm.stk[slot][2] = bits; }
+    else atomicAdd(&sm.ctr[5], 1u);          // overflow: handled by the LSD fallback
+}
+
+// MSD refinement of one large group on its next (up to) 8 key bits, in place
+// via (K2, V2); sub-buckets are sorted at once (lanes / waves) or pushed.
+__device__ void msd_refine(uint64_t* K, uint32_t* V, uint64_t* K2, uint32_t* V2, uint32_t s, uint32_t m,
+                           uint32_t bits, Bwt2Smem& sm)
+{
+    const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
+    const uint32_t db = bits < 8 ? bits : 8;
+    const uint32_t sh = bits - db;
+    const uint64_t dm = (1ull << db) - 1ull;
+    if (tid < 256) sm.rh[tid] = 0;
+    __syncthreads();
+    for (uint32_t i = tid; i < m; i += B2T) atomicAdd(&sm.rh[(uint32_t)((K[s + i] >> sh) & dm)], 1u);
+    __syncthreads();
+    if (tid < 64) {
+        uint32_t a0 = sm.rh[4 * tid], a1 = sm.rh[4 * tid + 1], a2 = sm.rh[4 * tid + 2], a3 = sm.rh[4 * tid + 3];
+        uint32_t sum = a0 + a1 + a2 + a3;
+        uint32_t e = wave_incl_scan_add(sum) - sum;
+        sm.rs[4 * tid] = e; sm.rs[4 * tid + 1] = e + a0; sm.rs[4 * tid + 2] = e + a0 + a1;
+        sm.rs[4 * tid + 3] = e + a0 + a1 + a2;
+    }
+    __syncthreads();
+    if (tid < 256) sm.rc[tid] = sm.rs[tid];
+    __syncthreads();
+    for (uint32_t i = tid; i < m; i += B2T) {
+        uint64_t k = K[s + i];
+        uint32_t pos = atomicAdd(&sm.rc[(uint32_t)((k >> sh) & dm)], 1u);
+        K2[s + pos] = k;
+        V2[s + pos] = V[s + i];
+    }
+    __syncthreads();
+    for (uint32_t i = tid; i < m; i += B2T) { K[s + i] = K2[s + i]; V[s + i] = V2[s + i]; }
+    __syncthreads();
+    // sub-buckets
+    if (tid < 256) {
+        uint32_t c = sm.rh[tid];
+        if (c >= 2 && c <= (uint32_t)TCAP) lane_insertion_sort(K, V, s + sm.rs[tid], c);
+        else if (c > (uint32_t)WCAP && sh > 0) push_large(sm, s + sm.rs[tid], c, sh);
+    }
+    for (int d0 = wid * 64; d0 < 256; d0 += B2W * 64) {
+        uint32_t c = sm.rh[d0 + lane];
+        uint64_t want = __ballot(c > (uint32_t)TCAP && c <= (uint32_t)WCAP);
+        while (want) {
+            int l = __ffsll((unsigned long long)want) - 1;
+            want &= want - 1;
+            sort_small(K, V, s + sm.rs[d0 + l], sm.rh[d0 + l], sm, wid);
+        }
+    }
+    __syncthreads();
+}
+
+// Sort every listed group [s, s+m) of (K, V) by its low `bits` key bits:
+// lanes take groups of <= TCAP elements, waves groups of <= WCAP, and larger
+// groups are refined MSD-first 8 bits at a time by the whole workgroup.
 // groups: pairs (start, size) in global memory; returns after a barrier.
 __device__ void sort_groups(uint64_t* K, uint32_t* V, uint64_t* K2, uint32_t* V2, const uint32_t* groups, uint32_t ng,
                             int bits, Bwt2Smem& sm)
 {
     const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
-    // lane-level
     for (uint32_t g = tid; g < ng; g += B2T) {
         uint32_t m = groups[2 * g + 1];
         if (m <= (uint32_t)TCAP) lane_insertion_sort(K, V, groups[2 * g], m);
     }
-    if (tid == 0) sm.ctr[4] = 0;
+    if (tid == 0) { sm.ctr[4] = 0; sm.ctr[5] = 0; }
     __syncthreads();
-    // wave-level
     for (uint32_t base = (uint32_t)wid * 64; base < ng; base += B2W * 64) {
         uint32_t g = base + lane;
         uint32_t m = (g < ng) ? groups[2 * g + 1] : 0u;
         uint64_t want = __ballot(m > (uint32_t)TCAP && m <= (uint32_t)WCAP);
-        uint64_t big = __ballot(m > (uint32_t)WCAP);
+        if (m > (uint32_t)WCAP) push_large(sm, groups[2 * g], m, (uint32_t)bits);
         while (want) {
             int l = __ffsll((unsigned long long)want) - 1;
             want &= want - 1;
-            uint32_t s = groups[2 * (base + l)];
-            uint32_t mm = groups[2 * (base + l) + 1];
-            if (mm <= 64) wave_rank_sort(K, V, s, mm);
-            else wave_bitonic_sort(K, V, s, mm, sm.u.wave.key[wid], sm.u.wave.val[wid]);
-            wave_sync_lds();
-        }
-        if (big && lane == 0) {
-            uint64_t bb = big;
-            while (bb) {
-                int l = __ffsll((unsigned long long)bb) - 1;
-                bb &= bb - 1;
-                uint32_t slot = atomicAdd(&sm.ctr[4], 1u);
-                if (slot < (uint32_t)LCAP) {
-                    sm.large[slot][0] = groups[2 * (base + l)];
-                    sm.large[slot][1] = groups[2 * (base + l) + 1];
-                }
-            }
+            sort_small(K, V, groups[2 * (base + l)], groups[2 * (base + l) + 1], sm, wid);
         }
     }
     __syncthreads();
-    const uint32_t nlarge = sm.ctr[4];
-    const uint32_t nl = nlarge < (uint32_t)LCAP ? nlarge : (uint32_t)LCAP;
-    for (uint32_t q = 0; q < nl; ++q) {
-        uint32_t s = sm.large[q][0], m = sm.large[q][1];
+    // depth-first MSD refinement of large groups (LIFO stack in LDS)
+    for (;;) {
         __syncthreads();
-        wg_radix_group(K, V, K2, V2, s, m, bits, sm);
+        uint32_t top = sm.ctr[4] < (uint32_t)LCAP ? sm.ctr[4] : (uint32_t)LCAP;
+        if (top == 0) break;
+        uint32_t s = sm.stk[top - 1][0], m = sm.stk[top - 1][1], rb = sm.stk[top - 1][2];
+        __syncthreads();
+        if (tid == 0) sm.ctr[4] = top - 1;
+        __syncthreads();
+        msd_refine(K, V, K2, V2, s, m, rb, sm);
     }
-    if (nlarge > (uint32_t)LCAP) {
-        // overflow (pathological): every remaining large group, found again by scanning
+    if (sm.ctr[5]) {
+        // stack overflow (pathological): finish every still-large group with stable LSD
+        // radix; sorting an already sorted range is harmless
+        __syncthreads();
         for (uint32_t g = 0; g < ng; ++g) {
             uint32_t m = groups[2 * g + 1];
-            if (m <= (uint32_t)WCAP) continue;
-            // skip those already done: the first LCAP large groups in list order
-            // (the LDS list was filled in wave order, so redo all: sorting is idempotent)
-            wg_radix_group(K, V, K2, V2, groups[2 * g], m, bits, sm);
+            if (m > (uint32_t)WCAP) wg_radix_group(K, V, K2, V2, groups[2 * g], m, bits, sm);
         }
     }
     __syncthreads();
