@@ -40,6 +40,17 @@ struct EvTimer {
 
 static uint64_t round_up(uint64_t x, uint64_t m) { return (x + m - 1) / m * m; }
 
+uint32_t* Encoder::PinnedCtr::get()
+{
+    if (!p) HIP_CHECK(hipHostMalloc(reinterpret_cast<void**>(&p), 64 * sizeof(uint32_t), hipHostMallocDefault));
+    return p;
+}
+
+Encoder::PinnedCtr::~PinnedCtr()
+{
+    if (p) (void)hipHostFree(p);
+}
+
 void Encoder::plan(const uint8_t* d_text, const std::vector<StreamIn>& streams, int bs100k, hipStream_t st,
                    std::vector<StreamOut>& outs, Stats* stats)
 {
@@ -174,9 +185,11 @@ void Encoder::plan(const uint8_t* d_text, const std::vector<StreamIn>& streams, 
         uint32_t cnt = std::min(batch, nb - b0);
         {
             EvTimer tb(st, stats ? &stats->bwt : nullptr);
+            // STARCH_BWT=lsd selects the one-workgroup-per-block prefix-doubling sort of
+            // bz2_bwt.hip (kept as an independent implementation for cross-checks)
             static const bool lsd = [] { const char* e = getenv("STARCH_BWT"); return e && !strcmp(e, "lsd"); }();
             if (lsd) launch_bwt(d_blocks, b0, cnt, d_blkbytes, blk_stride_, scr, d_stats, st);
-            else launch_bwt2(d_blocks, b0, cnt, d_blkbytes, blk_stride_, scr, d_stats, st);
+            else launch_bwt3(d_blocks, b0, cnt, d_blkbytes, blk_stride_, scr, b_bwt3, h_ctr_.get(), d_stats, st);
             HIP_CHECK(hipMemcpyAsync(hb.data() + b0, d_blocks + b0, cnt * sizeof(BlockDesc), hipMemcpyDeviceToHost,
                                      st));
             HIP_CHECK(hipStreamSynchronize(st));
@@ -205,6 +218,7 @@ void Encoder::plan(const uint8_t* d_text, const std::vector<StreamIn>& streams, 
     HIP_CHECK(hipStreamSynchronize(st));
     if (stats) {
         stats->bwt_rounds += hstats[0];
+        stats->bwt_tied += hstats[2];
         for (auto& b : hb) stats->rle_bytes += b.n;
     }
     // stream sizes: 32 header bits + blocks + 80 trailer bits, padded to a byte

@@ -214,6 +214,7 @@ void encode_device(starch_ctx* c, const uint8_t* d_bed, uint64_t n, const starch
     c->stats.rle_bytes = bst.rle_bytes;
     c->stats.bwt_rounds = bst.bwt_rounds;
     c->stats.periodic_blocks = bst.periodic_blocks;
+    c->stats.bwt_tied = bst.bwt_tied;
     c->stats.ms_transform = ms_t;
     c->stats.ms_rle = bst.rle;
     c->stats.ms_bwt = bst.bwt;
