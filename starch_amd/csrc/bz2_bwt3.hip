@@ -25,12 +25,18 @@
 //   k3_sort_lds buckets <= 256: one wave; <= 1024/2048/4096: one workgroup;
 //               keys in registers, stable LSD radix with an LDS exchange,
 //               only over the key bits that vary inside the bucket
-//   -- every sort writes SA, RK (= head position of the rotation's group) and
-//      lists groups of equal keys --
-//   k3_gather   doubling round r: key(q) = RK[(SA[q] + D*2^(r-1)) mod n] for
+//   -- every sort writes SA and lists the groups of equal keys --
+//   k3_gather_text  text rounds: a tied group is re-sorted by the NEXT D'
+//               symbols of each rotation, packed straight from the block text
+//               (D' = 52/B so 12 key bits stay free); enough for BED text,
+//               where ties are rare and short
+//   k3_rk_*     blocks still tied after the text rounds (long repeats,
+//               periodic blocks): dense RK = head position of every
+//               rotation's group, then prefix doubling --
+//   k3_gather   doubling round r: key(q) = RK[(SA[q] + h0*2^(r-1)) mod n] for
 //               the tied rotations only; the same part/sort kernels re-sort
-//               the groups.  A round in which no group of a block splits
-//               proves the block periodic.
+//               the groups and update RK.  A round in which no group of a
+//               block splits proves the block periodic.
 //
 // Scratch (BwtScratch, per batch slot, stride S elements): K2/SA = keys and
 // rotations in bucket order; K/V = ping-pong for the MSD partition (and the
@@ -61,7 +67,8 @@ constexpr uint32_t W_MAX = 64, S_MAX = 256, M1_MAX = 1024, M2_MAX = 2048, M3_MAX
 constexpr uint32_t RBITS = 20;          // rank bits (n <= 899,985 < 2^20)
 
 // counters (u32) in the meta buffer
-enum { C_W = 0, C_S, C_M1, C_M2, C_M3, C_L0, C_L1, C_T0, C_T1, C_TIE_ELEMS, C_ERR, C_N = 16 };
+enum { C_W = 0, C_S, C_M1, C_M2, C_M3, C_L0, C_L1, C_T0, C_T1, C_TIE_ELEMS, C_ERR, C_TS0, C_TS1, C_N = 16 };
+constexpr uint32_t TEXT_ROUNDS = 4;     // max text-extension rounds before doubling
 
 // item = slot[63:52] | start[51:32] | size[31:12] | parity[7] | shift[6:0]
 __device__ __forceinline__ uint64_t mk_item(uint32_t slot, uint32_t s, uint32_t m, uint32_t shift, uint32_t par)
@@ -84,6 +91,9 @@ struct Lists {
     uint64_t* l[2];         // m > 4096 (MSD partition), ping-pong by level
     uint64_t* t[2];         // tie groups, ping-pong by round
     uint32_t* sD;           // per slot: D (symbols per key)
+    uint32_t* sDp;          // per slot: D' (symbols per text-round key, 12 top bits free)
+    uint32_t* tied;         // per slot: still tied when doubling starts
+    uint8_t* sym;           // per slot: 256-byte symbol map
     uint32_t* gin;          // per slot: groups entering this round
     uint32_t* runs;         // per slot: runs produced this round
     uint32_t* periodic;     // per slot
@@ -99,6 +109,7 @@ struct Ctx {
     Lists L;
     uint32_t lsel;          // L list that part/classify pushes into
     uint32_t tsel;          // tie list the sorts push into
+    uint32_t mode;          // 0: SA only (round 0, text rounds); 1: doubling (RK, runs)
 };
 
 __device__ __forceinline__ int bits_for3(uint32_t x) { return x ? 32 - __clz(x) : 0; }
@@ -259,7 +270,9 @@ __global__ void __launch_bounds__(ST) k3_scan(Ctx c)
     if (tid == 0) {
         c.blocks[b].n_in_use = nin;
         c.L.sD[slot] = (uint32_t)g.D;
+        c.L.sDp[slot] = (uint32_t)((64 - PDIG) / g.B);
     }
+    if (tid < 256) c.L.sym[(uint64_t)slot * 256 + tid] = sym[tid];
     const uint32_t ntile = (n + PTILE - 1) / PTILE;
     uint4* th = reinterpret_cast<uint4*>(c.scr.K + (uint64_t)slot * c.scr.stride);   // [tile][PNB/4]
     uint4* tot = th + (uint64_t)MAXT * (PNB / 4);
@@ -309,7 +322,6 @@ __global__ void __launch_bounds__(PT) k3_scatter(Ctx c)
     for (int i = tid; i < PNB; i += PT) { sm.cnt[i] = th[i]; sm.tot[i] = tot[i]; }
     uint64_t* K2 = c.scr.K2 + so;
     uint32_t* SA = c.scr.SA + so;
-    uint32_t* RK = c.scr.RK + so;
     for (uint32_t sub = 0; sub < PSUBS; ++sub) {
         const uint32_t r0 = t0 + sub * PSUB;
         if (r0 >= n) break;
@@ -328,10 +340,7 @@ __global__ void __launch_bounds__(PT) k3_scatter(Ctx c)
                 const uint32_t r = r0 + o + k;
                 K2[p] = key;
                 SA[p] = r;
-                if (sm.tot[bk] == 1u) {
-                    RK[r] = p;
-                    if (r == 0) c.blocks[b].orig_ptr = p;
-                }
+                if (r == 0 && sm.tot[bk] == 1u) c.blocks[b].orig_ptr = p;
                 key = ((key << g.B) | sm.tb[o + k + g.D]) & g.mask;
             }
         }
@@ -388,7 +397,7 @@ __global__ void __launch_bounds__(LT) k3_part_l(Ctx c, const uint64_t* __restric
         if (cc == 1) {
             const uint32_t v = dv[ss];
             if (!par) SA[ss] = v;
-            RK[v] = s + ss;
+            if (c.mode) RK[v] = s + ss;
             if (v == 0) c.blocks[b].orig_ptr = s + ss;
             nruns = 1;
         } else if (cc > M3_MAX && sh2 == 0) {
@@ -403,7 +412,7 @@ __global__ void __launch_bounds__(LT) k3_part_l(Ctx c, const uint64_t* __restric
     }
     if (tid < 256) {
         const uint32_t r = wave_reduce_add(nruns);
-        if ((tid & 63) == 0 && r) atomicAdd(&c.L.runs[slot], r);
+        if (c.mode && (tid & 63) == 0 && r) atomicAdd(&c.L.runs[slot], r);
     }
     __syncthreads();
     const uint32_t nbig = big[256];
@@ -413,12 +422,13 @@ __global__ void __launch_bounds__(LT) k3_part_l(Ctx c, const uint64_t* __restric
         for (uint32_t i = tid; i < cc; i += LT) {
             const uint32_t v = dv[ss + i];
             if (!par) SA[ss + i] = v;
-            RK[v] = s + ss;
+            if (c.mode) RK[v] = s + ss;
             if (v == 0) c.blocks[b].orig_ptr = s + ss + i;
         }
         if (tid == 0) {
             const uint32_t o = atomicAdd(c.L.ctr + C_T0 + c.tsel, 1u);
             c.L.t[c.tsel][o] = mk_item(slot, s + ss, cc, 0, 0);
+            atomicAdd(c.L.ctr + C_TS0 + c.tsel, cc);
         }
     }
 }
@@ -432,11 +442,16 @@ __device__ __forceinline__ void emit_sorted(const Ctx& c, uint32_t slot, uint32_
     const uint64_t so = (uint64_t)slot * c.scr.stride;
     if (valid) {
         c.scr.SA[so + s + j] = v;
-        c.scr.RK[so + v] = s + hp;
+        if (c.mode) c.scr.RK[so + v] = s + hp;
         if (v == 0) c.blocks[c.b0 + slot].orig_ptr = s + j;
     }
     const bool tie = valid && end && j > hp;
-    wave_push(c.L.ctr + C_T0 + c.tsel, c.L.t[c.tsel], tie, mk_item(slot, s + hp, j - hp + 1, 0, 0));
+    const uint64_t tb = __ballot(tie);
+    if (tb) {
+        wave_push(c.L.ctr + C_T0 + c.tsel, c.L.t[c.tsel], tie, mk_item(slot, s + hp, j - hp + 1, 0, 0));
+        const uint32_t te = wave_reduce_add<uint32_t>(tie ? j - hp + 1 : 0u);
+        if ((threadIdx.x & 63) == 0) atomicAdd(c.L.ctr + C_TS0 + c.tsel, te);
+    }
     runs_acc += (uint32_t)__popcll(__ballot(valid && end));
 }
 
@@ -472,7 +487,7 @@ __global__ void __launch_bounds__(256) k3_sort_w(Ctx c, const uint64_t* __restri
     const uint32_t hp = wave_incl_scan_max<uint32_t>(head ? (uint32_t)lane : 0u);
     uint32_t runs = 0;
     emit_sorted(c, slot, s, (uint32_t)lane, val, valid, hp, end, runs);
-    if (lane == 0) atomicAdd(&c.L.runs[slot], runs);
+    if (c.mode && lane == 0) atomicAdd(&c.L.runs[slot], runs);
 }
 
 // ---------------------------------------------------------------------------
@@ -504,7 +519,14 @@ __global__ void __launch_bounds__(256) k3_sort_lds(Ctx c, const uint64_t* __rest
     constexpr uint64_t KMASK = (1ull << KEYB) - 1ull;
     constexpr int DPT = 256 / (64 * NW);           // digits per thread in the offset scan
     static_assert(CAP <= (1 << IDXB), "index does not fit");
+    constexpr int DB = CAP <= 256 ? 8 : (CAP <= 1024 ? 10 : 11);   // MSD digit bits
+    constexpr int NBIN = 1 << DB;
+    constexpr int T = NW * 64;
+    constexpr int BPT = NBIN / T;                  // bins per thread
+    constexpr uint32_t LIMIT = 256 / E;            // largest sub-bucket ranked by comparison
     __shared__ uint64_t xk_all[IPW][CAP];
+    __shared__ uint32_t bst_all[IPW][NBIN + 1];   // sub-bucket starts
+    __shared__ uint32_t bcur_all[IPW][NBIN];      // scatter cursors
     __shared__ uint32_t cnt_all[4][256];
     __shared__ uint32_t sc_all[IPW][NW + 1];
     __shared__ uint64_t red_all[4];
@@ -550,8 +572,85 @@ __global__ void __launch_bounds__(256) k3_sort_lds(Ctx c, const uint64_t* __rest
     if ((diff >> KEYB) && tid % (64 * NW) == 0) atomicOr(&c.L.ctr[C_ERR], 1u);   // top bits not shared
 
     bool moved = false;
-    for (int dbit = 0; dbit < KEYB; dbit += 8) {
-        if (((diff & KMASK) >> dbit & 0xffull) == 0) continue;    // uniform per group
+    const uint64_t kdiff = diff & KMASK;
+    if (kdiff) {
+        // ---- one MSD digit (the DB bits below the highest varying bit), then every
+        // element ranks itself inside its sub-bucket by direct comparison ----
+        uint32_t* bst = bst_all[g];
+        uint32_t* bcur = bcur_all[g];
+        const int tg = wid * 64 + lane;
+        const int hb = 63 - __clzll((long long)kdiff);
+        const int lo = hb + 1 - DB > 0 ? hb + 1 - DB : 0;
+        for (int q = tg; q < NBIN; q += T) bcur[q] = 0;
+        gsync<NW>();
+        uint32_t dg[E];
+#pragma unroll
+        for (int e = 0; e < E; ++e) {
+            dg[e] = (uint32_t)(((k[e] & KMASK) >> lo) & (uint64_t)(NBIN - 1));
+            if ((uint32_t)(wid * 64 * E + e * 64 + lane) < m) atomicAdd(&bcur[dg[e]], 1u);
+        }
+        gsync<NW>();
+        uint32_t loc[BPT], sum = 0, mx = 0;
+#pragma unroll
+        for (int q = 0; q < BPT; ++q) {
+            loc[q] = bcur[tg * BPT + q];
+            sum += loc[q];
+            mx = loc[q] > mx ? loc[q] : mx;
+        }
+        const uint32_t incl = wave_incl_scan_add(sum);
+        uint32_t run = incl - sum;
+#pragma unroll
+        for (int d = 32; d >= 1; d >>= 1) { const uint32_t o = __shfl_xor(mx, d, 64); mx = o > mx ? o : mx; }
+        if constexpr (NW > 1) {
+            if (lane == 63) sc[wid] = incl;
+            if (lane == 0) wmax_all[wave] = mx;
+            __syncthreads();
+            for (int w = 0; w < wid; ++w) run += sc[w];
+            mx = 0;
+            for (int w = 0; w < NW; ++w) mx = wmax_all[w0 + w] > mx ? wmax_all[w0 + w] : mx;
+        }
+        if (mx <= LIMIT) {                         // uniform per group
+#pragma unroll
+            for (int q = 0; q < BPT; ++q) { bst[tg * BPT + q] = run; bcur[tg * BPT + q] = run; run += loc[q]; }
+            if (tg == T - 1) bst[NBIN] = run;
+            gsync<NW>();
+            uint32_t p[E];
+#pragma unroll
+            for (int e = 0; e < E; ++e) {
+                p[e] = 0;
+                if ((uint32_t)(wid * 64 * E + e * 64 + lane) < m) { p[e] = atomicAdd(&bcur[dg[e]], 1u); xk[p[e]] = k[e]; }
+            }
+            gsync<NW>();
+#pragma unroll
+            for (int e = 0; e < E; ++e) {
+                const uint32_t i = (uint32_t)(wid * 64 * E + e * 64 + lane);
+                if (i < m) {
+                    const uint32_t bs = bst[dg[e]], be = bst[dg[e] + 1];
+                    const uint64_t km = k[e] & KMASK;
+                    uint32_t r = 0;
+                    for (uint32_t q = bs; q < be; ++q) {
+                        const uint64_t kq = xk[q] & KMASK;
+                        r += (kq < km || (kq == km && q < p[e])) ? 1u : 0u;
+                    }
+                    p[e] = bs + r;
+                } else {
+                    p[e] = i;                      // pads keep the tail
+                }
+            }
+            gsync<NW>();
+#pragma unroll
+            for (int e = 0; e < E; ++e) xk[p[e]] = k[e];
+            gsync<NW>();
+#pragma unroll
+            for (int e = 0; e < E; ++e) k[e] = xk[wid * 64 * E + e * 64 + lane];
+            moved = true;
+        } else {
+            gsync<NW>();                           // bcur/sc reads done before the LSD passes
+        }
+    }
+    bool lsd_moved = false;
+    for (int dbit = 0; dbit < KEYB && !moved; dbit += 8) {
+        if ((kdiff >> dbit & 0xffull) == 0) continue;    // uniform per group
         for (int q = lane; q < 256; q += 64) wcnt[q] = 0;
         wave_sync_lds3();
         uint32_t dg[E], rk[E], ld[E], ret[E];
@@ -610,8 +709,9 @@ __global__ void __launch_bounds__(256) k3_sort_lds(Ctx c, const uint64_t* __rest
         gsync<NW>();
 #pragma unroll
         for (int e = 0; e < E; ++e) k[e] = xk[wid * 64 * E + e * 64 + lane];
-        moved = true;
+        lsd_moved = true;
     }
+    moved |= lsd_moved;
     if (!moved) {
 #pragma unroll
         for (int e = 0; e < E; ++e) xk[wid * 64 * E + e * 64 + lane] = k[e];
@@ -672,14 +772,14 @@ __global__ void __launch_bounds__(256) k3_sort_lds(Ctx c, const uint64_t* __rest
         const bool end = valid && (!ties || j + 1 == m || ((xk[j + 1] ^ k[e]) & KMASK) != 0);
         emit_sorted(c, slot, s, j, v[e], valid, hp[e], end, runs);
     }
-    if (lane == 0 && runs) atomicAdd(&c.L.runs[slot], runs);
+    if (c.mode && lane == 0 && runs) atomicAdd(&c.L.runs[slot], runs);
 }
 
 // ---------------------------------------------------------------------------
 // doubling round: gather keys of tied rotations, classify their groups
 // ---------------------------------------------------------------------------
 __global__ void __launch_bounds__(256) k3_gather(Ctx c, const uint64_t* __restrict__ items, uint32_t nitems,
-                                                  uint32_t round)
+                                                  uint32_t round, uint32_t rtext)
 {
     const int lane = threadIdx.x & 63;
     const uint32_t i = blockIdx.x * 256 + threadIdx.x;
@@ -691,7 +791,7 @@ __global__ void __launch_bounds__(256) k3_gather(Ctx c, const uint64_t* __restri
     if (active) {
         active = c.L.periodic[slot] == 0;
         n = c.blocks[c.b0 + slot].n;
-        const uint64_t h = (uint64_t)c.L.sD[slot] << (round - 1);
+        const uint64_t h = ((uint64_t)c.L.sD[slot] + (uint64_t)rtext * c.L.sDp[slot]) << (round - 1);
         if (active && h >= n) {   // sorted on >= n symbols: remaining ties are equal rotations
             c.L.periodic[slot] = 1;
             active = false;
@@ -723,6 +823,93 @@ __global__ void __launch_bounds__(256) k3_gather(Ctx c, const uint64_t* __restri
     if (active) atomicAdd(&c.L.gin[slot], 1u);
     const uint32_t tied = wave_reduce_add<uint32_t>(active ? m : 0u);
     if (lane == 0 && tied) atomicAdd(&c.L.ctr[C_TIE_ELEMS], tied);
+}
+
+// text round r >= 1: key(q) = D' symbols of rotation SA[q] starting D + (r-1)*D'
+// symbols in (the group already agrees on everything before that)
+__device__ __forceinline__ uint64_t text_key(const uint8_t* blk, const uint8_t* sym, uint32_t n, uint32_t pos,
+                                             uint32_t Dp, uint32_t B)
+{
+    uint64_t key = 0;
+    for (uint32_t k = 0; k < Dp; ++k) {
+        key = (key << B) | sym[blk[pos]];
+        if (++pos == n) pos = 0;
+    }
+    return key;
+}
+
+__global__ void __launch_bounds__(256) k3_gather_text(Ctx c, const uint64_t* __restrict__ items, uint32_t nitems,
+                                                       uint32_t r)
+{
+    const int lane = threadIdx.x & 63;
+    const uint32_t i = blockIdx.x * 256 + threadIdx.x;
+    const bool active = i < nitems;
+    const uint64_t item = active ? items[i] : 0;
+    const uint32_t slot = it_slot(item), s = it_start(item), m = it_size(item);
+    const uint32_t b = c.b0 + slot;
+    const uint32_t n = c.blocks[b].n;
+    const uint32_t D = c.L.sD[slot], Dp = c.L.sDp[slot];
+    uint32_t B = 8;
+    for (uint32_t q = 1; q <= 8; ++q)
+        if (64 / q == D) { B = q; break; }       // D = 64 / B is distinct for B = 1..8
+    const uint32_t off = (uint32_t)(((uint64_t)D + (uint64_t)(r - 1) * Dp) % n);
+    const uint8_t* blk = c.blkbytes + (uint64_t)b * c.stride;
+    const uint8_t* sym = c.L.sym + (uint64_t)slot * 256;
+    const uint64_t so = (uint64_t)slot * c.scr.stride;
+    if (active && m <= 64) {
+        for (uint32_t q = s; q < s + m; ++q) {
+            uint32_t pos = c.scr.SA[so + q] + off;
+            if (pos >= n) pos -= n;
+            c.scr.K2[so + q] = text_key(blk, sym, n, pos, Dp, B);
+        }
+    }
+    uint64_t bigm = __ballot(active && m > 64);
+    while (bigm) {
+        const int l = __ffsll((unsigned long long)bigm) - 1;
+        bigm &= bigm - 1;
+        const uint32_t ls = __shfl(s, l, 64), lm = __shfl(m, l, 64), lslot = __shfl(slot, l, 64);
+        const uint32_t ln = __shfl(n, l, 64), loff = __shfl(off, l, 64), lDp = __shfl(Dp, l, 64),
+                       lB = __shfl(B, l, 64);
+        const uint8_t* lblk = c.blkbytes + (uint64_t)(c.b0 + lslot) * c.stride;
+        const uint8_t* lsym = c.L.sym + (uint64_t)lslot * 256;
+        const uint64_t lso = (uint64_t)lslot * c.scr.stride;
+        for (uint32_t q = ls + lane; q < ls + lm; q += 64) {
+            uint32_t pos = c.scr.SA[lso + q] + loff;
+            if (pos >= ln) pos -= ln;
+            c.scr.K2[lso + q] = text_key(lblk, lsym, ln, pos, lDp, lB);
+        }
+    }
+    wave_classify(c, active, slot, s, m, Dp * B, 0);
+    const uint32_t tied = wave_reduce_add<uint32_t>(active ? m : 0u);
+    if (lane == 0 && tied) atomicAdd(&c.L.ctr[C_TIE_ELEMS], tied);
+}
+
+// ---- switch to doubling: dense ranks for the blocks that are still tied ----
+__global__ void k3_mark_tied(Ctx c, const uint64_t* __restrict__ items, uint32_t nitems)
+{
+    const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
+    if (i < nitems) c.L.tied[it_slot(items[i])] = 1;
+}
+
+__global__ void __launch_bounds__(256) k3_rk_dense(Ctx c)
+{
+    const uint32_t slot = blockIdx.y;
+    if (!c.L.tied[slot]) return;
+    const uint32_t n = c.blocks[c.b0 + slot].n;
+    const uint64_t so = (uint64_t)slot * c.scr.stride;
+    for (uint32_t j = blockIdx.x * 256 + threadIdx.x; j < n; j += gridDim.x * 256) c.scr.RK[so + c.scr.SA[so + j]] = j;
+}
+
+__global__ void __launch_bounds__(256) k3_rk_groups(Ctx c, const uint64_t* __restrict__ items, uint32_t nitems)
+{
+    // one wave per group
+    const int lane = threadIdx.x & 63;
+    const uint32_t gi = blockIdx.x * 4 + (threadIdx.x >> 6);
+    if (gi >= nitems) return;
+    const uint64_t item = items[gi];
+    const uint32_t slot = it_slot(item), s = it_start(item), m = it_size(item);
+    const uint64_t so = (uint64_t)slot * c.scr.stride;
+    for (uint32_t q = s + lane; q < s + m; q += 64) c.scr.RK[so + c.scr.SA[so + q]] = s;
 }
 
 __global__ void k3_round_end(Ctx c, uint32_t nb)
@@ -761,7 +948,7 @@ void launch_bwt3(BlockDesc* blocks, uint32_t b0, uint32_t nb, const uint8_t* blk
     const uint64_t N = (uint64_t)nb * scr.stride;
     const uint64_t cap_s = N / (W_MAX + 1) + 64, cap_m1 = N / (S_MAX + 1) + 64, cap_m2 = N / (M1_MAX + 1) + 64,
                    cap_m3 = N / (M2_MAX + 1) + 64, cap_l = N / (M3_MAX + 1) + 64;
-    const uint64_t words = C_N * 2 + 5ull * nb + 2 * (cap_s + cap_m1 + cap_m2 + cap_m3 + 2 * cap_l) + 64;
+    const uint64_t words = C_N * 2 + 7ull * nb + 64ull * nb + 2 * (cap_s + cap_m1 + cap_m2 + cap_m3 + 2 * cap_l) + 64;
     uint32_t* mw = meta.as<uint32_t>(words);
     Ctx c;
     c.blocks = blocks;
@@ -775,7 +962,10 @@ void launch_bwt3(BlockDesc* blocks, uint32_t b0, uint32_t nb, const uint8_t* blk
     c.L.runs = c.L.gin + nb;
     c.L.periodic = c.L.runs + nb;
     c.L.rounds = c.L.periodic + nb;
-    uintptr_t p = reinterpret_cast<uintptr_t>(c.L.rounds + nb);
+    c.L.sDp = c.L.rounds + nb;
+    c.L.tied = c.L.sDp + nb;
+    c.L.sym = reinterpret_cast<uint8_t*>(c.L.tied + nb);
+    uintptr_t p = reinterpret_cast<uintptr_t>(c.L.sym + 256ull * nb);
     p = (p + 7) & ~(uintptr_t)7;
     c.L.s = reinterpret_cast<uint64_t*>(p);
     c.L.m1 = c.L.s + cap_s;
@@ -788,7 +978,8 @@ void launch_bwt3(BlockDesc* blocks, uint32_t b0, uint32_t nb, const uint8_t* blk
     c.L.t[1] = reinterpret_cast<uint64_t*>(scr.V2);
     c.lsel = 0;
     c.tsel = 0;
-    HIP_CHECK(hipMemsetAsync(mw, 0, (2 * C_N + 5ull * nb) * sizeof(uint32_t), st));
+    c.mode = 0;
+    HIP_CHECK(hipMemsetAsync(mw, 0, (2 * C_N + 7ull * nb) * sizeof(uint32_t), st));
 
     auto read_ctr = [&]() {
         HIP_CHECK(hipMemcpyAsync(hctr, c.L.ctr, C_N * sizeof(uint32_t), hipMemcpyDeviceToHost, st));
@@ -828,21 +1019,51 @@ void launch_bwt3(BlockDesc* blocks, uint32_t b0, uint32_t nb, const uint8_t* blk
     hipLaunchKernelGGL(k3_scatter, dim3(MAXT, nb), dim3(PT), 0, st, c);
     HIP_CHECK(hipGetLastError());
     sort_groups();
-    hipLaunchKernelGGL(k3_round_end, dim3((nb + 255) / 256), dim3(256), 0, st, c, nb);
-    // ---- doubling rounds on tied rotations ----
-    for (uint32_t round = 1;; ++round) {
+    // ---- text rounds: extend the tied rotations' keys from the block text ----
+    uint32_t rtext = 0;
+    uint64_t prev_tied = ~0ull;
+    bool done = false;
+    for (;;) {
         read_ctr();
         const uint32_t nt = hctr[C_T0 + c.tsel];
-        if (nt == 0) break;
-        if (round > 40) throw StarchError(-10, "bwt3: doubling did not converge");
+        const uint64_t tied = hctr[C_TS0 + c.tsel];
+        if (nt == 0) { done = true; break; }
+        if (rtext == TEXT_ROUNDS || (rtext > 0 && 2 * tied > prev_tied)) break;   // long repeats: double
+        prev_tied = tied;
+        ++rtext;
         const uint32_t cur = c.tsel;
         c.tsel ^= 1u;
         HIP_CHECK(hipMemsetAsync(c.L.ctr + C_T0 + c.tsel, 0, sizeof(uint32_t), st));
-        hipLaunchKernelGGL(k3_gather, dim3((nt + 255) / 256), dim3(256), 0, st, c, c.L.t[cur], nt, round);
+        HIP_CHECK(hipMemsetAsync(c.L.ctr + C_TS0 + c.tsel, 0, sizeof(uint32_t), st));
+        hipLaunchKernelGGL(k3_gather_text, dim3((nt + 255) / 256), dim3(256), 0, st, c, c.L.t[cur], nt, rtext);
         HIP_CHECK(hipGetLastError());
         HIP_CHECK(hipMemsetAsync(c.L.ctr + C_T0 + cur, 0, sizeof(uint32_t), st));
         sort_groups();
-        hipLaunchKernelGGL(k3_round_end, dim3((nb + 255) / 256), dim3(256), 0, st, c, nb);
+    }
+    // ---- prefix doubling on the blocks still tied ----
+    if (!done) {
+        const uint32_t nt = hctr[C_T0 + c.tsel];
+        const uint64_t* T = c.L.t[c.tsel];
+        hipLaunchKernelGGL(k3_mark_tied, dim3((nt + 255) / 256), dim3(256), 0, st, c, T, nt);
+        hipLaunchKernelGGL(k3_rk_dense, dim3(64, nb), dim3(256), 0, st, c);
+        hipLaunchKernelGGL(k3_rk_groups, dim3((nt + 3) / 4), dim3(256), 0, st, c, T, nt);
+        HIP_CHECK(hipGetLastError());
+        c.mode = 1;
+        for (uint32_t round = 1;; ++round) {
+            if (round > 1) read_ctr();
+            const uint32_t n2 = hctr[C_T0 + c.tsel];
+            if (n2 == 0) break;
+            if (round > 40) throw StarchError(-10, "bwt3: doubling did not converge");
+            const uint32_t cur = c.tsel;
+            c.tsel ^= 1u;
+            HIP_CHECK(hipMemsetAsync(c.L.ctr + C_T0 + c.tsel, 0, sizeof(uint32_t), st));
+            HIP_CHECK(hipMemsetAsync(c.L.ctr + C_TS0 + c.tsel, 0, sizeof(uint32_t), st));
+            hipLaunchKernelGGL(k3_gather, dim3((n2 + 255) / 256), dim3(256), 0, st, c, c.L.t[cur], n2, round, rtext);
+            HIP_CHECK(hipGetLastError());
+            HIP_CHECK(hipMemsetAsync(c.L.ctr + C_T0 + cur, 0, sizeof(uint32_t), st));
+            sort_groups();
+            hipLaunchKernelGGL(k3_round_end, dim3((nb + 255) / 256), dim3(256), 0, st, c, nb);
+        }
     }
     hipLaunchKernelGGL(k3_finish, dim3((nb + 255) / 256), dim3(256), 0, st, c, nb, stats);
     HIP_CHECK(hipGetLastError());
