@@ -13,6 +13,7 @@ struct BwtScratch {            // 40 bytes per rotation per batch slot
     uint32_t* RK;
     uint32_t* U;
     uint32_t* U2;
+    uint8_t* LL;               // last column bytes, sorted order (block[(ptr[i]-1) mod n])
     uint64_t stride;           // elements per slot
 };
 
@@ -23,6 +24,9 @@ void launch_bwt(BlockDesc* blocks, uint32_t b0, uint32_t nb, const uint8_t* blkb
 void launch_bwt3(BlockDesc* blocks, uint32_t b0, uint32_t nb, const uint8_t* blkbytes, uint64_t stride,
                  const BwtScratch& scr, DevBuf& meta, uint32_t* hctr, unsigned long long* stats, hipStream_t st);
 void launch_fallback(BlockDesc* blocks, uint32_t b0, const uint32_t* which, uint32_t nwhich,
+                     const uint8_t* blkbytes, uint64_t stride, const BwtScratch& scr, hipStream_t st);
+// last column for blocks whose SA was produced elsewhere (fallback / LSD path)
+void launch_last_col(const BlockDesc* blocks, uint32_t b0, const uint32_t* which, uint32_t nwhich,
                      const uint8_t* blkbytes, uint64_t stride, const BwtScratch& scr, hipStream_t st);
 void launch_mtf(BlockDesc* blocks, uint32_t b0, uint32_t nb, const uint8_t* blkbytes, uint64_t stride,
                 const BwtScratch& scr, uint16_t* mtfv, uint64_t mtf_stride, Tables* tabs, hipStream_t st);

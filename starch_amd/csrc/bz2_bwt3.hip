@@ -340,7 +340,10 @@ __global__ void __launch_bounds__(PT) k3_scatter(Ctx c)
                 const uint32_t r = r0 + o + k;
                 K2[p] = key;
                 SA[p] = r;
-                if (r == 0 && sm.tot[bk] == 1u) c.blocks[b].orig_ptr = p;
+                if (sm.tot[bk] == 1u) {                 // final: last-column byte, origPtr
+                    c.scr.LL[so + p] = blk[r ? r - 1 : n - 1];
+                    if (r == 0) c.blocks[b].orig_ptr = p;
+                }
                 key = ((key << g.B) | sm.tb[o + k + g.D]) & g.mask;
             }
         }
@@ -370,7 +373,10 @@ __global__ void __launch_bounds__(LT) k3_part_l(Ctx c, const uint64_t* __restric
     uint64_t* dk = (par ? c.scr.K2 : c.scr.K) + base;
     uint32_t* dv = (par ? c.scr.SA : c.scr.V) + base;
     uint32_t* SA = c.scr.SA + base;
+    uint8_t* LLs = c.scr.LL + base;
     uint32_t* RK = c.scr.RK + (uint64_t)slot * c.scr.stride;
+    const uint32_t n = c.blocks[b].n;
+    const uint8_t* blk = c.blkbytes + (uint64_t)b * c.stride;
     const uint32_t db = shift < 8 ? shift : 8;
     const uint32_t sh2 = shift - db;
     const uint64_t dmask = (1ull << db) - 1ull;
@@ -397,6 +403,7 @@ __global__ void __launch_bounds__(LT) k3_part_l(Ctx c, const uint64_t* __restric
         if (cc == 1) {
             const uint32_t v = dv[ss];
             if (!par) SA[ss] = v;
+            LLs[ss] = blk[v ? v - 1 : n - 1];
             if (c.mode) RK[v] = s + ss;
             if (v == 0) c.blocks[b].orig_ptr = s + ss;
             nruns = 1;
@@ -422,6 +429,7 @@ __global__ void __launch_bounds__(LT) k3_part_l(Ctx c, const uint64_t* __restric
         for (uint32_t i = tid; i < cc; i += LT) {
             const uint32_t v = dv[ss + i];
             if (!par) SA[ss + i] = v;
+            LLs[ss + i] = blk[v ? v - 1 : n - 1];
             if (c.mode) RK[v] = s + ss;
             if (v == 0) c.blocks[b].orig_ptr = s + ss + i;
         }
@@ -437,11 +445,13 @@ __global__ void __launch_bounds__(LT) k3_part_l(Ctx c, const uint64_t* __restric
 // Called by every thread of a wave with (j = sorted position in the group,
 // key, val, valid, hp = head position of j's run, end = j ends its run).
 __device__ __forceinline__ void emit_sorted(const Ctx& c, uint32_t slot, uint32_t s, uint32_t j, uint32_t v,
-                                            bool valid, uint32_t hp, bool end, uint32_t& runs_acc)
+                                            bool valid, uint32_t hp, bool end, uint32_t& runs_acc, uint32_t n,
+                                            const uint8_t* blk)
 {
     const uint64_t so = (uint64_t)slot * c.scr.stride;
     if (valid) {
         c.scr.SA[so + s + j] = v;
+        c.scr.LL[so + s + j] = blk[v ? v - 1 : n - 1];   // last column (bz:compress.c:166-168)
         if (c.mode) c.scr.RK[so + v] = s + hp;
         if (v == 0) c.blocks[c.b0 + slot].orig_ptr = s + j;
     }
@@ -486,7 +496,9 @@ __global__ void __launch_bounds__(256) k3_sort_w(Ctx c, const uint64_t* __restri
     const bool end = valid && ((uint32_t)lane + 1 == m || skey[wid][lane + 1] != key);
     const uint32_t hp = wave_incl_scan_max<uint32_t>(head ? (uint32_t)lane : 0u);
     uint32_t runs = 0;
-    emit_sorted(c, slot, s, (uint32_t)lane, val, valid, hp, end, runs);
+    const uint32_t bn = c.blocks[c.b0 + slot].n;
+    emit_sorted(c, slot, s, (uint32_t)lane, val, valid, hp, end, runs, bn,
+                c.blkbytes + (uint64_t)(c.b0 + slot) * c.stride);
     if (c.mode && lane == 0) atomicAdd(&c.L.runs[slot], runs);
 }
 
@@ -765,12 +777,14 @@ __global__ void __launch_bounds__(256) k3_sort_lds(Ctx c, const uint64_t* __rest
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     gsync<NW>();
     uint32_t runs = 0;
+    const uint32_t bn = c.blocks[c.b0 + slot].n;
+    const uint8_t* blk = c.blkbytes + (uint64_t)(c.b0 + slot) * c.stride;
 #pragma unroll
     for (int e = 0; e < E; ++e) {
         const uint32_t j = (uint32_t)(wid * 64 * E + e * 64 + lane);
         const bool valid = j < m;
         const bool end = valid && (!ties || j + 1 == m || ((xk[j + 1] ^ k[e]) & KMASK) != 0);
-        emit_sorted(c, slot, s, j, v[e], valid, hp[e], end, runs);
+        emit_sorted(c, slot, s, j, v[e], valid, hp[e], end, runs, bn, blk);
     }
     if (c.mode && lane == 0 && runs) atomicAdd(&c.L.runs[slot], runs);
 }

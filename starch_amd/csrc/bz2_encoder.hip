@@ -156,16 +156,16 @@ void Encoder::plan(const uint8_t* d_text, const std::vector<StreamIn>& streams, 
     uint8_t* d_sel = b_sel.as<uint8_t>((uint64_t)nb * 2 * kMaxSelectors);
     uint32_t* d_gbits = b_gbits.as<uint32_t>((uint64_t)nb * kMaxSelectors);
     HIP_CHECK(hipMemGetInfo(&free_b, &total_b));
-    const uint64_t per_slot = blk_stride_ * 40ull;
+    const uint64_t per_slot = blk_stride_ * 41ull;       // 40 B of sort scratch + 1 B last column
     uint64_t max_batch = std::max<uint64_t>(1, (uint64_t)(free_b * 0.45) / per_slot);
     uint32_t batch = (uint32_t)std::min<uint64_t>({(uint64_t)nb, max_batch, 2048ull});
     if (b_bwt.cap < batch * per_slot) {
         // allocate the whole batch scratch once
-        b_bwt.get(batch * per_slot);
+        b_bwt.get(batch * per_slot + 4096);
     }
     BwtScratch scr;
     {
-        uint8_t* base = static_cast<uint8_t*>(b_bwt.get(batch * per_slot));
+        uint8_t* base = static_cast<uint8_t*>(b_bwt.get(batch * per_slot + 4096));   // + tail pad for line reads
         uint64_t S = blk_stride_;
         scr.stride = S;
         scr.K = reinterpret_cast<uint64_t*>(base);
@@ -176,6 +176,7 @@ void Encoder::plan(const uint8_t* d_text, const std::vector<StreamIn>& streams, 
         scr.RK = scr.SA + S * batch;
         scr.U = scr.RK + S * batch;
         scr.U2 = scr.U + S * batch;
+        scr.LL = reinterpret_cast<uint8_t*>(scr.U2 + S * batch);
     }
     unsigned long long* d_stats = reinterpret_cast<unsigned long long*>(d_scal);
     HIP_CHECK(hipMemsetAsync(d_stats, 0, 4 * sizeof(uint64_t), st));
@@ -188,8 +189,10 @@ void Encoder::plan(const uint8_t* d_text, const std::vector<StreamIn>& streams, 
             // STARCH_BWT=lsd selects the one-workgroup-per-block prefix-doubling sort of
             // bz2_bwt.hip (kept as an independent implementation for cross-checks)
             static const bool lsd = [] { const char* e = getenv("STARCH_BWT"); return e && !strcmp(e, "lsd"); }();
-            if (lsd) launch_bwt(d_blocks, b0, cnt, d_blkbytes, blk_stride_, scr, d_stats, st);
-            else launch_bwt3(d_blocks, b0, cnt, d_blkbytes, blk_stride_, scr, b_bwt3, h_ctr_.get(), d_stats, st);
+            if (lsd) {
+                launch_bwt(d_blocks, b0, cnt, d_blkbytes, blk_stride_, scr, d_stats, st);
+                launch_last_col(d_blocks, b0, nullptr, cnt, d_blkbytes, blk_stride_, scr, st);
+            } else launch_bwt3(d_blocks, b0, cnt, d_blkbytes, blk_stride_, scr, b_bwt3, h_ctr_.get(), d_stats, st);
             HIP_CHECK(hipMemcpyAsync(hb.data() + b0, d_blocks + b0, cnt * sizeof(BlockDesc), hipMemcpyDeviceToHost,
                                      st));
             HIP_CHECK(hipStreamSynchronize(st));
@@ -200,6 +203,7 @@ void Encoder::plan(const uint8_t* d_text, const std::vector<StreamIn>& streams, 
                 HIP_CHECK(hipMemcpyAsync(d_which, which.data(), which.size() * sizeof(uint32_t),
                                          hipMemcpyHostToDevice, st));
                 launch_fallback(d_blocks, b0, d_which, (uint32_t)which.size(), d_blkbytes, blk_stride_, scr, st);
+                launch_last_col(d_blocks, b0, d_which, (uint32_t)which.size(), d_blkbytes, blk_stride_, scr, st);
                 if (stats) stats->periodic_blocks += which.size();
             }
         }

@@ -1,26 +1,32 @@
-// starch_amd/csrc/bz2_mtf.hip -- last column, move-to-front and RUNA/RUNB
-// coding on MI355X (restates makeMaps_e + generateMTFValues,
-// bz:compress.c:105-231).
+// starch_amd/csrc/bz2_mtf.hip -- move-to-front and RUNA/RUNB coding on MI355X
+// (restates makeMaps_e + generateMTFValues, bz:compress.c:105-231).
 //
-// One 1024-thread workgroup per block, the block split into C contiguous
-// chunks.  MTF is made parallel by the chunk decomposition
+// Input: the block's last column, written by the block sort next to SA
+// (BwtScratch::LL, raw bytes block[(ptr[i]-1) mod n]); mapped to sequence
+// symbols (makeMaps_e) through an LDS table.
+//
+// One 1024-thread workgroup per block, the block split into 1024 contiguous
+// chunks of 128-byte lines.  MTF is made parallel by the chunk decomposition
 //     state(c+1) = local(c) ++ (state(c) \ local(c)),
 // where local(c) lists chunk c's symbols by last occurrence (most recent
-// first).  The map L -> local ++ (L \ local) composes associatively, so every
-// chunk's start state is an exclusive scan over chunks.  Alphabets of <= 16
-// symbols (BED3 transforms) keep the whole list as 16 nibbles of a u64 in a
-// register (C = 1024 chunks): finding a symbol is a SWAR zero-nibble search
-// and the move-to-front is three masks and a shift.  Larger alphabets use
-// byte lists in LDS (C = 256).  The zero runs of the index stream are then
-// coded in bijective base 2 (RUNA = 0, RUNB = 1); a run may span chunks, so
-// per-chunk (leading zeros, trailing zeros, all-zero, interior symbols)
-// summaries are scanned once to place every chunk's output.
+// first); the map composes associatively, so every chunk's start state is an
+// exclusive scan.  Alphabets of <= 16 symbols (BED3 transforms) keep the list
+// as 16 nibbles of a u64 in a register: finding a symbol is a SWAR zero-nibble
+// search and the move-to-front three masks and a shift.  Each lane reads its
+// chunk as whole 128-byte lines (8 x 16-B loads), so every line is fetched
+// once; the backward pass that builds local(c) stops as soon as all symbols
+// of the block have been seen.  Zero runs may cross chunks; the
+// (leading zeros, trailing zeros, inner outputs) summaries form a monoid whose
+// scan places every chunk's output, and the MTF is simply re-run to emit
+// (cheaper than storing the index stream).  Larger alphabets (nInUse > 16)
+// keep byte lists in LDS (256 chunks, sequential start states).
 #include "bz2_bwt.hpp"
 
 namespace bz {
 
 constexpr int MT = 1024;
 constexpr int NCH_BIG = 256;
+constexpr uint32_t LINE = 128;
 
 struct NibState {          // transform L -> list ++ (L \ set)
     uint64_t list;         // nibble i = i-th symbol
@@ -48,245 +54,394 @@ __device__ __forceinline__ uint64_t lowmask4(uint32_t k)   // k nibbles
 
 __device__ __forceinline__ uint32_t nsym_run(uint32_t z) { return z ? (31 - __clz(z + 1)) : 0; }
 
-struct ChunkSum {
-    uint32_t lz, tz, len, inner;   // leading/trailing zero counts, length, output symbols after the first non-zero
-    uint32_t has_nz;
-    uint32_t zin;                  // zeros entering the chunk (filled by the scan)
-    uint32_t out;                  // output offset (filled by the scan)
-    uint32_t pad;
+// zero-run summary of a symbol range (monoid, applied left to right)
+struct RunSum {
+    uint32_t nz;      // has a non-zero MTF index
+    uint32_t lz;      // leading zeros (all zeros: the length)
+    uint32_t tz;      // trailing zeros
+    uint32_t inner;   // outputs after the first non-zero symbol, trailing run excluded
 };
 
-// NIB: alphabets <= 16 (register nibble lists); !NIB: byte lists in LDS.  A
-// block is handled by exactly one of the two instantiations.
-template <bool NIB>
-__global__ void __launch_bounds__(MT) k_mtf(BlockDesc* __restrict__ blocks, uint32_t b0,
-                                             const uint8_t* __restrict__ blkbytes, uint64_t stride, BwtScratch scr,
-                                             uint16_t* __restrict__ mtfv_all, uint64_t mtf_stride,
-                                             Tables* __restrict__ tabs)
+__device__ __forceinline__ RunSum run_compose(const RunSum& a, const RunSum& b)
 {
-    constexpr uint32_t C = NIB ? MT : NCH_BIG;
-    constexpr int NF = 4;                      // frequency histogram copies
-    __shared__ ChunkSum cs_sh[C];
+    RunSum r;
+    if (!a.nz) {
+        r.nz = b.nz; r.lz = a.lz + b.lz; r.tz = b.tz; r.inner = b.inner;
+    } else if (!b.nz) {
+        r.nz = 1; r.lz = a.lz; r.tz = a.tz + b.lz; r.inner = a.inner;
+    } else {
+        r.nz = 1; r.lz = a.lz; r.tz = b.tz; r.inner = a.inner + nsym_run(a.tz + b.lz) + 1 + b.inner;
+    }
+    return r;
+}
+
+__device__ __forceinline__ RunSum shfl_up_rs(const RunSum& v, int d)
+{
+    RunSum r;
+    r.nz = __shfl_up(v.nz, d, 64);
+    r.lz = __shfl_up(v.lz, d, 64);
+    r.tz = __shfl_up(v.tz, d, 64);
+    r.inner = __shfl_up(v.inner, d, 64);
+    return r;
+}
+
+// one MTF step on the nibble list; returns the index of s
+__device__ __forceinline__ uint32_t nib_mtf(uint64_t& L, uint32_t s)
+{
+    const uint64_t x = L ^ (0x1111111111111111ull * s);
+    const uint64_t t = x | (x >> 1) | (x >> 2) | (x >> 3);
+    const uint64_t zn = ~t & 0x1111111111111111ull;
+    const uint32_t k = (uint32_t)__builtin_ctzll(zn) >> 2;
+    L = (L & ~lowmask4(k + 1)) | ((L & lowmask4(k)) << 4) | (uint64_t)s;
+    return k;
+}
+
+// Visit the bytes of one 128-byte line (all eight 16-B loads issued first, so
+// the line is fetched once) as f(offset, byte); eight explicit pieces keep
+// every index a compile-time constant (no scratch arrays).
+template <bool FWD, class F>
+__device__ __forceinline__ void piece(const uint4 v, int base, F& f)
+{
+    const uint32_t w[4] = {v.x, v.y, v.z, v.w};
+#pragma unroll
+    for (int kk = 0; kk < 16; ++kk) {
+        const int k = FWD ? kk : 15 - kk;
+        f(base + k, (w[k >> 2] >> (8 * (k & 3))) & 0xffu);
+    }
+}
+
+template <bool FWD, class F>
+__device__ __forceinline__ void visit_line(const uint8_t* p, F&& f)
+{
+    const uint4* q = reinterpret_cast<const uint4*>(p);
+    const uint4 v0 = q[0], v1 = q[1], v2 = q[2], v3 = q[3], v4 = q[4], v5 = q[5], v6 = q[6], v7 = q[7];
+    if (FWD) {
+        piece<FWD>(v0, 0, f); piece<FWD>(v1, 16, f); piece<FWD>(v2, 32, f); piece<FWD>(v3, 48, f);
+        piece<FWD>(v4, 64, f); piece<FWD>(v5, 80, f); piece<FWD>(v6, 96, f); piece<FWD>(v7, 112, f);
+    } else {
+        piece<FWD>(v7, 112, f); piece<FWD>(v6, 96, f); piece<FWD>(v5, 80, f); piece<FWD>(v4, 64, f);
+        piece<FWD>(v3, 48, f); piece<FWD>(v2, 32, f); piece<FWD>(v1, 16, f); piece<FWD>(v0, 0, f);
+    }
+}
+
+// u16 output through a 128-bit shift register: whole 16-byte stores once the
+// write position is 8-aligned, scalar stores at the two ends of the chunk.
+struct Out16 {
+    uint16_t* base;
+    uint32_t o;       // next index
+    uint32_t o_al;    // first 8-aligned index at or after the chunk's first output
+    uint64_t lo, hi;
+    __device__ __forceinline__ void init(uint16_t* b, uint32_t start)
+    {
+        base = b; o = start; o_al = (start + 7u) & ~7u; lo = 0; hi = 0;
+    }
+    __device__ __forceinline__ void put(uint32_t sym)
+    {
+        if (o < o_al) {
+            base[o] = (uint16_t)sym;
+        } else {
+            lo = (lo >> 16) | (hi << 48);
+            hi = (hi >> 16) | ((uint64_t)sym << 48);
+            if ((o & 7u) == 7u) {
+                *reinterpret_cast<uint4*>(base + (o - 7u)) =
+                    make_uint4((uint32_t)lo, (uint32_t)(lo >> 32), (uint32_t)hi, (uint32_t)(hi >> 32));
+            }
+        }
+        ++o;
+    }
+    __device__ __forceinline__ void flush()
+    {
+        if (o <= o_al) return;
+        const uint32_t k = o & 7u;               // symbols held: the top k of the register
+        for (uint32_t i = 0; i < k; ++i) {
+            const uint32_t bit = 128u - 16u * k + 16u * i;
+            const uint32_t v = bit >= 64 ? (uint32_t)(hi >> (bit - 64)) : (uint32_t)((lo >> bit) | (bit ? (hi << (64 - bit)) : 0));
+            base[(o & ~7u) + i] = (uint16_t)v;
+        }
+    }
+};
+
+__device__ __forceinline__ void put_run(Out16& out, uint32_t z)   // bijective base 2: RUNA = 0, RUNB = 1
+{
+    while (z) {
+        const uint32_t d = ((z - 1) & 1u) ? 1u : 0u;
+        out.put(d);
+        z = (z - (d + 1)) >> 1;
+    }
+}
+
+__global__ void __launch_bounds__(MT) k_mtf_nib(BlockDesc* __restrict__ blocks, uint32_t b0,
+                                                 const uint8_t* __restrict__ LL, uint64_t ll_stride,
+                                                 uint16_t* __restrict__ mtfv_all, uint64_t mtf_stride)
+{
+    __shared__ NibState nst[MT];
+    __shared__ RunSum wsum[MT / 64];
+    __shared__ uint8_t seq[256];
+    __shared__ RunSum total_sh;
+
+    const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
+    const uint32_t slot = blockIdx.x;
+    const uint32_t b = b0 + slot;
+    const uint32_t n = blocks[b].n;
+    const uint32_t nin = blocks[b].n_in_use;
+    if (nin > 16) return;                       // uniform per workgroup: k_mtf_big
+    if (tid < 256) {                            // makeMaps_e: unseqToSeq
+        uint32_t c = tid, below = 0;
+        for (uint32_t j = 0; j < (c >> 5); ++j) below += __popc(blocks[b].in_use[j]);
+        below += __popc(blocks[b].in_use[c >> 5] & ((1u << (c & 31)) - 1u));
+        seq[c] = (uint8_t)below;
+    }
+    __syncthreads();
+    const uint8_t* ll = LL + (uint64_t)slot * ll_stride;
+    uint16_t* mtfv = mtfv_all + (uint64_t)b * mtf_stride;
+    const uint32_t csz = ((n + MT - 1) / MT + LINE - 1) & ~(LINE - 1);
+    const uint32_t a = tid * csz;
+    const uint32_t e = a + csz < n ? a + csz : n;
+    const bool mine = a < e;
+
+    // ---- pass 1: local recency list, backward, stop once every symbol is seen ----
+    NibState loc;
+    loc.list = 0; loc.set = 0; loc.cnt = 0;
+    if (mine) {
+        for (uint32_t j0 = a + ((e - 1 - a) & ~(LINE - 1));; j0 -= LINE) {
+            const uint32_t lim = e - j0;
+            visit_line<false>(ll + j0, [&](int k, uint32_t byte) {
+                if ((uint32_t)k < lim) {
+                    const uint32_t s = seq[byte];
+                    if (!((loc.set >> s) & 1u)) {
+                        loc.set |= 1u << s;
+                        loc.list |= (uint64_t)s << (4 * loc.cnt);
+                        ++loc.cnt;
+                    }
+                }
+            });
+            if (loc.cnt == nin || j0 == a) break;
+        }
+    }
+    nst[tid] = loc;
+    __syncthreads();
+    for (int d = 1; d < MT; d <<= 1) {          // inclusive scan of the composition
+        NibState v = (tid >= d) ? nib_compose(nst[tid - d], nst[tid]) : nst[tid];
+        __syncthreads();
+        nst[tid] = v;
+        __syncthreads();
+    }
+    NibState ident;
+    ident.list = 0;
+    for (uint32_t i = 0; i < nin; ++i) ident.list |= (uint64_t)i << (4 * i);
+    ident.set = (1u << nin) - 1u;
+    ident.cnt = nin;
+    const uint64_t L0 = (tid ? nib_compose(ident, nst[tid - 1]) : ident).list;
+
+    // ---- pass 2: zero-run summary of the chunk's MTF indices ----
+    RunSum rs;
+    rs.nz = 0; rs.lz = 0; rs.tz = 0; rs.inner = 0;
+    if (mine) {
+        uint64_t L = L0;
+        uint32_t z = 0;
+        for (uint32_t j0 = a; j0 < e; j0 += LINE) {
+            const uint32_t lim = e - j0;
+            visit_line<true>(ll + j0, [&](int k, uint32_t byte) {
+                if ((uint32_t)k < lim) {
+                    const uint32_t x = nib_mtf(L, seq[byte]);
+                    if (x == 0) {
+                        ++z;
+                    } else {
+                        if (!rs.nz) { rs.lz = z; rs.nz = 1; } else { rs.inner += 1 + nsym_run(z); }
+                        z = 0;
+                    }
+                }
+            });
+        }
+        if (!rs.nz) rs.lz = z; else rs.tz = z;
+    }
+    // ---- exclusive scan of the summaries ----
+    RunSum inc = rs;
+#pragma unroll
+    for (int d = 1; d < 64; d <<= 1) {
+        const RunSum o = shfl_up_rs(inc, d);
+        if (lane >= d) inc = run_compose(o, inc);
+    }
+    if (lane == 63) wsum[wid] = inc;
+    __syncthreads();
+    RunSum pre;
+    pre.nz = 0; pre.lz = 0; pre.tz = 0; pre.inner = 0;
+    for (int w = 0; w < wid; ++w) pre = run_compose(pre, wsum[w]);
+    RunSum ex = shfl_up_rs(inc, 1);
+    if (lane == 0) { ex.nz = 0; ex.lz = 0; ex.tz = 0; ex.inner = 0; }
+    ex = run_compose(pre, ex);
+    if (tid == MT - 1) total_sh = run_compose(ex, rs);
+    const uint32_t zin = ex.nz ? ex.tz : ex.lz;
+    const uint32_t obase = ex.nz ? nsym_run(ex.lz) + 1 + ex.inner : 0;
+
+    // ---- pass 3: re-run the MTF and emit ----
+    if (mine) {
+        Out16 out;
+        out.init(mtfv, obase);
+        uint64_t L = L0;
+        uint32_t z = zin;
+        for (uint32_t j0 = a; j0 < e; j0 += LINE) {
+            const uint32_t lim = e - j0;
+            visit_line<true>(ll + j0, [&](int k, uint32_t byte) {
+                if ((uint32_t)k < lim) {
+                    const uint32_t x = nib_mtf(L, seq[byte]);
+                    if (x == 0) {
+                        ++z;
+                    } else {
+                        put_run(out, z);
+                        out.put(x + 1);
+                        z = 0;
+                    }
+                }
+            });
+        }
+        out.flush();
+    }
+    __syncthreads();
+    if (tid == 0) {
+        const RunSum T = total_sh;
+        uint32_t z = T.nz ? T.tz : T.lz;
+        uint32_t o = T.nz ? nsym_run(T.lz) + 1 + T.inner : 0;
+        while (z) {
+            const uint32_t d = ((z - 1) & 1u) ? 1u : 0u;
+            mtfv[o++] = (uint16_t)d;
+            z = (z - (d + 1)) >> 1;
+        }
+        mtfv[o++] = (uint16_t)(nin + 1);       // EOB
+        blocks[b].n_mtf = o;
+    }
+}
+
+// ---- alphabets > 16: byte lists in LDS, 256 chunks; also produces mtfFreq ----
+__global__ void __launch_bounds__(MT) k_mtf_big(BlockDesc* __restrict__ blocks, uint32_t b0,
+                                                 const uint8_t* __restrict__ LL, uint64_t ll_stride,
+                                                 uint8_t* __restrict__ scratch, uint64_t scratch_stride,
+                                                 uint16_t* __restrict__ mtfv_all, uint64_t mtf_stride,
+                                                 Tables* __restrict__ tabs)
+{
+    constexpr uint32_t C = NCH_BIG;
+    constexpr int NF = 4;
+    __shared__ RunSum cs_sh[C];
     __shared__ uint8_t seq[256];
     __shared__ uint32_t freq[NF][258];
     __shared__ uint32_t scan_sh[MT / 64 + 1];
     __shared__ uint32_t tail[2];
+    __shared__ uint8_t lst[256 * NCH_BIG];   // [pos][chunk]
+    __shared__ uint32_t seen[NCH_BIG][8];
+    __shared__ uint8_t st[256], st2[256], fl[256];
+    __shared__ uint32_t lcnt[NCH_BIG];
+    __shared__ uint32_t zin_sh[C], out_sh[C];
 
     const int tid = threadIdx.x;
     const uint32_t slot = blockIdx.x;
     const uint32_t b = b0 + slot;
     const uint32_t n = blocks[b].n;
-    const uint8_t* blk = blkbytes + (uint64_t)b * stride;
-    const uint64_t so = slot * scr.stride;
-    const uint32_t* SA = scr.SA + so;
-    uint8_t* ll = reinterpret_cast<uint8_t*>(scr.K + so);
-    uint8_t* idx = reinterpret_cast<uint8_t*>(scr.K2 + so);
-    uint8_t* locl = reinterpret_cast<uint8_t*>(scr.V2 + so);
-    uint8_t* sstate = reinterpret_cast<uint8_t*>(scr.U2 + so);
-    uint16_t* mtfv = mtfv_all + (uint64_t)b * mtf_stride;
-
-    if (tid < 256) {   // makeMaps_e: unseqToSeq
-        uint32_t c = tid;
-        uint32_t below = 0;
+    const uint32_t nin = blocks[b].n_in_use;
+    if (nin <= 16) return;
+    if (tid < 256) {
+        uint32_t c = tid, below = 0;
         for (uint32_t j = 0; j < (c >> 5); ++j) below += __popc(blocks[b].in_use[j]);
         below += __popc(blocks[b].in_use[c >> 5] & ((1u << (c & 31)) - 1u));
         seq[c] = (uint8_t)below;
     }
     for (int i = tid; i < NF * 258; i += MT) (&freq[0][0])[i] = 0;
-    const uint32_t nin = blocks[b].n_in_use;
-    if (NIB != (nin <= 16)) return;            // uniform per workgroup
-    __syncthreads();
-    for (uint32_t j = tid; j < n; j += MT) {   // last column (bz:compress.c:166-168)
-        uint32_t p = SA[j];
-        p = p ? p - 1 : n - 1;
-        ll[j] = seq[blk[p]];
-    }
-    __syncthreads();
-
-    // chunks are 16-byte aligned so every lane moves its bytes with 16-B loads
-    const uint32_t csz = ((n + C - 1) / C + 15u) & ~15u;
+    const uint8_t* ll = LL + (uint64_t)slot * ll_stride;
+    uint8_t* idx = scratch + (uint64_t)slot * scratch_stride;            // MTF indices
+    uint8_t* locl = idx + ((n + 255u) & ~255u);                          // per-chunk local lists
+    uint8_t* sstate = locl + 256ull * C;                                 // per-chunk start states
+    uint16_t* mtfv = mtfv_all + (uint64_t)b * mtf_stride;
+    const uint32_t csz = (n + C - 1) / C;
     const uint32_t a = tid * csz;
     uint32_t e = a + csz;
     if (e > n) e = n;
     const bool mine = (uint32_t)tid < C && a < e;
-
-    if constexpr (NIB) {
-        __shared__ NibState nst[MT];
-        // local recency list of this chunk
-        NibState loc;
-        loc.list = 0; loc.set = 0; loc.cnt = 0;
-        if (mine) {
-            for (uint32_t j0 = a + ((e - a - 1) & ~15u);; j0 -= 16) {
-                const uint4 v = *reinterpret_cast<const uint4*>(ll + j0);
-                const uint32_t w[4] = {v.x, v.y, v.z, v.w};
-#pragma unroll
-                for (int k = 15; k >= 0; --k) {
-                    if (j0 + k < e) {
-                        uint32_t s = (w[k >> 2] >> (8 * (k & 3))) & 0xffu;
-                        if (!((loc.set >> s) & 1u)) {
-                            loc.set |= 1u << s;
-                            loc.list |= (uint64_t)s << (4 * loc.cnt);
-                            ++loc.cnt;
-                        }
-                    }
-                }
-                if (j0 == a) break;
-            }
-        }
-        nst[tid] = loc;
-        __syncthreads();
-        for (int d = 1; d < MT; d <<= 1) {      // inclusive scan of the composition
-            NibState v = (tid >= d) ? nib_compose(nst[tid - d], nst[tid]) : nst[tid];
-            __syncthreads();
-            nst[tid] = v;
-            __syncthreads();
-        }
-        // start state = (exclusive prefix) applied to the identity list 0..nin-1
-        NibState ident;
-        ident.list = 0;
-        for (uint32_t i = 0; i < nin; ++i) ident.list |= (uint64_t)i << (4 * i);
-        ident.set = nin >= 32 ? 0xffffffffu : ((1u << nin) - 1u);
-        ident.cnt = nin;
-        NibState pre = tid ? nib_compose(ident, nst[tid - 1]) : ident;
-        uint64_t L = pre.list;
-        ChunkSum cs;
-        cs.lz = 0; cs.tz = 0; cs.len = e > a ? e - a : 0; cs.inner = 0; cs.has_nz = 0; cs.zin = 0; cs.out = 0;
-        if (mine) {
-            uint32_t z = 0;
-            for (uint32_t j0 = a; j0 < e; j0 += 16) {
-                const uint4 v = *reinterpret_cast<const uint4*>(ll + j0);
-                const uint32_t w[4] = {v.x, v.y, v.z, v.w};
-                uint32_t o[4] = {0, 0, 0, 0};
-#pragma unroll
-                for (int q = 0; q < 16; ++q) {
-                    if (j0 + q < e) {
-                        const uint32_t s = (w[q >> 2] >> (8 * (q & 3))) & 0xffu;
-                        const uint64_t x = L ^ (0x1111111111111111ull * s);
-                        const uint64_t t = x | (x >> 1) | (x >> 2) | (x >> 3);
-                        const uint64_t zn = ~t & 0x1111111111111111ull;
-                        const uint32_t k = (uint32_t)__builtin_ctzll(zn) >> 2;
-                        L = (L & ~lowmask4(k + 1)) | ((L & lowmask4(k)) << 4) | (uint64_t)s;
-                        o[q >> 2] |= k << (8 * (q & 3));
-                        if (k == 0) {
-                            ++z;
-                        } else {
-                            if (!cs.has_nz) { cs.lz = z; cs.has_nz = 1; } else { cs.inner += 1 + nsym_run(z); }
-                            z = 0;
-                        }
-                    }
-                }
-                *reinterpret_cast<uint4*>(idx + j0) = make_uint4(o[0], o[1], o[2], o[3]);
-            }
-            if (!cs.has_nz) cs.lz = z;
-            cs.tz = z;
-        }
-        if ((uint32_t)tid < C) cs_sh[tid] = cs;
-    } else {
-        // ---- alphabets > 16: byte lists in LDS, 256 chunks ----
-        __shared__ uint8_t lst[256 * NCH_BIG];   // [pos][chunk]
-        __shared__ uint32_t seen[NCH_BIG][8];
-        __shared__ uint8_t st[256], st2[256], fl[256];
-        __shared__ uint32_t lcnt[NCH_BIG];
-        if (tid < NCH_BIG) for (int j = 0; j < 8; ++j) seen[tid][j] = 0;
-        __syncthreads();
-        if ((uint32_t)tid < C) {
-            uint32_t cnt = 0;
-            uint8_t* out = locl + (uint64_t)tid * 256;
-            for (uint32_t j = e; j > a && a < e; --j) {
-                uint32_t s = ll[j - 1];
-                uint32_t bit = 1u << (s & 31);
-                if (!(seen[tid][s >> 5] & bit)) { seen[tid][s >> 5] |= bit; out[cnt++] = (uint8_t)s; }
-            }
-            lcnt[tid] = cnt;
-        }
-        if (tid < 256) { st[tid] = (uint8_t)tid; fl[tid] = 0; }
-        __syncthreads();
-        for (uint32_t c = 0; c < C; ++c) {   // list state at each chunk start (sequential)
-            const uint32_t cnt = lcnt[c];
-            const uint8_t* lc = locl + (uint64_t)c * 256;
-            if (tid < (int)nin) sstate[(uint64_t)c * 256 + tid] = st[tid];
-            if (tid < (int)cnt) fl[lc[tid]] = 1;
-            __syncthreads();
-            uint32_t keep = (tid < (int)nin && !fl[st[tid]]) ? 1u : 0u;
-            uint32_t pre = block_excl_scan_add<uint32_t>(keep, scan_sh, (uint32_t*)nullptr);
-            if (keep) st2[cnt + pre] = st[tid];
-            if (tid < (int)cnt) st2[tid] = lc[tid];
-            __syncthreads();
-            if (tid < (int)nin) st[tid] = st2[tid];
-            if (tid < (int)cnt) fl[lc[tid]] = 0;
-            __syncthreads();
-        }
-        ChunkSum cs;
-        cs.lz = 0; cs.tz = 0; cs.len = e > a ? e - a : 0; cs.inner = 0; cs.has_nz = 0; cs.zin = 0; cs.out = 0;
-        if (mine) {
-            for (uint32_t k = 0; k < nin; ++k) lst[k * NCH_BIG + tid] = sstate[(uint64_t)tid * 256 + k];
-            uint32_t z = 0;
-            for (uint32_t j = a; j < e; ++j) {
-                uint8_t s = ll[j];
-                uint8_t cur = lst[tid];
-                uint32_t k = 0;
-                if (cur != s) {   // bz:compress.c:197-211
-                    uint8_t carry_v = cur;
-                    k = 1;
-                    for (;;) {
-                        uint8_t nxt = lst[k * NCH_BIG + tid];
-                        lst[k * NCH_BIG + tid] = carry_v;
-                        if (nxt == s || k >= 255) break;
-                        carry_v = nxt;
-                        ++k;
-                    }
-                    lst[tid] = s;
-                }
-                idx[j] = (uint8_t)k;
-                if (k == 0) { ++z; continue; }
-                if (!cs.has_nz) { cs.lz = z; cs.has_nz = 1; } else { cs.inner += 1 + nsym_run(z); }
-                z = 0;
-            }
-            if (!cs.has_nz) cs.lz = z;
-            cs.tz = z;
-        }
-        if ((uint32_t)tid < C) cs_sh[tid] = cs;
-    }
+    if (tid < NCH_BIG) for (int j = 0; j < 8; ++j) seen[tid][j] = 0;
     __syncthreads();
-    // ---- place every chunk's output: zeros entering each chunk, output offsets ----
-    if (tid == 0) {
-        uint32_t zin = 0, out = 0;
-        for (uint32_t c = 0; c < C; ++c) {
-            ChunkSum& s = cs_sh[c];
-            s.zin = zin;
-            s.out = out;
-            if (s.has_nz) {
-                out += 1 + nsym_run(zin + s.lz) + s.inner;
-                zin = s.tz;
-            } else {
-                zin += s.len;
-            }
+    if ((uint32_t)tid < C) {
+        uint32_t cnt = 0;
+        uint8_t* out = locl + (uint64_t)tid * 256;
+        for (uint32_t j = e; j > a && a < e; --j) {
+            uint32_t s = seq[ll[j - 1]];
+            uint32_t bit = 1u << (s & 31);
+            if (!(seen[tid][s >> 5] & bit)) { seen[tid][s >> 5] |= bit; out[cnt++] = (uint8_t)s; }
+            if (cnt == nin) break;
         }
-        tail[0] = zin;     // zeros after the last non-zero
-        tail[1] = out;
+        lcnt[tid] = cnt;
+    }
+    if (tid < 256) { st[tid] = (uint8_t)tid; fl[tid] = 0; }
+    __syncthreads();
+    for (uint32_t c = 0; c < C; ++c) {   // list state at each chunk start (sequential)
+        const uint32_t cnt = lcnt[c];
+        const uint8_t* lc = locl + (uint64_t)c * 256;
+        if (tid < (int)nin) sstate[(uint64_t)c * 256 + tid] = st[tid];
+        if (tid < (int)cnt) fl[lc[tid]] = 1;
+        __syncthreads();
+        uint32_t keep = (tid < (int)nin && !fl[st[tid]]) ? 1u : 0u;
+        uint32_t pre = block_excl_scan_add<uint32_t>(keep, scan_sh, (uint32_t*)nullptr);
+        if (keep) st2[cnt + pre] = st[tid];
+        if (tid < (int)cnt) st2[tid] = lc[tid];
+        __syncthreads();
+        if (tid < (int)nin) st[tid] = st2[tid];
+        if (tid < (int)cnt) fl[lc[tid]] = 0;
+        __syncthreads();
+    }
+    RunSum cs;
+    cs.nz = 0; cs.lz = 0; cs.tz = 0; cs.inner = 0;
+    if (mine) {
+        for (uint32_t k = 0; k < nin; ++k) lst[k * NCH_BIG + tid] = sstate[(uint64_t)tid * 256 + k];
+        uint32_t z = 0;
+        for (uint32_t j = a; j < e; ++j) {
+            uint8_t s = seq[ll[j]];
+            uint8_t cur = lst[tid];
+            uint32_t k = 0;
+            if (cur != s) {   // bz:compress.c:197-211
+                uint8_t carry_v = cur;
+                k = 1;
+                for (;;) {
+                    uint8_t nxt = lst[k * NCH_BIG + tid];
+                    lst[k * NCH_BIG + tid] = carry_v;
+                    if (nxt == s || k >= 255) break;
+                    carry_v = nxt;
+                    ++k;
+                }
+                lst[tid] = s;
+            }
+            idx[j] = (uint8_t)k;
+            if (k == 0) { ++z; continue; }
+            if (!cs.nz) { cs.lz = z; cs.nz = 1; } else { cs.inner += 1 + nsym_run(z); }
+            z = 0;
+        }
+        if (!cs.nz) cs.lz = z; else cs.tz = z;
+    }
+    if ((uint32_t)tid < C) cs_sh[tid] = cs;
+    __syncthreads();
+    if (tid == 0) {
+        RunSum p;
+        p.nz = 0; p.lz = 0; p.tz = 0; p.inner = 0;
+        for (uint32_t c = 0; c < C; ++c) {
+            zin_sh[c] = p.nz ? p.tz : p.lz;
+            out_sh[c] = p.nz ? nsym_run(p.lz) + 1 + p.inner : 0;
+            p = run_compose(p, cs_sh[c]);
+        }
+        tail[0] = p.nz ? p.tz : p.lz;
+        tail[1] = p.nz ? nsym_run(p.lz) + 1 + p.inner : 0;
     }
     __syncthreads();
     const int wv = (tid >> 6) & (NF - 1);
     if (mine) {
-        const ChunkSum cs = cs_sh[tid];
-        uint32_t o = cs.out;
-        uint32_t z = cs.zin;
-        for (uint32_t j0 = a; j0 < e; j0 += 16) {
-            const uint4 vv = *reinterpret_cast<const uint4*>(idx + j0);
-            const uint64_t lo = ((uint64_t)vv.y << 32) | vv.x, hi = ((uint64_t)vv.w << 32) | vv.z;
-            const uint32_t qn = (e - j0) < 16u ? (e - j0) : 16u;
-            for (uint32_t q = 0; q < qn; ++q) {
-                const uint32_t v = (uint32_t)((q < 8 ? (lo >> (8 * q)) : (hi >> (8 * (q - 8)))) & 0xffu);
-                if (v == 0) { ++z; continue; }
-                while (z) {
-                    uint32_t d = ((z - 1) & 1u) ? 1u : 0u;       // RUNB : RUNA
-                    mtfv[o++] = (uint16_t)d;
-                    atomicAdd(&freq[wv][d], 1u);
-                    z = (z - (d + 1)) >> 1;
-                }
-                mtfv[o++] = (uint16_t)(v + 1);
-                atomicAdd(&freq[wv][v + 1], 1u);
+        uint32_t o = out_sh[tid];
+        uint32_t z = zin_sh[tid];
+        for (uint32_t j = a; j < e; ++j) {
+            const uint32_t v = idx[j];
+            if (v == 0) { ++z; continue; }
+            while (z) {
+                uint32_t d = ((z - 1) & 1u) ? 1u : 0u;       // RUNB : RUNA
+                mtfv[o++] = (uint16_t)d;
+                atomicAdd(&freq[wv][d], 1u);
+                z = (z - (d + 1)) >> 1;
             }
+            mtfv[o++] = (uint16_t)(v + 1);
+            atomicAdd(&freq[wv][v + 1], 1u);
         }
     }
     __syncthreads();
@@ -310,13 +465,41 @@ __global__ void __launch_bounds__(MT) k_mtf(BlockDesc* __restrict__ blocks, uint
     }
 }
 
+// last column from SA, for blocks the batch-wide sort did not finish (periodic
+// blocks after k_fallback_exact; every block on the STARCH_BWT=lsd path)
+__global__ void k_last_col(const BlockDesc* __restrict__ blocks, uint32_t b0, const uint32_t* __restrict__ which,
+                           uint32_t nwhich, const uint8_t* __restrict__ blkbytes, uint64_t stride, BwtScratch scr)
+{
+    const uint32_t k = blockIdx.y;
+    if (k >= nwhich) return;
+    const uint32_t slot = which ? which[k] : k;
+    const uint32_t b = b0 + slot;
+    const uint32_t n = blocks[b].n;
+    const uint8_t* blk = blkbytes + (uint64_t)b * stride;
+    const uint64_t so = (uint64_t)slot * scr.stride;
+    for (uint32_t j = blockIdx.x * blockDim.x + threadIdx.x; j < n; j += gridDim.x * blockDim.x) {
+        const uint32_t p = scr.SA[so + j];
+        scr.LL[so + j] = blk[p ? p - 1 : n - 1];
+    }
+}
+
+void launch_last_col(const BlockDesc* blocks, uint32_t b0, const uint32_t* which, uint32_t nwhich,
+                     const uint8_t* blkbytes, uint64_t stride, const BwtScratch& scr, hipStream_t st)
+{
+    if (!nwhich) return;
+    hipLaunchKernelGGL(k_last_col, dim3(32, nwhich), dim3(256), 0, st, blocks, b0, which, nwhich, blkbytes, stride, scr);
+    HIP_CHECK(hipGetLastError());
+}
+
 void launch_mtf(BlockDesc* blocks, uint32_t b0, uint32_t nb, const uint8_t* blkbytes, uint64_t stride,
                 const BwtScratch& scr, uint16_t* mtfv, uint64_t mtf_stride, Tables* tabs, hipStream_t st)
 {
-    hipLaunchKernelGGL(k_mtf<true>, dim3(nb), dim3(MT), 0, st, blocks, b0, blkbytes, stride, scr, mtfv, mtf_stride,
-                       tabs);
-    hipLaunchKernelGGL(k_mtf<false>, dim3(nb), dim3(MT), 0, st, blocks, b0, blkbytes, stride, scr, mtfv, mtf_stride,
-                       tabs);
+    (void)blkbytes;
+    (void)stride;
+    hipLaunchKernelGGL(k_mtf_nib, dim3(nb), dim3(MT), 0, st, blocks, b0, scr.LL, scr.stride, mtfv, mtf_stride);
+    // large alphabets: index bytes + per-chunk lists in the (free) key scratch
+    hipLaunchKernelGGL(k_mtf_big, dim3(nb), dim3(MT), 0, st, blocks, b0, scr.LL, scr.stride,
+                       reinterpret_cast<uint8_t*>(scr.K), scr.stride * sizeof(uint64_t), mtfv, mtf_stride, tabs);
     HIP_CHECK(hipGetLastError());
 }
 

@@ -98,6 +98,7 @@ __global__ void __launch_bounds__(TT) k_tables(BlockDesc* __restrict__ blocks, u
     uint32_t* gbits = gbits_all + (uint64_t)b * kMaxSelectors;
     const uint32_t n_mtf = blocks[b].n_mtf;
     const int32_t alpha = (int32_t)blocks[b].n_in_use + 2;
+    if (alpha <= 32) return;                       // uniform: k_tables32
     const int ng = n_mtf < 200 ? 2 : n_mtf < 600 ? 3 : n_mtf < 1200 ? 4 : n_mtf < 2400 ? 5 : 6;
     const uint32_t nsel = (n_mtf + 49) / 50;
 
@@ -264,12 +265,229 @@ __global__ void __launch_bounds__(TT) k_tables(BlockDesc* __restrict__ blocks, u
     }
 }
 
+// ---------------------------------------------------------------------------
+// k_tables32: the same computation for alphabets <= 32 (every BED transform).
+// Each 50-symbol group's histogram (32 u8 counts) is built once and kept in
+// HBM; a group's cost against all six tables is then sum_v count_v * plen[v]
+// where plen packs the six code lengths in 10-bit fields of a u64 (a group
+// costs at most 50 * 17 = 850 per table, so fields never carry) -- the packed
+// cost trick of bz:compress.c:379-398 widened to six tables; the first minimum
+// wins (bz:compress.c:399-401).  Per-table symbol frequencies go to per-wave
+// LDS copies, one atomic per (group, symbol present).
+// ---------------------------------------------------------------------------
+constexpr int T32 = 1024;
+constexpr int NW32 = T32 / 64;
+
+__device__ __forceinline__ uint32_t byte_of(const uint32_t (&h)[8], int v)
+{
+    return (h[v >> 2] >> (8 * (v & 3))) & 0xffu;
+}
+
+__global__ void __launch_bounds__(T32) k_tables32(BlockDesc* __restrict__ blocks, uint32_t b0,
+                                                   const uint16_t* __restrict__ mtfv_all, uint64_t mtf_stride,
+                                                   Tables* __restrict__ tabs, uint8_t* __restrict__ sel_all,
+                                                   uint32_t* __restrict__ gbits_all, uint4* __restrict__ hist_all,
+                                                   uint64_t hist_stride)
+{
+    __shared__ HuffSmem hs;
+    __shared__ uint8_t len[6][258];
+    __shared__ uint64_t plen[32];
+    __shared__ uint32_t rf[NW32][6][32];
+    __shared__ uint32_t rfreq[6][258];
+    __shared__ uint32_t freq[258];
+    __shared__ uint32_t hl[8][T32];
+    __shared__ uint8_t sel_l[kMaxSelectors];
+    __shared__ unsigned long long hdr_bits;
+
+    const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
+    const uint32_t b = b0 + blockIdx.x;
+    const int32_t alpha = (int32_t)blocks[b].n_in_use + 2;
+    if (alpha > 32) return;                        // uniform: k_tables handles it
+    const uint16_t* mtfv = mtfv_all + (uint64_t)b * mtf_stride;
+    uint8_t* sel = sel_all + (uint64_t)b * (2 * kMaxSelectors);
+    uint8_t* selmtf = sel + kMaxSelectors;
+    uint32_t* gbits = gbits_all + (uint64_t)b * kMaxSelectors;
+    uint4* hist = hist_all + (uint64_t)blockIdx.x * hist_stride;     // [group][2] x uint4
+    const uint32_t n_mtf = blocks[b].n_mtf;
+    const int ng = n_mtf < 200 ? 2 : n_mtf < 600 ? 3 : n_mtf < 1200 ? 4 : n_mtf < 2400 ? 5 : 6;
+    const uint32_t nsel = (n_mtf + 49) / 50;
+
+    for (int i = tid; i < 258; i += T32) freq[i] = 0;
+    for (int i = tid; i < 6 * 258; i += T32) (&len[0][0])[i] = 15;   // BZ_GREATER_ICOST
+    __syncthreads();
+    // ---- per-group histograms (+ mtfFreq) ----
+    for (uint32_t g0 = 0; g0 < nsel; g0 += T32) {
+        const uint32_t g = g0 + tid;
+        uint32_t h[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+        if (g < nsel) {
+#pragma unroll
+            for (int q = 0; q < 8; ++q) hl[q][tid] = 0;
+            const uint32_t gs = g * 50;
+            const uint32_t ge = gs + 50 < n_mtf ? gs + 50 : n_mtf;
+            const uint32_t* m32 = reinterpret_cast<const uint32_t*>(mtfv + gs);   // gs even: 4-B aligned
+            for (uint32_t i = gs; i < ge; i += 2) {
+                const uint32_t w = m32[(i - gs) >> 1];
+                const uint32_t v0 = w & 0xffffu, v1 = w >> 16;
+                atomicAdd(&hl[v0 >> 2][tid], 1u << (8 * (v0 & 3)));
+                if (i + 1 < ge) atomicAdd(&hl[v1 >> 2][tid], 1u << (8 * (v1 & 3)));
+            }
+#pragma unroll
+            for (int q = 0; q < 8; ++q) h[q] = hl[q][tid];
+            hist[2 * g] = make_uint4(h[0], h[1], h[2], h[3]);
+            hist[2 * g + 1] = make_uint4(h[4], h[5], h[6], h[7]);
+        }
+        // mtfFreq: wave sums of u16 pairs, one lane adds
+#pragma unroll
+        for (int q = 0; q < 8; ++q) {
+            if (4 * q >= alpha) break;
+            uint32_t ev = h[q] & 0x00ff00ffu, od = (h[q] >> 8) & 0x00ff00ffu;
+            ev = wave_reduce_add(ev);
+            od = wave_reduce_add(od);
+            if (lane == 0) {
+                if (ev & 0xffffu) atomicAdd(&freq[4 * q], ev & 0xffffu);
+                if (od & 0xffffu) atomicAdd(&freq[4 * q + 1], od & 0xffffu);
+                if (ev >> 16) atomicAdd(&freq[4 * q + 2], ev >> 16);
+                if (od >> 16) atomicAdd(&freq[4 * q + 3], od >> 16);
+            }
+        }
+    }
+    __syncthreads();
+    if (tid == 0) {   // initial equal-frequency bands (bz:compress.c:280-317)
+        int32_t parts = ng, rem = (int32_t)n_mtf, gs = 0;
+        while (parts > 0) {
+            int32_t target = rem / parts, ge = gs - 1, acc = 0;
+            while (acc < target && ge < alpha - 1) { ++ge; acc += (int32_t)freq[ge]; }
+            if (ge > gs && parts != ng && parts != 1 && ((ng - parts) % 2 == 1)) { acc -= (int32_t)freq[ge]; --ge; }
+            for (int32_t v = 0; v < alpha; ++v) len[parts - 1][v] = (v >= gs && v <= ge) ? 0 : 15;
+            --parts;
+            gs = ge + 1;
+            rem -= acc;
+        }
+    }
+    if (tid < 258) tabs[b].freq[tid] = freq[tid];
+    __syncthreads();
+    for (int iter = 0; iter < 4; ++iter) {                         // BZ_N_ITERS
+        if (tid < alpha) {
+            uint64_t pl = 0;
+            for (int t = 0; t < 6; ++t) pl |= (uint64_t)len[t][tid] << (10 * t);
+            plen[tid] = pl;
+        }
+        for (int i = tid; i < NW32 * 6 * 32; i += T32) (&rf[0][0][0])[i] = 0;
+        __syncthreads();
+        for (uint32_t g = tid; g < nsel; g += T32) {
+            const uint4 h0 = hist[2 * g], h1 = hist[2 * g + 1];
+            const uint32_t h[8] = {h0.x, h0.y, h0.z, h0.w, h1.x, h1.y, h1.z, h1.w};
+            uint64_t cost = 0;
+#pragma unroll
+            for (int v = 0; v < 32; ++v) {
+                if (v < alpha) cost += (uint64_t)byte_of(h, v) * plen[v];
+            }
+            int bt = 0;
+            uint32_t bc = (uint32_t)cost & 1023u;
+            for (int t = 1; t < ng; ++t) {
+                const uint32_t ct = (uint32_t)(cost >> (10 * t)) & 1023u;
+                if (ct < bc) { bc = ct; bt = t; }
+            }
+            sel_l[g] = (uint8_t)bt;
+#pragma unroll
+            for (int v = 0; v < 32; ++v) {
+                if (v < alpha) {
+                    const uint32_t cnt = byte_of(h, v);
+                    if (cnt) atomicAdd(&rf[wid][bt][v], cnt);
+                }
+            }
+        }
+        __syncthreads();
+        if (tid < 6 * 32) {
+            const int t = tid >> 5, v = tid & 31;
+            uint32_t a = 0;
+            for (int w = 0; w < NW32; ++w) a += rf[w][t][v];
+            if (v < alpha) rfreq[t][v] = a;
+        }
+        __syncthreads();
+        if (tid < ng) hb_make_lengths(len[tid], rfreq[tid], alpha, 17, hs.heap[tid], hs.weight[tid], hs.parent[tid]);
+        __syncthreads();
+    }
+    for (uint32_t g = tid; g < nsel; g += T32) sel[g] = sel_l[g];
+    // selector MTF (bz:compress.c:461-478) and header size
+    if (tid == 0) {
+        uint8_t pos[6];
+        for (int i = 0; i < ng; ++i) pos[i] = (uint8_t)i;
+        uint64_t sbits = 0;
+        for (uint32_t i = 0; i < nsel; ++i) {
+            uint8_t want = sel_l[i];
+            int j = 0;
+            uint8_t carry_v = pos[0];
+            while (carry_v != want && j < 5) { ++j; uint8_t t = pos[j]; pos[j] = carry_v; carry_v = t; }
+            pos[0] = carry_v;
+            selmtf[i] = (uint8_t)j;
+            sbits += (uint64_t)j + 1;
+        }
+        uint32_t used16 = 0;
+        for (int i = 0; i < 16; ++i) {
+            uint32_t w = blocks[b].in_use[i >> 1];
+            uint32_t half = (i & 1) ? (w >> 16) : (w & 0xffffu);
+            if (half) ++used16;
+        }
+        uint64_t tbits = 0;
+        for (int t = 0; t < ng; ++t) {
+            int32_t cur = len[t][0];
+            tbits += 5;
+            for (int32_t i = 0; i < alpha; ++i) {
+                int32_t d = (int32_t)len[t][i] - cur;
+                tbits += 1 + 2 * (uint64_t)(d < 0 ? -d : d);
+                cur = len[t][i];
+            }
+        }
+        hdr_bits = 48 + 32 + 1 + 24 + 16 + 16ull * used16 + 3 + 15 + sbits + tbits;
+        blocks[b].hdr_bits = (uint32_t)hdr_bits;
+    }
+    // canonical codes (bz:huffman.c:152-166)
+    if (tid < ng) {
+        int32_t mn = 32, mx = 0;
+        for (int32_t i = 0; i < alpha; ++i) {
+            int32_t l = len[tid][i];
+            if (l > mx) mx = l;
+            if (l < mn) mn = l;
+        }
+        int32_t v = 0;
+        for (int32_t L = mn; L <= mx; ++L) {
+            for (int32_t i = 0; i < alpha; ++i) if (len[tid][i] == L) tabs[b].code[tid][i] = (uint32_t)v++;
+            v <<= 1;
+        }
+        for (int32_t i = 0; i < alpha; ++i) tabs[b].len[tid][i] = len[tid][i];
+    }
+    __syncthreads();
+    // data bits per group with the final tables
+    uint64_t local = 0;
+    for (uint32_t g = tid; g < nsel; g += T32) {
+        const uint4 h0 = hist[2 * g], h1 = hist[2 * g + 1];
+        const uint32_t h[8] = {h0.x, h0.y, h0.z, h0.w, h1.x, h1.y, h1.z, h1.w};
+        const uint8_t* L = len[sel_l[g]];
+        uint32_t bits = 0;
+#pragma unroll
+        for (int v = 0; v < 32; ++v) if (v < alpha) bits += byte_of(h, v) * L[v];
+        gbits[g] = bits;
+        local += bits;
+    }
+    local = wave_reduce_add(local);
+    if (lane == 0) atomicAdd(&hdr_bits, (unsigned long long)local);
+    __syncthreads();
+    if (tid == 0) {
+        blocks[b].bits = hdr_bits;
+        blocks[b].n_groups = (uint32_t)ng;
+        blocks[b].n_sel = nsel;
+    }
+}
+
 void launch_tables(BlockDesc* blocks, uint32_t b0, uint32_t nb, const uint16_t* mtfv, uint64_t mtf_stride,
                    Tables* tabs, uint8_t* sel, uint32_t* gbits, const BwtScratch& scr, hipStream_t st)
 {
     // per-group histograms live in the (now free) block-sort key scratch
     uint8_t* hist = reinterpret_cast<uint8_t*>(scr.K);
     const uint64_t hist_stride = scr.stride * sizeof(uint64_t);
+    hipLaunchKernelGGL(k_tables32, dim3(nb), dim3(T32), 0, st, blocks, b0, mtfv, mtf_stride, tabs, sel, gbits,
+                       reinterpret_cast<uint4*>(scr.K), hist_stride / sizeof(uint4));
     hipLaunchKernelGGL(k_tables, dim3(nb), dim3(TT), 0, st, blocks, b0, mtfv, mtf_stride, tabs, sel, gbits, hist,
                        hist_stride);
     HIP_CHECK(hipGetLastError());
