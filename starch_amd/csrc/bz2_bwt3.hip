@@ -445,13 +445,12 @@ __global__ void __launch_bounds__(LT) k3_part_l(Ctx c, const uint64_t* __restric
 // Called by every thread of a wave with (j = sorted position in the group,
 // key, val, valid, hp = head position of j's run, end = j ends its run).
 __device__ __forceinline__ void emit_sorted(const Ctx& c, uint32_t slot, uint32_t s, uint32_t j, uint32_t v,
-                                            bool valid, uint32_t hp, bool end, uint32_t& runs_acc, uint32_t n,
-                                            const uint8_t* blk)
+                                            uint32_t llb, bool valid, uint32_t hp, bool end, uint32_t& runs_acc)
 {
     const uint64_t so = (uint64_t)slot * c.scr.stride;
     if (valid) {
         c.scr.SA[so + s + j] = v;
-        c.scr.LL[so + s + j] = blk[v ? v - 1 : n - 1];   // last column (bz:compress.c:166-168)
+        c.scr.LL[so + s + j] = (uint8_t)llb;             // last column (bz:compress.c:166-168)
         if (c.mode) c.scr.RK[so + v] = s + hp;
         if (v == 0) c.blocks[c.b0 + slot].orig_ptr = s + j;
     }
@@ -483,12 +482,15 @@ __global__ void __launch_bounds__(256) k3_sort_w(Ctx c, const uint64_t* __restri
     const bool valid = (uint32_t)lane < m;
     const uint64_t k = valid ? sk[lane] : ~0ull;
     const uint32_t v = valid ? sv[lane] : 0u;
+    const uint32_t bn = c.blocks[c.b0 + slot].n;
+    const uint8_t* blk = c.blkbytes + (uint64_t)(c.b0 + slot) * c.stride;
+    const uint32_t vl = valid ? (v | ((uint32_t)blk[v ? v - 1 : bn - 1] << 20)) : 0u;   // rotation | last-column byte
     uint32_t r = 0;
     for (uint32_t j = 0; j < m; ++j) {
         const uint64_t kj = __shfl(k, (int)j, 64);
         r += (kj < k || (kj == k && (int)j < lane)) ? 1u : 0u;
     }
-    if (valid) { skey[wid][r] = k; sval[wid][r] = v; }
+    if (valid) { skey[wid][r] = k; sval[wid][r] = vl; }
     wave_sync_lds3();
     const uint64_t key = valid ? skey[wid][lane] : 0;
     const uint32_t val = valid ? sval[wid][lane] : 0;
@@ -496,9 +498,7 @@ __global__ void __launch_bounds__(256) k3_sort_w(Ctx c, const uint64_t* __restri
     const bool end = valid && ((uint32_t)lane + 1 == m || skey[wid][lane + 1] != key);
     const uint32_t hp = wave_incl_scan_max<uint32_t>(head ? (uint32_t)lane : 0u);
     uint32_t runs = 0;
-    const uint32_t bn = c.blocks[c.b0 + slot].n;
-    emit_sorted(c, slot, s, (uint32_t)lane, val, valid, hp, end, runs, bn,
-                c.blkbytes + (uint64_t)(c.b0 + slot) * c.stride);
+    emit_sorted(c, slot, s, (uint32_t)lane, val & 0xFFFFFu, val >> 20, valid, hp, end, runs);
     if (c.mode && lane == 0) atomicAdd(&c.L.runs[slot], runs);
 }
 
@@ -537,6 +537,7 @@ __global__ void __launch_bounds__(256) k3_sort_lds(Ctx c, const uint64_t* __rest
     constexpr int BPT = NBIN / T;                  // bins per thread
     constexpr uint32_t LIMIT = 256 / E;            // largest sub-bucket ranked by comparison
     __shared__ uint64_t xk_all[IPW][CAP];
+    __shared__ uint32_t vb_all[IPW][CAP];          // rotation | last-column byte << 20, by group index
     __shared__ uint32_t bst_all[IPW][NBIN + 1];   // sub-bucket starts
     __shared__ uint32_t bcur_all[IPW][NBIN];      // scatter cursors
     __shared__ uint32_t cnt_all[4][256];
@@ -561,15 +562,26 @@ __global__ void __launch_bounds__(256) k3_sort_lds(Ctx c, const uint64_t* __rest
     uint64_t k[E];
     const uint64_t k0 = sk[0];
     uint64_t diff = 0;
+    {
+        uint32_t vv[E];
 #pragma unroll
-    for (int e = 0; e < E; ++e) {
-        const uint32_t i = (uint32_t)(wid * 64 * E + e * 64 + lane);
-        if (i < m) {
-            const uint64_t x = sk[i];
-            diff |= x ^ k0;
-            k[e] = (x & KMASK) | ((uint64_t)i << KEYB);
-        } else {
-            k[e] = ~0ull;                          // pads: max key, last in stable order
+        for (int e = 0; e < E; ++e) {
+            const uint32_t i = (uint32_t)(wid * 64 * E + e * 64 + lane);
+            vv[e] = i < m ? sv[i] : 0u;
+        }
+        const uint32_t bn = c.blocks[c.b0 + slot].n;
+        const uint8_t* blk = c.blkbytes + (uint64_t)(c.b0 + slot) * c.stride;
+#pragma unroll
+        for (int e = 0; e < E; ++e) {
+            const uint32_t i = (uint32_t)(wid * 64 * E + e * 64 + lane);
+            if (i < m) {
+                const uint64_t x = sk[i];
+                diff |= x ^ k0;
+                k[e] = (x & KMASK) | ((uint64_t)i << KEYB);
+                vb_all[g][i] = vv[e] | ((uint32_t)blk[vv[e] ? vv[e] - 1 : bn - 1] << 20);
+            } else {
+                k[e] = ~0ull;                          // pads: max key, last in stable order
+            }
         }
     }
 #pragma unroll
@@ -767,24 +779,16 @@ __global__ void __launch_bounds__(256) k3_sort_lds(Ctx c, const uint64_t* __rest
             for (int e = 0; e < E; ++e) hp[e] = hp[e] > pre ? hp[e] : pre;
         }
     }
-    // gather every value before any lane overwrites the group's SA range in place
-    uint32_t v[E];
-#pragma unroll
-    for (int e = 0; e < E; ++e) {
-        const uint32_t j = (uint32_t)(wid * 64 * E + e * 64 + lane);
-        v[e] = j < m ? sv[(uint32_t)(k[e] >> KEYB)] : 0u;
-    }
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    gsync<NW>();
+    // values were loaded (and their last-column bytes gathered) before the sort;
+    // every global read of the group's SA range happened before any write
     uint32_t runs = 0;
-    const uint32_t bn = c.blocks[c.b0 + slot].n;
-    const uint8_t* blk = c.blkbytes + (uint64_t)(c.b0 + slot) * c.stride;
 #pragma unroll
     for (int e = 0; e < E; ++e) {
         const uint32_t j = (uint32_t)(wid * 64 * E + e * 64 + lane);
         const bool valid = j < m;
+        const uint32_t vb = valid ? vb_all[g][(uint32_t)(k[e] >> KEYB)] : 0u;
         const bool end = valid && (!ties || j + 1 == m || ((xk[j + 1] ^ k[e]) & KMASK) != 0);
-        emit_sorted(c, slot, s, j, v[e], valid, hp[e], end, runs, bn, blk);
+        emit_sorted(c, slot, s, j, vb & 0xFFFFFu, vb >> 20, valid, hp[e], end, runs);
     }
     if (c.mode && lane == 0 && runs) atomicAdd(&c.L.runs[slot], runs);
 }

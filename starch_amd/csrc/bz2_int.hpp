@@ -37,6 +37,42 @@ static inline uint32_t host_mulmod(uint32_t a, uint32_t b)
     return r;
 }
 
+// ---- move-to-front on a list of <= 16 symbols kept as nibbles of a u64 ----
+struct NibState {          // transform L -> list ++ (L \ set)
+    uint64_t list;         // nibble i = i-th symbol
+    uint32_t set;          // 16-bit symbol set
+    uint32_t cnt;
+};
+
+__device__ __forceinline__ NibState nib_compose(const NibState& c, const NibState& d)   // apply c, then d
+{
+    NibState r;
+    r.list = d.list;
+    r.cnt = d.cnt;
+    for (uint32_t i = 0; i < c.cnt; ++i) {
+        uint32_t sym = (uint32_t)(c.list >> (4 * i)) & 15u;
+        if (!((d.set >> sym) & 1u)) { r.list |= (uint64_t)sym << (4 * r.cnt); ++r.cnt; }
+    }
+    r.set = c.set | d.set;
+    return r;
+}
+
+__device__ __forceinline__ uint64_t lowmask4(uint32_t k)   // k nibbles
+{
+    return k >= 16 ? ~0ull : ((1ull << (4 * k)) - 1ull);
+}
+
+// one MTF step on the nibble list; returns the index of s
+__device__ __forceinline__ uint32_t nib_mtf(uint64_t& L, uint32_t s)
+{
+    const uint64_t x = L ^ (0x1111111111111111ull * s);
+    const uint64_t t = x | (x >> 1) | (x >> 2) | (x >> 3);
+    const uint64_t zn = ~t & 0x1111111111111111ull;
+    const uint32_t k = (uint32_t)__builtin_ctzll(zn) >> 2;
+    L = (L & ~lowmask4(k + 1)) | ((L & lowmask4(k)) << 4) | (uint64_t)s;
+    return k;
+}
+
 void upload_crc_constants();
 
 // bz2_rle.hip launch wrappers

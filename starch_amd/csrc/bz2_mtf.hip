@@ -28,30 +28,6 @@ constexpr int MT = 1024;
 constexpr int NCH_BIG = 256;
 constexpr uint32_t LINE = 128;
 
-struct NibState {          // transform L -> list ++ (L \ set)
-    uint64_t list;         // nibble i = i-th symbol
-    uint32_t set;          // 16-bit symbol set
-    uint32_t cnt;
-};
-
-__device__ __forceinline__ NibState nib_compose(const NibState& c, const NibState& d)   // apply c, then d
-{
-    NibState r;
-    r.list = d.list;
-    r.cnt = d.cnt;
-    for (uint32_t i = 0; i < c.cnt; ++i) {
-        uint32_t sym = (uint32_t)(c.list >> (4 * i)) & 15u;
-        if (!((d.set >> sym) & 1u)) { r.list |= (uint64_t)sym << (4 * r.cnt); ++r.cnt; }
-    }
-    r.set = c.set | d.set;
-    return r;
-}
-
-__device__ __forceinline__ uint64_t lowmask4(uint32_t k)   // k nibbles
-{
-    return k >= 16 ? ~0ull : ((1ull << (4 * k)) - 1ull);
-}
-
 __device__ __forceinline__ uint32_t nsym_run(uint32_t z) { return z ? (31 - __clz(z + 1)) : 0; }
 
 // zero-run summary of a symbol range (monoid, applied left to right)
@@ -83,17 +59,6 @@ __device__ __forceinline__ RunSum shfl_up_rs(const RunSum& v, int d)
     r.tz = __shfl_up(v.tz, d, 64);
     r.inner = __shfl_up(v.inner, d, 64);
     return r;
-}
-
-// one MTF step on the nibble list; returns the index of s
-__device__ __forceinline__ uint32_t nib_mtf(uint64_t& L, uint32_t s)
-{
-    const uint64_t x = L ^ (0x1111111111111111ull * s);
-    const uint64_t t = x | (x >> 1) | (x >> 2) | (x >> 3);
-    const uint64_t zn = ~t & 0x1111111111111111ull;
-    const uint32_t k = (uint32_t)__builtin_ctzll(zn) >> 2;
-    L = (L & ~lowmask4(k + 1)) | ((L & lowmask4(k)) << 4) | (uint64_t)s;
-    return k;
 }
 
 // Visit the bytes of one 128-byte line (all eight 16-B loads issued first, so

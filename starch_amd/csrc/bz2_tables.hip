@@ -297,7 +297,8 @@ __global__ void __launch_bounds__(T32) k_tables32(BlockDesc* __restrict__ blocks
     __shared__ uint32_t freq[258];
     __shared__ uint32_t hl[8][T32];
     __shared__ uint8_t sel_l[kMaxSelectors];
-    __shared__ unsigned long long hdr_bits;
+    __shared__ NibState nst[T32];
+    __shared__ unsigned long long hdr_bits, sbits_sh;
 
     const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
     const uint32_t b = b0 + blockIdx.x;
@@ -323,13 +324,16 @@ __global__ void __launch_bounds__(T32) k_tables32(BlockDesc* __restrict__ blocks
 #pragma unroll
             for (int q = 0; q < 8; ++q) hl[q][tid] = 0;
             const uint32_t gs = g * 50;
-            const uint32_t ge = gs + 50 < n_mtf ? gs + 50 : n_mtf;
+            const uint32_t cnt = gs + 50 < n_mtf ? 50u : n_mtf - gs;
             const uint32_t* m32 = reinterpret_cast<const uint32_t*>(mtfv + gs);   // gs even: 4-B aligned
-            for (uint32_t i = gs; i < ge; i += 2) {
-                const uint32_t w = m32[(i - gs) >> 1];
-                const uint32_t v0 = w & 0xffffu, v1 = w >> 16;
-                atomicAdd(&hl[v0 >> 2][tid], 1u << (8 * (v0 & 3)));
-                if (i + 1 < ge) atomicAdd(&hl[v1 >> 2][tid], 1u << (8 * (v1 & 3)));
+            uint32_t wv[25];
+#pragma unroll
+            for (int q = 0; q < 25; ++q) wv[q] = (2u * q < cnt) ? m32[q] : 0u;   // all loads in flight
+#pragma unroll
+            for (int q = 0; q < 25; ++q) {
+                const uint32_t v0 = wv[q] & 0xffffu, v1 = wv[q] >> 16;
+                if (2u * q < cnt) atomicAdd(&hl[v0 >> 2][tid], 1u << (8 * (v0 & 3)));
+                if (2u * q + 1 < cnt) atomicAdd(&hl[v1 >> 2][tid], 1u << (8 * (v1 & 3)));
             }
 #pragma unroll
             for (int q = 0; q < 8; ++q) h[q] = hl[q][tid];
@@ -374,8 +378,11 @@ __global__ void __launch_bounds__(T32) k_tables32(BlockDesc* __restrict__ blocks
         }
         for (int i = tid; i < NW32 * 6 * 32; i += T32) (&rf[0][0][0])[i] = 0;
         __syncthreads();
+        uint4 n0 = make_uint4(0, 0, 0, 0), n1 = n0;
+        if ((uint32_t)tid < nsel) { n0 = hist[2 * tid]; n1 = hist[2 * tid + 1]; }
         for (uint32_t g = tid; g < nsel; g += T32) {
-            const uint4 h0 = hist[2 * g], h1 = hist[2 * g + 1];
+            const uint4 h0 = n0, h1 = n1;
+            if (g + T32 < nsel) { n0 = hist[2 * (g + T32)]; n1 = hist[2 * (g + T32) + 1]; }   // prefetch
             const uint32_t h[8] = {h0.x, h0.y, h0.z, h0.w, h1.x, h1.y, h1.z, h1.w};
             uint64_t cost = 0;
 #pragma unroll
@@ -409,20 +416,44 @@ __global__ void __launch_bounds__(T32) k_tables32(BlockDesc* __restrict__ blocks
         __syncthreads();
     }
     for (uint32_t g = tid; g < nsel; g += T32) sel[g] = sel_l[g];
-    // selector MTF (bz:compress.c:461-478) and header size
-    if (tid == 0) {
-        uint8_t pos[6];
-        for (int i = 0; i < ng; ++i) pos[i] = (uint8_t)i;
-        uint64_t sbits = 0;
-        for (uint32_t i = 0; i < nsel; ++i) {
-            uint8_t want = sel_l[i];
-            int j = 0;
-            uint8_t carry_v = pos[0];
-            while (carry_v != want && j < 5) { ++j; uint8_t t = pos[j]; pos[j] = carry_v; carry_v = t; }
-            pos[0] = carry_v;
-            selmtf[i] = (uint8_t)j;
-            sbits += (uint64_t)j + 1;
+    // selector MTF (bz:compress.c:461-478): contiguous ranges per thread, start
+    // lists by a scan of the recency-list composition (as in k_mtf_nib)
+    {
+        const uint32_t per = (nsel + T32 - 1) / T32;
+        const uint32_t a = tid * per, e = a + per < nsel ? a + per : nsel;
+        NibState loc;
+        loc.list = 0; loc.set = 0; loc.cnt = 0;
+        for (uint32_t i = e; i > a; --i) {
+            const uint32_t sv = sel_l[i - 1];
+            if (!((loc.set >> sv) & 1u)) { loc.set |= 1u << sv; loc.list |= (uint64_t)sv << (4 * loc.cnt); ++loc.cnt; }
         }
+        nst[tid] = loc;
+        __syncthreads();
+        for (int d = 1; d < T32; d <<= 1) {
+            NibState v = (tid >= d) ? nib_compose(nst[tid - d], nst[tid]) : nst[tid];
+            __syncthreads();
+            nst[tid] = v;
+            __syncthreads();
+        }
+        NibState ident;
+        ident.list = 0x543210ull & lowmask4((uint32_t)ng);
+        ident.set = (1u << ng) - 1u;
+        ident.cnt = (uint32_t)ng;
+        uint64_t L = (tid ? nib_compose(ident, nst[tid - 1]) : ident).list;
+        uint64_t sb = 0;
+        for (uint32_t i = a; i < e; ++i) {
+            const uint32_t j = nib_mtf(L, sel_l[i]);
+            selmtf[i] = (uint8_t)j;
+            sb += j + 1;
+        }
+        sb = wave_reduce_add(sb);
+        if (tid == 0) sbits_sh = 0;
+        __syncthreads();
+        if (lane == 0) atomicAdd(&sbits_sh, (unsigned long long)sb);
+        __syncthreads();
+    }
+    if (tid == 0) {
+        const uint64_t sbits = sbits_sh;
         uint32_t used16 = 0;
         for (int i = 0; i < 16; ++i) {
             uint32_t w = blocks[b].in_use[i >> 1];
