@@ -304,11 +304,26 @@ __global__ void __launch_bounds__(ST) k3_scan(Ctx c)
 // ---------------------------------------------------------------------------
 // k3_scatter: (key, rotation) -> bucket order in (K2, SA); singletons final
 // ---------------------------------------------------------------------------
-__global__ void __launch_bounds__(PT) k3_scatter(Ctx c)
+// Workgroup L of a 1-D grid -> (slot, tile) with slot = L mod 8 inside each
+// group of 8 slots: workgroups are dealt round-robin over the 8 XCDs, so all
+// tiles of a block run on one XCD and its scattered writes meet in one L2
+// (placement is a speed matter only, MI355X_MICROARCH.md "Workgroup dispatch").
+__device__ __forceinline__ bool xcd_slot_tile(uint32_t L, uint32_t ntile, uint32_t nb, uint32_t& slot,
+                                              uint32_t& tile)
+{
+    const uint32_t grp = L / (8u * ntile), r = L % (8u * ntile);
+    slot = grp * 8u + (r & 7u);
+    tile = r >> 3;
+    return slot < nb;
+}
+
+__global__ void __launch_bounds__(PT) k3_scatter(Ctx c, uint32_t nb)
 {
     __shared__ PartSmem sm;
     const int tid = threadIdx.x;
-    const uint32_t slot = blockIdx.y, b = c.b0 + slot, tile = blockIdx.x;
+    uint32_t slot, tile;
+    if (!xcd_slot_tile(blockIdx.x, MAXT, nb, slot, tile)) return;
+    const uint32_t b = c.b0 + slot;
     const uint32_t n = c.blocks[b].n;
     const uint32_t t0 = tile * PTILE;
     if (t0 >= n) return;
@@ -340,10 +355,7 @@ __global__ void __launch_bounds__(PT) k3_scatter(Ctx c)
                 const uint32_t r = r0 + o + k;
                 K2[p] = key;
                 SA[p] = r;
-                if (sm.tot[bk] == 1u) {                 // final: last-column byte, origPtr
-                    c.scr.LL[so + p] = blk[r ? r - 1 : n - 1];
-                    if (r == 0) c.blocks[b].orig_ptr = p;
-                }
+                if (r == 0 && sm.tot[bk] == 1u) c.blocks[b].orig_ptr = p;
                 key = ((key << g.B) | sm.tb[o + k + g.D]) & g.mask;
             }
         }
@@ -373,7 +385,6 @@ __global__ void __launch_bounds__(LT) k3_part_l(Ctx c, const uint64_t* __restric
     uint64_t* dk = (par ? c.scr.K2 : c.scr.K) + base;
     uint32_t* dv = (par ? c.scr.SA : c.scr.V) + base;
     uint32_t* SA = c.scr.SA + base;
-    uint8_t* LLs = c.scr.LL + base;
     uint32_t* RK = c.scr.RK + (uint64_t)slot * c.scr.stride;
     const uint32_t n = c.blocks[b].n;
     const uint8_t* blk = c.blkbytes + (uint64_t)b * c.stride;
@@ -403,7 +414,6 @@ __global__ void __launch_bounds__(LT) k3_part_l(Ctx c, const uint64_t* __restric
         if (cc == 1) {
             const uint32_t v = dv[ss];
             if (!par) SA[ss] = v;
-            LLs[ss] = blk[v ? v - 1 : n - 1];
             if (c.mode) RK[v] = s + ss;
             if (v == 0) c.blocks[b].orig_ptr = s + ss;
             nruns = 1;
@@ -429,7 +439,6 @@ __global__ void __launch_bounds__(LT) k3_part_l(Ctx c, const uint64_t* __restric
         for (uint32_t i = tid; i < cc; i += LT) {
             const uint32_t v = dv[ss + i];
             if (!par) SA[ss + i] = v;
-            LLs[ss + i] = blk[v ? v - 1 : n - 1];
             if (c.mode) RK[v] = s + ss;
             if (v == 0) c.blocks[b].orig_ptr = s + ss + i;
         }
@@ -450,7 +459,6 @@ __device__ __forceinline__ void emit_sorted(const Ctx& c, uint32_t slot, uint32_
     const uint64_t so = (uint64_t)slot * c.scr.stride;
     if (valid) {
         c.scr.SA[so + s + j] = v;
-        c.scr.LL[so + s + j] = (uint8_t)llb;             // last column (bz:compress.c:166-168)
         if (c.mode) c.scr.RK[so + v] = s + hp;
         if (v == 0) c.blocks[c.b0 + slot].orig_ptr = s + j;
     }
@@ -482,9 +490,7 @@ __global__ void __launch_bounds__(256) k3_sort_w(Ctx c, const uint64_t* __restri
     const bool valid = (uint32_t)lane < m;
     const uint64_t k = valid ? sk[lane] : ~0ull;
     const uint32_t v = valid ? sv[lane] : 0u;
-    const uint32_t bn = c.blocks[c.b0 + slot].n;
-    const uint8_t* blk = c.blkbytes + (uint64_t)(c.b0 + slot) * c.stride;
-    const uint32_t vl = valid ? (v | ((uint32_t)blk[v ? v - 1 : bn - 1] << 20)) : 0u;   // rotation | last-column byte
+    const uint32_t vl = v;
     uint32_t r = 0;
     for (uint32_t j = 0; j < m; ++j) {
         const uint64_t kj = __shfl(k, (int)j, 64);
@@ -498,7 +504,7 @@ __global__ void __launch_bounds__(256) k3_sort_w(Ctx c, const uint64_t* __restri
     const bool end = valid && ((uint32_t)lane + 1 == m || skey[wid][lane + 1] != key);
     const uint32_t hp = wave_incl_scan_max<uint32_t>(head ? (uint32_t)lane : 0u);
     uint32_t runs = 0;
-    emit_sorted(c, slot, s, (uint32_t)lane, val & 0xFFFFFu, val >> 20, valid, hp, end, runs);
+    emit_sorted(c, slot, s, (uint32_t)lane, val, 0u, valid, hp, end, runs);
     if (c.mode && lane == 0) atomicAdd(&c.L.runs[slot], runs);
 }
 
@@ -537,7 +543,7 @@ __global__ void __launch_bounds__(256) k3_sort_lds(Ctx c, const uint64_t* __rest
     constexpr int BPT = NBIN / T;                  // bins per thread
     constexpr uint32_t LIMIT = 256 / E;            // largest sub-bucket ranked by comparison
     __shared__ uint64_t xk_all[IPW][CAP];
-    __shared__ uint32_t vb_all[IPW][CAP];          // rotation | last-column byte << 20, by group index
+    __shared__ uint32_t vb_all[IPW][CAP];          // rotations by group index
     __shared__ uint32_t bst_all[IPW][NBIN + 1];   // sub-bucket starts
     __shared__ uint32_t bcur_all[IPW][NBIN];      // scatter cursors
     __shared__ uint32_t cnt_all[4][256];
@@ -569,8 +575,6 @@ __global__ void __launch_bounds__(256) k3_sort_lds(Ctx c, const uint64_t* __rest
             const uint32_t i = (uint32_t)(wid * 64 * E + e * 64 + lane);
             vv[e] = i < m ? sv[i] : 0u;
         }
-        const uint32_t bn = c.blocks[c.b0 + slot].n;
-        const uint8_t* blk = c.blkbytes + (uint64_t)(c.b0 + slot) * c.stride;
 #pragma unroll
         for (int e = 0; e < E; ++e) {
             const uint32_t i = (uint32_t)(wid * 64 * E + e * 64 + lane);
@@ -578,7 +582,7 @@ __global__ void __launch_bounds__(256) k3_sort_lds(Ctx c, const uint64_t* __rest
                 const uint64_t x = sk[i];
                 diff |= x ^ k0;
                 k[e] = (x & KMASK) | ((uint64_t)i << KEYB);
-                vb_all[g][i] = vv[e] | ((uint32_t)blk[vv[e] ? vv[e] - 1 : bn - 1] << 20);
+                vb_all[g][i] = vv[e];
             } else {
                 k[e] = ~0ull;                          // pads: max key, last in stable order
             }
@@ -788,7 +792,7 @@ __global__ void __launch_bounds__(256) k3_sort_lds(Ctx c, const uint64_t* __rest
         const bool valid = j < m;
         const uint32_t vb = valid ? vb_all[g][(uint32_t)(k[e] >> KEYB)] : 0u;
         const bool end = valid && (!ties || j + 1 == m || ((xk[j + 1] ^ k[e]) & KMASK) != 0);
-        emit_sorted(c, slot, s, j, vb & 0xFFFFFu, vb >> 20, valid, hp[e], end, runs);
+        emit_sorted(c, slot, s, j, vb, 0u, valid, hp[e], end, runs);
     }
     if (c.mode && lane == 0 && runs) atomicAdd(&c.L.runs[slot], runs);
 }
@@ -1034,7 +1038,7 @@ void launch_bwt3(BlockDesc* blocks, uint32_t b0, uint32_t nb, const uint8_t* blk
     // ---- round 0: packed prefix keys ----
     hipLaunchKernelGGL(k3_hist, dim3(MAXT, nb), dim3(PT), 0, st, c);
     hipLaunchKernelGGL(k3_scan, dim3(nb), dim3(ST), 0, st, c);
-    hipLaunchKernelGGL(k3_scatter, dim3(MAXT, nb), dim3(PT), 0, st, c);
+    hipLaunchKernelGGL(k3_scatter, dim3(MAXT * ((nb + 7) / 8 * 8)), dim3(PT), 0, st, c, nb);
     HIP_CHECK(hipGetLastError());
     sort_groups();
     // ---- text rounds: extend the tied rotations' keys from the block text ----

@@ -90,7 +90,7 @@ void Encoder::plan(const uint8_t* d_text, const std::vector<StreamIn>& streams, 
     uint32_t* d_carry = b_tile_carry.as<uint32_t>(ntiles + 1);
     uint32_t* d_tw = b_tile_w.as<uint32_t>(ntiles + 1);
     uint64_t* d_twpre = b_tile_wpre.as<uint64_t>(ntiles + 1);
-    uint8_t* d_tpos = b_tpos.as<uint8_t>(text_end + 16);
+    uint8_t* d_tpos = b_tpos.as<uint8_t>(ntiles * kTB + 16);            // tile-aligned
     uint64_t* d_scal = b_scal.as<uint64_t>(nstreams_ + 16);
     HIP_CHECK(hipMemsetAsync(d_twpre, 0, (ntiles + 1) * sizeof(uint64_t), st));
     if (ntiles) {
@@ -136,7 +136,7 @@ void Encoder::plan(const uint8_t* d_text, const std::vector<StreamIn>& streams, 
         rle_emit(d_text, d_tiles, ntiles, d_twpre, d_tile0, d_tpos, d_streams, d_first, d_nblk, d_blocks, d_blkbytes,
                      blk_stride_, st);
     }
-    rle_crc(d_text, d_blocks, nb, st);
+    rle_crc(d_text, d_blocks, nb, b_crc.as<uint32_t>((uint64_t)nb * kCrcMaxChunks), st);
     HIP_CHECK(hipGetLastError());
     t_rle.stop();
     if (stats) stats->n_blocks += nb;
@@ -189,10 +189,8 @@ void Encoder::plan(const uint8_t* d_text, const std::vector<StreamIn>& streams, 
             // STARCH_BWT=lsd selects the one-workgroup-per-block prefix-doubling sort of
             // bz2_bwt.hip (kept as an independent implementation for cross-checks)
             static const bool lsd = [] { const char* e = getenv("STARCH_BWT"); return e && !strcmp(e, "lsd"); }();
-            if (lsd) {
-                launch_bwt(d_blocks, b0, cnt, d_blkbytes, blk_stride_, scr, d_stats, st);
-                launch_last_col(d_blocks, b0, nullptr, cnt, d_blkbytes, blk_stride_, scr, st);
-            } else launch_bwt3(d_blocks, b0, cnt, d_blkbytes, blk_stride_, scr, b_bwt3, h_ctr_.get(), d_stats, st);
+            if (lsd) launch_bwt(d_blocks, b0, cnt, d_blkbytes, blk_stride_, scr, d_stats, st);
+            else launch_bwt3(d_blocks, b0, cnt, d_blkbytes, blk_stride_, scr, b_bwt3, h_ctr_.get(), d_stats, st);
             HIP_CHECK(hipMemcpyAsync(hb.data() + b0, d_blocks + b0, cnt * sizeof(BlockDesc), hipMemcpyDeviceToHost,
                                      st));
             HIP_CHECK(hipStreamSynchronize(st));
@@ -203,9 +201,9 @@ void Encoder::plan(const uint8_t* d_text, const std::vector<StreamIn>& streams, 
                 HIP_CHECK(hipMemcpyAsync(d_which, which.data(), which.size() * sizeof(uint32_t),
                                          hipMemcpyHostToDevice, st));
                 launch_fallback(d_blocks, b0, d_which, (uint32_t)which.size(), d_blkbytes, blk_stride_, scr, st);
-                launch_last_col(d_blocks, b0, d_which, (uint32_t)which.size(), d_blkbytes, blk_stride_, scr, st);
                 if (stats) stats->periodic_blocks += which.size();
             }
+            launch_last_col(d_blocks, b0, nullptr, cnt, d_blkbytes, blk_stride_, scr, st);
         }
         {
             EvTimer tm(st, stats ? &stats->mtf : nullptr);

@@ -90,6 +90,7 @@ void rle_compact(const BlockDesc* tmp, const uint64_t* slot0, const uint32_t* nb
 void rle_emit(const uint8_t* text, const TileDesc* tiles, uint64_t ntiles, const uint64_t* wpre, const uint64_t* tile0,
               const uint8_t* tpos, const StreamIn* streams, const uint32_t* first, const uint32_t* nblk,
               BlockDesc* blocks, uint8_t* blk, uint64_t stride, hipStream_t st);
-void rle_crc(const uint8_t* text, BlockDesc* blocks, uint32_t nb, hipStream_t st);
+constexpr uint32_t kCrcMaxChunks = 128;       // per block (k_crc_chunks)
+void rle_crc(const uint8_t* text, BlockDesc* blocks, uint32_t nb, uint32_t* creg, hipStream_t st);
 
 }  // namespace bz

@@ -430,21 +430,45 @@ __global__ void __launch_bounds__(MT) k_mtf_big(BlockDesc* __restrict__ blocks, 
     }
 }
 
-// last column from SA, for blocks the batch-wide sort did not finish (periodic
-// blocks after k_fallback_exact; every block on the STARCH_BWT=lsd path)
-__global__ void k_last_col(const BlockDesc* __restrict__ blocks, uint32_t b0, const uint32_t* __restrict__ which,
-                           uint32_t nwhich, const uint8_t* __restrict__ blkbytes, uint64_t stride, BwtScratch scr)
+// Last column L[j] = block[(SA[j] - 1) mod n] (bz:compress.c:166-168) for the
+// listed batch slots (which == nullptr: slots 0..nwhich-1).  The text gather is
+// random within the block, so all tiles of a block run on one XCD (workgroup L
+// -> slot L mod 8 inside groups of 8; round-robin XCD dealing) and small tiles
+// keep ~2 blocks per XCD in flight: the 900 KB block text stays in that XCD's
+// 4 MB L2 instead of costing an HBM line per byte.
+constexpr uint32_t LC_PER = 16;                    // elements per lane, all loads in flight
+constexpr uint32_t LC_TILE = 256 * LC_PER;
+
+__global__ void __launch_bounds__(256) k_last_col(const BlockDesc* __restrict__ blocks, uint32_t b0,
+                                                   const uint32_t* __restrict__ which, uint32_t nwhich,
+                                                   uint32_t ntile, const uint8_t* __restrict__ blkbytes,
+                                                   uint64_t stride, BwtScratch scr)
 {
-    const uint32_t k = blockIdx.y;
+    const uint32_t L = blockIdx.x;
+    const uint32_t grp = L / (8u * ntile), r = L % (8u * ntile);
+    const uint32_t k = grp * 8u + (r & 7u), tile = r >> 3;
     if (k >= nwhich) return;
     const uint32_t slot = which ? which[k] : k;
     const uint32_t b = b0 + slot;
     const uint32_t n = blocks[b].n;
     const uint8_t* blk = blkbytes + (uint64_t)b * stride;
     const uint64_t so = (uint64_t)slot * scr.stride;
-    for (uint32_t j = blockIdx.x * blockDim.x + threadIdx.x; j < n; j += gridDim.x * blockDim.x) {
-        const uint32_t p = scr.SA[so + j];
-        scr.LL[so + j] = blk[p ? p - 1 : n - 1];
+    const uint32_t j = tile * LC_TILE + threadIdx.x * LC_PER;
+    if (j >= n) return;
+    if (j + LC_PER <= n) {
+        const uint4* sp = reinterpret_cast<const uint4*>(scr.SA + so + j);
+        const uint4 p0 = sp[0], p1 = sp[1], p2 = sp[2], p3 = sp[3];
+        const uint32_t p[16] = {p0.x, p0.y, p0.z, p0.w, p1.x, p1.y, p1.z, p1.w,
+                                p2.x, p2.y, p2.z, p2.w, p3.x, p3.y, p3.z, p3.w};
+        uint32_t w[4] = {0, 0, 0, 0};
+#pragma unroll
+        for (int t = 0; t < 16; ++t) w[t >> 2] |= (uint32_t)blk[p[t] ? p[t] - 1 : n - 1] << (8 * (t & 3));
+        *reinterpret_cast<uint4*>(scr.LL + so + j) = make_uint4(w[0], w[1], w[2], w[3]);
+    } else {
+        for (uint32_t t = j; t < n; ++t) {
+            const uint32_t pp = scr.SA[so + t];
+            scr.LL[so + t] = blk[pp ? pp - 1 : n - 1];
+        }
     }
 }
 
@@ -452,7 +476,10 @@ void launch_last_col(const BlockDesc* blocks, uint32_t b0, const uint32_t* which
                      const uint8_t* blkbytes, uint64_t stride, const BwtScratch& scr, hipStream_t st)
 {
     if (!nwhich) return;
-    hipLaunchKernelGGL(k_last_col, dim3(32, nwhich), dim3(256), 0, st, blocks, b0, which, nwhich, blkbytes, stride, scr);
+    const uint32_t ntile = (uint32_t)((scr.stride + LC_TILE - 1) / LC_TILE);
+    const uint32_t grid = ntile * ((nwhich + 7) / 8 * 8);
+    hipLaunchKernelGGL(k_last_col, dim3(grid), dim3(256), 0, st, blocks, b0, which, nwhich, ntile, blkbytes, stride,
+                       scr);
     HIP_CHECK(hipGetLastError());
 }
 

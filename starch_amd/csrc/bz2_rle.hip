@@ -13,13 +13,18 @@
 //                   joins a full block only when it is a single byte supplied
 //                   with the finishing call (bz:bzlib.c:393-397)
 //   5. k_rle_emit   materialise each block's RLE1 bytes + inUse map
-//   6. k_block_crc  CRC-32/BZIP2 of each block's input bytes via GF(2) combine
+//   6. k_crc_chunks + k_crc_final
+//                   CRC-32/BZIP2 of each block's input bytes: slice-by-4 CRC of
+//                   16-byte strips, GF(2) combine of strips -> chunks -> block
+// Every lane handles one 16-byte strip, loaded with one or two aligned 16-B
+// loads (any text alignment); tpos is stored tile-aligned (tile t at t*4096).
 #include "bz2_int.hpp"
 
 namespace bz {
 
 __constant__ uint32_t c_pow8[64];   // x^(8*2^k) mod P, P = 0x04c11db7 (MSB-first)
 __constant__ uint32_t c_crc_tab[256];
+__constant__ uint32_t c_crc_tab4[4][256];   // [k][i]: register after byte i then k zero bytes
 
 void upload_crc_constants()
 {
@@ -36,6 +41,13 @@ void upload_crc_constants()
     for (int k = 1; k < 64; ++k) pw[k] = host_mulmod(pw[k - 1], pw[k - 1]);
     HIP_CHECK(hipMemcpyToSymbol(HIP_SYMBOL(c_pow8), pw, sizeof(pw)));
     HIP_CHECK(hipMemcpyToSymbol(HIP_SYMBOL(c_crc_tab), tab, sizeof(tab)));
+    uint32_t tab4[4][256];
+    for (uint32_t i = 0; i < 256; ++i) {
+        uint32_t r = tab[i];
+        tab4[0][i] = r;
+        for (int k = 1; k < 4; ++k) { r = (r << 8) ^ tab[r >> 24]; tab4[k][i] = r; }
+    }
+    HIP_CHECK(hipMemcpyToSymbol(HIP_SYMBOL(c_crc_tab4), tab4, sizeof(tab4)));
     done = true;
 }
 
@@ -86,6 +98,35 @@ __global__ void k_tiles(const uint64_t* __restrict__ seg_tile0, const StreamIn* 
     tiles[t] = d;
 }
 
+// 16 bytes at p (any alignment): one aligned 16-B load, plus the next one only
+// when it holds needed bytes below `lim` (so nothing past the data is touched).
+__device__ __forceinline__ uint4 load16u(const uint8_t* p, const uint8_t* lim)
+{
+    const uintptr_t a = reinterpret_cast<uintptr_t>(p);
+    const uint4* q = reinterpret_cast<const uint4*>(a & ~(uintptr_t)15);
+    const uint32_t sh = (uint32_t)(a & 15u);
+    const uint4 x = q[0];
+    if (sh == 0) return x;
+    const uint4 y = (reinterpret_cast<const uint8_t*>(q + 1) < lim) ? q[1] : make_uint4(0, 0, 0, 0);
+    const uint32_t w0 = x.x, w1 = x.y, w2 = x.z, w3 = x.w, w4 = y.x, w5 = y.y, w6 = y.z, w7 = y.w;
+    const uint32_t bi = sh & 3u;
+    uint32_t a0, a1, a2, a3, a4;
+    switch (sh >> 2) {
+    case 0: a0 = w0; a1 = w1; a2 = w2; a3 = w3; a4 = w4; break;
+    case 1: a0 = w1; a1 = w2; a2 = w3; a3 = w4; a4 = w5; break;
+    case 2: a0 = w2; a1 = w3; a2 = w4; a3 = w5; a4 = w6; break;
+    default: a0 = w3; a1 = w4; a2 = w5; a3 = w6; a4 = w7; break;
+    }
+    return make_uint4(__builtin_amdgcn_alignbyte(a1, a0, bi), __builtin_amdgcn_alignbyte(a2, a1, bi),
+                      __builtin_amdgcn_alignbyte(a3, a2, bi), __builtin_amdgcn_alignbyte(a4, a3, bi));
+}
+
+__device__ __forceinline__ uint32_t byte16(const uint4& v, int k)
+{
+    const uint32_t w = k < 4 ? v.x : k < 8 ? v.y : k < 12 ? v.z : v.w;
+    return (w >> (8 * (k & 3))) & 0xffu;
+}
+
 struct RunSum {
     uint32_t len, trail;
     int first, last;
@@ -104,38 +145,78 @@ __device__ __forceinline__ RunSum rs_combine(const RunSum& A, const RunSum& B)
     return R;
 }
 
-__device__ __forceinline__ RunSum strip_summary(const uint8_t* p, int cnt)
+__device__ __forceinline__ RunSum strip_summary(const uint4& v, int cnt)
 {
     RunSum r;
     r.len = 0; r.trail = 0; r.first = -1; r.last = -1; r.uni = true;
     if (cnt <= 0) return r;
     r.len = cnt;
-    r.first = p[0];
-    int last = p[0];
+    r.first = (int)byte16(v, 0);
+    int last = r.first;
     uint32_t tr = 1;
-    for (int k = 1; k < cnt; ++k) {
-        int c = p[k];
-        if (c == last) ++tr; else { tr = 1; r.uni = false; }
-        last = c;
+#pragma unroll
+    for (int k = 1; k < 16; ++k) {
+        if (k < cnt) {
+            const int c = (int)byte16(v, k);
+            if (c == last) ++tr; else { tr = 1; r.uni = false; }
+            last = c;
+        }
     }
     r.last = last;
     r.trail = tr;
     return r;
 }
 
+__device__ __forceinline__ RunSum rs_shfl_up(const RunSum& v, int d)
+{
+    RunSum r;
+    r.len = __shfl_up(v.len, d, 64);
+    r.trail = __shfl_up(v.trail, d, 64);
+    r.first = __shfl_up(v.first, d, 64);
+    r.last = __shfl_up(v.last, d, 64);
+    r.uni = __shfl_up((int)v.uni, d, 64) != 0;
+    return r;
+}
+
+// inclusive scan of strip summaries over a 256-thread workgroup; returns this
+// thread's exclusive prefix combined after `init`, and the tile total
+__device__ __forceinline__ RunSum rs_block_scan(const RunSum& mine, const RunSum& init, RunSum* wsh, RunSum* total)
+{
+    const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
+    RunSum inc = mine;
+#pragma unroll
+    for (int d = 1; d < 64; d <<= 1) {
+        const RunSum o = rs_shfl_up(inc, d);
+        if (lane >= d) inc = rs_combine(o, inc);
+    }
+    if (lane == 63) wsh[wid] = inc;
+    __syncthreads();
+    RunSum pre = init;
+    for (int w = 0; w < wid; ++w) pre = rs_combine(pre, wsh[w]);
+    RunSum ex = rs_shfl_up(inc, 1);
+    if (lane == 0) { ex.len = 0; ex.trail = 0; ex.first = -1; ex.last = -1; ex.uni = true; }
+    if (total) {
+        RunSum t = init;
+        for (int w = 0; w < 4; ++w) t = rs_combine(t, wsh[w]);
+        *total = t;
+    }
+    return rs_combine(pre, ex);
+}
+
 __global__ void __launch_bounds__(256) k_rle_sum(const uint8_t* __restrict__ text, const TileDesc* __restrict__ tiles,
                                                   TileSum* __restrict__ sums)
 {
-    __shared__ RunSum sh[256];
+    __shared__ RunSum wsh[4];
     TileDesc d = tiles[blockIdx.x];
     int off = threadIdx.x * 16;
     int cnt = (int)d.len - off;
     cnt = cnt < 0 ? 0 : (cnt > 16 ? 16 : cnt);
-    sh[threadIdx.x] = strip_summary(text + d.beg + off, cnt);
-    __syncthreads();
+    const uint4 v = cnt > 0 ? load16u(text + d.beg + off, text + d.beg + d.len) : make_uint4(0, 0, 0, 0);
+    RunSum none;
+    none.len = 0; none.trail = 0; none.first = -1; none.last = -1; none.uni = true;
+    RunSum acc;
+    (void)rs_block_scan(strip_summary(v, cnt), none, wsh, &acc);
     if (threadIdx.x == 0) {
-        RunSum acc = sh[0];
-        for (int k = 1; k < 256; ++k) acc = rs_combine(acc, sh[k]);
         TileSum o;
         o.first = (uint8_t)acc.first;
         o.last = (uint8_t)acc.last;
@@ -205,39 +286,35 @@ __global__ void __launch_bounds__(256) k_rle_pos(const uint8_t* __restrict__ tex
                                                   const uint32_t* __restrict__ carry, uint8_t* __restrict__ tpos,
                                                   uint32_t* __restrict__ tile_w)
 {
-    __shared__ RunSum sh[256];
-    __shared__ uint32_t inc[256];
+    __shared__ RunSum rsh[4];
     __shared__ uint32_t wsh[5];
     TileDesc d = tiles[blockIdx.x];
     int off = threadIdx.x * 16;
     int cnt = (int)d.len - off;
     cnt = cnt < 0 ? 0 : (cnt > 16 ? 16 : cnt);
-    const uint8_t* p = text + d.beg + off;
-    sh[threadIdx.x] = strip_summary(p, cnt);
-    __syncthreads();
-    if (threadIdx.x == 0) {
-        uint32_t c = carry[blockIdx.x];
-        RunSum acc;
-        acc.len = c; acc.trail = c; acc.uni = true;
-        acc.first = acc.last = (d.len ? text[d.beg] : -1);
-        for (int k = 0; k < 256; ++k) {
-            RunSum S = sh[k];
-            inc[k] = (acc.len > 0 && S.len > 0 && acc.last == S.first) ? acc.trail : 0;
-            acc = rs_combine(acc, S);
-        }
-    }
-    __syncthreads();
-    uint32_t run = inc[threadIdx.x];
+    const uint4 v = cnt > 0 ? load16u(text + d.beg + off, text + d.beg + d.len) : make_uint4(0, 0, 0, 0);
+    const RunSum S = strip_summary(v, cnt);
+    RunSum init;
+    const uint32_t c = carry[blockIdx.x];
+    init.len = c; init.trail = c; init.uni = true;
+    init.first = init.last = (d.len ? (int)text[d.beg] : -1);
+    const RunSum P = rs_block_scan(S, init, rsh, (RunSum*)nullptr);
+    uint32_t run = (P.len > 0 && S.len > 0 && P.last == S.first) ? P.trail : 0;
     uint32_t w = 0;
     int prev = -1;
-    for (int k = 0; k < cnt; ++k) {
-        int c = p[k];
-        if (k > 0) run = (c == prev) ? run + 1 : 0;
-        prev = c;
-        uint32_t t = run % 255u;
-        tpos[d.beg + off + k] = (uint8_t)t;
-        w += rle_w(t);
+    uint32_t tw[4] = {0, 0, 0, 0};
+#pragma unroll
+    for (int k = 0; k < 16; ++k) {
+        if (k < cnt) {
+            const int ch = (int)byte16(v, k);
+            if (k > 0) run = (ch == prev) ? run + 1 : 0;
+            prev = ch;
+            const uint32_t t = run % 255u;
+            tw[k >> 2] |= t << (8 * (k & 3));
+            w += rle_w(t);
+        }
     }
+    *reinterpret_cast<uint4*>(tpos + (uint64_t)blockIdx.x * kTB + off) = make_uint4(tw[0], tw[1], tw[2], tw[3]);
     uint32_t tot;
     (void)block_excl_scan_add<uint32_t>(w, wsh, &tot);
     if (threadIdx.x == 0) tile_w[blockIdx.x] = tot;
@@ -263,7 +340,7 @@ __global__ void k_stream_w(const uint64_t* __restrict__ seg_tile0, const uint64_
 // tile's byte weights for the crossing byte q, then a ballot over the next 256
 // bytes for the first chunk start p >= q (chunks are at most 255 bytes).
 __global__ void __launch_bounds__(64) k_cut(const StreamIn* __restrict__ streams, const uint64_t* __restrict__ seg_tile0,
-                                             const uint64_t* __restrict__ tile_wpre, const uint8_t* __restrict__ tpos,
+                                             const uint64_t* __restrict__ tile_wpre, const uint8_t* __restrict__ tpos_t,
                                              uint32_t nstreams, uint32_t nblock_max, const uint64_t* __restrict__ slot0,
                                              BlockDesc* __restrict__ tmp, uint32_t* __restrict__ nblk)
 {
@@ -271,6 +348,8 @@ __global__ void __launch_bounds__(64) k_cut(const StreamIn* __restrict__ streams
     const int lane = threadIdx.x;
     const uint64_t beg = streams[s].text_off, end = beg + streams[s].text_len;
     const uint64_t t0 = seg_tile0[s], t1 = seg_tile0[s + 1];
+    // tile-aligned tpos: text position y of this stream -> tile t0 + (y-beg)/kTB
+    const uint8_t* tpos = tpos_t + t0 * kTB - beg;
     const uint64_t w0 = tile_wpre[t0], wend = tile_wpre[t1] - w0;
     const bool frj = streams[s].final_run_joins != 0;
     uint64_t bs = beg, wbs = 0;
@@ -379,8 +458,13 @@ __global__ void __launch_bounds__(256) k_rle_emit(const uint8_t* __restrict__ te
     int off = threadIdx.x * 16;
     int cnt = (int)d.len - off;
     cnt = cnt < 0 ? 0 : (cnt > 16 ? 16 : cnt);
+    // tpos of this stream, indexed by text position (tiles of a stream are consecutive)
+    const uint8_t* tp = tpos + (uint64_t)blockIdx.x * kTB - d.beg;
+    const uint4 tv = *reinterpret_cast<const uint4*>(tpos + (uint64_t)blockIdx.x * kTB + off);
+    const uint4 xv = cnt > 0 ? load16u(text + d.beg + off, text + d.beg + d.len) : make_uint4(0, 0, 0, 0);
     uint32_t w = 0;
-    for (int k = 0; k < cnt; ++k) w += rle_w(tpos[d.beg + off + k]);
+#pragma unroll
+    for (int k = 0; k < 16; ++k) if (k < cnt) w += rle_w(byte16(tv, k));
     uint32_t pre = block_excl_scan_add<uint32_t>(w, wsh, (uint32_t*)nullptr);   // contains __syncthreads
     const uint32_t b0 = bsel;
     const uint32_t bl = sfirst[s] + snblk[s];
@@ -390,8 +474,8 @@ __global__ void __launch_bounds__(256) k_rle_emit(const uint8_t* __restrict__ te
     for (int k = 0; k < cnt; ++k) {
         uint64_t i = d.beg + off + k;
         while (i >= bend && b + 1 < bl) { ++b; bend = blocks[b].in_end; wb = blocks[b].w_beg; }
-        uint32_t t = tpos[i];
-        uint8_t c = text[i];
+        const uint32_t t = byte16(tv, k);
+        const uint8_t c = (uint8_t)byte16(xv, k);
         uint8_t* o = blk + (uint64_t)b * stride + (W - wb);
         int slot = (b == b0) ? 0 : 1;
         if (t < 3) {
@@ -399,7 +483,7 @@ __global__ void __launch_bounds__(256) k_rle_emit(const uint8_t* __restrict__ te
             if (t == 0) atomicOr(&used[slot][c >> 5], 1u << (c & 31));
         } else if (t == 3) {
             uint64_t j = i + 1;
-            while (j < send && tpos[j] != 0) ++j;
+            while (j < send && tp[j] != 0) ++j;
             uint32_t L = (uint32_t)(j - i) + 3;
             uint8_t cnt_byte = (uint8_t)(L - 4);
             o[0] = c;
@@ -416,33 +500,63 @@ __global__ void __launch_bounds__(256) k_rle_emit(const uint8_t* __restrict__ te
     }
 }
 
-// CRC-32/BZIP2 of [in_beg, in_end) per block; one 256-thread workgroup per block.
+// CRC-32/BZIP2 of [in_beg, in_end) per block (bz:bzlib_private.h:155-172).
 // R(A||B) = R(A)*x^(8|B|) + R(B) (mod P); crc = ~(0xffffffff*x^(8n) + R(all)).
-__global__ void __launch_bounds__(256) k_block_crc(const uint8_t* __restrict__ text, BlockDesc* __restrict__ blocks)
+// k_crc_chunks: workgroup (c, block) takes chunk c (CRC_SUB-byte sub-chunks,
+// up to CRC_MAXC chunks per block); each lane a 16-byte strip by slice-by-4
+// table lookups, strips combined by a 256-lane tree.  k_crc_final: one wave per
+// block combines the chunk registers.
+constexpr uint32_t CRC_SUB = 4096;
+constexpr uint32_t CRC_MAXC = 128;
+
+__device__ __forceinline__ uint64_t crc_chunk_bytes(uint64_t span)
 {
-    __shared__ uint32_t tab[256];
+    uint64_t c = (span + CRC_MAXC - 1) / CRC_MAXC;
+    c = (c + CRC_SUB - 1) / CRC_SUB * CRC_SUB;
+    return c < CRC_SUB ? CRC_SUB : c;
+}
+
+__global__ void __launch_bounds__(256) k_crc_chunks(const uint8_t* __restrict__ text,
+                                                     const BlockDesc* __restrict__ blocks, uint32_t* __restrict__ creg)
+{
+    __shared__ uint32_t t4[4][256];
     __shared__ uint32_t rr[256];
     __shared__ uint32_t ll[256];
-    tab[threadIdx.x] = c_crc_tab[threadIdx.x];
-    const BlockDesc bd = blocks[blockIdx.x];
-    const uint64_t beg = bd.in_beg, end = bd.in_end;
-    __syncthreads();
-    uint32_t acc = 0;   // raw register over processed prefix
-    for (uint64_t c0 = beg; c0 < end; c0 += 4096) {
-        uint64_t a = c0 + threadIdx.x * 16;
-        uint64_t e = a + 16;
-        if (e > end) e = end;
-        uint32_t r = 0, n = 0;
-        for (uint64_t i = a; i < e; ++i) { r = (r << 8) ^ tab[(r >> 24) ^ text[i]]; ++n; }
+    const uint32_t c = blockIdx.x, b = blockIdx.y;
+    const uint64_t beg = blocks[b].in_beg, end = blocks[b].in_end;
+    const uint64_t csz = crc_chunk_bytes(end - beg);
+    const uint64_t cb = beg + (uint64_t)c * csz;
+    if (cb >= end) return;
+    const uint64_t ce = cb + csz < end ? cb + csz : end;
+    for (int i = threadIdx.x; i < 1024; i += 256) (&t4[0][0])[i] = (&c_crc_tab4[0][0])[i];
+    uint32_t acc = 0;
+    for (uint64_t c0 = cb; c0 < ce; c0 += CRC_SUB) {
+        const uint64_t a = c0 + threadIdx.x * 16;
+        const uint32_t n = a < ce ? (uint32_t)(ce - a < 16 ? ce - a : 16) : 0u;
+        uint32_t r = 0;
+        __syncthreads();
+        if (n) {
+            const uint4 v = load16u(text + a, text + ce);
+            if (n == 16) {
+                const uint32_t ws[4] = {v.x, v.y, v.z, v.w};
+#pragma unroll
+                for (int q = 0; q < 4; ++q) {
+                    const uint32_t x = r ^ __builtin_bswap32(ws[q]);   // bytes in stream order, MSB-first
+                    r = t4[3][x >> 24] ^ t4[2][(x >> 16) & 255u] ^ t4[1][(x >> 8) & 255u] ^ t4[0][x & 255u];
+                }
+            } else {
+                for (uint32_t k = 0; k < n; ++k) r = (r << 8) ^ t4[0][(r >> 24) ^ byte16(v, (int)k)];
+            }
+        }
         rr[threadIdx.x] = r;
-        ll[threadIdx.x] = (a < end) ? n : 0;
+        ll[threadIdx.x] = n;
         __syncthreads();
         for (int step = 1; step < 256; step <<= 1) {
             if ((threadIdx.x & (2 * step - 1)) == 0) {
-                uint32_t j = threadIdx.x + step;
-                uint32_t lb = ll[j];
+                const uint32_t j = threadIdx.x + step;
+                const uint32_t lb = ll[j];
                 if (lb) {
-                    uint32_t m = (lb == (uint32_t)(16 * step)) ? c_pow8[4 + __builtin_ctz(step)] : xpow8(lb);
+                    const uint32_t m = (lb == (uint32_t)(16 * step)) ? c_pow8[4 + __builtin_ctz(step)] : xpow8(lb);
                     rr[threadIdx.x] = mulmod(rr[threadIdx.x], m) ^ rr[j];
                     ll[threadIdx.x] += lb;
                 }
@@ -450,16 +564,42 @@ __global__ void __launch_bounds__(256) k_block_crc(const uint8_t* __restrict__ t
             __syncthreads();
         }
         if (threadIdx.x == 0) {
-            uint32_t lc = ll[0];
-            uint32_t m = (lc == 4096u) ? c_pow8[12] : xpow8(lc);
+            const uint32_t lc = ll[0];
+            const uint32_t m = (lc == CRC_SUB) ? c_pow8[12] : xpow8(lc);
             acc = mulmod(acc, m) ^ rr[0];
         }
-        __syncthreads();
     }
-    if (threadIdx.x == 0) {
-        uint32_t m = xpow8(end - beg);
-        blocks[blockIdx.x].crc = ~(mulmod(0xffffffffu, m) ^ acc);
+    if (threadIdx.x == 0) creg[(uint64_t)b * CRC_MAXC + c] = acc;
+}
+
+__global__ void __launch_bounds__(64) k_crc_final(const uint32_t* __restrict__ creg, BlockDesc* __restrict__ blocks)
+{
+    const uint32_t b = blockIdx.x;
+    const int lane = threadIdx.x;
+    const uint64_t beg = blocks[b].in_beg, end = blocks[b].in_end;
+    const uint64_t csz = crc_chunk_bytes(end - beg);
+    const uint32_t nch = (uint32_t)((end - beg + csz - 1) / csz);
+    // lane l folds chunks 2l, 2l+1 (CRC_MAXC = 128 = 2 * 64); then a wave tree
+    uint32_t r = 0;
+    uint64_t len = 0;
+    for (int q = 0; q < 2; ++q) {
+        const uint32_t k = 2u * lane + q;
+        if (k < nch) {
+            const uint64_t cb = beg + (uint64_t)k * csz;
+            const uint64_t cl = (end - cb) < csz ? end - cb : csz;
+            r = mulmod(r, xpow8(cl)) ^ creg[(uint64_t)b * CRC_MAXC + k];
+            len += cl;
+        }
     }
+    for (int step = 1; step < 64; step <<= 1) {
+        const uint32_t ro = __shfl_down(r, step, 64);
+        const uint64_t lo = __shfl_down(len, step, 64);
+        if ((lane & (2 * step - 1)) == 0 && lane + step < 64 && lo) {
+            r = mulmod(r, xpow8(lo)) ^ ro;
+            len += lo;
+        }
+    }
+    if (lane == 0) blocks[b].crc = ~(mulmod(0xffffffffu, xpow8(end - beg)) ^ r);
 }
 
 // ---------------------------------------------------------------------------
@@ -507,9 +647,11 @@ void rle_emit(const uint8_t* text, const TileDesc* tiles, uint64_t ntiles, const
     hipLaunchKernelGGL(k_rle_emit, dim3((unsigned)ntiles), dim3(256), 0, st, text, tiles, wpre, tile0, tpos, streams,
                        first, nblk, blocks, blk, stride);
 }
-void rle_crc(const uint8_t* text, BlockDesc* blocks, uint32_t nb, hipStream_t st)
+void rle_crc(const uint8_t* text, BlockDesc* blocks, uint32_t nb, uint32_t* creg, hipStream_t st)
 {
-    if (nb) hipLaunchKernelGGL(k_block_crc, dim3(nb), dim3(256), 0, st, text, blocks);
+    if (!nb) return;
+    hipLaunchKernelGGL(k_crc_chunks, dim3(CRC_MAXC, nb), dim3(256), 0, st, text, blocks, creg);
+    hipLaunchKernelGGL(k_crc_final, dim3(nb), dim3(64), 0, st, creg, blocks);
 }
 
 }  // namespace bz
