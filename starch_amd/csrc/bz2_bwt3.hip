@@ -1,6 +1,6 @@
 // starch_amd/csrc/bz2_bwt3.hip -- block sort v3 (the default): a batch-wide
-// segmented sort of every rotation of every block, then prefix doubling on
-// the rotations whose packed prefix keys tie.
+// segmented sort of every rotation of every block, then refinement of the
+// rotations whose packed prefix keys tie.
 //
 // Contract (same as k_bwt, bz2_bwt.hip): SA = the exact sorted order of the
 // cyclic rotations of every non-periodic block (BZ2_blockSort's ptr[],
@@ -9,39 +9,45 @@
 // k_fallback_exact, which reproduces fallbackSort's tie order.
 //
 // Why this shape: a 900 KB transformed-BED block almost never needs more than
-// its packed D-symbol prefix (D = 64 / ceil(log2 nInUse) symbols in a u64 key;
-// 16 for BED3 text): measured on cfg2 blocks, ~5 tied pairs per 900k
-// rotations; cfg4 (narrowPeak) ~0.8 %.  So the work is a segmented sort of
-// (block, 64-bit key) pairs, done for ALL blocks of a batch at once so every
-// CU is busy, instead of one workgroup walking one block:
+// its packed D-symbol prefix (D = 64 / B symbols of B = ceil(log2 nInUse)
+// bits in a u64 key; 16 for BED3 text): measured on cfg2 blocks, ~5 tied
+// pairs per 900k rotations; cfg4 (narrowPeak) ~0.8 %.  So the work is a
+// segmented sort of (block, 64-bit key) pairs, done for ALL blocks of a batch
+// at once:
 //
-//   k3_hist     per 32k-rotation tile: keys rolled from the block text in
-//               LDS, 4096-bucket histogram of the top 12 key bits
-//   k3_scan     per block: bucket starts, per-tile cursors (deterministic
-//               offsets, no global atomics), bucket -> size class lists
-//   k3_scatter  per tile: keys again, (key, rotation) scattered to buckets
-//   k3_part_l   buckets > 4096: MSD partition on the next 8 bits, repeated
+//   k3_pss      packed symbol stream (PSS) of every block: its symbols as
+//               B-bit fields, MSB first, in u64 words, wrapped past the end;
+//               the key of rotation r is bits [rB, rB+KB) -- two word loads
+//               and a shift, so keys are never stored
+//   k3_hist     per 32k-rotation tile: 4096-bucket histogram of the top 12 bits
+//   k3_scan     per block: bucket starts, per-tile cursors, size-class lists
+//   k3_scatter  rotations -> bucket order in SA.  Persistent, per-XCD queues:
+//               each XCD streams ITS blocks one at a time, so the scattered
+//               4-B writes of a block meet in that XCD's 4 MB L2
+//   k3_bin_*    every work list is binned by block into 8 per-XCD segments
+//               (blocks x, x+8, ... in order), so the persistent kernels below
+//               touch ~one block's PSS per XCD at a time (L2-resident)
+//   k3_part_l   buckets > 4096: MSD partition on the next 8 key bits, repeated
 //   k3_sort_w   buckets <= 64: one wave, rank by comparison
 //   k3_sort_lds buckets <= 256: one wave; <= 1024/2048/4096: one workgroup;
-//               keys in registers, stable LSD radix with an LDS exchange,
-//               only over the key bits that vary inside the bucket
+//               one MSD digit then ranking by comparison (LSD radix when a
+//               sub-bucket is large), keys in registers, LDS exchange
 //   -- every sort writes SA and lists the groups of equal keys --
-//   k3_gather_text  text rounds: a tied group is re-sorted by the NEXT D'
-//               symbols of each rotation, packed straight from the block text
-//               (D' = 52/B so 12 key bits stay free); enough for BED text,
-//               where ties are rare and short
+//   text rounds a tied group is re-sorted by its NEXT D' = 52/B symbols, read
+//               from the PSS at an offset (12 key bits stay free for the packed
+//               group index); enough for BED text, where ties are short
 //   k3_rk_*     blocks still tied after the text rounds (long repeats,
 //               periodic blocks): dense RK = head position of every
 //               rotation's group, then prefix doubling --
 //   k3_gather   doubling round r: key(q) = RK[(SA[q] + h0*2^(r-1)) mod n] for
-//               the tied rotations only; the same part/sort kernels re-sort
-//               the groups and update RK.  A round in which no group of a
-//               block splits proves the block periodic.
+//               the tied rotations only (K2); the same kernels re-sort the
+//               groups and update RK.  A round in which no group of a block
+//               splits proves the block periodic.
 //
-// Scratch (BwtScratch, per batch slot, stride S elements): K2/SA = keys and
-// rotations in bucket order; K/V = ping-pong for the MSD partition (and the
-// per-tile cursors before that); RK ranks; U = wave-class list; U2/V2 = the
-// tie-group lists of consecutive rounds (u64 items).
+// Scratch (BwtScratch, per batch slot, stride S elements): SA/V = rotations in
+// bucket order (V: partition ping-pong); K = PSS + per-tile cursors (round 0,
+// text rounds), key ping-pong while doubling; K2 = doubling keys; RK ranks;
+// U = wave-class list; U2/V2 = tie-group lists of consecutive rounds (u64).
 #include "bz2_int.hpp"
 #include "bz2_bwt.hpp"
 
@@ -53,22 +59,19 @@
 namespace bz {
 namespace {
 
-constexpr int PT = 256;                 // partition threads
-constexpr int PE = 32;                  // rotations per thread per sub-tile
-constexpr int PSUB = PT * PE;           // 8192-rotation sub-tile
-constexpr int PSUBS = 4;
-constexpr int PTILE = PSUB * PSUBS;     // 32768-rotation tile (one workgroup)
+constexpr int PT = 256;                 // hist threads
+constexpr int PTILE = 32768;            // rotations per partition tile
 constexpr int PDIG = 12;
 constexpr int PNB = 1 << PDIG;          // 4096 top-level buckets per block
 constexpr int MAXT = (900064 + PTILE - 1) / PTILE;   // tiles per block (bs <= 9)
-// size classes: W rank-by-compare (one wave), S wave-private LDS radix,
-// M1..M3 workgroup LDS radix, L MSD partition
+// size classes: W rank-by-compare (one wave), S wave-private LDS sort,
+// M1..M3 workgroup LDS sort, L MSD partition
 constexpr uint32_t W_MAX = 64, S_MAX = 256, M1_MAX = 1024, M2_MAX = 2048, M3_MAX = 4096;
 constexpr uint32_t RBITS = 20;          // rank bits (n <= 899,985 < 2^20)
+constexpr uint32_t TEXT_ROUNDS = 4;     // max text-extension rounds before doubling
 
 // counters (u32) in the meta buffer
 enum { C_W = 0, C_S, C_M1, C_M2, C_M3, C_L0, C_L1, C_T0, C_T1, C_TIE_ELEMS, C_ERR, C_TS0, C_TS1, C_N = 16 };
-constexpr uint32_t TEXT_ROUNDS = 4;     // max text-extension rounds before doubling
 
 // item = slot[63:52] | start[51:32] | size[31:12] | parity[7] | shift[6:0]
 __device__ __forceinline__ uint64_t mk_item(uint32_t slot, uint32_t s, uint32_t m, uint32_t shift, uint32_t par)
@@ -81,6 +84,15 @@ __device__ __forceinline__ uint32_t it_size(uint64_t x) { return (uint32_t)(x >>
 __device__ __forceinline__ uint32_t it_par(uint64_t x) { return (uint32_t)(x >> 7) & 1u; }
 __device__ __forceinline__ uint32_t it_shift(uint64_t x) { return (uint32_t)x & 127u; }
 
+struct Geo {                   // per block key geometry
+    uint32_t B;                // bits per symbol
+    uint32_t D;                // symbols per round-0 key (KB = D*B bits)
+    uint32_t Dp;               // symbols per text-round key (52/B)
+    uint32_t KB;
+};
+
+__host__ __device__ constexpr uint64_t pss_words(uint64_t stride) { return stride / 8 + 64; }
+
 struct Lists {
     uint32_t* ctr;          // C_N counters
     uint64_t* w;            // m <= 64
@@ -90,14 +102,12 @@ struct Lists {
     uint64_t* m3;           // m <= 4096
     uint64_t* l[2];         // m > 4096 (MSD partition), ping-pong by level
     uint64_t* t[2];         // tie groups, ping-pong by round
-    uint32_t* sD;           // per slot: D (symbols per key)
-    uint32_t* sDp;          // per slot: D' (symbols per text-round key, 12 top bits free)
-    uint32_t* tied;         // per slot: still tied when doubling starts
-    uint8_t* sym;           // per slot: 256-byte symbol map
+    Geo* geo;               // per slot
     uint32_t* gin;          // per slot: groups entering this round
     uint32_t* runs;         // per slot: runs produced this round
     uint32_t* periodic;     // per slot
     uint32_t* rounds;       // per slot: doubling rounds with work
+    uint32_t* tied;         // per slot: still tied when doubling starts
 };
 
 struct Ctx {
@@ -107,9 +117,14 @@ struct Ctx {
     uint64_t stride;        // block byte stride
     BwtScratch scr;
     Lists L;
+    uint32_t nb;
     uint32_t lsel;          // L list that part/classify pushes into
     uint32_t tsel;          // tie list the sorts push into
     uint32_t mode;          // 0: SA only (round 0, text rounds); 1: doubling (RK, runs)
+    uint32_t keysrc;        // 0: PSS at the text-round offset; 1: K2/K (doubling)
+    uint32_t rtext;         // text round (0: round 0)
+    uint32_t* qhead;        // 8 queue heads of the current persistent launch
+    const uint32_t* qseg;   // 9 per-XCD segment offsets of the current binned list
 };
 
 __device__ __forceinline__ int bits_for3(uint32_t x) { return x ? 32 - __clz(x) : 0; }
@@ -154,7 +169,51 @@ __device__ __forceinline__ void wave_classify(const Ctx& c, bool pred, uint32_t 
     wave_push(c.L.ctr + C_L0 + c.lsel, c.L.l[c.lsel], pred && m > M3_MAX, it);
 }
 
-// symbol map of a block (rank among used byte values), 256 threads or more
+// bits [bit, bit+nbits) of a packed symbol stream, right-aligned (1 <= nbits <= 64)
+__device__ __forceinline__ uint64_t pss_bits(const uint64_t* __restrict__ w, uint64_t bit, uint32_t nbits)
+{
+    const uint64_t q = bit >> 6;
+    const uint32_t p = (uint32_t)(bit & 63u);
+    const uint64_t a = w[q];
+    const uint64_t v = p ? ((a << p) | (w[q + 1] >> (64u - p))) : a;
+    return v >> (64u - nbits);
+}
+
+// Key of a group element: rotation r (PSS modes) or group position q (K2/K).
+struct KeySrc {
+    const uint64_t* pss;
+    const uint64_t* k;      // doubling keys of this group's buffer (K2 or K by parity), slot base
+    uint32_t B, kbits, n, off, usek;
+    __device__ __forceinline__ uint64_t operator()(uint64_t q, uint32_t r) const
+    {
+        if (usek) return k[q];
+        uint32_t rr = r + off;
+        if (rr >= n) rr -= n;
+        return pss_bits(pss, (uint64_t)rr * B, kbits);
+    }
+};
+
+__device__ __forceinline__ KeySrc key_src(const Ctx& c, uint32_t slot, uint32_t par)
+{
+    KeySrc k;
+    const uint64_t so = (uint64_t)slot * c.scr.stride;
+    const Geo g = c.L.geo[slot];
+    k.n = c.blocks[c.b0 + slot].n;
+    k.B = g.B;
+    k.usek = c.keysrc;
+    k.pss = c.scr.K + so;
+    k.k = (par ? c.scr.K : c.scr.K2) + so;
+    if (c.rtext == 0) {
+        k.kbits = g.KB;
+        k.off = 0;
+    } else {
+        k.kbits = g.Dp * g.B;
+        k.off = (uint32_t)(((uint64_t)g.D + (uint64_t)(c.rtext - 1) * g.Dp) % k.n);
+    }
+    return k;
+}
+
+// symbol map of a block (rank among used byte values), >= 256 threads
 __device__ __forceinline__ void load_sym(const BlockDesc& bd, uint8_t* sym, uint32_t* nin_out)
 {
     const int tid = threadIdx.x;
@@ -169,87 +228,92 @@ __device__ __forceinline__ void load_sym(const BlockDesc& bd, uint8_t* sym, uint
     *nin_out = nin;
 }
 
-struct KeyGeo {
-    int B, D, KB;
-    uint64_t mask;
-};
-__device__ __forceinline__ KeyGeo key_geo(uint32_t nin)
+// persistent-kernel job fetch: one lane pops, the value is broadcast
+__device__ __forceinline__ uint32_t wg_pop(const Ctx& c, const uint32_t* qs, uint32_t* job_sh, uint32_t x)
 {
-    KeyGeo g;
-    g.B = nin > 1 ? bits_for3(nin - 1) : 1;
-    g.D = 64 / g.B;
-    g.KB = g.D * g.B;
-    g.mask = g.KB == 64 ? ~0ull : ((1ull << g.KB) - 1ull);
-    return g;
+    if (threadIdx.x == 0) *job_sh = xq_pop(c.qhead, qs, x);
+    __syncthreads();
+    const uint32_t j = *job_sh;
+    __syncthreads();
+    return j;
 }
 
-// Load the symbols of rotations [r0, r0 + cnt + D - 1) (cyclic) into tb.
-__device__ __forceinline__ void load_text(const uint8_t* blk, uint32_t n, uint32_t r0, uint32_t cnt, int D,
-                                          const uint8_t* sym, uint8_t* tb)
+__device__ __forceinline__ uint32_t wave_pop(const Ctx& c, const uint32_t* qs, uint32_t x)
 {
-    const int tid = threadIdx.x;
-    const uint32_t len = cnt + (uint32_t)D - 1u;
-    if ((uint64_t)r0 + PSUB + 64 <= n) {
-        const uint32_t* w = reinterpret_cast<const uint32_t*>(blk + r0);
-        uint32_t* o = reinterpret_cast<uint32_t*>(tb);
-        for (uint32_t i = tid; i < (PSUB + 64) / 4; i += PT) {
-            uint32_t x = w[i];
-            o[i] = (uint32_t)sym[x & 255u] | ((uint32_t)sym[(x >> 8) & 255u] << 8) |
-                   ((uint32_t)sym[(x >> 16) & 255u] << 16) | ((uint32_t)sym[x >> 24] << 24);
-        }
-    } else {
-        for (uint32_t i = tid; i < len; i += PT) {
-            uint32_t p = r0 + i;
-            if (p >= n) p %= n;
-            tb[i] = sym[blk[p]];
-        }
-    }
+    uint32_t j = 0;
+    if ((threadIdx.x & 63) == 0) j = xq_pop(c.qhead, qs, x);
+    return (uint32_t)__shfl((int)j, 0, 64);
 }
 
-struct PartSmem {
-    uint32_t cnt[PNB];       // histogram / cursors
-    uint32_t tot[PNB];       // block totals (scatter: singleton test)
-    uint8_t tb[PSUB + 64 + 16];
-    uint8_t sym[256];
-};
+// queue sizes of a binned list (LDS), before the first pop
+__device__ __forceinline__ void load_qsizes_binned(const Ctx& c, uint32_t* qs)
+{
+    if (threadIdx.x < 8) qs[threadIdx.x] = c.qseg[threadIdx.x + 1] - c.qseg[threadIdx.x];
+    __syncthreads();
+}
 
 // ---------------------------------------------------------------------------
-// k3_hist: per-tile bucket histogram -> thist[slot][tile][4096] (in K)
+// k3_pss: packed symbol stream; also the block's key geometry and nInUse
+// ---------------------------------------------------------------------------
+__global__ void __launch_bounds__(256) k3_pss(Ctx c)
+{
+    __shared__ uint8_t sym[256];
+    const uint32_t slot = blockIdx.y, b = c.b0 + slot;
+    const uint32_t n = c.blocks[b].n;
+    uint32_t nin;
+    load_sym(c.blocks[b], sym, &nin);
+    const uint32_t B = nin > 1 ? (uint32_t)bits_for3(nin - 1) : 1u;
+    const uint32_t nw = (uint32_t)(((uint64_t)(n + 128) * B + 63) / 64 + 1);
+    if (blockIdx.x == 0 && threadIdx.x == 0) {
+        Geo g;
+        g.B = B;
+        g.D = 64 / B;
+        g.KB = g.D * B;
+        g.Dp = (64 - PDIG) / B;
+        c.L.geo[slot] = g;
+        c.blocks[b].n_in_use = nin;
+    }
+    __syncthreads();
+    const uint32_t w = blockIdx.x * 256 + threadIdx.x;
+    if (w >= nw) return;
+    const uint8_t* blk = c.blkbytes + (uint64_t)b * c.stride;
+    const uint64_t bit0 = (uint64_t)w * 64;
+    const uint64_t j0 = bit0 / B, j1 = (bit0 + 63) / B;
+    uint64_t word = 0;
+    for (uint64_t j = j0; j <= j1; ++j) {
+        const uint64_t s = sym[blk[j < n ? j : j % n]];
+        const int sh = 64 - (int)B - (int)(j * B - bit0);
+        word |= sh >= 0 ? (s << sh) : (s >> (-sh));
+    }
+    c.scr.K[(uint64_t)slot * c.scr.stride + w] = word;
+}
+
+// tile cursors / totals live in K after the PSS
+__device__ __forceinline__ uint32_t* tile_hist(const Ctx& c, uint32_t slot)
+{
+    return reinterpret_cast<uint32_t*>(c.scr.K + (uint64_t)slot * c.scr.stride + pss_words(c.scr.stride));
+}
+
+// ---------------------------------------------------------------------------
+// k3_hist: per-tile bucket histogram -> thist[slot][tile][4096]
 // ---------------------------------------------------------------------------
 __global__ void __launch_bounds__(PT) k3_hist(Ctx c)
 {
-    __shared__ PartSmem sm;
-    const int tid = threadIdx.x;
+    __shared__ uint32_t cnt[PNB];
     const uint32_t slot = blockIdx.y, b = c.b0 + slot, tile = blockIdx.x;
     const uint32_t n = c.blocks[b].n;
     const uint32_t t0 = tile * PTILE;
     if (t0 >= n) return;
-    uint32_t nin;
-    load_sym(c.blocks[b], sm.sym, &nin);
-    const KeyGeo g = key_geo(nin);
-    const uint8_t* blk = c.blkbytes + (uint64_t)b * c.stride;
-    for (int i = tid; i < PNB; i += PT) sm.cnt[i] = 0;
-    for (uint32_t sub = 0; sub < PSUBS; ++sub) {
-        const uint32_t r0 = t0 + sub * PSUB;
-        if (r0 >= n) break;
-        const uint32_t cnt = min((uint32_t)PSUB, n - r0);
-        __syncthreads();
-        load_text(blk, n, r0, cnt, g.D, sm.sym, sm.tb);
-        __syncthreads();
-        const uint32_t o = tid * PE;
-        if (o < cnt) {
-            uint64_t key = 0;
-            for (int k = 0; k < g.D; ++k) key = (key << g.B) | sm.tb[o + k];
-            const uint32_t e = min((uint32_t)PE, cnt - o);
-            for (uint32_t k = 0; k < e; ++k) {
-                atomicAdd(&sm.cnt[(uint32_t)(key >> (g.KB - PDIG))], 1u);
-                key = ((key << g.B) | sm.tb[o + k + g.D]) & g.mask;
-            }
-        }
-    }
+    const uint32_t B = c.L.geo[slot].B;
+    const uint64_t* pss = c.scr.K + (uint64_t)slot * c.scr.stride;
+    for (int i = threadIdx.x; i < PNB; i += PT) cnt[i] = 0;
     __syncthreads();
-    uint32_t* th = reinterpret_cast<uint32_t*>(c.scr.K + (uint64_t)slot * c.scr.stride) + (uint64_t)tile * PNB;
-    for (int i = tid; i < PNB; i += PT) th[i] = sm.cnt[i];
+    const uint32_t e = n - t0 < (uint32_t)PTILE ? n - t0 : (uint32_t)PTILE;
+    for (uint32_t k = threadIdx.x; k < e; k += PT)
+        atomicAdd(&cnt[(uint32_t)pss_bits(pss, (uint64_t)(t0 + k) * B, PDIG)], 1u);
+    __syncthreads();
+    uint32_t* th = tile_hist(c, slot) + (uint64_t)tile * PNB;
+    for (int i = threadIdx.x; i < PNB; i += PT) th[i] = cnt[i];
 }
 
 // ---------------------------------------------------------------------------
@@ -260,21 +324,11 @@ constexpr int ST = 1024;              // k3_scan threads: 4 buckets each
 __global__ void __launch_bounds__(ST) k3_scan(Ctx c)
 {
     __shared__ uint32_t scan_sh[ST / 64 + 1];
-    __shared__ uint8_t sym[256];
     const int tid = threadIdx.x;
     const uint32_t slot = blockIdx.x, b = c.b0 + slot;
     const uint32_t n = c.blocks[b].n;
-    uint32_t nin;
-    load_sym(c.blocks[b], sym, &nin);
-    const KeyGeo g = key_geo(nin);
-    if (tid == 0) {
-        c.blocks[b].n_in_use = nin;
-        c.L.sD[slot] = (uint32_t)g.D;
-        c.L.sDp[slot] = (uint32_t)((64 - PDIG) / g.B);
-    }
-    if (tid < 256) c.L.sym[(uint64_t)slot * 256 + tid] = sym[tid];
     const uint32_t ntile = (n + PTILE - 1) / PTILE;
-    uint4* th = reinterpret_cast<uint4*>(c.scr.K + (uint64_t)slot * c.scr.stride);   // [tile][PNB/4]
+    uint4* th = reinterpret_cast<uint4*>(tile_hist(c, slot));   // [tile][PNB/4]
     uint4* tot = th + (uint64_t)MAXT * (PNB / 4);
     uint4 a = make_uint4(0, 0, 0, 0);
     for (uint32_t k = 0; k < ntile; ++k) {
@@ -291,7 +345,7 @@ __global__ void __launch_bounds__(ST) k3_scan(Ctx c)
         x = run;
         run.x += v.x; run.y += v.y; run.z += v.z; run.w += v.w;
     }
-    const uint32_t shift = (uint32_t)(g.KB - PDIG);
+    const uint32_t shift = c.L.geo[slot].KB - PDIG;
     const uint32_t cnt4[4] = {a.x, a.y, a.z, a.w};
     uint32_t st = pre;
 #pragma unroll
@@ -302,68 +356,129 @@ __global__ void __launch_bounds__(ST) k3_scan(Ctx c)
 }
 
 // ---------------------------------------------------------------------------
-// k3_scatter: (key, rotation) -> bucket order in (K2, SA); singletons final
+// k3_scatter: rotations -> bucket order in SA (persistent, per-XCD block
+// streams: queue x holds the tiles of blocks x, x+8, ... in order)
 // ---------------------------------------------------------------------------
-// Workgroup L of a 1-D grid -> (slot, tile) with slot = L mod 8 inside each
-// group of 8 slots: workgroups are dealt round-robin over the 8 XCDs, so all
-// tiles of a block run on one XCD and its scattered writes meet in one L2
-// (placement is a speed matter only, MI355X_MICROARCH.md "Workgroup dispatch").
-__device__ __forceinline__ bool xcd_slot_tile(uint32_t L, uint32_t ntile, uint32_t nb, uint32_t& slot,
-                                              uint32_t& tile)
+constexpr int SCT = 1024;
+
+__global__ void __launch_bounds__(SCT) k3_scatter(Ctx c)
 {
-    const uint32_t grp = L / (8u * ntile), r = L % (8u * ntile);
-    slot = grp * 8u + (r & 7u);
-    tile = r >> 3;
-    return slot < nb;
+    __shared__ uint32_t cur[PNB], tot[PNB];
+    __shared__ uint32_t qs[8];
+    __shared__ uint32_t job_sh;
+    const int tid = threadIdx.x;
+    const uint32_t x = xcc_id();
+    if (tid < 8) qs[tid] = ((uint32_t)tid < c.nb ? (c.nb - tid + 7) / 8 : 0u) * MAXT;
+    __syncthreads();
+    for (;;) {
+        const uint32_t job = wg_pop(c, qs, &job_sh, x);
+        if (job == 0xFFFFFFFFu) break;
+        const uint32_t y = job >> 28, k = job & 0x0FFFFFFFu;
+        const uint32_t slot = y + 8u * (k / MAXT), tile = k % MAXT;
+        const uint32_t b = c.b0 + slot;
+        const uint32_t n = c.blocks[b].n;
+        const uint32_t t0 = tile * PTILE;
+        if (t0 >= n) continue;                       // uniform
+        const uint64_t so = (uint64_t)slot * c.scr.stride;
+        const uint32_t* th = tile_hist(c, slot);
+        for (int i = tid; i < PNB; i += SCT) { cur[i] = th[(uint64_t)tile * PNB + i]; tot[i] = th[(uint64_t)MAXT * PNB + i]; }
+        __syncthreads();
+        const uint32_t B = c.L.geo[slot].B;
+        const uint64_t* pss = c.scr.K + so;
+        uint32_t* SA = c.scr.SA + so;
+        const uint32_t e = n - t0 < (uint32_t)PTILE ? n - t0 : (uint32_t)PTILE;
+        for (uint32_t q = tid; q < e; q += SCT) {
+            const uint32_t r = t0 + q;
+            const uint32_t d = (uint32_t)pss_bits(pss, (uint64_t)r * B, PDIG);
+            const uint32_t p = atomicAdd(&cur[d], 1u);
+            SA[p] = r;
+            if (r == 0 && tot[d] == 1u) c.blocks[b].orig_ptr = p;
+        }
+        __syncthreads();
+    }
 }
 
-__global__ void __launch_bounds__(PT) k3_scatter(Ctx c, uint32_t nb)
+// ---------------------------------------------------------------------------
+// binning of a work list by block into per-XCD segments (blocks x, x+8, ...)
+// ---------------------------------------------------------------------------
+constexpr uint32_t BIN_CH = 8192;     // items per binning workgroup (at least)
+constexpr uint32_t BIN_MAXWG = 1024;
+
+__global__ void __launch_bounds__(256) k3_bin_hist(const uint64_t* __restrict__ in, uint32_t n, uint32_t nb,
+                                                    uint32_t ch, uint32_t* __restrict__ hist)
 {
-    __shared__ PartSmem sm;
+    __shared__ uint32_t h[4096];
+    for (uint32_t i = threadIdx.x; i < nb; i += 256) h[i] = 0;
+    __syncthreads();
+    const uint32_t a = blockIdx.x * ch, e = a + ch < n ? a + ch : n;
+    for (uint32_t i = a + threadIdx.x; i < e; i += 256) atomicAdd(&h[it_slot(in[i])], 1u);
+    __syncthreads();
+    for (uint32_t i = threadIdx.x; i < nb; i += 256) hist[(uint64_t)blockIdx.x * nb + i] = h[i];
+}
+
+// one workgroup: per-block totals, XCD-ordered exclusive scan, per-(chunk,
+// block) write offsets in place; seg[x] = start of XCD x's segment
+__global__ void __launch_bounds__(1024) k3_bin_scan(uint32_t* __restrict__ hist, uint32_t nwg, uint32_t nb,
+                                                     uint32_t* __restrict__ seg)
+{
+    __shared__ uint32_t tot[4096];
+    __shared__ uint32_t scan_sh[1024 / 64 + 1];
     const int tid = threadIdx.x;
-    uint32_t slot, tile;
-    if (!xcd_slot_tile(blockIdx.x, MAXT, nb, slot, tile)) return;
-    const uint32_t b = c.b0 + slot;
-    const uint32_t n = c.blocks[b].n;
-    const uint32_t t0 = tile * PTILE;
-    if (t0 >= n) return;
-    uint32_t nin;
-    load_sym(c.blocks[b], sm.sym, &nin);
-    const KeyGeo g = key_geo(nin);
-    const uint8_t* blk = c.blkbytes + (uint64_t)b * c.stride;
-    const uint64_t so = (uint64_t)slot * c.scr.stride;
-    const uint32_t* th = reinterpret_cast<const uint32_t*>(c.scr.K + so) + (uint64_t)tile * PNB;
-    const uint32_t* tot = reinterpret_cast<const uint32_t*>(c.scr.K + so) + (uint64_t)MAXT * PNB;
-    for (int i = tid; i < PNB; i += PT) { sm.cnt[i] = th[i]; sm.tot[i] = tot[i]; }
-    uint64_t* K2 = c.scr.K2 + so;
-    uint32_t* SA = c.scr.SA + so;
-    for (uint32_t sub = 0; sub < PSUBS; ++sub) {
-        const uint32_t r0 = t0 + sub * PSUB;
-        if (r0 >= n) break;
-        const uint32_t cnt = min((uint32_t)PSUB, n - r0);
-        __syncthreads();
-        load_text(blk, n, r0, cnt, g.D, sm.sym, sm.tb);
-        __syncthreads();
-        const uint32_t o = tid * PE;
-        if (o < cnt) {
-            uint64_t key = 0;
-            for (int k = 0; k < g.D; ++k) key = (key << g.B) | sm.tb[o + k];
-            const uint32_t e = min((uint32_t)PE, cnt - o);
-            for (uint32_t k = 0; k < e; ++k) {
-                const uint32_t bk = (uint32_t)(key >> (g.KB - PDIG));
-                const uint32_t p = atomicAdd(&sm.cnt[bk], 1u);
-                const uint32_t r = r0 + o + k;
-                K2[p] = key;
-                SA[p] = r;
-                if (r == 0 && sm.tot[bk] == 1u) c.blocks[b].orig_ptr = p;
-                key = ((key << g.B) | sm.tb[o + k + g.D]) & g.mask;
+    for (uint32_t s = tid; s < nb; s += 1024) {
+        uint32_t t = 0;
+        for (uint32_t w = 0; w < nwg; ++w) t += hist[(uint64_t)w * nb + s];
+        tot[s] = t;
+    }
+    __syncthreads();
+    const uint32_t NS = (nb + 7) / 8;               // blocks per XCD segment (upper bound)
+    // XCD-ordered sequence j -> block s = (j / NS) + 8 * (j % NS); 4 entries per thread
+    uint32_t v[4], sum = 0;
+#pragma unroll
+    for (int q = 0; q < 4; ++q) {
+        const uint32_t j = tid * 4 + q;
+        const uint32_t s = (j / NS) + 8u * (j % NS);
+        v[q] = (j < 8 * NS && s < nb) ? tot[s] : 0u;
+        sum += v[q];
+    }
+    uint32_t total = 0;
+    uint32_t run = block_excl_scan_add<uint32_t>(sum, scan_sh, &total);
+#pragma unroll
+    for (int q = 0; q < 4; ++q) {
+        const uint32_t j = tid * 4 + q;
+        const uint32_t s = (j / NS) + 8u * (j % NS);
+        if (j < 8 * NS && (j % NS) == 0) seg[j / NS] = run;
+        if (j < 8 * NS && s < nb) {
+            uint32_t r = run;
+            for (uint32_t w = 0; w < nwg; ++w) {
+                uint32_t& hv = hist[(uint64_t)w * nb + s];
+                const uint32_t t = hv;
+                hv = r;
+                r += t;
             }
         }
+        run += v[q];
+    }
+    if (tid == 0) seg[8] = total;
+}
+
+__global__ void __launch_bounds__(256) k3_bin_scatter(const uint64_t* __restrict__ in, uint32_t n, uint32_t nb,
+                                                       uint32_t ch, const uint32_t* __restrict__ hist,
+                                                       uint64_t* __restrict__ out)
+{
+    __shared__ uint32_t cur[4096];
+    for (uint32_t i = threadIdx.x; i < nb; i += 256) cur[i] = hist[(uint64_t)blockIdx.x * nb + i];
+    __syncthreads();
+    const uint32_t a = blockIdx.x * ch, e = a + ch < n ? a + ch : n;
+    for (uint32_t i = a + threadIdx.x; i < e; i += 256) {
+        const uint64_t it = in[i];
+        out[atomicAdd(&cur[it_slot(it)], 1u)] = it;
     }
 }
 
 // ---------------------------------------------------------------------------
 // k3_part_l: MSD partition of one large group on its next <= 8 key bits
+// (persistent over a binned list; values ping-pong SA <-> V, and in doubling
+// mode the K2 <-> K keys with them)
 // ---------------------------------------------------------------------------
 constexpr int LT = 512;
 constexpr int LW = LT / 64;
@@ -374,87 +489,97 @@ __global__ void __launch_bounds__(LT) k3_part_l(Ctx c, const uint64_t* __restric
     __shared__ uint32_t st[256], cur[256], cntd[256];
     __shared__ uint32_t scan_sh[LW + 1];
     __shared__ uint32_t big[257];
+    __shared__ uint32_t qs[8];
+    __shared__ uint32_t job_sh;
     const int tid = threadIdx.x, wid = tid >> 6;
-    const uint64_t item = items[blockIdx.x];
-    const uint32_t slot = it_slot(item), s = it_start(item), m = it_size(item), shift = it_shift(item),
-                   par = it_par(item);
-    const uint32_t b = c.b0 + slot;
-    const uint64_t base = (uint64_t)slot * c.scr.stride + s;
-    const uint64_t* sk = (par ? c.scr.K : c.scr.K2) + base;
-    const uint32_t* sv = (par ? c.scr.V : c.scr.SA) + base;
-    uint64_t* dk = (par ? c.scr.K2 : c.scr.K) + base;
-    uint32_t* dv = (par ? c.scr.SA : c.scr.V) + base;
-    uint32_t* SA = c.scr.SA + base;
-    uint32_t* RK = c.scr.RK + (uint64_t)slot * c.scr.stride;
-    const uint32_t n = c.blocks[b].n;
-    const uint8_t* blk = c.blkbytes + (uint64_t)b * c.stride;
-    const uint32_t db = shift < 8 ? shift : 8;
-    const uint32_t sh2 = shift - db;
-    const uint64_t dmask = (1ull << db) - 1ull;
-    for (int i = tid; i < LW * 256; i += LT) (&wh[0][0])[i] = 0;
-    if (tid == 0) big[256] = 0;
-    __syncthreads();
-    for (uint32_t i = tid; i < m; i += LT) atomicAdd(&wh[wid][(uint32_t)((sk[i] >> sh2) & dmask)], 1u);
-    __syncthreads();
-    uint32_t tcount = 0;
-    if (tid < 256) for (int w = 0; w < LW; ++w) tcount += wh[w][tid];
-    const uint32_t pre = block_excl_scan_add<uint32_t>(tid < 256 ? tcount : 0u, scan_sh, (uint32_t*)nullptr);
-    if (tid < 256) { st[tid] = pre; cur[tid] = pre; cntd[tid] = tcount; }
-    __syncthreads();
-    for (uint32_t i = tid; i < m; i += LT) {
-        const uint64_t k = sk[i];
-        const uint32_t p = atomicAdd(&cur[(uint32_t)((k >> sh2) & dmask)], 1u);
-        dk[p] = k;
-        dv[p] = sv[i];
-    }
-    __syncthreads();
-    uint32_t nruns = 0;
-    if (tid < 256) {
-        const uint32_t cc = cntd[tid], ss = st[tid];
-        if (cc == 1) {
-            const uint32_t v = dv[ss];
-            if (!par) SA[ss] = v;
-            if (c.mode) RK[v] = s + ss;
-            if (v == 0) c.blocks[b].orig_ptr = s + ss;
-            nruns = 1;
-        } else if (cc > M3_MAX && sh2 == 0) {
-            big[atomicAdd(&big[256], 1u)] = tid;   // all keys equal: one group
-            nruns = 1;
+    const uint32_t x = xcc_id();
+    load_qsizes_binned(c, qs);
+    for (;;) {
+        const uint32_t job = wg_pop(c, qs, &job_sh, x);
+        if (job == 0xFFFFFFFFu) break;
+        const uint64_t item = items[c.qseg[job >> 28] + (job & 0x0FFFFFFFu)];
+        const uint32_t slot = it_slot(item), s = it_start(item), m = it_size(item), shift = it_shift(item),
+                       par = it_par(item);
+        const uint32_t b = c.b0 + slot;
+        const uint64_t so = (uint64_t)slot * c.scr.stride;
+        const uint64_t base = so + s;
+        const KeySrc ks = key_src(c, slot, par);
+        const uint32_t* sv = (par ? c.scr.V : c.scr.SA) + base;
+        uint32_t* dv = (par ? c.scr.SA : c.scr.V) + base;
+        uint64_t* dk = (par ? c.scr.K2 : c.scr.K) + base;      // doubling keys only
+        uint32_t* SA = c.scr.SA + base;
+        uint32_t* RK = c.scr.RK + so;
+        const uint32_t db = shift < 8 ? shift : 8;
+        const uint32_t sh2 = shift - db;
+        const uint64_t dmask = (1ull << db) - 1ull;
+        for (int i = tid; i < LW * 256; i += LT) (&wh[0][0])[i] = 0;
+        if (tid == 0) big[256] = 0;
+        __syncthreads();
+        for (uint32_t i = tid; i < m; i += LT)
+            atomicAdd(&wh[wid][(uint32_t)((ks(s + i, sv[i]) >> sh2) & dmask)], 1u);
+        __syncthreads();
+        uint32_t tcount = 0;
+        if (tid < 256) for (int w = 0; w < LW; ++w) tcount += wh[w][tid];
+        const uint32_t pre = block_excl_scan_add<uint32_t>(tid < 256 ? tcount : 0u, scan_sh, (uint32_t*)nullptr);
+        if (tid < 256) { st[tid] = pre; cur[tid] = pre; cntd[tid] = tcount; }
+        __syncthreads();
+        for (uint32_t i = tid; i < m; i += LT) {
+            const uint32_t v = sv[i];
+            const uint64_t k = ks(s + i, v);
+            const uint32_t p = atomicAdd(&cur[(uint32_t)((k >> sh2) & dmask)], 1u);
+            dv[p] = v;
+            if (c.keysrc) dk[p] = k;
         }
-    }
-    if (tid < 256) {
-        const uint32_t cc = cntd[tid];
-        const bool push = cc >= 2 && !(cc > M3_MAX && sh2 == 0);
-        wave_classify(c, push, slot, s + st[tid], cc, sh2, par ^ 1u);
-    }
-    if (tid < 256) {
-        const uint32_t r = wave_reduce_add(nruns);
-        if (c.mode && (tid & 63) == 0 && r) atomicAdd(&c.L.runs[slot], r);
-    }
-    __syncthreads();
-    const uint32_t nbig = big[256];
-    for (uint32_t q = 0; q < nbig; ++q) {
-        const uint32_t d = big[q];
-        const uint32_t ss = st[d], cc = cntd[d];
-        for (uint32_t i = tid; i < cc; i += LT) {
-            const uint32_t v = dv[ss + i];
-            if (!par) SA[ss + i] = v;
-            if (c.mode) RK[v] = s + ss;
-            if (v == 0) c.blocks[b].orig_ptr = s + ss + i;
+        __syncthreads();
+        uint32_t nruns = 0;
+        if (tid < 256) {
+            const uint32_t cc = cntd[tid], ss = st[tid];
+            if (cc == 1) {
+                const uint32_t v = dv[ss];
+                if (!par) SA[ss] = v;
+                if (c.mode) RK[v] = s + ss;
+                if (v == 0) c.blocks[b].orig_ptr = s + ss;
+                nruns = 1;
+            } else if (cc > M3_MAX && sh2 == 0) {
+                big[atomicAdd(&big[256], 1u)] = tid;   // all keys equal: one group
+                nruns = 1;
+            }
         }
-        if (tid == 0) {
-            const uint32_t o = atomicAdd(c.L.ctr + C_T0 + c.tsel, 1u);
-            c.L.t[c.tsel][o] = mk_item(slot, s + ss, cc, 0, 0);
-            atomicAdd(c.L.ctr + C_TS0 + c.tsel, cc);
+        if (tid < 256) {
+            const uint32_t cc = cntd[tid];
+            const bool push = cc >= 2 && !(cc > M3_MAX && sh2 == 0);
+            wave_classify(c, push, slot, s + st[tid], cc, sh2, par ^ 1u);
         }
+        if (tid < 256) {
+            const uint32_t r = wave_reduce_add(nruns);
+            if (c.mode && (tid & 63) == 0 && r) atomicAdd(&c.L.runs[slot], r);
+        }
+        __syncthreads();
+        const uint32_t nbig = big[256];
+        for (uint32_t q = 0; q < nbig; ++q) {
+            const uint32_t d = big[q];
+            const uint32_t ss = st[d], cc = cntd[d];
+            for (uint32_t i = tid; i < cc; i += LT) {
+                const uint32_t v = dv[ss + i];
+                if (!par) SA[ss + i] = v;
+                if (c.mode) RK[v] = s + ss;
+                if (v == 0) c.blocks[b].orig_ptr = s + ss + i;
+            }
+            if (tid == 0) {
+                const uint32_t o = atomicAdd(c.L.ctr + C_T0 + c.tsel, 1u);
+                c.L.t[c.tsel][o] = mk_item(slot, s + ss, cc, 0, 0);
+                atomicAdd(c.L.ctr + C_TS0 + c.tsel, cc);
+            }
+        }
+        __syncthreads();
     }
 }
 
 // Finish a sorted group: SA, RK, origPtr, tie groups, run count.
 // Called by every thread of a wave with (j = sorted position in the group,
-// key, val, valid, hp = head position of j's run, end = j ends its run).
+// v = rotation, valid, hp = head position of j's run, end = j ends its run).
 __device__ __forceinline__ void emit_sorted(const Ctx& c, uint32_t slot, uint32_t s, uint32_t j, uint32_t v,
-                                            uint32_t llb, bool valid, uint32_t hp, bool end, uint32_t& runs_acc)
+                                            bool valid, uint32_t hp, bool end, uint32_t& runs_acc)
 {
     const uint64_t so = (uint64_t)slot * c.scr.stride;
     if (valid) {
@@ -473,52 +598,58 @@ __device__ __forceinline__ void emit_sorted(const Ctx& c, uint32_t slot, uint32_
 }
 
 // ---------------------------------------------------------------------------
-// k3_sort_w: groups of <= 64, one wave each
+// k3_sort_w: groups of <= 64, one wave each (persistent, per wave)
 // ---------------------------------------------------------------------------
-__global__ void __launch_bounds__(256) k3_sort_w(Ctx c, const uint64_t* __restrict__ items, uint32_t nitems)
+__global__ void __launch_bounds__(256) k3_sort_w(Ctx c, const uint64_t* __restrict__ items)
 {
     __shared__ uint64_t skey[4][W_MAX + 1];
     __shared__ uint32_t sval[4][W_MAX];
     const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
-    const uint32_t idx = blockIdx.x * 4 + wid;
-    if (idx >= nitems) return;                     // whole wave; no workgroup barrier below
-    const uint64_t item = items[idx];
-    const uint32_t slot = it_slot(item), s = it_start(item), m = it_size(item), par = it_par(item);
-    const uint64_t base = (uint64_t)slot * c.scr.stride + s;
-    const uint64_t* sk = (par ? c.scr.K : c.scr.K2) + base;
-    const uint32_t* sv = (par ? c.scr.V : c.scr.SA) + base;
-    const bool valid = (uint32_t)lane < m;
-    const uint64_t k = valid ? sk[lane] : ~0ull;
-    const uint32_t v = valid ? sv[lane] : 0u;
-    const uint32_t vl = v;
-    uint32_t r = 0;
-    for (uint32_t j = 0; j < m; ++j) {
-        const uint64_t kj = __shfl(k, (int)j, 64);
-        r += (kj < k || (kj == k && (int)j < lane)) ? 1u : 0u;
+    // static assignment: workgroup L works XCD segment L mod 8 (the XCD it runs
+    // on under round-robin dealing), its waves striding over the segment
+    const uint32_t xs = blockIdx.x & 7u, nwk = (gridDim.x >> 3) * 4u;
+    const uint32_t e_end = c.qseg[xs + 1];
+    for (uint32_t it = c.qseg[xs] + (blockIdx.x >> 3) * 4u + wid; it < e_end; it += nwk) {
+        const uint64_t item = items[it];
+        const uint32_t slot = it_slot(item), s = it_start(item), m = it_size(item), par = it_par(item);
+        const uint64_t base = (uint64_t)slot * c.scr.stride + s;
+        const uint32_t* sv = (par ? c.scr.V : c.scr.SA) + base;
+        const KeySrc ks = key_src(c, slot, par);
+        const bool valid = (uint32_t)lane < m;
+        const uint32_t v = valid ? sv[lane] : 0u;
+        const uint64_t k = valid ? ks(s + lane, v) : ~0ull;
+        uint32_t r = 0;
+        for (uint32_t j = 0; j < m; ++j) {
+            const uint64_t kj = __shfl(k, (int)j, 64);
+            r += (kj < k || (kj == k && (int)j < lane)) ? 1u : 0u;
+        }
+        wave_sync_lds3();                                // previous group's reads are done
+        if (valid) { skey[wid][r] = k; sval[wid][r] = v; }
+        wave_sync_lds3();
+        const uint64_t key = valid ? skey[wid][lane] : 0;
+        const uint32_t val = valid ? sval[wid][lane] : 0;
+        const bool head = valid && (lane == 0 || skey[wid][lane - 1] != key);
+        const bool end = valid && ((uint32_t)lane + 1 == m || skey[wid][lane + 1] != key);
+        const uint32_t hp = wave_incl_scan_max<uint32_t>(head ? (uint32_t)lane : 0u);
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");   // SA reads of this group done before the writes
+        uint32_t runs = 0;
+        emit_sorted(c, slot, s, (uint32_t)lane, val, valid, hp, end, runs);
+        if (c.mode && lane == 0) atomicAdd(&c.L.runs[slot], runs);
     }
-    if (valid) { skey[wid][r] = k; sval[wid][r] = vl; }
-    wave_sync_lds3();
-    const uint64_t key = valid ? skey[wid][lane] : 0;
-    const uint32_t val = valid ? sval[wid][lane] : 0;
-    const bool head = valid && (lane == 0 || skey[wid][lane - 1] != key);
-    const bool end = valid && ((uint32_t)lane + 1 == m || skey[wid][lane + 1] != key);
-    const uint32_t hp = wave_incl_scan_max<uint32_t>(head ? (uint32_t)lane : 0u);
-    uint32_t runs = 0;
-    emit_sorted(c, slot, s, (uint32_t)lane, val, 0u, valid, hp, end, runs);
-    if (c.mode && lane == 0) atomicAdd(&c.L.runs[slot], runs);
 }
 
 // ---------------------------------------------------------------------------
 // k3_sort_lds<NW, E>: groups of <= NW*64*E rotations sorted by NW waves
 // (NW = 1: four independent wave-private sorts per workgroup, no workgroup
-// barrier; NW = 4: one group per workgroup).  Stable LSD radix on 8-bit
-// digits over only the key bits that vary inside the group.  The group-local
-// index rides in the key's constant top bits (every group's keys share at
-// least 12 top bits: the bucket digit, the partition digits, or the unused
-// bits of a < 2^20 rank), so each pass exchanges one u64 per element through
-// LDS.  Ranking: 8 ballots give each lane its peers with the same digit; one
-// lane per peer set adds the set's size to the wave's digit counter with a
-// returning LDS atomic (all E atomics in flight, in program order).
+// barrier; NW = 4: one group per workgroup).  Persistent over a binned list.
+// The group-local index rides in the key's constant top bits (every group's
+// keys share at least 12 top bits: the bucket digit, the partition digits, or
+// unused high bits), so each exchange moves one u64 per element through LDS.
+// Primary path: one MSD digit (the DB bits below the highest varying bit),
+// then every element ranks itself inside its sub-bucket by comparison.  When
+// a sub-bucket exceeds LIMIT: stable LSD radix over the varying 8-bit digits
+// (8 ballots find a lane's digit peers; one lane per peer set adds the set's
+// size to the wave's counter with a returning LDS atomic).
 // ---------------------------------------------------------------------------
 template <int NW>
 __device__ __forceinline__ void gsync()
@@ -528,7 +659,7 @@ __device__ __forceinline__ void gsync()
 }
 
 template <int NW, int E>
-__global__ void __launch_bounds__(256) k3_sort_lds(Ctx c, const uint64_t* __restrict__ items, uint32_t nitems)
+__global__ void __launch_bounds__(256) k3_sort_lds(Ctx c, const uint64_t* __restrict__ items)
 {
     constexpr int IPW = 4 / NW;                    // groups per workgroup
     constexpr int CAP = NW * 64 * E;
@@ -553,20 +684,23 @@ __global__ void __launch_bounds__(256) k3_sort_lds(Ctx c, const uint64_t* __rest
     __shared__ uint32_t flag_all[4];
     const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
     const int g = wave / NW, wid = wave % NW, w0 = g * NW;
-    const uint32_t gi = blockIdx.x * IPW + g;
-    if (gi >= nitems) return;                      // NW = 1: per wave; NW = 4: IPW = 1, whole workgroup
     uint64_t* xk = xk_all[g];
     uint32_t* wcnt = cnt_all[wave];
     uint32_t* sc = sc_all[g];
-    const uint64_t item = items[gi];
+    const uint64_t lt = lanemask_lt();
+    // static assignment: workgroup L works XCD segment L mod 8 (the XCD it runs
+    // on under round-robin dealing); its IPW groups stride over the segment
+    const uint32_t xs = blockIdx.x & 7u, nwk = (gridDim.x >> 3) * (uint32_t)IPW;
+    const uint32_t e_end = c.qseg[xs + 1];
+    for (uint32_t it = c.qseg[xs] + (blockIdx.x >> 3) * (uint32_t)IPW + (uint32_t)g; it < e_end; it += nwk) {
+    const uint64_t item = items[it];
     const uint32_t slot = it_slot(item), s = it_start(item), m = it_size(item), par = it_par(item);
     const uint64_t base = (uint64_t)slot * c.scr.stride + s;
-    const uint64_t* sk = (par ? c.scr.K : c.scr.K2) + base;
     const uint32_t* sv = (par ? c.scr.V : c.scr.SA) + base;
-    const uint64_t lt = lanemask_lt();
+    const KeySrc ks = key_src(c, slot, par);
+    gsync<NW>();                                   // the previous group's LDS reads are done
 
     uint64_t k[E];
-    const uint64_t k0 = sk[0];
     uint64_t diff = 0;
     {
         uint32_t vv[E];
@@ -575,13 +709,14 @@ __global__ void __launch_bounds__(256) k3_sort_lds(Ctx c, const uint64_t* __rest
             const uint32_t i = (uint32_t)(wid * 64 * E + e * 64 + lane);
             vv[e] = i < m ? sv[i] : 0u;
         }
+        const uint64_t k0 = ks(s, sv[0]);
 #pragma unroll
         for (int e = 0; e < E; ++e) {
             const uint32_t i = (uint32_t)(wid * 64 * E + e * 64 + lane);
             if (i < m) {
-                const uint64_t x = sk[i];
-                diff |= x ^ k0;
-                k[e] = (x & KMASK) | ((uint64_t)i << KEYB);
+                const uint64_t kx = ks(s + i, vv[e]);
+                diff |= kx ^ k0;
+                k[e] = (kx & KMASK) | ((uint64_t)i << KEYB);
                 vb_all[g][i] = vv[e];
             } else {
                 k[e] = ~0ull;                          // pads: max key, last in stable order
@@ -602,8 +737,6 @@ __global__ void __launch_bounds__(256) k3_sort_lds(Ctx c, const uint64_t* __rest
     bool moved = false;
     const uint64_t kdiff = diff & KMASK;
     if (kdiff) {
-        // ---- one MSD digit (the DB bits below the highest varying bit), then every
-        // element ranks itself inside its sub-bucket by direct comparison ----
         uint32_t* bst = bst_all[g];
         uint32_t* bcur = bcur_all[g];
         const int tg = wid * 64 + lane;
@@ -724,9 +857,9 @@ __global__ void __launch_bounds__(256) k3_sort_lds(Ctx c, const uint64_t* __rest
                 uint32_t r = run;
 #pragma unroll
                 for (int w = 0; w < NW; ++w) {
-                    const uint32_t x = cnt_all[w0 + w][t * DPT + q];
+                    const uint32_t xx = cnt_all[w0 + w][t * DPT + q];
                     cnt_all[w0 + w][t * DPT + q] = r;
-                    r += x;
+                    r += xx;
                 }
                 run += loc[q];
             }
@@ -769,10 +902,10 @@ __global__ void __launch_bounds__(256) k3_sort_lds(Ctx c, const uint64_t* __rest
         for (int e = 0; e < E; ++e) {
             const uint32_t j = (uint32_t)(wid * 64 * E + e * 64 + lane);
             const bool head = j < m && (j == 0 || ((xk[j - 1] ^ k[e]) & KMASK) != 0);
-            uint32_t x = wave_incl_scan_max<uint32_t>(head ? j : 0u);
-            x = x > carry ? x : carry;
-            hp[e] = x;
-            carry = __shfl(x, 63, 64);
+            uint32_t xx = wave_incl_scan_max<uint32_t>(head ? j : 0u);
+            xx = xx > carry ? xx : carry;
+            hp[e] = xx;
+            carry = __shfl(xx, 63, 64);
         }
         if constexpr (NW > 1) {
             if (lane == 0) wmax_all[wave] = carry;
@@ -783,8 +916,9 @@ __global__ void __launch_bounds__(256) k3_sort_lds(Ctx c, const uint64_t* __rest
             for (int e = 0; e < E; ++e) hp[e] = hp[e] > pre ? hp[e] : pre;
         }
     }
-    // values were loaded (and their last-column bytes gathered) before the sort;
-    // every global read of the group's SA range happened before any write
+    // values were loaded before the sort; every global read of the group's SA
+    // range happened before any write (vmcnt drain, and the barriers above)
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     uint32_t runs = 0;
 #pragma unroll
     for (int e = 0; e < E; ++e) {
@@ -792,9 +926,26 @@ __global__ void __launch_bounds__(256) k3_sort_lds(Ctx c, const uint64_t* __rest
         const bool valid = j < m;
         const uint32_t vb = valid ? vb_all[g][(uint32_t)(k[e] >> KEYB)] : 0u;
         const bool end = valid && (!ties || j + 1 == m || ((xk[j + 1] ^ k[e]) & KMASK) != 0);
-        emit_sorted(c, slot, s, j, vb, 0u, valid, hp[e], end, runs);
+        emit_sorted(c, slot, s, j, vb, valid, hp[e], end, runs);
     }
     if (c.mode && lane == 0 && runs) atomicAdd(&c.L.runs[slot], runs);
+    }
+}
+
+// ---------------------------------------------------------------------------
+// text rounds: classify the tie groups (keys come from the PSS at an offset)
+// ---------------------------------------------------------------------------
+__global__ void __launch_bounds__(256) k3_classify_text(Ctx c, const uint64_t* __restrict__ items, uint32_t nitems)
+{
+    const int lane = threadIdx.x & 63;
+    const uint32_t i = blockIdx.x * 256 + threadIdx.x;
+    const bool active = i < nitems;
+    const uint64_t item = active ? items[i] : 0;
+    const uint32_t slot = it_slot(item), s = it_start(item), m = it_size(item);
+    const Geo g = c.L.geo[active ? slot : 0];
+    wave_classify(c, active, slot, s, m, g.Dp * g.B, 0);
+    const uint32_t tied = wave_reduce_add<uint32_t>(active ? m : 0u);
+    if (lane == 0 && tied) atomicAdd(&c.L.ctr[C_TIE_ELEMS], tied);
 }
 
 // ---------------------------------------------------------------------------
@@ -813,7 +964,8 @@ __global__ void __launch_bounds__(256) k3_gather(Ctx c, const uint64_t* __restri
     if (active) {
         active = c.L.periodic[slot] == 0;
         n = c.blocks[c.b0 + slot].n;
-        const uint64_t h = ((uint64_t)c.L.sD[slot] + (uint64_t)rtext * c.L.sDp[slot]) << (round - 1);
+        const Geo g = c.L.geo[slot];
+        const uint64_t h = ((uint64_t)g.D + (uint64_t)rtext * g.Dp) << (round - 1);
         if (active && h >= n) {   // sorted on >= n symbols: remaining ties are equal rotations
             c.L.periodic[slot] = 1;
             active = false;
@@ -843,65 +995,6 @@ __global__ void __launch_bounds__(256) k3_gather(Ctx c, const uint64_t* __restri
     }
     wave_classify(c, active, slot, s, m, RBITS, 0);
     if (active) atomicAdd(&c.L.gin[slot], 1u);
-    const uint32_t tied = wave_reduce_add<uint32_t>(active ? m : 0u);
-    if (lane == 0 && tied) atomicAdd(&c.L.ctr[C_TIE_ELEMS], tied);
-}
-
-// text round r >= 1: key(q) = D' symbols of rotation SA[q] starting D + (r-1)*D'
-// symbols in (the group already agrees on everything before that)
-__device__ __forceinline__ uint64_t text_key(const uint8_t* blk, const uint8_t* sym, uint32_t n, uint32_t pos,
-                                             uint32_t Dp, uint32_t B)
-{
-    uint64_t key = 0;
-    for (uint32_t k = 0; k < Dp; ++k) {
-        key = (key << B) | sym[blk[pos]];
-        if (++pos == n) pos = 0;
-    }
-    return key;
-}
-
-__global__ void __launch_bounds__(256) k3_gather_text(Ctx c, const uint64_t* __restrict__ items, uint32_t nitems,
-                                                       uint32_t r)
-{
-    const int lane = threadIdx.x & 63;
-    const uint32_t i = blockIdx.x * 256 + threadIdx.x;
-    const bool active = i < nitems;
-    const uint64_t item = active ? items[i] : 0;
-    const uint32_t slot = it_slot(item), s = it_start(item), m = it_size(item);
-    const uint32_t b = c.b0 + slot;
-    const uint32_t n = c.blocks[b].n;
-    const uint32_t D = c.L.sD[slot], Dp = c.L.sDp[slot];
-    uint32_t B = 8;
-    for (uint32_t q = 1; q <= 8; ++q)
-        if (64 / q == D) { B = q; break; }       // D = 64 / B is distinct for B = 1..8
-    const uint32_t off = (uint32_t)(((uint64_t)D + (uint64_t)(r - 1) * Dp) % n);
-    const uint8_t* blk = c.blkbytes + (uint64_t)b * c.stride;
-    const uint8_t* sym = c.L.sym + (uint64_t)slot * 256;
-    const uint64_t so = (uint64_t)slot * c.scr.stride;
-    if (active && m <= 64) {
-        for (uint32_t q = s; q < s + m; ++q) {
-            uint32_t pos = c.scr.SA[so + q] + off;
-            if (pos >= n) pos -= n;
-            c.scr.K2[so + q] = text_key(blk, sym, n, pos, Dp, B);
-        }
-    }
-    uint64_t bigm = __ballot(active && m > 64);
-    while (bigm) {
-        const int l = __ffsll((unsigned long long)bigm) - 1;
-        bigm &= bigm - 1;
-        const uint32_t ls = __shfl(s, l, 64), lm = __shfl(m, l, 64), lslot = __shfl(slot, l, 64);
-        const uint32_t ln = __shfl(n, l, 64), loff = __shfl(off, l, 64), lDp = __shfl(Dp, l, 64),
-                       lB = __shfl(B, l, 64);
-        const uint8_t* lblk = c.blkbytes + (uint64_t)(c.b0 + lslot) * c.stride;
-        const uint8_t* lsym = c.L.sym + (uint64_t)lslot * 256;
-        const uint64_t lso = (uint64_t)lslot * c.scr.stride;
-        for (uint32_t q = ls + lane; q < ls + lm; q += 64) {
-            uint32_t pos = c.scr.SA[lso + q] + loff;
-            if (pos >= ln) pos -= ln;
-            c.scr.K2[lso + q] = text_key(lblk, lsym, ln, pos, lDp, lB);
-        }
-    }
-    wave_classify(c, active, slot, s, m, Dp * B, 0);
     const uint32_t tied = wave_reduce_add<uint32_t>(active ? m : 0u);
     if (lane == 0 && tied) atomicAdd(&c.L.ctr[C_TIE_ELEMS], tied);
 }
@@ -966,11 +1059,15 @@ void launch_bwt3(BlockDesc* blocks, uint32_t b0, uint32_t nb, const uint8_t* blk
 {
     if (nb == 0) return;
     if (nb > 4095) throw StarchError(-2, "bwt3: batch too large");
-    if (2 * scr.stride < (uint64_t)(MAXT + 1) * PNB) throw StarchError(-2, "bwt3: block stride too small");
+    if (pss_words(scr.stride) * 2 + (uint64_t)(MAXT + 1) * PNB > 2 * scr.stride)
+        throw StarchError(-2, "bwt3: block stride too small");
     const uint64_t N = (uint64_t)nb * scr.stride;
     const uint64_t cap_s = N / (W_MAX + 1) + 64, cap_m1 = N / (S_MAX + 1) + 64, cap_m2 = N / (M1_MAX + 1) + 64,
                    cap_m3 = N / (M2_MAX + 1) + 64, cap_l = N / (M3_MAX + 1) + 64;
-    const uint64_t words = C_N * 2 + 7ull * nb + 64ull * nb + 2 * (cap_s + cap_m1 + cap_m2 + cap_m3 + 2 * cap_l) + 64;
+    const uint64_t nwg_bin = BIN_MAXWG;
+    constexpr uint32_t QSETS = 64, QSET = 32;                   // queue heads + segments per launch
+    const uint64_t words = 2 * C_N + 10ull * nb + QSETS * QSET + nwg_bin * nb +
+                           2 * (cap_s + cap_m1 + cap_m2 + cap_m3 + 2 * cap_l) + 64;
     uint32_t* mw = meta.as<uint32_t>(words);
     Ctx c;
     c.blocks = blocks;
@@ -978,16 +1075,17 @@ void launch_bwt3(BlockDesc* blocks, uint32_t b0, uint32_t nb, const uint8_t* blk
     c.blkbytes = blkbytes;
     c.stride = stride;
     c.scr = scr;
+    c.nb = nb;
     c.L.ctr = mw;
-    c.L.sD = mw + 2 * C_N;
-    c.L.gin = c.L.sD + nb;
+    c.L.gin = mw + 2 * C_N;
     c.L.runs = c.L.gin + nb;
     c.L.periodic = c.L.runs + nb;
     c.L.rounds = c.L.periodic + nb;
-    c.L.sDp = c.L.rounds + nb;
-    c.L.tied = c.L.sDp + nb;
-    c.L.sym = reinterpret_cast<uint8_t*>(c.L.tied + nb);
-    uintptr_t p = reinterpret_cast<uintptr_t>(c.L.sym + 256ull * nb);
+    c.L.tied = c.L.rounds + nb;
+    c.L.geo = reinterpret_cast<Geo*>(c.L.tied + nb);            // 4 words per slot
+    uint32_t* qpool = reinterpret_cast<uint32_t*>(c.L.geo + nb);
+    uint32_t* binh = qpool + QSETS * QSET;
+    uintptr_t p = reinterpret_cast<uintptr_t>(binh + nwg_bin * nb);
     p = (p + 7) & ~(uintptr_t)7;
     c.L.s = reinterpret_cast<uint64_t*>(p);
     c.L.m1 = c.L.s + cap_s;
@@ -1001,47 +1099,100 @@ void launch_bwt3(BlockDesc* blocks, uint32_t b0, uint32_t nb, const uint8_t* blk
     c.lsel = 0;
     c.tsel = 0;
     c.mode = 0;
-    HIP_CHECK(hipMemsetAsync(mw, 0, (2 * C_N + 7ull * nb) * sizeof(uint32_t), st));
+    c.keysrc = 0;
+    c.rtext = 0;
+    c.qhead = nullptr;
+    c.qseg = nullptr;
+    HIP_CHECK(hipMemsetAsync(mw, 0, (2 * C_N + 10ull * nb + QSETS * QSET) * sizeof(uint32_t), st));
 
+    uint32_t qnext = 0;
+    auto next_q = [&](uint32_t*& head, uint32_t*& seg) {
+        if (qnext == QSETS) {
+            HIP_CHECK(hipMemsetAsync(qpool, 0, QSETS * QSET * sizeof(uint32_t), st));
+            qnext = 0;
+        }
+        head = qpool + qnext * QSET;
+        seg = head + 16;
+        ++qnext;
+    };
     auto read_ctr = [&]() {
         HIP_CHECK(hipMemcpyAsync(hctr, c.L.ctr, C_N * sizeof(uint32_t), hipMemcpyDeviceToHost, st));
         HIP_CHECK(hipStreamSynchronize(st));
         if (hctr[C_ERR]) throw StarchError(-11, "bwt3: group keys do not share 12 top bits");
     };
-    // partition large groups level by level, then run the leaf sorts
+    int dev = 0;
+    HIP_CHECK(hipGetDevice(&dev));
+    static int ncu = 0;
+    if (!ncu) {
+        hipDeviceProp_t prop;
+        HIP_CHECK(hipGetDeviceProperties(&prop, dev));
+        ncu = prop.multiProcessorCount > 0 ? prop.multiProcessorCount : 256;
+    }
+    // bin a list (n items, device) into `out`; sets c.qseg/c.qhead for the next launch
+    auto bin = [&](const uint64_t* list, uint32_t n, uint64_t* out) {
+        uint32_t* head;
+        uint32_t* seg;
+        next_q(head, seg);
+        uint32_t nwg = (n + BIN_CH - 1) / BIN_CH;
+        if (nwg > BIN_MAXWG) nwg = BIN_MAXWG;
+        const uint32_t ch = (n + nwg - 1) / nwg;
+        hipLaunchKernelGGL(k3_bin_hist, dim3(nwg), dim3(256), 0, st, list, n, nb, ch, binh);
+        hipLaunchKernelGGL(k3_bin_scan, dim3(1), dim3(1024), 0, st, binh, nwg, nb, seg);
+        hipLaunchKernelGGL(k3_bin_scatter, dim3(nwg), dim3(256), 0, st, list, n, nb, ch, binh, out);
+        HIP_CHECK(hipGetLastError());
+        c.qhead = head;
+        c.qseg = seg;
+    };
+    // partition large groups level by level, then run the leaf sorts.  Binned
+    // copies go to K2 (free outside doubling) or, while doubling, to the tie
+    // list the gather has just consumed (capacity N/2 items either way).
     auto sort_groups = [&]() {
+        uint64_t* bout = c.keysrc ? c.L.t[c.tsel ^ 1u] : reinterpret_cast<uint64_t*>(scr.K2);
         uint32_t lsel = 0;
         for (int level = 0;; ++level) {
             read_ctr();
             const uint32_t nl = hctr[C_L0 + lsel];
             if (nl == 0) break;
             if (level > 64) throw StarchError(-10, "bwt3: partition did not converge");
+            bin(c.L.l[lsel], nl, bout);
             c.lsel = lsel ^ 1u;
             HIP_CHECK(hipMemsetAsync(c.L.ctr + C_L0 + (lsel ^ 1u), 0, sizeof(uint32_t), st));
-            hipLaunchKernelGGL(k3_part_l, dim3(nl), dim3(LT), 0, st, c, c.L.l[lsel]);
+            hipLaunchKernelGGL(k3_part_l, dim3(ncu * 2), dim3(LT), 0, st, c, bout);
             HIP_CHECK(hipGetLastError());
             HIP_CHECK(hipMemsetAsync(c.L.ctr + C_L0 + lsel, 0, sizeof(uint32_t), st));
             lsel ^= 1u;
         }
         c.lsel = 0;
         const uint32_t nw = hctr[C_W], ns = hctr[C_S], n1 = hctr[C_M1], n2 = hctr[C_M2], n3 = hctr[C_M3];
-        // largest groups first so the long workgroups start early
-        if (n3) hipLaunchKernelGGL((k3_sort_lds<4, 16>), dim3(n3), dim3(256), 0, st, c, c.L.m3, n3);
-        if (n2) hipLaunchKernelGGL((k3_sort_lds<4, 8>), dim3(n2), dim3(256), 0, st, c, c.L.m2, n2);
-        if (n1) hipLaunchKernelGGL((k3_sort_lds<4, 4>), dim3(n1), dim3(256), 0, st, c, c.L.m1, n1);
-        if (ns) hipLaunchKernelGGL((k3_sort_lds<1, 4>), dim3((ns + 3) / 4), dim3(256), 0, st, c, c.L.s, ns);
-        if (nw) hipLaunchKernelGGL(k3_sort_w, dim3((nw + 3) / 4), dim3(256), 0, st, c, c.L.w, nw);
+        // every launch reads its own binned copy; stream order lets them share one buffer
+        // grids: a multiple of 8 (static per-XCD segments), about one resident wave of workgroups
+        auto g8 = [](uint32_t x) { return dim3((x + 7) / 8 * 8); };
+        if (n3) { bin(c.L.m3, n3, bout); hipLaunchKernelGGL((k3_sort_lds<4, 16>), g8(ncu * 2), dim3(256), 0, st, c, bout); }
+        if (n2) { bin(c.L.m2, n2, bout); hipLaunchKernelGGL((k3_sort_lds<4, 8>), g8(ncu * 3), dim3(256), 0, st, c, bout); }
+        if (n1) { bin(c.L.m1, n1, bout); hipLaunchKernelGGL((k3_sort_lds<4, 4>), g8(ncu * 4), dim3(256), 0, st, c, bout); }
+        if (ns) { bin(c.L.s, ns, bout); hipLaunchKernelGGL((k3_sort_lds<1, 4>), g8(ncu * 5), dim3(256), 0, st, c, bout); }
+        if (nw) { bin(c.L.w, nw, bout); hipLaunchKernelGGL(k3_sort_w, g8(ncu * 8), dim3(256), 0, st, c, bout); }
         HIP_CHECK(hipGetLastError());
         HIP_CHECK(hipMemsetAsync(c.L.ctr + C_W, 0, 5 * sizeof(uint32_t), st));
     };
 
     // ---- round 0: packed prefix keys ----
-    hipLaunchKernelGGL(k3_hist, dim3(MAXT, nb), dim3(PT), 0, st, c);
-    hipLaunchKernelGGL(k3_scan, dim3(nb), dim3(ST), 0, st, c);
-    hipLaunchKernelGGL(k3_scatter, dim3(MAXT * ((nb + 7) / 8 * 8)), dim3(PT), 0, st, c, nb);
-    HIP_CHECK(hipGetLastError());
+    {
+        const uint32_t maxw = (uint32_t)pss_words(scr.stride);
+        hipLaunchKernelGGL(k3_pss, dim3((maxw + 255) / 256, nb), dim3(256), 0, st, c);
+        hipLaunchKernelGGL(k3_hist, dim3(MAXT, nb), dim3(PT), 0, st, c);
+        hipLaunchKernelGGL(k3_scan, dim3(nb), dim3(ST), 0, st, c);
+        uint32_t* head;
+        uint32_t* seg;
+        next_q(head, seg);
+        c.qhead = head;
+        c.qseg = nullptr;
+        // about one block in flight per XCD: MAXT workgroups of 1024 threads each
+        hipLaunchKernelGGL(k3_scatter, dim3(8 * MAXT), dim3(SCT), 0, st, c);
+        HIP_CHECK(hipGetLastError());
+    }
     sort_groups();
-    // ---- text rounds: extend the tied rotations' keys from the block text ----
+    // ---- text rounds: extend the tied rotations' keys from the PSS ----
     uint32_t rtext = 0;
     uint64_t prev_tied = ~0ull;
     bool done = false;
@@ -1053,11 +1204,12 @@ void launch_bwt3(BlockDesc* blocks, uint32_t b0, uint32_t nb, const uint8_t* blk
         if (rtext == TEXT_ROUNDS || (rtext > 0 && 2 * tied > prev_tied)) break;   // long repeats: double
         prev_tied = tied;
         ++rtext;
+        c.rtext = rtext;
         const uint32_t cur = c.tsel;
         c.tsel ^= 1u;
         HIP_CHECK(hipMemsetAsync(c.L.ctr + C_T0 + c.tsel, 0, sizeof(uint32_t), st));
         HIP_CHECK(hipMemsetAsync(c.L.ctr + C_TS0 + c.tsel, 0, sizeof(uint32_t), st));
-        hipLaunchKernelGGL(k3_gather_text, dim3((nt + 255) / 256), dim3(256), 0, st, c, c.L.t[cur], nt, rtext);
+        hipLaunchKernelGGL(k3_classify_text, dim3((nt + 255) / 256), dim3(256), 0, st, c, c.L.t[cur], nt);
         HIP_CHECK(hipGetLastError());
         HIP_CHECK(hipMemsetAsync(c.L.ctr + C_T0 + cur, 0, sizeof(uint32_t), st));
         sort_groups();
@@ -1071,6 +1223,7 @@ void launch_bwt3(BlockDesc* blocks, uint32_t b0, uint32_t nb, const uint8_t* blk
         hipLaunchKernelGGL(k3_rk_groups, dim3((nt + 3) / 4), dim3(256), 0, st, c, T, nt);
         HIP_CHECK(hipGetLastError());
         c.mode = 1;
+        c.keysrc = 1;
         for (uint32_t round = 1;; ++round) {
             if (round > 1) read_ctr();
             const uint32_t n2 = hctr[C_T0 + c.tsel];

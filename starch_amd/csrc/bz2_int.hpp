@@ -37,6 +37,30 @@ static inline uint32_t host_mulmod(uint32_t a, uint32_t b)
     return r;
 }
 
+// ---- per-XCD work queues (placement is a speed matter only) ----
+// A persistent workgroup reads the XCD it runs on and takes work from that
+// XCD's queue first, then steals from the others, so every queue drains
+// whatever the dispatcher does; work whose data should share an L2 (one
+// bzip2 block) is put in one queue.  MI355X_MICROARCH.md "Workgroup dispatch".
+__device__ __forceinline__ uint32_t xcc_id()
+{
+    return (uint32_t)__builtin_amdgcn_s_getreg(20 | (0 << 6) | (3 << 11)) & 7u;   // hwreg(HW_REG_XCC_ID, 0, 4)
+}
+
+// qsize[y] = items in queue y; returns (y << 28) | index, or ~0u when all are
+// drained.  Called by one lane.
+__device__ __forceinline__ uint32_t xq_pop(uint32_t* head, const uint32_t* qsize, uint32_t x)
+{
+    for (uint32_t t = 0; t < 8; ++t) {
+        const uint32_t y = (x + t) & 7u;
+        const uint32_t sz = qsize[y];
+        if (__hip_atomic_load(head + y, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) >= sz) continue;
+        const uint32_t i = atomicAdd(head + y, 1u);
+        if (i < sz) return (y << 28) | i;
+    }
+    return 0xFFFFFFFFu;
+}
+
 // ---- move-to-front on a list of <= 16 symbols kept as nibbles of a u64 ----
 struct NibState {          // transform L -> list ++ (L \ set)
     uint64_t list;         // nibble i = i-th symbol

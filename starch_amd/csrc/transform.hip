@@ -139,9 +139,22 @@ __device__ __forceinline__ bool is_c_space(uint8_t c)
     return c == ' ' || c == '\t' || c == '\n' || c == '\v' || c == '\f' || c == '\r';
 }
 
+// byte sources for the parser: global memory, or an LDS copy of [base, ...)
+struct GSrc {
+    const uint8_t* p;
+    __device__ __forceinline__ uint8_t operator[](uint64_t x) const { return p[x]; }
+};
+struct LSrc {
+    const uint8_t* t;
+    uint64_t base;
+    __device__ __forceinline__ uint8_t operator[](uint64_t x) const { return t[x - base]; }
+};
+
 // sscanf "%" SCNd64 on the C-string s[0..len) (hpp:306-307); glibc clamps on overflow.
-__device__ __forceinline__ bool scan_i64(const uint8_t* s, uint64_t len, int64_t& v)
+template <class S>
+__device__ __forceinline__ bool scan_i64(const S& src, uint64_t off, uint64_t len, int64_t& v)
 {
+    struct { const S& s; uint64_t o; __device__ uint8_t operator[](uint64_t i) const { return s[o + i]; } } s{src, off};
     uint64_t i = 0;
     while (i < len && is_c_space(s[i])) ++i;
     bool neg = false;
@@ -162,16 +175,18 @@ __device__ __forceinline__ bool scan_i64(const uint8_t* s, uint64_t len, int64_t
 }
 
 // effective C-string length (first NUL ends a token: strcmp/strlen/sscanf)
-__device__ __forceinline__ uint64_t cstr_len(const uint8_t* p, uint64_t n)
+template <class S>
+__device__ __forceinline__ uint64_t cstr_len(const S& s, uint64_t off, uint64_t n)
 {
-    for (uint64_t i = 0; i < n; ++i) if (p[i] == 0) return i;
+    for (uint64_t i = 0; i < n; ++i) if (s[off + i] == 0) return i;
     return n;
 }
 
 // Tokenize one line [ls, le) (le-1 is '\n'): fields per hpp:220-305.
 struct Fields { uint64_t b[4], e[4]; int tok; };
 
-__device__ __forceinline__ Fields tokenize(const uint8_t* bed, uint64_t ls, uint64_t le)
+template <class S>
+__device__ __forceinline__ Fields tokenize(const S& bed, uint64_t ls, uint64_t le)
 {
     Fields f;
     f.tok = 0;
@@ -189,7 +204,8 @@ __device__ __forceinline__ Fields tokenize(const uint8_t* bed, uint64_t ls, uint
 }
 
 // chromosome token only (bytes before the first tab; '\n' kept if no tab)
-__device__ __forceinline__ uint64_t chr_end(const uint8_t* bed, uint64_t ls)
+template <class S>
+__device__ __forceinline__ uint64_t chr_end(const S& bed, uint64_t ls)
 {
     uint64_t p = ls;
     for (;;) {
@@ -200,27 +216,26 @@ __device__ __forceinline__ uint64_t chr_end(const uint8_t* bed, uint64_t ls)
     }
 }
 
-__global__ void __launch_bounds__(kThreads)
-k_parse(const uint8_t* __restrict__ bed, const uint64_t* __restrict__ line_end, uint64_t nl,
-        int64_t* __restrict__ start, int64_t* __restrict__ stop, uint8_t* __restrict__ flags,
-        uint64_t* __restrict__ rem_beg, uint32_t* __restrict__ rem_len, uint32_t* __restrict__ chr_len,
-        uint32_t* __restrict__ any_fail)
+template <class S>
+__device__ __forceinline__ void parse_line(const S& bed, const uint64_t* __restrict__ line_end, uint64_t i,
+                                           int64_t* __restrict__ start, int64_t* __restrict__ stop,
+                                           uint8_t* __restrict__ flags, uint64_t* __restrict__ rem_beg,
+                                           uint32_t* __restrict__ rem_len, uint32_t* __restrict__ chr_len,
+                                           uint32_t* __restrict__ any_fail)
 {
-    uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
-    if (i >= nl) return;
-    uint64_t ls = i ? line_end[i - 1] : 0, le = line_end[i];
-    Fields f = tokenize(bed, ls, le);
+    const uint64_t ls = i ? line_end[i - 1] : 0, le = line_end[i];
+    const Fields f = tokenize(bed, ls, le);
     uint64_t len[4];
 #pragma unroll
-    for (int t = 0; t < 4; ++t) len[t] = cstr_len(bed + f.b[t], f.e[t] - f.b[t]);
+    for (int t = 0; t < 4; ++t) len[t] = cstr_len(bed, f.b[t], f.e[t] - f.b[t]);
     int64_t a = 0, b = 0;
-    bool aok = scan_i64(bed + f.b[1], len[1], a);
-    bool bok = scan_i64(bed + f.b[2], len[2], b);
+    const bool aok = scan_i64(bed, f.b[1], len[1], a);
+    const bool bok = scan_i64(bed, f.b[2], len[2], b);
     bool newseg = true;
     if (i > 0) {
-        uint64_t ps = (i > 1) ? line_end[i - 2] : 0;
-        uint64_t pe = chr_end(bed, ps);
-        uint64_t plen = cstr_len(bed + ps, pe - ps);
+        const uint64_t ps = (i > 1) ? line_end[i - 2] : 0;
+        const uint64_t pe = chr_end(bed, ps);
+        const uint64_t plen = cstr_len(bed, ps, pe - ps);
         if (plen == len[0]) {
             newseg = false;
             for (uint64_t k = 0; k < plen; ++k)
@@ -234,6 +249,43 @@ k_parse(const uint8_t* __restrict__ bed, const uint64_t* __restrict__ line_end, 
     rem_len[i] = (uint32_t)len[3];
     chr_len[i] = (uint32_t)len[0];
     if (!aok || !bok) atomicOr(any_fail, 1u);
+}
+
+// One workgroup per 256 lines.  The bytes of those lines and of the line
+// before them (its chromosome decides F_NEW_SEG) are staged in LDS with
+// coalesced 16-B loads when they fit; every thread then parses its line from
+// LDS.  Longer spans (very long lines) parse straight from global memory.
+constexpr uint32_t kParseCap = 24576;
+
+__global__ void __launch_bounds__(kThreads)
+k_parse(const uint8_t* __restrict__ bed, const uint64_t* __restrict__ line_end, uint64_t nl,
+        int64_t* __restrict__ start, int64_t* __restrict__ stop, uint8_t* __restrict__ flags,
+        uint64_t* __restrict__ rem_beg, uint32_t* __restrict__ rem_len, uint32_t* __restrict__ chr_len,
+        uint32_t* __restrict__ any_fail)
+{
+    __shared__ uint4 tb4[kParseCap / 16 + 2];
+    const uint64_t L0 = (uint64_t)blockIdx.x * kThreads;
+    const uint64_t i = L0 + threadIdx.x;
+    const uint64_t L1 = L0 + kThreads < nl ? L0 + kThreads : nl;
+    const uint64_t rb = L0 >= 2 ? line_end[L0 - 2] : 0;            // start of line L0-1 (or 0)
+    const uint64_t re = line_end[L1 - 1];
+    // 16-B aligned in absolute address terms (bed itself may be unaligned); a0 is
+    // bed-relative and may wrap below 0 -- LSrc indexes with modular arithmetic
+    const uintptr_t abs0 = reinterpret_cast<uintptr_t>(bed + rb) & ~(uintptr_t)15;
+    const uint64_t a0 = (uint64_t)(abs0 - reinterpret_cast<uintptr_t>(bed));
+    const uint64_t nw = (reinterpret_cast<uintptr_t>(bed + re) - abs0 + 15) / 16;
+    if (nw * 16 <= kParseCap) {
+        const uint4* src = reinterpret_cast<const uint4*>(abs0);
+        for (uint64_t w = threadIdx.x; w < nw; w += kThreads) tb4[w] = src[w];
+        __syncthreads();
+        if (i < nl) {
+            LSrc ls{reinterpret_cast<const uint8_t*>(tb4), a0};
+            parse_line(ls, line_end, i, start, stop, flags, rem_beg, rem_len, chr_len, any_fail);
+        }
+    } else if (i < nl) {
+        GSrc gs{bed};
+        parse_line(gs, line_end, i, start, stop, flags, rem_beg, rem_len, chr_len, any_fail);
+    }
 }
 
 // stale-value propagation: idx[i] = ok ? i+1 : 0  -> inclusive max-scan -> gather
