@@ -50,8 +50,13 @@ struct BitOut {
     }
 };
 
-constexpr int ET = 256;
+constexpr int ET = 1024;
 
+// One workgroup per block.  Thread 0 writes the fixed header (magic, CRC,
+// origPtr, inUse map, nGroups, nSelectors); the selectors' unary MTF codes
+// are written in parallel (contiguous selector ranges per thread, bit offsets
+// by a block scan); thread 0 writes the delta-coded lengths; then one
+// 50-symbol group per lane.
 __global__ void __launch_bounds__(ET) k_emit_block(const BlockDesc* __restrict__ blocks,
                                                     const uint16_t* __restrict__ mtfv_all, uint64_t mtf_stride,
                                                     const Tables* __restrict__ tabs, const uint8_t* __restrict__ sel_all,
@@ -71,13 +76,19 @@ __global__ void __launch_bounds__(ET) k_emit_block(const BlockDesc* __restrict__
         if (t < ng && v < alpha) { len[t][v] = tabs[b].len[t][v]; code[t][v] = tabs[b].code[t][v]; }
     }
     if (tid == 0) carry = 0;
-    __syncthreads();
     const uint16_t* mtfv = mtfv_all + (uint64_t)b * mtf_stride;
     const uint8_t* sel = sel_all + (uint64_t)b * (2 * kMaxSelectors);
     const uint8_t* selmtf = sel + kMaxSelectors;
     const uint32_t* gbits = gbits_all + (uint64_t)b * kMaxSelectors;
 
-    if (tid == 0) {   // block header, mapping table, selectors, code lengths
+    uint32_t used16 = 0;
+    for (int i = 0; i < 16; ++i) {
+        const uint32_t w = bd.in_use[i >> 1];
+        const uint32_t half = (i & 1) ? (w >> 16) : (w & 0xffffu);
+        if (half) used16 |= 1u << (15 - i);
+    }
+    const uint64_t sel0 = bd.bit_off + 48 + 32 + 1 + 24 + 16 + 16ull * __popc(used16) + 3 + 15;
+    if (tid == 0) {   // block header, mapping table, counts (bz:compress.c:496-544, 611-621)
         BitOut o;
         o.init(out32, bd.bit_off);
         o.put(24, 0x314159u);
@@ -85,27 +96,38 @@ __global__ void __launch_bounds__(ET) k_emit_block(const BlockDesc* __restrict__
         o.put(32, bd.crc);
         o.put(1, 0);
         o.put(24, bd.orig_ptr);
-        uint32_t u16 = 0;
+        o.put(16, used16);
         for (int i = 0; i < 16; ++i) {
-            uint32_t w = bd.in_use[i >> 1];
-            uint32_t half = (i & 1) ? (w >> 16) : (w & 0xffffu);
-            if (half) u16 |= 1u << (15 - i);
-        }
-        o.put(16, u16);
-        for (int i = 0; i < 16; ++i) {
-            if (!(u16 & (1u << (15 - i)))) continue;
-            uint32_t w = bd.in_use[i >> 1];
-            uint32_t half = (i & 1) ? (w >> 16) : (w & 0xffffu);
+            if (!(used16 & (1u << (15 - i)))) continue;
+            const uint32_t w = bd.in_use[i >> 1];
+            const uint32_t half = (i & 1) ? (w >> 16) : (w & 0xffffu);
             uint32_t bits = 0;
             for (int j = 0; j < 16; ++j) if (half & (1u << j)) bits |= 1u << (15 - j);
             o.put(16, bits);
         }
         o.put(3, (uint32_t)ng);
         o.put(15, bd.n_sel);
-        for (uint32_t i = 0; i < bd.n_sel; ++i) {
-            uint32_t j = selmtf[i];
+        o.finish();
+    }
+    // selectors, MTF-coded in unary (bz:compress.c:546-556)
+    const uint32_t per = (bd.n_sel + ET - 1) / ET;
+    const uint32_t sa = tid * per, se = sa + per < bd.n_sel ? sa + per : bd.n_sel;
+    uint32_t sb = 0;
+    for (uint32_t i = sa; i < se; ++i) sb += selmtf[i] + 1u;
+    uint32_t stot;
+    const uint32_t spre = block_excl_scan_add<uint32_t>(sb, scan_sh, &stot);
+    if (sa < se) {
+        BitOut o;
+        o.init(out32, sel0 + spre);
+        for (uint32_t i = sa; i < se; ++i) {
+            const uint32_t j = selmtf[i];
             o.put((int)j + 1, ((1u << j) - 1u) << 1);
         }
+        o.finish();
+    }
+    if (tid == 0) {   // coding tables, delta-coded lengths (bz:compress.c:558-575)
+        BitOut o;
+        o.init(out32, sel0 + stot);
         for (int t = 0; t < ng; ++t) {
             int cur = len[t][0];
             o.put(5, (uint32_t)cur);
@@ -130,9 +152,15 @@ __global__ void __launch_bounds__(ET) k_emit_block(const BlockDesc* __restrict__
             uint32_t gs = g * 50, ge = gs + 50;
             if (ge > bd.n_mtf) ge = bd.n_mtf;
             const int t = sel[g];
-            for (uint32_t i = gs; i < ge; ++i) {
-                uint32_t v = mtfv[i];
-                o.put(len[t][v], code[t][v]);
+            const uint32_t* m32 = reinterpret_cast<const uint32_t*>(mtfv + gs);   // gs even: 4-B aligned
+            for (uint32_t i = gs; i < ge; i += 2) {
+                const uint32_t w = m32[(i - gs) >> 1];
+                const uint32_t v0 = w & 0xffffu;
+                o.put(len[t][v0], code[t][v0]);
+                if (i + 1 < ge) {
+                    const uint32_t v1 = w >> 16;
+                    o.put(len[t][v1], code[t][v1]);
+                }
             }
             o.finish();
         }

@@ -86,14 +86,22 @@ __device__ __forceinline__ uint64_t lowmask4(uint32_t k)   // k nibbles
     return k >= 16 ? ~0ull : ((1ull << (4 * k)) - 1ull);
 }
 
-// one MTF step on the nibble list; returns the index of s
+// one MTF step on the nibble list; returns the index of s.  s must be in the
+// list (unused high nibbles are 0: the first match is the real position of 0).
+// Zero-nibble search on 32-bit halves, then a bit-select moves nibbles 0..k-1
+// up by one and puts s in front.
 __device__ __forceinline__ uint32_t nib_mtf(uint64_t& L, uint32_t s)
 {
-    const uint64_t x = L ^ (0x1111111111111111ull * s);
-    const uint64_t t = x | (x >> 1) | (x >> 2) | (x >> 3);
-    const uint64_t zn = ~t & 0x1111111111111111ull;
-    const uint32_t k = (uint32_t)__builtin_ctzll(zn) >> 2;
-    L = (L & ~lowmask4(k + 1)) | ((L & lowmask4(k)) << 4) | (uint64_t)s;
+    const uint32_t pat = s * 0x11111111u;
+    uint32_t xl = (uint32_t)L ^ pat, xh = (uint32_t)(L >> 32) ^ pat;
+    xl |= xl >> 1;
+    xl |= xl >> 2;
+    xh |= xh >> 1;
+    xh |= xh >> 2;
+    const uint32_t zl = ~xl & 0x11111111u, zh = ~xh & 0x11111111u;
+    const uint32_t k = zl ? ((uint32_t)__builtin_ctz(zl) >> 2) : 8u + ((uint32_t)__builtin_ctz(zh) >> 2);
+    const uint64_t m = (k >= 15u) ? ~0ull : ((1ull << (4u * k + 4u)) - 1ull);
+    L = (((L << 4) | (uint64_t)s) & m) | (L & ~m);
     return k;
 }
 

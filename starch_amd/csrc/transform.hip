@@ -188,18 +188,35 @@ struct Fields { uint64_t b[4], e[4]; int tok; };
 template <class S>
 __device__ __forceinline__ Fields tokenize(const S& bed, uint64_t ls, uint64_t le)
 {
-    Fields f;
-    f.tok = 0;
-    f.b[0] = ls;
+    // field bounds kept in scalars (a dynamically indexed array would live in
+    // scratch memory); same scan as the reference, including the byte after a
+    // tab not being tested for a tab
+    uint64_t b1 = 0, b2 = 0, b3 = 0, e0 = 0, e1 = 0, e2 = 0;
+    int tok = 0;
     uint64_t p = ls;
     for (;;) {
-        if (bed[p] == '\t' && f.tok != 3) { f.e[f.tok] = p; ++f.tok; ++p; f.b[f.tok] = p; }
+        if (bed[p] == '\t' && tok != 3) {
+            if (tok == 0) e0 = p; else if (tok == 1) e1 = p; else e2 = p;
+            ++tok;
+            ++p;
+            if (tok == 1) b1 = p; else if (tok == 2) b2 = p; else b3 = p;
+        }
         ++p;
         if (bed[p - 1] == '\n') break;
     }
-    f.e[f.tok] = p;
-    for (int t = f.tok + 1; t < 4; ++t) f.b[t] = f.e[t] = p;
-    if (f.tok >= 2) f.e[f.tok] -= 1;                // strip '\n' from stop or rem
+    Fields f;
+    f.tok = tok;
+    f.b[0] = ls;
+    f.b[1] = tok >= 1 ? b1 : p;
+    f.b[2] = tok >= 2 ? b2 : p;
+    f.b[3] = tok >= 3 ? b3 : p;
+    f.e[0] = tok >= 1 ? e0 : p;
+    f.e[1] = tok >= 2 ? e1 : p;
+    f.e[2] = tok >= 3 ? e2 : p;
+    f.e[3] = p;
+    if (tok >= 2) {                                 // strip '\n' from stop or rem
+        if (tok == 2) f.e[2] -= 1; else f.e[3] -= 1;
+    }
     return f;
 }
 
@@ -216,6 +233,58 @@ __device__ __forceinline__ uint64_t chr_end(const S& bed, uint64_t ls)
     }
 }
 
+// Parsed fields of line i (hpp:220-328): start/stop values, whether each
+// parsed, whether the chromosome differs from line i-1's, and the remainder.
+struct LineVals {
+    int64_t a, b;
+    uint64_t rem_b;
+    uint32_t rem_len, chr_len;
+    bool aok, bok, newseg;
+};
+
+template <class S>
+__device__ __forceinline__ LineVals parse_vals(const S& bed, const uint64_t* __restrict__ line_end, uint64_t i)
+{
+    LineVals r;
+    const uint64_t ls = i ? line_end[i - 1] : 0, le = line_end[i];
+    const Fields f = tokenize(bed, ls, le);
+    uint64_t len[4];
+#pragma unroll
+    for (int t = 0; t < 4; ++t) len[t] = cstr_len(bed, f.b[t], f.e[t] - f.b[t]);
+    r.a = 0;
+    r.b = 0;
+    r.aok = scan_i64(bed, f.b[1], len[1], r.a);
+    r.bok = scan_i64(bed, f.b[2], len[2], r.b);
+    r.newseg = true;
+    if (i > 0) {
+        const uint64_t ps = (i > 1) ? line_end[i - 2] : 0;
+        const uint64_t pe = chr_end(bed, ps);
+        const uint64_t plen = cstr_len(bed, ps, pe - ps);
+        if (plen == len[0]) {
+            r.newseg = false;
+            for (uint64_t k = 0; k < plen; ++k)
+                if (bed[ps + k] != bed[ls + k]) { r.newseg = true; break; }
+        }
+    }
+    r.rem_b = f.b[3];
+    r.rem_len = (uint32_t)len[3];
+    r.chr_len = (uint32_t)len[0];
+    return r;
+}
+
+// start/stop of line i only (the line before a workgroup's first line)
+template <class S>
+__device__ __forceinline__ void parse_ab(const S& bed, const uint64_t* __restrict__ line_end, uint64_t i, int64_t& a,
+                                         int64_t& b)
+{
+    const uint64_t ls = i ? line_end[i - 1] : 0, le = line_end[i];
+    const Fields f = tokenize(bed, ls, le);
+    a = 0;
+    b = 0;
+    scan_i64(bed, f.b[1], cstr_len(bed, f.b[1], f.e[1] - f.b[1]), a);
+    scan_i64(bed, f.b[2], cstr_len(bed, f.b[2], f.e[2] - f.b[2]), b);
+}
+
 template <class S>
 __device__ __forceinline__ void parse_line(const S& bed, const uint64_t* __restrict__ line_end, uint64_t i,
                                            int64_t* __restrict__ start, int64_t* __restrict__ stop,
@@ -223,32 +292,14 @@ __device__ __forceinline__ void parse_line(const S& bed, const uint64_t* __restr
                                            uint32_t* __restrict__ rem_len, uint32_t* __restrict__ chr_len,
                                            uint32_t* __restrict__ any_fail)
 {
-    const uint64_t ls = i ? line_end[i - 1] : 0, le = line_end[i];
-    const Fields f = tokenize(bed, ls, le);
-    uint64_t len[4];
-#pragma unroll
-    for (int t = 0; t < 4; ++t) len[t] = cstr_len(bed, f.b[t], f.e[t] - f.b[t]);
-    int64_t a = 0, b = 0;
-    const bool aok = scan_i64(bed, f.b[1], len[1], a);
-    const bool bok = scan_i64(bed, f.b[2], len[2], b);
-    bool newseg = true;
-    if (i > 0) {
-        const uint64_t ps = (i > 1) ? line_end[i - 2] : 0;
-        const uint64_t pe = chr_end(bed, ps);
-        const uint64_t plen = cstr_len(bed, ps, pe - ps);
-        if (plen == len[0]) {
-            newseg = false;
-            for (uint64_t k = 0; k < plen; ++k)
-                if (bed[ps + k] != bed[ls + k]) { newseg = true; break; }
-        }
-    }
-    start[i] = a;
-    stop[i] = b;
-    flags[i] = (aok ? F_START_OK : 0) | (bok ? F_STOP_OK : 0) | (newseg ? F_NEW_SEG : 0);
-    rem_beg[i] = f.b[3];
-    rem_len[i] = (uint32_t)len[3];
-    chr_len[i] = (uint32_t)len[0];
-    if (!aok || !bok) atomicOr(any_fail, 1u);
+    const LineVals r = parse_vals(bed, line_end, i);
+    start[i] = r.a;
+    stop[i] = r.b;
+    flags[i] = (r.aok ? F_START_OK : 0) | (r.bok ? F_STOP_OK : 0) | (r.newseg ? F_NEW_SEG : 0);
+    rem_beg[i] = r.rem_b;
+    rem_len[i] = r.rem_len;
+    chr_len[i] = r.chr_len;
+    if (!r.aok || !r.bok) atomicOr(any_fail, 1u);
 }
 
 // One workgroup per 256 lines.  The bytes of those lines and of the line
@@ -307,8 +358,17 @@ __global__ void k_gather_stale(const int64_t* __restrict__ cp, const uint64_t* _
 // --- per-line output length ----------------------------------------------------
 __device__ __forceinline__ int ndig_u64(uint64_t u)
 {
-    int d = 1;
-    while (u >= 10u) { u /= 10u; ++d; }
+    // compare against powers of ten (no 64-bit divisions)
+    if (u < 10000000000ull) {
+        const uint32_t w = (uint32_t)u;
+        if (u <= 0xFFFFFFFFull)
+            return 1 + (w >= 10u) + (w >= 100u) + (w >= 1000u) + (w >= 10000u) + (w >= 100000u) +
+                   (w >= 1000000u) + (w >= 10000000u) + (w >= 100000000u) + (w >= 1000000000u);
+        return 10;
+    }
+    int d = 10;
+    uint64_t p = 10000000000ull;
+    while (d < 20 && u >= p) { ++d; p = (d < 20) ? p * 10u : p; }
     return d;
 }
 // n_digits (hpp:559-581): |i| digits, INT64_MIN -> 1
@@ -364,10 +424,15 @@ k_line_len(const int64_t* __restrict__ start, const int64_t* __restrict__ stop, 
 __device__ __forceinline__ uint64_t put_dec(uint8_t* o, int64_t v)
 {
     uint64_t u = (v < 0) ? 0ull - (uint64_t)v : (uint64_t)v;
-    int nd = ndig_u64(u);
+    const int nd = ndig_u64(u);
     uint64_t k = 0;
     if (v < 0) o[k++] = '-';
-    for (int d = nd - 1; d >= 0; --d) { o[k + d] = (uint8_t)('0' + (u % 10u)); u /= 10u; }
+    if (u <= 0xFFFFFFFFull) {                          // 32-bit divisions
+        uint32_t w = (uint32_t)u;
+        for (int d = nd - 1; d >= 0; --d) { o[k + d] = (uint8_t)('0' + (w % 10u)); w /= 10u; }
+    } else {
+        for (int d = nd - 1; d >= 0; --d) { o[k + d] = (uint8_t)('0' + (u % 10u)); u /= 10u; }
+    }
     return k + nd;
 }
 
@@ -398,6 +463,375 @@ k_emit(const uint8_t* __restrict__ bed, const int64_t* __restrict__ start, const
         o += rl;
     }
     *o = '\n';
+}
+
+// --- fused two-pass transform -------------------------------------------------
+// Taken when every line's start and stop parse (the stale-value rule of
+// hpp:306-316 never fires).  Each workgroup owns 256 lines and stages their
+// bytes, plus the line before them, in LDS once per pass.  Pass 1 (k_tf1)
+// reduces the workgroup's output bytes and new-segment count; after a scan over
+// workgroups, pass 2 (k_tf2) re-parses, scans inside the workgroup, builds the
+// output text in LDS, stores it with coalesced 4-B writes and records the
+// segments that start in it.  No per-line array is materialised.
+//
+// Lines are parsed with a SWAR scanner over a 128-B register window (tab and
+// NUL masks, digit fields of 1..18 plain digits); a line it does not cover
+// (longer, NUL bytes, signs/spaces, 19+ digits, fewer than two tabs) takes the
+// byte-serial reference parser (parse_vals), which is the definition.
+
+constexpr uint32_t kStagePad = 256;    // reads past the staged span stay inside the LDS array
+
+__device__ __forceinline__ uint32_t eq4(uint32_t x, uint32_t pat)      // 4-bit mask: bytes of x == pat's
+{
+    const uint32_t t = x ^ pat;
+    const uint32_t z = ~(((t & 0x7f7f7f7fu) + 0x7f7f7f7fu) | t) & 0x80808080u;
+    return (((z >> 7) * 0x204081u) >> 21) & 15u;
+}
+__device__ __forceinline__ uint64_t lowbits(uint32_t n) { return n >= 64 ? ~0ull : ((1ull << n) - 1ull); }
+
+// first set bit >= pos of the 128-bit mask (lo, hi); 128 if none
+__device__ __forceinline__ uint32_t next_bit(uint64_t lo, uint64_t hi, uint32_t pos)
+{
+    if (pos < 64) {
+        const uint64_t m = lo & ~lowbits(pos);
+        if (m) return (uint32_t)__builtin_ctzll(m);
+        pos = 64;
+    }
+    if (pos >= 128) return 128;
+    const uint64_t m = hi & ~lowbits(pos - 64);
+    return m ? 64u + (uint32_t)__builtin_ctzll(m) : 128u;
+}
+
+// 1..18 plain digits at tb[b..b+n) -> v (sscanf gives the same value for them)
+__device__ __forceinline__ bool dig_fast(const uint8_t* tb, uint32_t b, uint32_t n, int64_t& v)
+{
+    if (n - 1u >= 18u) return false;
+    uint32_t x0 = 0, x1 = 0, p = 1, bad = 0;
+#pragma unroll
+    for (uint32_t k = 0; k < 18; ++k) {
+        const uint32_t d = (uint32_t)tb[b + k] - 48u;
+        if (k < n) {
+            bad |= (d > 9u) ? 1u : 0u;
+            if (k < 9) x0 = x0 * 10u + d;
+            else { x1 = x1 * 10u + d; p *= 10u; }
+        }
+    }
+    v = (int64_t)((uint64_t)x0 * p + x1);
+    return bad == 0;
+}
+
+// Fast parse of the line at stage index r0 (bed offset ls), len bytes incl. '\n'.
+// Fills a, b, chr_len, rem_b, rem_len (newseg is decided by the caller).
+__device__ __forceinline__ bool parse_fast(const uint8_t* tb, uint32_t r0, uint32_t len, uint64_t ls, LineVals& r)
+{
+    const uint32_t off = r0 & 15u, q = r0 - off, end = off + len;     // window-relative [off, end)
+    if (end > 128u) return false;
+    const uint4* tb4 = reinterpret_cast<const uint4*>(tb + q);
+    uint64_t tl = 0, th = 0, zl = 0, zh = 0;
+#pragma unroll
+    for (uint32_t k = 0; k < 8; ++k) {
+        if (16u * k < end) {
+            const uint4 v = tb4[k];
+            const uint64_t tm = (uint64_t)(eq4(v.x, 0x09090909u) | (eq4(v.y, 0x09090909u) << 4) |
+                                           (eq4(v.z, 0x09090909u) << 8) | (eq4(v.w, 0x09090909u) << 12));
+            const uint64_t zm = (uint64_t)(eq4(v.x, 0u) | (eq4(v.y, 0u) << 4) | (eq4(v.z, 0u) << 8) |
+                                           (eq4(v.w, 0u) << 12));
+            if (k < 4) { tl |= tm << (16 * k); zl |= zm << (16 * k); }
+            else { th |= tm << (16 * (k - 4)); zh |= zm << (16 * (k - 4)); }
+        }
+    }
+    const uint32_t e64 = end < 64u ? end : 64u, o64 = off < 64u ? off : 64u;
+    const uint64_t rl = lowbits(e64) & ~lowbits(o64);
+    const uint64_t rh = lowbits(end > 64u ? end - 64u : 0u) & ~lowbits(off > 64u ? off - 64u : 0u);
+    if ((zl & rl) | (zh & rh)) return false;                  // NUL bytes: C-string rules apply
+    const uint32_t nlp = end - 1u;                            // the '\n'
+    tl &= rl & ~(nlp < 64u ? (1ull << nlp) : 0ull);
+    th &= rh & ~(nlp >= 64u ? (1ull << (nlp - 64u)) : 0ull);
+    // the reference's scan does not test the byte after a tab for a tab (tokenize)
+    const uint32_t t1 = next_bit(tl, th, off);
+    if (t1 >= 128u) return false;
+    const uint32_t t2 = next_bit(tl, th, t1 + 2u);
+    if (t2 >= 128u) return false;
+    const uint32_t t3 = next_bit(tl, th, t2 + 2u);
+    const uint32_t e2 = t3 < 128u ? t3 : nlp;
+    if (!dig_fast(tb, q + t1 + 1u, t2 - t1 - 1u, r.a)) return false;
+    if (!dig_fast(tb, q + t2 + 1u, e2 - t2 - 1u, r.b)) return false;
+    r.aok = r.bok = true;
+    r.chr_len = t1 - off;
+    if (t3 < 128u) {
+        r.rem_b = ls + (t3 + 1u - off);
+        r.rem_len = nlp - (t3 + 1u);
+    } else {
+        r.rem_b = ls + len;
+        r.rem_len = 0;
+    }
+    return true;
+}
+
+// start/stop and chromosome length of line i, byte-serial (the line before a workgroup)
+template <class S>
+__device__ __forceinline__ void parse_abc(const S& bed, const uint64_t* __restrict__ line_end, uint64_t i, int64_t& a,
+                                          int64_t& b, uint32_t& clen)
+{
+    const uint64_t ls = i ? line_end[i - 1] : 0, le = line_end[i];
+    const Fields f = tokenize(bed, ls, le);
+    a = 0;
+    b = 0;
+    scan_i64(bed, f.b[1], cstr_len(bed, f.b[1], f.e[1] - f.b[1]), a);
+    scan_i64(bed, f.b[2], cstr_len(bed, f.b[2], f.e[2] - f.b[2]), b);
+    clen = (uint32_t)cstr_len(bed, f.b[0], f.e[0] - f.b[0]);
+}
+
+// LDS staging of bytes [start of line L0-1, end of line L1-1); false when they
+// do not fit in cap bytes (the workgroup then parses from global memory).
+__device__ __forceinline__ bool stage_lines(const uint8_t* __restrict__ bed, const uint64_t* __restrict__ line_end,
+                                            uint64_t L0, uint64_t L1, uint4* tb4, uint32_t cap, uint64_t& a0)
+{
+    const uint64_t rb = L0 >= 2 ? line_end[L0 - 2] : 0;
+    const uint64_t re = line_end[L1 - 1];
+    const uintptr_t abs0 = reinterpret_cast<uintptr_t>(bed + rb) & ~(uintptr_t)15;
+    a0 = (uint64_t)(abs0 - reinterpret_cast<uintptr_t>(bed));
+    const uint64_t nw = (reinterpret_cast<uintptr_t>(bed + re) - abs0 + 15) / 16;
+    if (nw * 16 > cap) return false;
+    const uint4* src = reinterpret_cast<const uint4*>(abs0);
+    for (uint64_t w = threadIdx.x; w < nw; w += kThreads) tb4[w] = src[w];
+    __syncthreads();
+    return true;
+}
+
+struct OutDesc { int64_t cd, v; bool emit_p; uint32_t len; };
+
+// hpp:430-470 -- pa/pb are line i-1's start/stop (ignored on a new segment)
+__device__ __forceinline__ OutDesc out_desc(const LineVals& r, int64_t pa, int64_t pb)
+{
+    OutDesc d;
+    const int64_t last_cd = r.newseg ? 0 : (int64_t)((uint64_t)pb - (uint64_t)pa);
+    const int64_t last_stop = r.newseg ? 0 : pb;
+    d.cd = (int64_t)((uint64_t)r.b - (uint64_t)r.a);
+    d.emit_p = (d.cd != last_cd);
+    d.v = (last_stop != 0) ? (int64_t)((uint64_t)r.a - (uint64_t)last_stop) : r.a;
+    uint32_t L = d.emit_p ? 2u + (uint32_t)n_digits_ref(d.cd) : 0u;
+    L += (uint32_t)dec_len(d.v) + 1u;
+    if (r.rem_len) L += 1u + r.rem_len;
+    d.len = L;
+    return d;
+}
+
+struct TfShared {                     // per-workgroup line exchange
+    int64_t a[kThreads + 1], b[kThreads + 1];
+    uint32_t cls[kThreads + 1], clen[kThreads + 1];
+};
+
+// Parse this thread's line (L0 + tid) and the line before it; returns whether
+// the line exists.  t.r.newseg follows hpp:393-407 (strcmp of chromosomes).
+struct TfLine {
+    LineVals r;
+    int64_t pa, pb;
+    uint64_t ls;
+};
+
+__device__ __forceinline__ bool tf_parse(const uint8_t* __restrict__ bed, const uint64_t* __restrict__ line_end,
+                                         uint64_t nl, uint64_t L0, bool staged, const uint8_t* tb, uint64_t a0,
+                                         TfShared& sh, TfLine& t)
+{
+    const uint32_t tid = threadIdx.x;
+    const uint64_t i = L0 + tid;
+    const bool have = i < nl;
+    bool fast = false;
+    t.ls = 0;
+    if (have) {
+        t.ls = i ? line_end[i - 1] : 0;
+        const uint64_t le = line_end[i];
+        if (staged) {
+            fast = parse_fast(tb, (uint32_t)(t.ls - a0), (uint32_t)(le - t.ls), t.ls, t.r);
+            if (!fast) t.r = parse_vals(LSrc{tb, a0}, line_end, i);
+        } else {
+            t.r = parse_vals(GSrc{bed}, line_end, i);
+        }
+        sh.a[tid + 1] = t.r.a;
+        sh.b[tid + 1] = t.r.b;
+        sh.cls[tid + 1] = (uint32_t)(t.ls - a0);
+        sh.clen[tid + 1] = t.r.chr_len;
+    }
+    if (tid == 0) {
+        int64_t a = 0, b = 0;
+        uint32_t clen = 0;
+        uint64_t pls = 0;
+        if (L0 > 0) {
+            pls = (L0 > 1) ? line_end[L0 - 2] : 0;
+            LineVals pr;
+            if (staged && parse_fast(tb, (uint32_t)(pls - a0), (uint32_t)(line_end[L0 - 1] - pls), pls, pr)) {
+                a = pr.a;
+                b = pr.b;
+                clen = pr.chr_len;
+            } else if (staged) {
+                parse_abc(LSrc{tb, a0}, line_end, L0 - 1, a, b, clen);
+            } else {
+                parse_abc(GSrc{bed}, line_end, L0 - 1, a, b, clen);
+            }
+        }
+        sh.a[0] = a;
+        sh.b[0] = b;
+        sh.cls[0] = (uint32_t)(pls - a0);
+        sh.clen[0] = clen;
+    }
+    __syncthreads();
+    if (!have) return false;
+    t.pa = sh.a[tid];
+    t.pb = sh.b[tid];
+    if (fast) {                          // chromosome vs. the previous line's
+        bool newseg = true;
+        if (i > 0) {
+            const uint32_t pc = sh.cls[tid], pcl = sh.clen[tid], cl = t.r.chr_len, c = (uint32_t)(t.ls - a0);
+            bool same = (pcl == cl);
+            for (uint32_t k = 0; same && k < cl; k += 8) {
+#pragma unroll
+                for (uint32_t j = 0; j < 8; ++j) {
+                    const bool e = tb[pc + k + j] == tb[c + k + j];
+                    if (k + j < cl) same = same && e;
+                }
+            }
+            newseg = !same;
+        }
+        t.r.newseg = newseg;
+    }
+    return true;
+}
+
+constexpr uint32_t kTf1Cap = kParseCap;
+constexpr uint32_t kTf2Cap = 16384;
+constexpr uint32_t kTfOutCap = 16384;
+
+__global__ void __launch_bounds__(kThreads)
+k_tf1(const uint8_t* __restrict__ bed, const uint64_t* __restrict__ line_end, uint64_t nl,
+      uint64_t* __restrict__ wg_len, uint32_t* __restrict__ wg_seg, uint32_t* __restrict__ any_fail)
+{
+    __shared__ uint4 tb4[(kTf1Cap + kStagePad) / 16];
+    __shared__ TfShared sh;
+    __shared__ uint64_t red[kThreads / 64];
+    const uint64_t L0 = (uint64_t)blockIdx.x * kThreads;
+    const uint64_t L1 = L0 + kThreads < nl ? L0 + kThreads : nl;
+    uint64_t a0 = 0;
+    const bool staged = stage_lines(bed, line_end, L0, L1, tb4, kTf1Cap, a0);
+    TfLine t;
+    uint64_t v = 0;
+    if (tf_parse(bed, line_end, nl, L0, staged, reinterpret_cast<const uint8_t*>(tb4), a0, sh, t)) {
+        if (!t.r.aok || !t.r.bok) atomicOr(any_fail, 1u);
+        v = ((uint64_t)out_desc(t.r, t.pa, t.pb).len << 20) | (t.r.newseg ? 1u : 0u);
+    }
+    v = wave_reduce_add(v);                     // bytes << 20 | segments (<= 256 per workgroup)
+    if ((threadIdx.x & 63) == 0) red[threadIdx.x >> 6] = v;
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        const uint64_t s = red[0] + red[1] + red[2] + red[3];
+        wg_len[blockIdx.x] = s >> 20;
+        wg_seg[blockIdx.x] = (uint32_t)(s & 0xFFFFFu);
+    }
+}
+
+template <class S>
+__device__ __forceinline__ void tf_write(const S& src, const TfLine& t, uint8_t* o)
+{
+    const OutDesc d = out_desc(t.r, t.pa, t.pb);
+    if (d.emit_p) {                                   // "p%ld\n" truncated to keep bytes (hpp:440,452)
+        const int keep = 2 + n_digits_ref(d.cd);
+        o[0] = 'p';
+        if (dec_len(d.cd) + 2 == keep) {
+            o[1 + put_dec(o + 1, d.cd)] = '\n';
+        } else {                                      // negative or INT64_MIN: the text is cut short
+            const uint64_t u = (d.cd < 0) ? 0ull - (uint64_t)d.cd : (uint64_t)d.cd;
+            const int nd = ndig_u64(u), sg = d.cd < 0 ? 1 : 0;
+            for (int j = 1; j < keep; ++j) {
+                const int q = j - 1 - sg;             // digit index, or the sign
+                uint8_t c;
+                if (q < 0) c = '-';
+                else if (q >= nd) c = '\n';
+                else {
+                    uint64_t x = u;
+                    for (int r = nd - 1 - q; r > 0; --r) x /= 10u;
+                    c = (uint8_t)('0' + x % 10u);
+                }
+                o[j] = c;
+            }
+        }
+        o += keep;
+    }
+    o += put_dec(o, d.v);
+    if (t.r.rem_len) {
+        *o++ = '\t';
+        for (uint32_t j = 0; j < t.r.rem_len; ++j) o[j] = src[t.r.rem_b + j];
+        o += t.r.rem_len;
+    }
+    *o = '\n';
+}
+
+__global__ void __launch_bounds__(kThreads)
+k_tf2(const uint8_t* __restrict__ bed, const uint64_t* __restrict__ line_end, uint64_t nl,
+      const uint64_t* __restrict__ wg_off, const uint64_t* __restrict__ wg_sego, uint8_t* __restrict__ text,
+      SegInfo* __restrict__ info)
+{
+    __shared__ uint4 tb4[(kTf2Cap + kStagePad) / 16];
+    __shared__ TfShared sh;
+    __shared__ uint32_t ob4[kTfOutCap / 4];
+    __shared__ uint64_t scan_sh[kThreads / 64 + 1];
+    const uint64_t L0 = (uint64_t)blockIdx.x * kThreads;
+    const uint64_t L1 = L0 + kThreads < nl ? L0 + kThreads : nl;
+    const uint64_t i = L0 + threadIdx.x;
+    uint64_t a0 = 0;
+    const bool staged = stage_lines(bed, line_end, L0, L1, tb4, kTf2Cap, a0);
+    const uint8_t* tb = reinterpret_cast<const uint8_t*>(tb4);
+    TfLine t;
+    const bool have = tf_parse(bed, line_end, nl, L0, staged, tb, a0, sh, t);
+    const uint64_t len = have ? out_desc(t.r, t.pa, t.pb).len : 0u;
+    const uint64_t ns = (have && t.r.newseg) ? 1u : 0u;
+    uint64_t tot = 0;
+    const uint64_t ex = block_excl_scan_add<uint64_t>((len << 20) | ns, scan_sh, &tot);
+    const uint64_t o0 = wg_off[blockIdx.x];
+    const uint64_t loc = ex >> 20, wlen = tot >> 20;
+    const bool in_lds = wlen <= kTfOutCap;
+    if (have) {
+        if (ns) {
+            SegInfo& s = info[wg_sego[blockIdx.x] + (ex & 0xFFFFFu)];
+            s.first_line = i;
+            s.name_off = t.ls;
+            s.name_len = t.r.chr_len;
+            s.text_off = o0 + loc;
+        }
+        uint8_t* ob = reinterpret_cast<uint8_t*>(ob4);
+        if (staged) {
+            const LSrc ls{tb, a0};
+            if (in_lds) tf_write(ls, t, ob + loc); else tf_write(ls, t, text + o0 + loc);
+        } else {
+            const GSrc gs{bed};
+            if (in_lds) tf_write(gs, t, ob + loc); else tf_write(gs, t, text + o0 + loc);
+        }
+    }
+    if (!in_lds) return;
+    __syncthreads();
+    const uint8_t* ob = reinterpret_cast<const uint8_t*>(ob4);
+    const uint32_t wl = (uint32_t)wlen;
+    uint32_t head = (uint32_t)((4u - (o0 & 3u)) & 3u);
+    head = head < wl ? head : wl;
+    if (threadIdx.x < head) text[o0 + threadIdx.x] = ob[threadIdx.x];
+    const uint32_t nw = (wl - head) / 4u;
+    uint32_t* dst = reinterpret_cast<uint32_t*>(text + o0 + head);
+    for (uint32_t w = threadIdx.x; w < nw; w += kThreads) {
+        const uint32_t q = head + 4u * w;
+        dst[w] = (uint32_t)ob[q] | ((uint32_t)ob[q + 1] << 8) | ((uint32_t)ob[q + 2] << 16) |
+                 ((uint32_t)ob[q + 3] << 24);
+    }
+    for (uint32_t k = head + 4u * nw + threadIdx.x; k < wl; k += kThreads) text[o0 + k] = ob[k];
+}
+
+// line_count / text_len of each segment from its successor (fused path)
+__global__ void k_seg_close(SegInfo* __restrict__ info, uint64_t nseg, uint64_t nl, uint64_t ttot)
+{
+    const uint64_t s = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (s >= nseg) return;
+    const uint64_t nf = (s + 1 < nseg) ? info[s + 1].first_line : nl;
+    const uint64_t nt = (s + 1 < nseg) ? info[s + 1].text_off : ttot;
+    info[s].line_count = nf - info[s].first_line;
+    info[s].text_len = nt - info[s].text_off;
 }
 
 // segment table: for each new-segment line, its ordinal -> first line
@@ -464,20 +898,39 @@ void TransformWorkspace::run(const uint8_t* d_bed, uint64_t n, hipStream_t st, T
     res.ff_pos = h[1];
     if (nl == 0) { res.n_segments = 0; res.text_bytes = 0; return; }
 
-    int64_t* start = b_start.as<int64_t>(nl);
-    int64_t* stop = b_stop.as<int64_t>(nl);
-    uint8_t* flags = b_flags.as<uint8_t>(nl);
-    uint64_t* rem_beg = b_rem_beg.as<uint64_t>(nl);
-    uint32_t* rem_len = b_rem_len.as<uint32_t>(nl);
-    uint32_t* chr_len = b_chr_len.as<uint32_t>(nl);
     uint32_t* any_fail = reinterpret_cast<uint32_t*>(scal + 5);
-    unsigned nb = (unsigned)ceil_div(nl, kThreads);
-    hipLaunchKernelGGL(k_parse, dim3(nb), dim3(kThreads), 0, st, d_bed, line_end, nl, start, stop, flags, rem_beg,
-                       rem_len, chr_len, any_fail);
+    const unsigned nb = (unsigned)ceil_div(nl, kThreads);
+    // fused path: pass 1 -> per-workgroup bytes / segments
+    uint64_t* wg_len = b_out_off.as<uint64_t>(2ull * nb + 2);
+    uint64_t* wg_off = wg_len + nb + 1;
+    uint32_t* wg_seg = b_seg_flag.as<uint32_t>(nb + 1);
+    uint64_t* wg_sego = b_seg_ord.as<uint64_t>(nb + 1);
+    hipLaunchKernelGGL(k_tf1, dim3(nb), dim3(kThreads), 0, st, d_bed, line_end, nl, wg_len, wg_seg, any_fail);
+    scan::excl_sum_u64(wg_len, wg_off, nb, scal + 4, b_tmp, st);
+    scan::excl_sum_u32_to_u64(wg_seg, wg_sego, nb, scal + 3, b_tmp, st);
     uint32_t fail = 0;
+    HIP_CHECK(hipMemcpyAsync(h, scal + 3, 2 * sizeof(uint64_t), hipMemcpyDeviceToHost, st));
     HIP_CHECK(hipMemcpyAsync(&fail, any_fail, sizeof(uint32_t), hipMemcpyDeviceToHost, st));
     HIP_CHECK(hipStreamSynchronize(st));
-    if (fail) {
+    uint64_t nseg = h[0], ttot = h[1];
+    SegInfo* info = nullptr;
+    if (!fail) {
+        info = b_seg_info.as<SegInfo>(nseg + 1);
+        text = b_text.as<uint8_t>(ttot + 64);
+        hipLaunchKernelGGL(k_tf2, dim3(nb), dim3(kThreads), 0, st, d_bed, line_end, nl, wg_off, wg_sego, text,
+                           info);
+        hipLaunchKernelGGL(k_seg_close, dim3((unsigned)ceil_div(nseg, 256)), dim3(256), 0, st, info, nseg, nl,
+                           ttot);
+    } else {
+        // general path: some start/stop does not parse (stale values, hpp:306-316)
+        int64_t* start = b_start.as<int64_t>(nl);
+        int64_t* stop = b_stop.as<int64_t>(nl);
+        uint8_t* flags = b_flags.as<uint8_t>(nl);
+        uint64_t* rem_beg = b_rem_beg.as<uint64_t>(nl);
+        uint32_t* rem_len = b_rem_len.as<uint32_t>(nl);
+        uint32_t* chr_len = b_chr_len.as<uint32_t>(nl);
+        hipLaunchKernelGGL(k_parse, dim3(nb), dim3(kThreads), 0, st, d_bed, line_end, nl, start, stop, flags,
+                           rem_beg, rem_len, chr_len, any_fail);
         uint64_t* idx = b_idx.as<uint64_t>(nl);
         for (int w = 0; w < 2; ++w) {
             hipLaunchKernelGGL(k_ok_index, dim3(nb), dim3(kThreads), 0, st, flags, nl,
@@ -489,26 +942,27 @@ void TransformWorkspace::run(const uint8_t* d_bed, uint64_t n, hipStream_t st, T
             HIP_CHECK(hipMemcpyAsync(cp, v, nl * sizeof(int64_t), hipMemcpyDeviceToDevice, st));
             hipLaunchKernelGGL(k_gather_stale, dim3(nb), dim3(kThreads), 0, st, cp, idx, nl, v);
         }
+        uint32_t* out_len = b_out_len.as<uint32_t>(nl);
+        uint32_t* seg_flag = b_seg_flag.as<uint32_t>(nl);
+        hipLaunchKernelGGL(k_line_len, dim3(nb), dim3(kThreads), 0, st, start, stop, flags, rem_len, nl, out_len,
+                           seg_flag);
+        uint64_t* out_off = b_out_off.as<uint64_t>(nl);
+        uint64_t* seg_ord = b_seg_ord.as<uint64_t>(nl);
+        scan::excl_sum_u32_to_u64(out_len, out_off, nl, scal + 4, b_tmp, st);
+        scan::excl_sum_u32_to_u64(seg_flag, seg_ord, nl, scal + 3, b_tmp, st);
+        HIP_CHECK(hipMemcpyAsync(h, scal + 3, 2 * sizeof(uint64_t), hipMemcpyDeviceToHost, st));
+        HIP_CHECK(hipStreamSynchronize(st));
+        nseg = h[0];
+        ttot = h[1];
+        uint64_t* seg_first = b_seg_first.as<uint64_t>(nseg + 1);
+        hipLaunchKernelGGL(k_seg_first, dim3(nb), dim3(kThreads), 0, st, seg_flag, seg_ord, nl, seg_first);
+        info = b_seg_info.as<SegInfo>(nseg + 1);
+        hipLaunchKernelGGL(k_seg_info, dim3((unsigned)ceil_div(nseg, 256)), dim3(256), 0, st, seg_first, nseg, nl,
+                           line_end, chr_len, out_off, ttot, info);
+        text = b_text.as<uint8_t>(ttot + 64);
+        hipLaunchKernelGGL(k_emit, dim3(nb), dim3(kThreads), 0, st, d_bed, start, stop, flags, rem_beg, rem_len,
+                           out_off, nl, text);
     }
-    uint32_t* out_len = b_out_len.as<uint32_t>(nl);
-    uint32_t* seg_flag = b_seg_flag.as<uint32_t>(nl);
-    hipLaunchKernelGGL(k_line_len, dim3(nb), dim3(kThreads), 0, st, start, stop, flags, rem_len, nl, out_len,
-                       seg_flag);
-    uint64_t* out_off = b_out_off.as<uint64_t>(nl);
-    uint64_t* seg_ord = b_seg_ord.as<uint64_t>(nl);
-    scan::excl_sum_u32_to_u64(out_len, out_off, nl, scal + 4, b_tmp, st);
-    scan::excl_sum_u32_to_u64(seg_flag, seg_ord, nl, scal + 3, b_tmp, st);
-    HIP_CHECK(hipMemcpyAsync(h, scal + 3, 2 * sizeof(uint64_t), hipMemcpyDeviceToHost, st));
-    HIP_CHECK(hipStreamSynchronize(st));
-    uint64_t nseg = h[0], ttot = h[1];
-    uint64_t* seg_first = b_seg_first.as<uint64_t>(nseg + 1);
-    hipLaunchKernelGGL(k_seg_first, dim3(nb), dim3(kThreads), 0, st, seg_flag, seg_ord, nl, seg_first);
-    SegInfo* info = b_seg_info.as<SegInfo>(nseg + 1);
-    hipLaunchKernelGGL(k_seg_info, dim3((unsigned)ceil_div(nseg, 256)), dim3(256), 0, st, seg_first, nseg, nl,
-                       line_end, chr_len, out_off, ttot, info);
-    text = b_text.as<uint8_t>(ttot + 64);
-    hipLaunchKernelGGL(k_emit, dim3(nb), dim3(kThreads), 0, st, d_bed, start, stop, flags, rem_beg, rem_len, out_off,
-                       nl, text);
     HIP_CHECK(hipGetLastError());
     res.n_segments = nseg;
     res.text_bytes = ttot;

@@ -111,6 +111,45 @@ def fuzz_bed(seed, nlines=60):
     return "".join(out).encode("latin-1")
 
 
+def parseable_fuzz_bed(seed, nlines=3000):
+    """Lines whose start and stop always parse (no stale values), in mixed
+    shapes: plain digits, signs and blanks, CRLF, 19-20 digit values, NUL bytes
+    in the chromosome or remainder, tab quirks, and runs of long lines so that
+    whole 256-line groups exceed the transform's LDS staging sizes."""
+    r = random.Random(seed)
+    chrs = ["chr1", "chr2", "chr10", "chrX", "c\x00hr", "chr1 "]
+    out, ci, pos = [], 0, 0
+    long_phase = 0
+    for i in range(nlines):
+        if i % 256 == 0 and r.random() < 0.3:
+            long_phase = r.choice([0, 90, 130, 400])
+        if r.random() < 0.01 or (i % 256 == 0 and r.random() < 0.2):
+            ci = r.randrange(len(chrs))
+            pos = 0
+        pos += r.randint(0, 300)
+        a, b = str(pos), str(pos + r.randint(0, 900))
+        k = r.random()
+        if k < 0.03:
+            a = r.choice([" ", "+", "  +", "0"]) + a
+        elif k < 0.05:
+            b = r.choice(["99999999999999999999", "9223372036854775807", "1234567890123456789",
+                          "123456789012345678"])
+        elif k < 0.06:
+            a = "-" + a
+        line = "%s\t%s\t%s" % (chrs[ci], a, b)
+        k = r.random()
+        if long_phase:
+            line += "\t" + "".join(r.choice("ACGT.") for _ in range(r.randint(long_phase // 2, long_phase)))
+        elif k < 0.2:
+            line += "\t" + r.choice(["id%d\t0\t+" % i, "a\x00b", "", "\t", "x\ty"])
+        if r.random() < 0.03:
+            line += "\r"
+        if r.random() < 0.02:
+            line = line.replace("\t", "\t\t", 1) if r.random() < 0.5 else line + "\t\t"
+        out.append(line + "\n")
+    return "".join(out).encode("latin-1")
+
+
 TRANSFORM_GENERATORS = {
     "cfg1_t10k": lambda: cfg1_bed(10000),
     "multi24_bed3": lambda: multi_chrom_bed(24, 400, seed=7, kind="bed3"),

@@ -42,6 +42,17 @@ def test_transform_matches_oracle_fuzz(ctx):
         assert segs == osegs
 
 
+def test_transform_fused_path_fuzz(ctx):
+    """All values parse: the fused two-pass kernels run, with fast (SWAR) and
+    byte-serial lines mixed inside and across 256-line groups."""
+    for seed in range(6):
+        data = corpus.parseable_fuzz_bed(seed=7000 + seed, nlines=3000 + 97 * seed)
+        text, segs = ctx.transform(data)
+        otext, osegs = oracle_lib.transform(data)
+        assert text == otext
+        assert segs == osegs
+
+
 def test_transform_empty_and_unterminated(ctx):
     assert ctx.transform(b"") == (b"", [])
     assert ctx.transform(b"chr1\t1\t2") == (b"", [])
