@@ -71,7 +71,7 @@ constexpr uint32_t RBITS = 20;          // rank bits (n <= 899,985 < 2^20)
 constexpr uint32_t TEXT_ROUNDS = 4;     // max text-extension rounds before doubling
 
 // counters (u32) in the meta buffer
-enum { C_W = 0, C_S, C_M1, C_M2, C_M3, C_L0, C_L1, C_T0, C_T1, C_TIE_ELEMS, C_ERR, C_TS0, C_TS1, C_N = 16 };
+enum { C_W = 0, C_S, C_M1, C_M2, C_M3, C_L0, C_L1, C_T0, C_T1, C_TIE_ELEMS, C_ERR, C_TS0, C_TS1, C_H, C_N = 16 };
 
 // item = slot[63:52] | start[51:32] | size[31:12] | parity[7] | shift[6:0]
 __device__ __forceinline__ uint64_t mk_item(uint32_t slot, uint32_t s, uint32_t m, uint32_t shift, uint32_t par)
@@ -191,6 +191,23 @@ struct KeySrc {
         if (rr >= n) rr -= n;
         return pss_bits(pss, (uint64_t)rr * B, kbits);
     }
+    // the key and the last-column symbol of rotation r (the symbol before it,
+    // mostly in the key's first word).  Doubling keys (usek): ls is left for
+    // last_sym() to fill from the block text.
+    __device__ __forceinline__ uint64_t key_ls(uint64_t q, uint32_t r, uint32_t& ls) const
+    {
+        if (usek) { ls = 0; return k[q]; }
+        uint32_t rr = r + off;
+        if (rr >= n) rr -= n;
+        const uint64_t bit = (uint64_t)rr * B;
+        const uint64_t wq = bit >> 6;
+        const uint32_t p = (uint32_t)(bit & 63u);
+        const uint64_t a = pss[wq];
+        const uint64_t v = p ? ((a << p) | (pss[wq + 1] >> (64u - p))) : a;
+        if (off == 0 && r != 0 && p >= B) ls = (uint32_t)((a << (p - B)) >> (64u - B));
+        else ls = (uint32_t)pss_bits(pss, (uint64_t)(r ? r - 1u : n - 1u) * B, B);
+        return v >> (64u - kbits);
+    }
 };
 
 __device__ __forceinline__ KeySrc key_src(const Ctx& c, uint32_t slot, uint32_t par)
@@ -211,6 +228,26 @@ __device__ __forceinline__ KeySrc key_src(const Ctx& c, uint32_t slot, uint32_t 
         k.off = (uint32_t)(((uint64_t)g.D + (uint64_t)(c.rtext - 1) * g.Dp) % k.n);
     }
     return k;
+}
+
+// Last-column symbol of rotation v: the rank (among the block's used byte
+// values) of block[(v - 1) mod n] -- what the MTF consumes.  Rounds 0 and text
+// rounds read it from the PSS; doubling rounds (PSS overwritten by keys) from
+// the block text.  Written next to every final SA entry, so no separate
+// gather pass over the block is needed.
+__device__ __forceinline__ uint8_t last_sym(const Ctx& c, uint32_t slot, uint32_t v)
+{
+    const uint32_t b = c.b0 + slot;
+    const uint32_t n = c.blocks[b].n;
+    const uint32_t p = v ? v - 1u : n - 1u;
+    if (!c.keysrc) {
+        const uint32_t B = c.L.geo[slot].B;
+        return (uint8_t)pss_bits(c.scr.K + (uint64_t)slot * c.scr.stride, (uint64_t)p * B, B);
+    }
+    const uint32_t byte = c.blkbytes[(uint64_t)b * c.stride + p];
+    uint32_t r = __popc(c.blocks[b].in_use[byte >> 5] & ((1u << (byte & 31u)) - 1u));
+    for (uint32_t j = 0; j < (byte >> 5); ++j) r += __popc(c.blocks[b].in_use[j]);
+    return (uint8_t)r;
 }
 
 // symbol map of a block (rank among used byte values), >= 256 threads
@@ -392,7 +429,10 @@ __global__ void __launch_bounds__(SCT) k3_scatter(Ctx c)
             const uint32_t d = (uint32_t)pss_bits(pss, (uint64_t)r * B, PDIG);
             const uint32_t p = atomicAdd(&cur[d], 1u);
             SA[p] = r;
-            if (r == 0 && tot[d] == 1u) c.blocks[b].orig_ptr = p;
+            if (tot[d] == 1u) {                      // singleton bucket: final
+                c.scr.LL[so + p] = (uint8_t)pss_bits(pss, (uint64_t)(r ? r - 1u : n - 1u) * B, B);
+                if (r == 0) c.blocks[b].orig_ptr = p;
+            }
         }
         __syncthreads();
     }
@@ -537,6 +577,7 @@ __global__ void __launch_bounds__(LT) k3_part_l(Ctx c, const uint64_t* __restric
             if (cc == 1) {
                 const uint32_t v = dv[ss];
                 if (!par) SA[ss] = v;
+                c.scr.LL[base + ss] = last_sym(c, slot, v);
                 if (c.mode) RK[v] = s + ss;
                 if (v == 0) c.blocks[b].orig_ptr = s + ss;
                 nruns = 1;
@@ -562,6 +603,7 @@ __global__ void __launch_bounds__(LT) k3_part_l(Ctx c, const uint64_t* __restric
             for (uint32_t i = tid; i < cc; i += LT) {
                 const uint32_t v = dv[ss + i];
                 if (!par) SA[ss + i] = v;
+                c.scr.LL[base + ss + i] = last_sym(c, slot, v);
                 if (c.mode) RK[v] = s + ss;
                 if (v == 0) c.blocks[b].orig_ptr = s + ss + i;
             }
@@ -577,13 +619,15 @@ __global__ void __launch_bounds__(LT) k3_part_l(Ctx c, const uint64_t* __restric
 
 // Finish a sorted group: SA, RK, origPtr, tie groups, run count.
 // Called by every thread of a wave with (j = sorted position in the group,
-// v = rotation, valid, hp = head position of j's run, end = j ends its run).
+// v = rotation, valid, hp = head position of j's run, end = j ends its run,
+// lsym = last-column symbol of v).
 __device__ __forceinline__ void emit_sorted(const Ctx& c, uint32_t slot, uint32_t s, uint32_t j, uint32_t v,
-                                            bool valid, uint32_t hp, bool end, uint32_t& runs_acc)
+                                            bool valid, uint32_t hp, bool end, uint32_t& runs_acc, uint32_t lsym)
 {
     const uint64_t so = (uint64_t)slot * c.scr.stride;
     if (valid) {
         c.scr.SA[so + s + j] = v;
+        c.scr.LL[so + s + j] = (uint8_t)lsym;
         if (c.mode) c.scr.RK[so + v] = s + hp;
         if (v == 0) c.blocks[c.b0 + slot].orig_ptr = s + j;
     }
@@ -617,14 +661,16 @@ __global__ void __launch_bounds__(256) k3_sort_w(Ctx c, const uint64_t* __restri
         const KeySrc ks = key_src(c, slot, par);
         const bool valid = (uint32_t)lane < m;
         const uint32_t v = valid ? sv[lane] : 0u;
-        const uint64_t k = valid ? ks(s + lane, v) : ~0ull;
+        uint32_t ls = 0;
+        const uint64_t k = valid ? ks.key_ls(s + lane, v, ls) : ~0ull;
+        if (valid && ks.usek) ls = last_sym(c, slot, v);
         uint32_t r = 0;
         for (uint32_t j = 0; j < m; ++j) {
             const uint64_t kj = __shfl(k, (int)j, 64);
             r += (kj < k || (kj == k && (int)j < lane)) ? 1u : 0u;
         }
         wave_sync_lds3();                                // previous group's reads are done
-        if (valid) { skey[wid][r] = k; sval[wid][r] = v; }
+        if (valid) { skey[wid][r] = k; sval[wid][r] = v | (ls << 24); }
         wave_sync_lds3();
         const uint64_t key = valid ? skey[wid][lane] : 0;
         const uint32_t val = valid ? sval[wid][lane] : 0;
@@ -633,7 +679,7 @@ __global__ void __launch_bounds__(256) k3_sort_w(Ctx c, const uint64_t* __restri
         const uint32_t hp = wave_incl_scan_max<uint32_t>(head ? (uint32_t)lane : 0u);
         asm volatile("s_waitcnt vmcnt(0)" ::: "memory");   // SA reads of this group done before the writes
         uint32_t runs = 0;
-        emit_sorted(c, slot, s, (uint32_t)lane, val, valid, hp, end, runs);
+        emit_sorted(c, slot, s, (uint32_t)lane, val & 0xFFFFFFu, valid, hp, end, runs, val >> 24);
         if (c.mode && lane == 0) atomicAdd(&c.L.runs[slot], runs);
     }
 }
@@ -659,7 +705,8 @@ __device__ __forceinline__ void gsync()
 }
 
 template <int NW, int E>
-__global__ void __launch_bounds__(256) k3_sort_lds(Ctx c, const uint64_t* __restrict__ items)
+__global__ void __launch_bounds__(256) k3_sort_lds(Ctx c, const uint64_t* __restrict__ items,
+                                                    const uint32_t* __restrict__ hard_n)
 {
     constexpr int IPW = 4 / NW;                    // groups per workgroup
     constexpr int CAP = NW * 64 * E;
@@ -690,9 +737,13 @@ __global__ void __launch_bounds__(256) k3_sort_lds(Ctx c, const uint64_t* __rest
     const uint64_t lt = lanemask_lt();
     // static assignment: workgroup L works XCD segment L mod 8 (the XCD it runs
     // on under round-robin dealing); its IPW groups stride over the segment
-    const uint32_t xs = blockIdx.x & 7u, nwk = (gridDim.x >> 3) * (uint32_t)IPW;
-    const uint32_t e_end = c.qseg[xs + 1];
-    for (uint32_t it = c.qseg[xs] + (blockIdx.x >> 3) * (uint32_t)IPW + (uint32_t)g; it < e_end; it += nwk) {
+    // (hard_n: an unbinned list of *hard_n groups, grid-strided)
+    const uint32_t xs = blockIdx.x & 7u;
+    const uint32_t nwk = hard_n ? gridDim.x * (uint32_t)IPW : (gridDim.x >> 3) * (uint32_t)IPW;
+    const uint32_t e_end = hard_n ? *hard_n : c.qseg[xs + 1];
+    const uint32_t it0 = hard_n ? blockIdx.x * (uint32_t)IPW + (uint32_t)g
+                                : c.qseg[xs] + (blockIdx.x >> 3) * (uint32_t)IPW + (uint32_t)g;
+    for (uint32_t it = it0; it < e_end; it += nwk) {
     const uint64_t item = items[it];
     const uint32_t slot = it_slot(item), s = it_start(item), m = it_size(item), par = it_par(item);
     const uint64_t base = (uint64_t)slot * c.scr.stride + s;
@@ -714,10 +765,12 @@ __global__ void __launch_bounds__(256) k3_sort_lds(Ctx c, const uint64_t* __rest
         for (int e = 0; e < E; ++e) {
             const uint32_t i = (uint32_t)(wid * 64 * E + e * 64 + lane);
             if (i < m) {
-                const uint64_t kx = ks(s + i, vv[e]);
+                uint32_t ls;
+                const uint64_t kx = ks.key_ls(s + i, vv[e], ls);
+                if (ks.usek) ls = last_sym(c, slot, vv[e]);
                 diff |= kx ^ k0;
                 k[e] = (kx & KMASK) | ((uint64_t)i << KEYB);
-                vb_all[g][i] = vv[e];
+                vb_all[g][i] = vv[e] | (ls << 24);
             } else {
                 k[e] = ~0ull;                          // pads: max key, last in stable order
             }
@@ -926,9 +979,272 @@ __global__ void __launch_bounds__(256) k3_sort_lds(Ctx c, const uint64_t* __rest
         const bool valid = j < m;
         const uint32_t vb = valid ? vb_all[g][(uint32_t)(k[e] >> KEYB)] : 0u;
         const bool end = valid && (!ties || j + 1 == m || ((xk[j + 1] ^ k[e]) & KMASK) != 0);
-        emit_sorted(c, slot, s, j, vb, valid, hp[e], end, runs);
+        emit_sorted(c, slot, s, j, vb & 0xFFFFFFu, valid, hp[e], end, runs, vb >> 24);
     }
     if (c.mode && lane == 0 && runs) atomicAdd(&c.L.runs[slot], runs);
+    }
+}
+
+// ---------------------------------------------------------------------------
+// k3_sort_grp<NW, E>: the common case of k3_sort_lds without its LSD path.
+// One MSD digit (the DB bits below the highest varying key bit) scatters the
+// group in LDS; then every element ranks itself inside its sub-bucket by
+// comparison, working in digit order so the lanes of a wave mostly share a
+// sub-bucket.  Ranking costs about sum(z^2) comparisons over the sub-bucket
+// sizes z: a group whose digit spreads it badly (sum z^2 > HARD_Q * m) is
+// left untouched and listed for k3_sort_lds.  While a group is sorted, the
+// next group's rotations and keys are already being loaded (software
+// pipeline: item two ahead, rotations and keys one ahead).
+// ---------------------------------------------------------------------------
+constexpr uint32_t HARD_Q = 32;
+
+template <int E>
+struct GrpIn {                 // one group's inputs, as loaded
+    uint64_t item;
+    KeySrc ks;
+    uint32_t v[E];
+    uint32_t v0;
+    uint64_t kx[E];
+    uint32_t ls[E];
+    uint64_t k0;
+};
+
+template <int NW, int E>
+__device__ __forceinline__ void grp_load_vals(const Ctx& c, GrpIn<E>& x, bool ok, int wid, int lane)
+{
+    const uint32_t slot = it_slot(x.item), s = it_start(x.item), m = ok ? it_size(x.item) : 0u,
+                   par = it_par(x.item);
+    const uint32_t* sv = (par ? c.scr.V : c.scr.SA) + (uint64_t)slot * c.scr.stride + s;
+    if (ok) x.ks = key_src(c, slot, par);
+#pragma unroll
+    for (int e = 0; e < E; ++e) {
+        const uint32_t i = (uint32_t)(wid * 64 * E + e * 64 + lane);
+        x.v[e] = i < m ? sv[i] : 0u;
+    }
+    x.v0 = m ? sv[0] : 0u;
+}
+
+template <int NW, int E>
+__device__ __forceinline__ void grp_load_keys(const Ctx& c, GrpIn<E>& x, bool ok, int wid, int lane)
+{
+    const uint32_t s = it_start(x.item), m = ok ? it_size(x.item) : 0u;
+#pragma unroll
+    for (int e = 0; e < E; ++e) {
+        const uint32_t i = (uint32_t)(wid * 64 * E + e * 64 + lane);
+        x.ls[e] = 0;
+        x.kx[e] = i < m ? x.ks.key_ls(s + i, x.v[e], x.ls[e]) : 0ull;
+        if (i < m && x.ks.usek) x.ls[e] = last_sym(c, it_slot(x.item), x.v[e]);
+    }
+    x.k0 = m ? x.ks(s, x.v0) : 0ull;
+}
+
+template <int NW, int E>
+__global__ void __launch_bounds__(256) k3_sort_grp(Ctx c, const uint64_t* __restrict__ items,
+                                                    uint64_t* __restrict__ hard)
+{
+    constexpr int IPW = 4 / NW;                    // groups per workgroup
+    constexpr int CAP = NW * 64 * E;
+    constexpr int IDXB = CAP <= 256 ? 8 : 12;      // packed local index bits
+    constexpr int KEYB = 64 - IDXB;
+    constexpr uint64_t KMASK = (1ull << KEYB) - 1ull;
+    static_assert(CAP <= (1 << IDXB), "index does not fit");
+    constexpr int DB = CAP <= 256 ? 8 : (CAP <= 1024 ? 10 : 11);   // MSD digit bits
+    constexpr int NBIN = 1 << DB;
+    constexpr int T = NW * 64;
+    constexpr int BPT = NBIN / T;                  // bins per thread
+    __shared__ uint64_t xk_all[IPW][CAP];
+    __shared__ uint32_t vb_all[IPW][CAP];          // rotations by group index
+    __shared__ uint32_t bst_all[IPW][NBIN + 1];    // sub-bucket starts
+    __shared__ uint32_t bcur_all[IPW][NBIN];       // scatter cursors
+    __shared__ uint32_t sc_all[IPW][NW + 1];
+    __shared__ uint64_t red_all[4];
+    __shared__ uint32_t wsq_all[4];
+    __shared__ uint32_t wmax_all[4];
+    __shared__ uint32_t flag_all[4];
+    const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+    const int g = wave / NW, wid = wave % NW, w0 = g * NW;
+    uint64_t* xk = xk_all[g];
+    uint32_t* sc = sc_all[g];
+    uint32_t* bst = bst_all[g];
+    uint32_t* bcur = bcur_all[g];
+    const int tg = wid * 64 + lane;
+    // static assignment: workgroup L works XCD segment L mod 8 (the XCD it runs
+    // on under round-robin dealing); its IPW groups stride over the segment
+    const uint32_t xs = blockIdx.x & 7u, nwk = (gridDim.x >> 3) * (uint32_t)IPW;
+    const uint32_t e_end = c.qseg[xs + 1];
+    uint32_t it = c.qseg[xs] + (blockIdx.x >> 3) * (uint32_t)IPW + (uint32_t)g;
+    GrpIn<E> cur, nxt;
+    cur.item = it < e_end ? items[it] : 0ull;
+    nxt.item = it + nwk < e_end ? items[it + nwk] : 0ull;
+    grp_load_vals<NW, E>(c, cur, it < e_end, wid, lane);
+    grp_load_keys<NW, E>(c, cur, it < e_end, wid, lane);
+    grp_load_vals<NW, E>(c, nxt, it + nwk < e_end, wid, lane);
+    uint64_t nitem2 = it + 2 * nwk < e_end ? items[it + 2 * nwk] : 0ull;
+    for (; it < e_end; it += nwk) {
+    const uint64_t item = cur.item;
+    const uint32_t slot = it_slot(item), s = it_start(item), m = it_size(item);
+    gsync<NW>();                                   // the previous group's LDS reads are done
+
+    uint64_t k[E];
+    uint64_t diff = 0;
+#pragma unroll
+    for (int e = 0; e < E; ++e) {
+        const uint32_t i = (uint32_t)(wid * 64 * E + e * 64 + lane);
+        if (i < m) {
+            diff |= cur.kx[e] ^ cur.k0;
+            k[e] = (cur.kx[e] & KMASK) | ((uint64_t)i << KEYB);
+            vb_all[g][i] = cur.v[e] | (cur.ls[e] << 24);
+        } else {
+            k[e] = ~0ull;                              // pads: max key, last in order
+        }
+    }
+#pragma unroll
+    for (int d = 32; d >= 1; d >>= 1) diff |= __shfl_xor(diff, d, 64);
+    if constexpr (NW > 1) {
+        if (lane == 0) red_all[wave] = diff;
+        __syncthreads();
+        diff = 0;
+#pragma unroll
+        for (int w = 0; w < NW; ++w) diff |= red_all[w0 + w];
+    }
+    if ((diff >> KEYB) && tg == 0) atomicOr(&c.L.ctr[C_ERR], 1u);   // top bits not shared
+
+    bool is_hard = false;
+    const uint64_t kdiff = diff & KMASK;
+    if (kdiff) {
+        const int hb = 63 - __clzll((long long)kdiff);
+        const int lo = hb + 1 - DB > 0 ? hb + 1 - DB : 0;
+        for (int q = tg; q < NBIN; q += T) bcur[q] = 0;
+        gsync<NW>();
+        uint32_t dg[E];
+#pragma unroll
+        for (int e = 0; e < E; ++e) {
+            dg[e] = (uint32_t)(((k[e] & KMASK) >> lo) & (uint64_t)(NBIN - 1));
+            if ((uint32_t)(wid * 64 * E + e * 64 + lane) < m) atomicAdd(&bcur[dg[e]], 1u);
+        }
+        gsync<NW>();
+        uint32_t loc[BPT], sum = 0, sq = 0;
+#pragma unroll
+        for (int q = 0; q < BPT; ++q) {
+            loc[q] = bcur[tg * BPT + q];
+            sum += loc[q];
+            sq += loc[q] * loc[q];
+        }
+        const uint32_t incl = wave_incl_scan_add(sum);
+        uint32_t run = incl - sum;
+        sq = wave_reduce_add(sq);
+        if constexpr (NW > 1) {
+            if (lane == 63) sc[wid] = incl;
+            if (lane == 0) wsq_all[wave] = sq;
+            __syncthreads();
+            for (int w = 0; w < wid; ++w) run += sc[w];
+            sq = 0;
+            for (int w = 0; w < NW; ++w) sq += wsq_all[w0 + w];
+        }
+        is_hard = sq > HARD_Q * m;                 // uniform per group
+        if (!is_hard) {
+#pragma unroll
+            for (int q = 0; q < BPT; ++q) { bst[tg * BPT + q] = run; bcur[tg * BPT + q] = run; run += loc[q]; }
+            if (tg == T - 1) bst[NBIN] = run;
+            gsync<NW>();
+#pragma unroll
+            for (int e = 0; e < E; ++e)
+                if ((uint32_t)(wid * 64 * E + e * 64 + lane) < m) xk[atomicAdd(&bcur[dg[e]], 1u)] = k[e];
+            gsync<NW>();
+            // rank in digit order: position j holds kj; its final place is
+            // bs + #{q in its sub-bucket: kq < kj, or kq == kj and q < j}
+            uint32_t pos[E];
+#pragma unroll
+            for (int e = 0; e < E; ++e) {
+                const uint32_t j = (uint32_t)(wid * 64 * E + e * 64 + lane);
+                pos[e] = j;
+                if (j < m) {
+                    const uint64_t kj = xk[j];
+                    const uint64_t km = kj & KMASK;
+                    const uint32_t d = (uint32_t)((km >> lo) & (uint64_t)(NBIN - 1));
+                    const uint32_t bs = bst[d], be = bst[d + 1];
+                    uint32_t r = 0;
+                    for (uint32_t q = bs; q < be; ++q) {
+                        const uint64_t kq = xk[q] & KMASK;
+                        r += (kq < km || (kq == km && q < j)) ? 1u : 0u;
+                    }
+                    pos[e] = bs + r;
+                    k[e] = kj;
+                }
+            }
+            gsync<NW>();
+#pragma unroll
+            for (int e = 0; e < E; ++e) xk[pos[e]] = k[e];
+        } else {
+            gsync<NW>();                           // bcur/sc reads done
+            if (tg == 0) hard[atomicAdd(&c.L.ctr[C_H], 1u)] = item;
+        }
+    } else {
+#pragma unroll
+        for (int e = 0; e < E; ++e) xk[wid * 64 * E + e * 64 + lane] = k[e];
+    }
+    // next group's keys (its rotations were loaded one group ago), the item after it
+    grp_load_keys<NW, E>(c, nxt, it + nwk < e_end, wid, lane);
+    const uint64_t nitem3 = it + 3 * nwk < e_end ? items[it + 3 * nwk] : 0ull;
+    if (!is_hard) {
+    gsync<NW>();
+#pragma unroll
+    for (int e = 0; e < E; ++e) k[e] = xk[wid * 64 * E + e * 64 + lane];
+    // runs of equal keys in sorted order j = wid*64*E + e*64 + lane
+    bool tie_here = false;
+#pragma unroll
+    for (int e = 0; e < E; ++e) {
+        const uint32_t j = (uint32_t)(wid * 64 * E + e * 64 + lane);
+        if (j > 0 && j < m && ((xk[j - 1] ^ k[e]) & KMASK) == 0) tie_here = true;
+    }
+    bool ties = __ballot(tie_here) != 0;
+    if constexpr (NW > 1) {
+        if (lane == 0) flag_all[wave] = ties ? 1u : 0u;
+        __syncthreads();
+        ties = false;
+        for (int w = 0; w < NW; ++w) ties |= flag_all[w0 + w] != 0;
+    }
+    uint32_t hp[E];
+    if (!ties) {
+#pragma unroll
+        for (int e = 0; e < E; ++e) hp[e] = (uint32_t)(wid * 64 * E + e * 64 + lane);
+    } else {
+        uint32_t carry = 0;
+#pragma unroll
+        for (int e = 0; e < E; ++e) {
+            const uint32_t j = (uint32_t)(wid * 64 * E + e * 64 + lane);
+            const bool head = j < m && (j == 0 || ((xk[j - 1] ^ k[e]) & KMASK) != 0);
+            uint32_t xx = wave_incl_scan_max<uint32_t>(head ? j : 0u);
+            xx = xx > carry ? xx : carry;
+            hp[e] = xx;
+            carry = __shfl(xx, 63, 64);
+        }
+        if constexpr (NW > 1) {
+            if (lane == 0) wmax_all[wave] = carry;
+            __syncthreads();
+            uint32_t pre = 0;
+            for (int w = 0; w < wid; ++w) pre = wmax_all[w0 + w] > pre ? wmax_all[w0 + w] : pre;
+#pragma unroll
+            for (int e = 0; e < E; ++e) hp[e] = hp[e] > pre ? hp[e] : pre;
+        }
+    }
+    // the group's SA range was read (values consumed above) before any write
+    uint32_t runs = 0;
+#pragma unroll
+    for (int e = 0; e < E; ++e) {
+        const uint32_t j = (uint32_t)(wid * 64 * E + e * 64 + lane);
+        const bool valid = j < m;
+        const uint32_t vb = valid ? vb_all[g][(uint32_t)(k[e] >> KEYB)] : 0u;
+        const bool end = valid && (!ties || j + 1 == m || ((xk[j + 1] ^ k[e]) & KMASK) != 0);
+        emit_sorted(c, slot, s, j, vb & 0xFFFFFFu, valid, hp[e], end, runs, vb >> 24);
+    }
+    if (c.mode && lane == 0 && runs) atomicAdd(&c.L.runs[slot], runs);
+    }
+    // rotate the pipeline: next group's rotations, the one after it
+    cur = nxt;
+    nxt.item = nitem2;
+    nitem2 = nitem3;
+    grp_load_vals<NW, E>(c, nxt, it + 2 * nwk < e_end, wid, lane);
     }
 }
 
@@ -1167,11 +1483,41 @@ void launch_bwt3(BlockDesc* blocks, uint32_t b0, uint32_t nb, const uint8_t* blk
         // every launch reads its own binned copy; stream order lets them share one buffer
         // grids: a multiple of 8 (static per-XCD segments), about one resident wave of workgroups
         auto g8 = [](uint32_t x) { return dim3((x + 7) / 8 * 8); };
-        if (n3) { bin(c.L.m3, n3, bout); hipLaunchKernelGGL((k3_sort_lds<4, 16>), g8(ncu * 2), dim3(256), 0, st, c, bout); }
-        if (n2) { bin(c.L.m2, n2, bout); hipLaunchKernelGGL((k3_sort_lds<4, 8>), g8(ncu * 3), dim3(256), 0, st, c, bout); }
-        if (n1) { bin(c.L.m1, n1, bout); hipLaunchKernelGGL((k3_sort_lds<4, 4>), g8(ncu * 4), dim3(256), 0, st, c, bout); }
-        if (ns) { bin(c.L.s, ns, bout); hipLaunchKernelGGL((k3_sort_lds<1, 4>), g8(ncu * 5), dim3(256), 0, st, c, bout); }
-        if (nw) { bin(c.L.w, nw, bout); hipLaunchKernelGGL(k3_sort_w, g8(ncu * 8), dim3(256), 0, st, c, bout); }
+        // static assignment needs every workgroup resident at once: one wave of
+        // workgroups, sized by the kernel's occupancy
+        auto resident = [&](const void* f) {
+            int per_cu = 0;
+            HIP_CHECK(hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, f, 256, 0));
+            return g8((uint32_t)ncu * (uint32_t)(per_cu > 0 ? per_cu : 1));
+        };
+        static const dim3 gm3 = resident(reinterpret_cast<const void*>(&k3_sort_lds<4, 16>));
+        static const dim3 gm2 = resident(reinterpret_cast<const void*>(&k3_sort_lds<4, 8>));
+        static const dim3 gm1 = resident(reinterpret_cast<const void*>(&k3_sort_lds<4, 4>));
+        static const dim3 gs = resident(reinterpret_cast<const void*>(&k3_sort_grp<1, 4>));
+        static const dim3 gw = resident(reinterpret_cast<const void*>(&k3_sort_w));
+        // M classes: k3_sort_lds (MSD digit + compare, LSD fallback); S: k3_sort_grp,
+        // then the groups it listed as hard (k3_sort_lds) from the class list it consumed
+        const uint32_t* hard_n = c.L.ctr + C_H;
+        auto clear_h = [&]() { HIP_CHECK(hipMemsetAsync(c.L.ctr + C_H, 0, sizeof(uint32_t), st)); };
+        if (n3) {
+            bin(c.L.m3, n3, bout);
+            hipLaunchKernelGGL((k3_sort_lds<4, 16>), gm3, dim3(256), 0, st, c, bout, nullptr);
+        }
+        if (n2) {
+            bin(c.L.m2, n2, bout);
+            hipLaunchKernelGGL((k3_sort_lds<4, 8>), gm2, dim3(256), 0, st, c, bout, nullptr);
+        }
+        if (n1) {
+            bin(c.L.m1, n1, bout);
+            hipLaunchKernelGGL((k3_sort_lds<4, 4>), gm1, dim3(256), 0, st, c, bout, nullptr);
+        }
+        if (ns) {
+            bin(c.L.s, ns, bout);
+            clear_h();
+            hipLaunchKernelGGL((k3_sort_grp<1, 4>), gs, dim3(256), 0, st, c, bout, c.L.s);
+            hipLaunchKernelGGL((k3_sort_lds<1, 4>), dim3(ncu / 2), dim3(256), 0, st, c, c.L.s, hard_n);
+        }
+        if (nw) { bin(c.L.w, nw, bout); hipLaunchKernelGGL(k3_sort_w, gw, dim3(256), 0, st, c, bout); }
         HIP_CHECK(hipGetLastError());
         HIP_CHECK(hipMemsetAsync(c.L.ctr + C_W, 0, 5 * sizeof(uint32_t), st));
     };

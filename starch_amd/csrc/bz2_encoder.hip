@@ -203,7 +203,11 @@ void Encoder::plan(const uint8_t* d_text, const std::vector<StreamIn>& streams, 
                 launch_fallback(d_blocks, b0, d_which, (uint32_t)which.size(), d_blkbytes, blk_stride_, scr, st);
                 if (stats) stats->periodic_blocks += which.size();
             }
-            launch_last_col(d_blocks, b0, nullptr, cnt, d_blkbytes, blk_stride_, scr, st);
+            // the v3 sort writes the last column next to SA; the v1 sort and the
+            // fallback (periodic blocks) leave it to the gather kernel
+            if (lsd) launch_last_col(d_blocks, b0, nullptr, cnt, d_blkbytes, blk_stride_, scr, st);
+            else if (!which.empty())
+                launch_last_col(d_blocks, b0, d_which, (uint32_t)which.size(), d_blkbytes, blk_stride_, scr, st);
         }
         {
             EvTimer tm(st, stats ? &stats->mtf : nullptr);

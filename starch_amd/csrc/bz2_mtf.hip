@@ -1,9 +1,9 @@
 // starch_amd/csrc/bz2_mtf.hip -- move-to-front and RUNA/RUNB coding on MI355X
 // (restates makeMaps_e + generateMTFValues, bz:compress.c:105-231).
 //
-// Input: the block's last column, written by the block sort next to SA
-// (BwtScratch::LL, raw bytes block[(ptr[i]-1) mod n]); mapped to sequence
-// symbols (makeMaps_e) through an LDS table.
+// Input: the block's last column as sequence symbols (makeMaps_e ranks of
+// block[(ptr[i]-1) mod n]), BwtScratch::LL, written by the block sort next
+// to SA (k_last_col below for blocks sorted by the fallback).
 //
 // One 1024-thread workgroup per block, the block split into 1024 contiguous
 // chunks of 128-byte lines.  MTF is made parallel by the chunk decomposition
@@ -141,7 +141,6 @@ __global__ void __launch_bounds__(MT) k_mtf_nib(BlockDesc* __restrict__ blocks, 
 {
     __shared__ NibState nst[MT];
     __shared__ RunSum wsum[MT / 64];
-    __shared__ uint8_t seq[256];
     __shared__ RunSum total_sh;
 
     const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
@@ -150,13 +149,6 @@ __global__ void __launch_bounds__(MT) k_mtf_nib(BlockDesc* __restrict__ blocks, 
     const uint32_t n = blocks[b].n;
     const uint32_t nin = blocks[b].n_in_use;
     if (nin > 16) return;                       // uniform per workgroup: k_mtf_big
-    if (tid < 256) {                            // makeMaps_e: unseqToSeq
-        uint32_t c = tid, below = 0;
-        for (uint32_t j = 0; j < (c >> 5); ++j) below += __popc(blocks[b].in_use[j]);
-        below += __popc(blocks[b].in_use[c >> 5] & ((1u << (c & 31)) - 1u));
-        seq[c] = (uint8_t)below;
-    }
-    __syncthreads();
     const uint8_t* ll = LL + (uint64_t)slot * ll_stride;
     uint16_t* mtfv = mtfv_all + (uint64_t)b * mtf_stride;
     const uint32_t csz = ((n + MT - 1) / MT + LINE - 1) & ~(LINE - 1);
@@ -172,7 +164,7 @@ __global__ void __launch_bounds__(MT) k_mtf_nib(BlockDesc* __restrict__ blocks, 
             const uint32_t lim = e - j0;
             visit_line<false>(ll + j0, [&](int k, uint32_t byte) {
                 if ((uint32_t)k < lim) {
-                    const uint32_t s = seq[byte];
+                    const uint32_t s = byte;
                     if (!((loc.set >> s) & 1u)) {
                         loc.set |= 1u << s;
                         loc.list |= (uint64_t)s << (4 * loc.cnt);
@@ -208,7 +200,7 @@ __global__ void __launch_bounds__(MT) k_mtf_nib(BlockDesc* __restrict__ blocks, 
             const uint32_t lim = e - j0;
             visit_line<true>(ll + j0, [&](int k, uint32_t byte) {
                 if ((uint32_t)k < lim) {
-                    const uint32_t x = nib_mtf(L, seq[byte]);
+                    const uint32_t x = nib_mtf(L, byte);
                     if (x == 0) {
                         ++z;
                     } else {
@@ -249,7 +241,7 @@ __global__ void __launch_bounds__(MT) k_mtf_nib(BlockDesc* __restrict__ blocks, 
             const uint32_t lim = e - j0;
             visit_line<true>(ll + j0, [&](int k, uint32_t byte) {
                 if ((uint32_t)k < lim) {
-                    const uint32_t x = nib_mtf(L, seq[byte]);
+                    const uint32_t x = nib_mtf(L, byte);
                     if (x == 0) {
                         ++z;
                     } else {
@@ -287,7 +279,6 @@ __global__ void __launch_bounds__(MT) k_mtf_big(BlockDesc* __restrict__ blocks, 
     constexpr uint32_t C = NCH_BIG;
     constexpr int NF = 4;
     __shared__ RunSum cs_sh[C];
-    __shared__ uint8_t seq[256];
     __shared__ uint32_t freq[NF][258];
     __shared__ uint32_t scan_sh[MT / 64 + 1];
     __shared__ uint32_t tail[2];
@@ -303,12 +294,6 @@ __global__ void __launch_bounds__(MT) k_mtf_big(BlockDesc* __restrict__ blocks, 
     const uint32_t n = blocks[b].n;
     const uint32_t nin = blocks[b].n_in_use;
     if (nin <= 16) return;
-    if (tid < 256) {
-        uint32_t c = tid, below = 0;
-        for (uint32_t j = 0; j < (c >> 5); ++j) below += __popc(blocks[b].in_use[j]);
-        below += __popc(blocks[b].in_use[c >> 5] & ((1u << (c & 31)) - 1u));
-        seq[c] = (uint8_t)below;
-    }
     for (int i = tid; i < NF * 258; i += MT) (&freq[0][0])[i] = 0;
     const uint8_t* ll = LL + (uint64_t)slot * ll_stride;
     uint8_t* idx = scratch + (uint64_t)slot * scratch_stride;            // MTF indices
@@ -326,7 +311,7 @@ __global__ void __launch_bounds__(MT) k_mtf_big(BlockDesc* __restrict__ blocks, 
         uint32_t cnt = 0;
         uint8_t* out = locl + (uint64_t)tid * 256;
         for (uint32_t j = e; j > a && a < e; --j) {
-            uint32_t s = seq[ll[j - 1]];
+            uint32_t s = ll[j - 1];
             uint32_t bit = 1u << (s & 31);
             if (!(seen[tid][s >> 5] & bit)) { seen[tid][s >> 5] |= bit; out[cnt++] = (uint8_t)s; }
             if (cnt == nin) break;
@@ -356,7 +341,7 @@ __global__ void __launch_bounds__(MT) k_mtf_big(BlockDesc* __restrict__ blocks, 
         for (uint32_t k = 0; k < nin; ++k) lst[k * NCH_BIG + tid] = sstate[(uint64_t)tid * 256 + k];
         uint32_t z = 0;
         for (uint32_t j = a; j < e; ++j) {
-            uint8_t s = seq[ll[j]];
+            uint8_t s = ll[j];
             uint8_t cur = lst[tid];
             uint32_t k = 0;
             if (cur != s) {   // bz:compress.c:197-211
@@ -430,7 +415,7 @@ __global__ void __launch_bounds__(MT) k_mtf_big(BlockDesc* __restrict__ blocks, 
     }
 }
 
-// Last column L[j] = block[(SA[j] - 1) mod n] (bz:compress.c:166-168) for the
+// Last column L[j] = unseqToSeq[block[(SA[j] - 1) mod n]] (bz:compress.c:166-168) for the
 // listed batch slots (which == nullptr: slots 0..nwhich-1).  The text gather is
 // random within the block, so all tiles of a block run on one XCD (workgroup L
 // -> slot L mod 8 inside groups of 8; round-robin XCD dealing) and small tiles
@@ -444,6 +429,7 @@ __global__ void __launch_bounds__(256) k_last_col(const BlockDesc* __restrict__ 
                                                    uint32_t ntile, const uint8_t* __restrict__ blkbytes,
                                                    uint64_t stride, BwtScratch scr)
 {
+    __shared__ uint8_t seq[256];
     const uint32_t L = blockIdx.x;
     const uint32_t grp = L / (8u * ntile), r = L % (8u * ntile);
     const uint32_t k = grp * 8u + (r & 7u), tile = r >> 3;
@@ -451,6 +437,13 @@ __global__ void __launch_bounds__(256) k_last_col(const BlockDesc* __restrict__ 
     const uint32_t slot = which ? which[k] : k;
     const uint32_t b = b0 + slot;
     const uint32_t n = blocks[b].n;
+    {                                                // makeMaps_e: unseqToSeq
+        const uint32_t c = threadIdx.x;
+        uint32_t below = __popc(blocks[b].in_use[c >> 5] & ((1u << (c & 31)) - 1u));
+        for (uint32_t j = 0; j < (c >> 5); ++j) below += __popc(blocks[b].in_use[j]);
+        seq[c] = (uint8_t)below;
+    }
+    __syncthreads();
     const uint8_t* blk = blkbytes + (uint64_t)b * stride;
     const uint64_t so = (uint64_t)slot * scr.stride;
     const uint32_t j = tile * LC_TILE + threadIdx.x * LC_PER;
@@ -462,12 +455,12 @@ __global__ void __launch_bounds__(256) k_last_col(const BlockDesc* __restrict__ 
                                 p2.x, p2.y, p2.z, p2.w, p3.x, p3.y, p3.z, p3.w};
         uint32_t w[4] = {0, 0, 0, 0};
 #pragma unroll
-        for (int t = 0; t < 16; ++t) w[t >> 2] |= (uint32_t)blk[p[t] ? p[t] - 1 : n - 1] << (8 * (t & 3));
+        for (int t = 0; t < 16; ++t) w[t >> 2] |= (uint32_t)seq[blk[p[t] ? p[t] - 1 : n - 1]] << (8 * (t & 3));
         *reinterpret_cast<uint4*>(scr.LL + so + j) = make_uint4(w[0], w[1], w[2], w[3]);
     } else {
         for (uint32_t t = j; t < n; ++t) {
             const uint32_t pp = scr.SA[so + t];
-            scr.LL[so + t] = blk[pp ? pp - 1 : n - 1];
+            scr.LL[so + t] = seq[blk[pp ? pp - 1 : n - 1]];
         }
     }
 }

@@ -502,74 +502,75 @@ __global__ void __launch_bounds__(256) k_rle_emit(const uint8_t* __restrict__ te
 
 // CRC-32/BZIP2 of [in_beg, in_end) per block (bz:bzlib_private.h:155-172).
 // R(A||B) = R(A)*x^(8|B|) + R(B) (mod P); crc = ~(0xffffffff*x^(8n) + R(all)).
-// k_crc_chunks: workgroup (c, block) takes chunk c (CRC_SUB-byte sub-chunks,
-// up to CRC_MAXC chunks per block); each lane a 16-byte strip by slice-by-4
-// table lookups, strips combined by a 256-lane tree.  k_crc_final: one wave per
-// block combines the chunk registers.
-constexpr uint32_t CRC_SUB = 4096;
+// k_crc_chunks: each wave takes one chunk of a block (up to CRC_MAXC chunks,
+// whole 8 KB spans); every lane runs slice-by-4 over its own 128-byte line of
+// a span (eight 16-B loads in flight), and the 64 line registers are folded by
+// a 6-level shuffle tree whose multipliers are the x^(8*128*2^l) constants.
+// k_crc_final: one wave per block combines the chunk registers.
+constexpr uint32_t CRC_LANE = 128;                // bytes per lane per span
+constexpr uint32_t CRC_SPAN = 64 * CRC_LANE;      // 8 KB per wave per span
 constexpr uint32_t CRC_MAXC = 128;
+constexpr int CRC_WPB = 4;                        // chunks (waves) per workgroup
 
 __device__ __forceinline__ uint64_t crc_chunk_bytes(uint64_t span)
 {
     uint64_t c = (span + CRC_MAXC - 1) / CRC_MAXC;
-    c = (c + CRC_SUB - 1) / CRC_SUB * CRC_SUB;
-    return c < CRC_SUB ? CRC_SUB : c;
+    c = (c + CRC_SPAN - 1) / CRC_SPAN * CRC_SPAN;
+    return c < CRC_SPAN ? CRC_SPAN : c;
 }
 
-__global__ void __launch_bounds__(256) k_crc_chunks(const uint8_t* __restrict__ text,
-                                                     const BlockDesc* __restrict__ blocks, uint32_t* __restrict__ creg)
+__global__ void __launch_bounds__(64 * CRC_WPB) k_crc_chunks(const uint8_t* __restrict__ text,
+                                                             const BlockDesc* __restrict__ blocks,
+                                                             uint32_t* __restrict__ creg)
 {
     __shared__ uint32_t t4[4][256];
-    __shared__ uint32_t rr[256];
-    __shared__ uint32_t ll[256];
-    const uint32_t c = blockIdx.x, b = blockIdx.y;
+    for (int i = threadIdx.x; i < 1024; i += 64 * CRC_WPB) (&t4[0][0])[i] = (&c_crc_tab4[0][0])[i];
+    __syncthreads();
+    const int lane = threadIdx.x & 63;
+    const uint32_t c = blockIdx.x * CRC_WPB + (threadIdx.x >> 6), b = blockIdx.y;
     const uint64_t beg = blocks[b].in_beg, end = blocks[b].in_end;
     const uint64_t csz = crc_chunk_bytes(end - beg);
     const uint64_t cb = beg + (uint64_t)c * csz;
-    if (cb >= end) return;
+    if (c >= CRC_MAXC || cb >= end) return;          // per wave; no barriers below
     const uint64_t ce = cb + csz < end ? cb + csz : end;
-    for (int i = threadIdx.x; i < 1024; i += 256) (&t4[0][0])[i] = (&c_crc_tab4[0][0])[i];
     uint32_t acc = 0;
-    for (uint64_t c0 = cb; c0 < ce; c0 += CRC_SUB) {
-        const uint64_t a = c0 + threadIdx.x * 16;
-        const uint32_t n = a < ce ? (uint32_t)(ce - a < 16 ? ce - a : 16) : 0u;
+    for (uint64_t c0 = cb; c0 < ce; c0 += CRC_SPAN) {
+        const uint64_t a = c0 + (uint64_t)lane * CRC_LANE;
+        const uint32_t n = a < ce ? (uint32_t)(ce - a < CRC_LANE ? ce - a : CRC_LANE) : 0u;
+        uint4 v[8];
+#pragma unroll
+        for (int k = 0; k < 8; ++k)
+            v[k] = (16u * k < n) ? load16u(text + a + 16 * k, text + ce) : make_uint4(0, 0, 0, 0);
         uint32_t r = 0;
-        __syncthreads();
-        if (n) {
-            const uint4 v = load16u(text + a, text + ce);
-            if (n == 16) {
-                const uint32_t ws[4] = {v.x, v.y, v.z, v.w};
+#pragma unroll
+        for (int k = 0; k < 8; ++k) {
+            const uint32_t m = n > 16u * k ? (n - 16u * k < 16u ? n - 16u * k : 16u) : 0u;
+            if (m == 16) {
+                const uint32_t ws[4] = {v[k].x, v[k].y, v[k].z, v[k].w};
 #pragma unroll
                 for (int q = 0; q < 4; ++q) {
                     const uint32_t x = r ^ __builtin_bswap32(ws[q]);   // bytes in stream order, MSB-first
                     r = t4[3][x >> 24] ^ t4[2][(x >> 16) & 255u] ^ t4[1][(x >> 8) & 255u] ^ t4[0][x & 255u];
                 }
             } else {
-                for (uint32_t k = 0; k < n; ++k) r = (r << 8) ^ t4[0][(r >> 24) ^ byte16(v, (int)k)];
+                for (uint32_t q = 0; q < m; ++q) r = (r << 8) ^ t4[0][(r >> 24) ^ byte16(v[k], (int)q)];
             }
         }
-        rr[threadIdx.x] = r;
-        ll[threadIdx.x] = n;
-        __syncthreads();
-        for (int step = 1; step < 256; step <<= 1) {
-            if ((threadIdx.x & (2 * step - 1)) == 0) {
-                const uint32_t j = threadIdx.x + step;
-                const uint32_t lb = ll[j];
-                if (lb) {
-                    const uint32_t m = (lb == (uint32_t)(16 * step)) ? c_pow8[4 + __builtin_ctz(step)] : xpow8(lb);
-                    rr[threadIdx.x] = mulmod(rr[threadIdx.x], m) ^ rr[j];
-                    ll[threadIdx.x] += lb;
-                }
+        uint32_t len = n;
+#pragma unroll
+        for (int l = 0; l < 6; ++l) {                // lane i absorbs lane i + 2^l
+            const int step = 1 << l;
+            const uint32_t ro = __shfl_down(r, step, 64);
+            const uint32_t lo = __shfl_down(len, step, 64);
+            if ((lane & (2 * step - 1)) == 0 && lo) {
+                const uint32_t mul = (lo == CRC_LANE * (uint32_t)step) ? c_pow8[7 + l] : xpow8(lo);
+                r = mulmod(r, mul) ^ ro;
+                len += lo;
             }
-            __syncthreads();
         }
-        if (threadIdx.x == 0) {
-            const uint32_t lc = ll[0];
-            const uint32_t m = (lc == CRC_SUB) ? c_pow8[12] : xpow8(lc);
-            acc = mulmod(acc, m) ^ rr[0];
-        }
+        if (lane == 0) acc = mulmod(acc, len == CRC_SPAN ? c_pow8[13] : xpow8(len)) ^ r;
     }
-    if (threadIdx.x == 0) creg[(uint64_t)b * CRC_MAXC + c] = acc;
+    if (lane == 0) creg[(uint64_t)b * CRC_MAXC + c] = acc;
 }
 
 __global__ void __launch_bounds__(64) k_crc_final(const uint32_t* __restrict__ creg, BlockDesc* __restrict__ blocks)
@@ -650,7 +651,7 @@ void rle_emit(const uint8_t* text, const TileDesc* tiles, uint64_t ntiles, const
 void rle_crc(const uint8_t* text, BlockDesc* blocks, uint32_t nb, uint32_t* creg, hipStream_t st)
 {
     if (!nb) return;
-    hipLaunchKernelGGL(k_crc_chunks, dim3(CRC_MAXC, nb), dim3(256), 0, st, text, blocks, creg);
+    hipLaunchKernelGGL(k_crc_chunks, dim3(CRC_MAXC / CRC_WPB, nb), dim3(64 * CRC_WPB), 0, st, text, blocks, creg);
     hipLaunchKernelGGL(k_crc_final, dim3(nb), dim3(64), 0, st, creg, blocks);
 }
 
