@@ -666,7 +666,8 @@ __global__ void __launch_bounds__(256) k3_sort_w(Ctx c, const uint64_t* __restri
         if (valid && ks.usek) ls = last_sym(c, slot, v);
         uint32_t r = 0;
         for (uint32_t j = 0; j < m; ++j) {
-            const uint64_t kj = __shfl(k, (int)j, 64);
+            const uint64_t kj = ((uint64_t)(uint32_t)__builtin_amdgcn_readlane((int)(k >> 32), (int)j) << 32) |
+                                (uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)k, (int)j);
             r += (kj < k || (kj == k && (int)j < lane)) ? 1u : 0u;
         }
         wave_sync_lds3();                                // previous group's reads are done
@@ -776,8 +777,7 @@ __global__ void __launch_bounds__(256) k3_sort_lds(Ctx c, const uint64_t* __rest
             }
         }
     }
-#pragma unroll
-    for (int d = 32; d >= 1; d >>= 1) diff |= __shfl_xor(diff, d, 64);
+    diff = wave_reduce_or64(diff);
     if constexpr (NW > 1) {
         if (lane == 0) red_all[wave] = diff;
         __syncthreads();
@@ -813,8 +813,7 @@ __global__ void __launch_bounds__(256) k3_sort_lds(Ctx c, const uint64_t* __rest
         }
         const uint32_t incl = wave_incl_scan_add(sum);
         uint32_t run = incl - sum;
-#pragma unroll
-        for (int d = 32; d >= 1; d >>= 1) { const uint32_t o = __shfl_xor(mx, d, 64); mx = o > mx ? o : mx; }
+        mx = wave_reduce_max(mx);
         if constexpr (NW > 1) {
             if (lane == 63) sc[wid] = incl;
             if (lane == 0) wmax_all[wave] = mx;
@@ -958,7 +957,7 @@ __global__ void __launch_bounds__(256) k3_sort_lds(Ctx c, const uint64_t* __rest
             uint32_t xx = wave_incl_scan_max<uint32_t>(head ? j : 0u);
             xx = xx > carry ? xx : carry;
             hp[e] = xx;
-            carry = __shfl(xx, 63, 64);
+            carry = (uint32_t)__builtin_amdgcn_readlane((int)xx, 63);
         }
         if constexpr (NW > 1) {
             if (lane == 0) wmax_all[wave] = carry;
@@ -1098,8 +1097,7 @@ __global__ void __launch_bounds__(256) k3_sort_grp(Ctx c, const uint64_t* __rest
             k[e] = ~0ull;                              // pads: max key, last in order
         }
     }
-#pragma unroll
-    for (int d = 32; d >= 1; d >>= 1) diff |= __shfl_xor(diff, d, 64);
+    diff = wave_reduce_or64(diff);
     if constexpr (NW > 1) {
         if (lane == 0) red_all[wave] = diff;
         __syncthreads();
@@ -1217,7 +1215,7 @@ __global__ void __launch_bounds__(256) k3_sort_grp(Ctx c, const uint64_t* __rest
             uint32_t xx = wave_incl_scan_max<uint32_t>(head ? j : 0u);
             xx = xx > carry ? xx : carry;
             hp[e] = xx;
-            carry = __shfl(xx, 63, 64);
+            carry = (uint32_t)__builtin_amdgcn_readlane((int)xx, 63);
         }
         if constexpr (NW > 1) {
             if (lane == 0) wmax_all[wave] = carry;

@@ -84,6 +84,82 @@ __device__ __forceinline__ T wave_reduce_add(T v)
 
 // Block-wide exclusive sum; `sh` must hold blockDim.x/64 + 1 elements.
 // Returns the exclusive prefix for this thread; *total gets the block sum.
+// 32-bit versions on DPP row shifts and row broadcasts (VALU, no LDS
+// round trip; gfx9 family): Hillis-Steele inside each 16-lane row, then
+// row_bcast:15 / row_bcast:31 carry row totals upward.  Every lane of the wave
+// must be active (same contract as the shuffle forms).
+__device__ __forceinline__ uint32_t dpp_up(uint32_t v, int ctrl_shr)   // 0 where the source is out of row
+{
+    switch (ctrl_shr) {
+    case 1: return (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x111, 0xf, 0xf, true);
+    case 2: return (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x112, 0xf, 0xf, true);
+    case 4: return (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x114, 0xf, 0xf, true);
+    default: return (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x118, 0xf, 0xf, true);
+    }
+}
+__device__ __forceinline__ uint32_t dpp_bc15(uint32_t v)
+{
+    return (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x142, 0xa, 0xf, false);
+}
+__device__ __forceinline__ uint32_t dpp_bc31(uint32_t v)
+{
+    return (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x143, 0xc, 0xf, false);
+}
+
+template <>
+__device__ __forceinline__ uint32_t wave_incl_scan_add<uint32_t>(uint32_t v)
+{
+    v += dpp_up(v, 1);
+    v += dpp_up(v, 2);
+    v += dpp_up(v, 4);
+    v += dpp_up(v, 8);
+    v += dpp_bc15(v);
+    v += dpp_bc31(v);
+    return v;
+}
+
+template <>
+__device__ __forceinline__ uint32_t wave_incl_scan_max<uint32_t>(uint32_t v)
+{
+    uint32_t t;
+    t = dpp_up(v, 1); v = t > v ? t : v;
+    t = dpp_up(v, 2); v = t > v ? t : v;
+    t = dpp_up(v, 4); v = t > v ? t : v;
+    t = dpp_up(v, 8); v = t > v ? t : v;
+    t = dpp_bc15(v); v = t > v ? t : v;
+    t = dpp_bc31(v); v = t > v ? t : v;
+    return v;
+}
+
+__device__ __forceinline__ uint32_t wave_incl_scan_or(uint32_t v)
+{
+    v |= dpp_up(v, 1);
+    v |= dpp_up(v, 2);
+    v |= dpp_up(v, 4);
+    v |= dpp_up(v, 8);
+    v |= dpp_bc15(v);
+    v |= dpp_bc31(v);
+    return v;
+}
+
+template <>
+__device__ __forceinline__ uint32_t wave_reduce_add<uint32_t>(uint32_t v)
+{
+    return (uint32_t)__builtin_amdgcn_readlane((int)wave_incl_scan_add<uint32_t>(v), 63);
+}
+
+__device__ __forceinline__ uint64_t wave_reduce_or64(uint64_t v)
+{
+    const uint32_t lo = wave_incl_scan_or((uint32_t)v), hi = wave_incl_scan_or((uint32_t)(v >> 32));
+    return ((uint64_t)(uint32_t)__builtin_amdgcn_readlane((int)hi, 63) << 32) |
+           (uint32_t)__builtin_amdgcn_readlane((int)lo, 63);
+}
+
+__device__ __forceinline__ uint32_t wave_reduce_max(uint32_t v)
+{
+    return (uint32_t)__builtin_amdgcn_readlane((int)wave_incl_scan_max<uint32_t>(v), 63);
+}
+
 template <class T>
 __device__ __forceinline__ T block_excl_scan_add(T v, T* sh, T* total)
 {
