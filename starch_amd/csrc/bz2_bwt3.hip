@@ -51,9 +51,11 @@
 #include "bz2_int.hpp"
 #include "bz2_bwt.hpp"
 
+#include <stdio.h>
 #include <string.h>
 
 #include <algorithm>
+#include <type_traits>
 #include <vector>
 
 namespace bz {
@@ -66,12 +68,13 @@ constexpr int PNB = 1 << PDIG;          // 4096 top-level buckets per block
 constexpr int MAXT = (900064 + PTILE - 1) / PTILE;   // tiles per block (bs <= 9)
 // size classes: W rank-by-compare (one wave), S wave-private LDS sort,
 // M1..M3 workgroup LDS sort, L MSD partition
-constexpr uint32_t W_MAX = 64, S_MAX = 256, M1_MAX = 1024, M2_MAX = 2048, M3_MAX = 4096;
+constexpr uint32_t W_MAX = 64, S1_MAX = 128, S_MAX = 256, M1_MAX = 1024, M2_MAX = 2048, M3_MAX = 4096;
 constexpr uint32_t RBITS = 20;          // rank bits (n <= 899,985 < 2^20)
 constexpr uint32_t TEXT_ROUNDS = 4;     // max text-extension rounds before doubling
 
 // counters (u32) in the meta buffer
-enum { C_W = 0, C_S, C_M1, C_M2, C_M3, C_L0, C_L1, C_T0, C_T1, C_TIE_ELEMS, C_ERR, C_TS0, C_TS1, C_H, C_N = 16 };
+enum { C_W = 0, C_S, C_S2, C_M1, C_M2, C_M3, C_L0, C_L1, C_T0, C_T1, C_TIE_ELEMS, C_ERR, C_TS0, C_TS1, C_H, C_DBG2,
+       C_DBGL, C_N = 24 };
 
 // item = slot[63:52] | start[51:32] | size[31:12] | parity[7] | shift[6:0]
 __device__ __forceinline__ uint64_t mk_item(uint32_t slot, uint32_t s, uint32_t m, uint32_t shift, uint32_t par)
@@ -96,7 +99,8 @@ __host__ __device__ constexpr uint64_t pss_words(uint64_t stride) { return strid
 struct Lists {
     uint32_t* ctr;          // C_N counters
     uint64_t* w;            // m <= 64
-    uint64_t* s;            // m <= 256
+    uint64_t* s;            // m <= 128
+    uint64_t* s2;           // m <= 256
     uint64_t* m1;           // m <= 1024
     uint64_t* m2;           // m <= 2048
     uint64_t* m3;           // m <= 4096
@@ -162,7 +166,8 @@ __device__ __forceinline__ void wave_classify(const Ctx& c, bool pred, uint32_t 
 {
     const uint64_t it = mk_item(slot, s, m, shift, par);
     wave_push(c.L.ctr + C_W, c.L.w, pred && m <= W_MAX, it);
-    wave_push(c.L.ctr + C_S, c.L.s, pred && m > W_MAX && m <= S_MAX, it);
+    wave_push(c.L.ctr + C_S, c.L.s, pred && m > W_MAX && m <= S1_MAX, it);
+    wave_push(c.L.ctr + C_S2, c.L.s2, pred && m > S1_MAX && m <= S_MAX, it);
     wave_push(c.L.ctr + C_M1, c.L.m1, pred && m > S_MAX && m <= M1_MAX, it);
     wave_push(c.L.ctr + C_M2, c.L.m2, pred && m > M1_MAX && m <= M2_MAX, it);
     wave_push(c.L.ctr + C_M3, c.L.m3, pred && m > M2_MAX && m <= M3_MAX, it);
@@ -191,22 +196,27 @@ struct KeySrc {
         if (rr >= n) rr -= n;
         return pss_bits(pss, (uint64_t)rr * B, kbits);
     }
-    // the key and the last-column symbol of rotation r (the symbol before it,
-    // mostly in the key's first word).  Doubling keys (usek): ls is left for
-    // last_sym() to fill from the block text.
-    __device__ __forceinline__ uint64_t key_ls(uint64_t q, uint32_t r, uint32_t& ls) const
+    // PSS key of rotation r, branch-free (two word loads, a funnel shift)
+    __device__ __forceinline__ uint64_t key_pss(uint32_t r) const
     {
-        if (usek) { ls = 0; return k[q]; }
         uint32_t rr = r + off;
-        if (rr >= n) rr -= n;
+        rr = rr >= n ? rr - n : rr;
         const uint64_t bit = (uint64_t)rr * B;
-        const uint64_t wq = bit >> 6;
+        const uint64_t q = bit >> 6;
         const uint32_t p = (uint32_t)(bit & 63u);
-        const uint64_t a = pss[wq];
-        const uint64_t v = p ? ((a << p) | (pss[wq + 1] >> (64u - p))) : a;
-        if (off == 0 && r != 0 && p >= B) ls = (uint32_t)((a << (p - B)) >> (64u - B));
-        else ls = (uint32_t)pss_bits(pss, (uint64_t)(r ? r - 1u : n - 1u) * B, B);
+        const uint64_t v = (pss[q] << p) | ((pss[q + 1] >> 1) >> (63u - p));
         return v >> (64u - kbits);
+    }
+    // ... and the last-column symbol of r (the symbol before it), also branch-free
+    __device__ __forceinline__ uint64_t key_pss(uint32_t r, uint32_t& ls) const
+    {
+        const uint32_t pr = r ? r - 1u : n - 1u;
+        const uint64_t pbit = (uint64_t)pr * B;
+        const uint64_t pq = pbit >> 6;
+        const uint32_t pp = (uint32_t)(pbit & 63u);
+        const uint64_t pv = (pss[pq] << pp) | ((pss[pq + 1] >> 1) >> (63u - pp));
+        ls = (uint32_t)(pv >> (64u - B));
+        return key_pss(r);
     }
 };
 
@@ -248,6 +258,26 @@ __device__ __forceinline__ uint8_t last_sym(const Ctx& c, uint32_t slot, uint32_
     uint32_t r = __popc(c.blocks[b].in_use[byte >> 5] & ((1u << (byte & 31u)) - 1u));
     for (uint32_t j = 0; j < (byte >> 5); ++j) r += __popc(c.blocks[b].in_use[j]);
     return (uint8_t)r;
+}
+
+// key of the group element at position q holding rotation v: doubling keys
+// (DBL) or the PSS; ls = its last-column symbol
+template <bool DBL>
+__device__ __forceinline__ uint64_t elem_key(const Ctx& c, const KeySrc& ks, uint32_t slot, uint64_t q, uint32_t v,
+                                             uint32_t& ls)
+{
+    if constexpr (DBL) {
+        ls = last_sym(c, slot, v);
+        return ks.k[q];
+    } else {
+        return ks.key_pss(v, ls);
+    }
+}
+template <bool DBL>
+__device__ __forceinline__ uint64_t elem_key(const KeySrc& ks, uint64_t q, uint32_t v)
+{
+    if constexpr (DBL) return ks.k[q];
+    else return ks.key_pss(v);
 }
 
 // symbol map of a block (rank among used byte values), >= 256 threads
@@ -523,6 +553,7 @@ __global__ void __launch_bounds__(256) k3_bin_scatter(const uint64_t* __restrict
 constexpr int LT = 512;
 constexpr int LW = LT / 64;
 
+template <bool DBL>
 __global__ void __launch_bounds__(LT) k3_part_l(Ctx c, const uint64_t* __restrict__ items)
 {
     __shared__ uint32_t wh[LW][256];
@@ -556,7 +587,7 @@ __global__ void __launch_bounds__(LT) k3_part_l(Ctx c, const uint64_t* __restric
         if (tid == 0) big[256] = 0;
         __syncthreads();
         for (uint32_t i = tid; i < m; i += LT)
-            atomicAdd(&wh[wid][(uint32_t)((ks(s + i, sv[i]) >> sh2) & dmask)], 1u);
+            atomicAdd(&wh[wid][(uint32_t)((elem_key<DBL>(ks, s + i, sv[i]) >> sh2) & dmask)], 1u);
         __syncthreads();
         uint32_t tcount = 0;
         if (tid < 256) for (int w = 0; w < LW; ++w) tcount += wh[w][tid];
@@ -565,10 +596,10 @@ __global__ void __launch_bounds__(LT) k3_part_l(Ctx c, const uint64_t* __restric
         __syncthreads();
         for (uint32_t i = tid; i < m; i += LT) {
             const uint32_t v = sv[i];
-            const uint64_t k = ks(s + i, v);
+            const uint64_t k = elem_key<DBL>(ks, s + i, v);
             const uint32_t p = atomicAdd(&cur[(uint32_t)((k >> sh2) & dmask)], 1u);
             dv[p] = v;
-            if (c.keysrc) dk[p] = k;
+            if constexpr (DBL) dk[p] = k;
         }
         __syncthreads();
         uint32_t nruns = 0;
@@ -644,6 +675,7 @@ __device__ __forceinline__ void emit_sorted(const Ctx& c, uint32_t slot, uint32_
 // ---------------------------------------------------------------------------
 // k3_sort_w: groups of <= 64, one wave each (persistent, per wave)
 // ---------------------------------------------------------------------------
+template <bool DBL>
 __global__ void __launch_bounds__(256) k3_sort_w(Ctx c, const uint64_t* __restrict__ items)
 {
     __shared__ uint64_t skey[4][W_MAX + 1];
@@ -660,10 +692,11 @@ __global__ void __launch_bounds__(256) k3_sort_w(Ctx c, const uint64_t* __restri
         const uint32_t* sv = (par ? c.scr.V : c.scr.SA) + base;
         const KeySrc ks = key_src(c, slot, par);
         const bool valid = (uint32_t)lane < m;
-        const uint32_t v = valid ? sv[lane] : 0u;
-        uint32_t ls = 0;
-        const uint64_t k = valid ? ks.key_ls(s + lane, v, ls) : ~0ull;
-        if (valid && ks.usek) ls = last_sym(c, slot, v);
+        const uint32_t li = valid ? (uint32_t)lane : 0u;         // loads stay unconditional
+        const uint32_t v = sv[li];
+        uint32_t ls;
+        uint64_t k = elem_key<DBL>(c, ks, slot, s + li, v, ls);
+        if (!valid) k = ~0ull;
         uint32_t r = 0;
         for (uint32_t j = 0; j < m; ++j) {
             const uint64_t kj = ((uint64_t)(uint32_t)__builtin_amdgcn_readlane((int)(k >> 32), (int)j) << 32) |
@@ -698,6 +731,19 @@ __global__ void __launch_bounds__(256) k3_sort_w(Ctx c, const uint64_t* __restri
 // (8 ballots find a lane's digit peers; one lane per peer set adds the set's
 // size to the wave's counter with a returning LDS atomic).
 // ---------------------------------------------------------------------------
+// rank of key km (at position j) among positions [rs, re) of xk: keys below
+// it, and equal keys at earlier positions
+template <uint64_t KMASK>
+__device__ __forceinline__ uint32_t rank_in(const uint64_t* xk, uint32_t rs, uint32_t re, uint64_t km, uint32_t j)
+{
+    uint32_t r = 0;
+    for (uint32_t q = rs; q < re; ++q) {
+        const uint64_t a = xk[q] & KMASK;
+        r += (a < km || (a == km && q < j)) ? 1u : 0u;
+    }
+    return r;
+}
+
 template <int NW>
 __device__ __forceinline__ void gsync()
 {
@@ -705,8 +751,13 @@ __device__ __forceinline__ void gsync()
     else __syncthreads();
 }
 
-template <int NW, int E>
-__global__ void __launch_bounds__(256) k3_sort_lds(Ctx c, const uint64_t* __restrict__ items,
+// register budget (waves per SIMD) of the sort kernels: keeps a few groups
+// resident per CU while their loads are in flight
+constexpr int sort_wpe(int NW, int E) { return NW == 4 && E == 8 ? 3 : 1; }
+
+template <int NW, int E, bool DBL>
+__global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(sort_wpe(NW, E))))
+k3_sort_lds(Ctx c, const uint64_t* __restrict__ items,
                                                     const uint32_t* __restrict__ hard_n)
 {
     constexpr int IPW = 4 / NW;                    // groups per workgroup
@@ -716,7 +767,7 @@ __global__ void __launch_bounds__(256) k3_sort_lds(Ctx c, const uint64_t* __rest
     constexpr uint64_t KMASK = (1ull << KEYB) - 1ull;
     constexpr int DPT = 256 / (64 * NW);           // digits per thread in the offset scan
     static_assert(CAP <= (1 << IDXB), "index does not fit");
-    constexpr int DB = CAP <= 256 ? 8 : (CAP <= 1024 ? 10 : 11);   // MSD digit bits
+    constexpr int DB = CAP <= 128 ? 7 : (CAP <= 256 ? 8 : (CAP <= 1024 ? 10 : 11));   // MSD digit bits
     constexpr int NBIN = 1 << DB;
     constexpr int T = NW * 64;
     constexpr int BPT = NBIN / T;                  // bins per thread
@@ -727,6 +778,10 @@ __global__ void __launch_bounds__(256) k3_sort_lds(Ctx c, const uint64_t* __rest
     __shared__ uint32_t bcur_all[IPW][NBIN];      // scatter cursors
     __shared__ uint32_t cnt_all[4][256];
     __shared__ uint32_t sc_all[IPW][NW + 1];
+    constexpr int NB2 = NW == 1 ? 256 : 1024;      // second-digit bins
+    constexpr uint32_t LIMIT2 = 512 / E;           // largest second-level sub-bucket ranked by comparison
+    __shared__ uint32_t c2_all[IPW][NB2 + 1];
+    __shared__ uint32_t sc2_all[IPW][NW + 1];
     __shared__ uint64_t red_all[4];
     __shared__ uint32_t wmax_all[4];
     __shared__ uint32_t flag_all[4];
@@ -755,23 +810,27 @@ __global__ void __launch_bounds__(256) k3_sort_lds(Ctx c, const uint64_t* __rest
     uint64_t k[E];
     uint64_t diff = 0;
     {
-        uint32_t vv[E];
+        // every load unconditional (pads read element 0): all in flight at once
+        uint32_t vv[E], ls[E];
+        uint64_t kx[E];
 #pragma unroll
         for (int e = 0; e < E; ++e) {
             const uint32_t i = (uint32_t)(wid * 64 * E + e * 64 + lane);
-            vv[e] = i < m ? sv[i] : 0u;
+            vv[e] = sv[i < m ? i : 0u];
         }
-        const uint64_t k0 = ks(s, sv[0]);
+        const uint64_t k0 = elem_key<DBL>(ks, s, sv[0]);
+#pragma unroll
+        for (int e = 0; e < E; ++e) {
+            const uint32_t i = (uint32_t)(wid * 64 * E + e * 64 + lane);
+            kx[e] = elem_key<DBL>(c, ks, slot, s + (i < m ? i : 0u), vv[e], ls[e]);
+        }
 #pragma unroll
         for (int e = 0; e < E; ++e) {
             const uint32_t i = (uint32_t)(wid * 64 * E + e * 64 + lane);
             if (i < m) {
-                uint32_t ls;
-                const uint64_t kx = ks.key_ls(s + i, vv[e], ls);
-                if (ks.usek) ls = last_sym(c, slot, vv[e]);
-                diff |= kx ^ k0;
-                k[e] = (kx & KMASK) | ((uint64_t)i << KEYB);
-                vb_all[g][i] = vv[e] | (ls << 24);
+                diff |= kx[e] ^ k0;
+                k[e] = (kx[e] & KMASK) | ((uint64_t)i << KEYB);
+                vb_all[g][i] = vv[e] | (ls[e] << 24);
             } else {
                 k[e] = ~0ull;                          // pads: max key, last in stable order
             }
@@ -822,32 +881,25 @@ __global__ void __launch_bounds__(256) k3_sort_lds(Ctx c, const uint64_t* __rest
             mx = 0;
             for (int w = 0; w < NW; ++w) mx = wmax_all[w0 + w] > mx ? wmax_all[w0 + w] : mx;
         }
-        if (mx <= LIMIT) {                         // uniform per group
-#pragma unroll
-            for (int q = 0; q < BPT; ++q) { bst[tg * BPT + q] = run; bcur[tg * BPT + q] = run; run += loc[q]; }
-            if (tg == T - 1) bst[NBIN] = run;
-            gsync<NW>();
+        // rank every element inside its final sub-bucket [rs, re) by comparison
+        // (p = its scatter position: the tie-break), then move keys into place
+        // rank in digit order: position j holds kj, whose final sub-bucket
+        // [rs, re) range_of() recomputes from the key (lanes of a row mostly
+        // share a sub-bucket: equal trip counts, broadcast LDS reads); then
+        // move keys into place
+        auto rank_place = [&](auto&& range_of) {
             uint32_t p[E];
 #pragma unroll
             for (int e = 0; e < E; ++e) {
-                p[e] = 0;
-                if ((uint32_t)(wid * 64 * E + e * 64 + lane) < m) { p[e] = atomicAdd(&bcur[dg[e]], 1u); xk[p[e]] = k[e]; }
-            }
-            gsync<NW>();
-#pragma unroll
-            for (int e = 0; e < E; ++e) {
-                const uint32_t i = (uint32_t)(wid * 64 * E + e * 64 + lane);
-                if (i < m) {
-                    const uint32_t bs = bst[dg[e]], be = bst[dg[e] + 1];
-                    const uint64_t km = k[e] & KMASK;
-                    uint32_t r = 0;
-                    for (uint32_t q = bs; q < be; ++q) {
-                        const uint64_t kq = xk[q] & KMASK;
-                        r += (kq < km || (kq == km && q < p[e])) ? 1u : 0u;
-                    }
-                    p[e] = bs + r;
-                } else {
-                    p[e] = i;                      // pads keep the tail
+                const uint32_t j = (uint32_t)(wid * 64 * E + e * 64 + lane);
+                p[e] = j;                          // pads keep the tail
+                if (j < m) {
+                    const uint64_t kj = xk[j];
+                    const uint64_t km = kj & KMASK;
+                    uint32_t rs, re;
+                    range_of(km, rs, re);
+                    p[e] = rs + rank_in<KMASK>(xk, rs, re, km, j);
+                    k[e] = kj;
                 }
             }
             gsync<NW>();
@@ -856,11 +908,136 @@ __global__ void __launch_bounds__(256) k3_sort_lds(Ctx c, const uint64_t* __rest
             gsync<NW>();
 #pragma unroll
             for (int e = 0; e < E; ++e) k[e] = xk[wid * 64 * E + e * 64 + lane];
+        };
+        if (mx <= LIMIT) {                         // uniform per group
+#pragma unroll
+            for (int q = 0; q < BPT; ++q) { bst[tg * BPT + q] = run; bcur[tg * BPT + q] = run; run += loc[q]; }
+            if (tg == T - 1) bst[NBIN] = run;
+            gsync<NW>();
+#pragma unroll
+            for (int e = 0; e < E; ++e)
+                if ((uint32_t)(wid * 64 * E + e * 64 + lane) < m) xk[atomicAdd(&bcur[dg[e]], 1u)] = k[e];
+            gsync<NW>();
+            rank_place([&](uint64_t km, uint32_t& rs, uint32_t& re) {
+                const uint32_t d = (uint32_t)((km >> lo) & (uint64_t)(NBIN - 1));
+                rs = bst[d];
+                re = bst[d + 1];
+            });
             moved = true;
+        } else if (lo > 0) {
+            // Second MSD digit for the sub-buckets larger than LIMIT: the w2 bits
+            // right below the first digit, counted per (big sub-bucket, digit)
+            // bin; bins are numbered in key order, so one exclusive scan places
+            // them all.  Sub-buckets <= LIMIT keep their first-digit place.
+            uint32_t* c2 = c2_all[g];
+            uint32_t* sc2 = sc2_all[g];
+            uint32_t nbl = 0;
+#pragma unroll
+            for (int q = 0; q < BPT; ++q) nbl += loc[q] > LIMIT ? 1u : 0u;
+            const uint32_t binc = wave_incl_scan_add(nbl);
+            uint32_t bb = binc - nbl, nbig = 0;
+            if constexpr (NW > 1) {
+                if (lane == 63) sc2[wid] = binc;
+                __syncthreads();
+                for (int w = 0; w < NW; ++w) { if (w < wid) bb += sc2[w]; nbig += sc2[w]; }
+            } else {
+                nbig = (uint32_t)__builtin_amdgcn_readlane((int)binc, 63);
+            }
+            uint32_t w2 = 0;
+            while (w2 < 6 && (nbig << (w2 + 1)) <= (uint32_t)NB2) ++w2;
+            if (w2 > (uint32_t)lo) w2 = (uint32_t)lo;
+            const int lo2 = lo - (int)w2;
+            const uint32_t nb2 = nbig << w2;
+#pragma unroll
+            for (int q = 0; q < BPT; ++q) {
+                bst[tg * BPT + q] = run;
+                bcur[tg * BPT + q] = loc[q] > LIMIT ? (0x80000000u | ((bb++) << w2)) : run;
+                run += loc[q];
+            }
+            if (tg == T - 1) bst[NBIN] = run;
+            for (uint32_t q = (uint32_t)tg; q < nb2; q += T) c2[q] = 0;
+            gsync<NW>();
+            uint32_t b2[E];
+#pragma unroll
+            for (int e = 0; e < E; ++e) {
+                b2[e] = ~0u;
+                if ((uint32_t)(wid * 64 * E + e * 64 + lane) < m) {
+                    const uint32_t x = bcur[dg[e]];
+                    if (x >> 31) {
+                        b2[e] = (x & 0x7FFFFFFFu) + (uint32_t)(((k[e] & KMASK) >> lo2) & ((1ull << w2) - 1ull));
+                        atomicAdd(&c2[b2[e]], 1u);
+                    }
+                }
+            }
+            gsync<NW>();
+            constexpr int BPT2 = (NB2 + T - 1) / T;
+            uint32_t l2[BPT2], s2 = 0, m2 = 0;
+#pragma unroll
+            for (int q = 0; q < BPT2; ++q) {
+                const uint32_t ix = (uint32_t)(tg * BPT2 + q);
+                l2[q] = ix < nb2 ? c2[ix] : 0u;
+                s2 += l2[q];
+                m2 = l2[q] > m2 ? l2[q] : m2;
+            }
+            const uint32_t inc2 = wave_incl_scan_add(s2);
+            uint32_t r2 = inc2 - s2;
+            m2 = wave_reduce_max(m2);
+            if constexpr (NW > 1) {
+                __syncthreads();                   // sc2 reads (nbig) done
+                if (lane == 63) sc2[wid] = inc2;
+                if (lane == 0) wmax_all[wave] = m2;
+                __syncthreads();
+                for (int w = 0; w < wid; ++w) r2 += sc2[w];
+                for (int w = 0; w < NW; ++w) m2 = wmax_all[w0 + w] > m2 ? wmax_all[w0 + w] : m2;
+            }
+#pragma unroll
+            for (int q = 0; q < BPT2; ++q) {
+                const uint32_t ix = (uint32_t)(tg * BPT2 + q);
+                if (ix < nb2) c2[ix] = r2;
+                r2 += l2[q];
+            }
+            gsync<NW>();
+            if (m2 <= LIMIT2) {                    // uniform per group
+                // c2 = bin starts among the big sub-buckets' elements; an
+                // element's place: its sub-bucket's start + (bin cursor - the
+                // start of the sub-bucket's first bin)
+                uint32_t sb[E];
+#pragma unroll
+                for (int e = 0; e < E; ++e) sb[e] = b2[e] != ~0u ? c2[bcur[dg[e]] & 0x7FFFFFFFu] : 0u;
+                gsync<NW>();
+#pragma unroll
+                for (int e = 0; e < E; ++e) {
+                    if ((uint32_t)(wid * 64 * E + e * 64 + lane) < m) {
+                        const uint32_t p = b2[e] != ~0u ? bst[dg[e]] + atomicAdd(&c2[b2[e]], 1u) - sb[e]
+                                                        : atomicAdd(&bcur[dg[e]], 1u);
+                        xk[p] = k[e];
+                    }
+                }
+                gsync<NW>();
+                // after the scatter c2[b] = end of bin b = start of bin b + 1;
+                // big sub-buckets still carry their tag in bcur
+                rank_place([&](uint64_t km, uint32_t& rs, uint32_t& re) {
+                    const uint32_t d = (uint32_t)((km >> lo) & (uint64_t)(NBIN - 1));
+                    const uint32_t x = bcur[d];
+                    if (x >> 31) {
+                        const uint32_t base = x & 0x7FFFFFFFu;
+                        const uint32_t b = base + (uint32_t)((km >> lo2) & ((1ull << w2) - 1ull));
+                        const uint32_t s0 = base ? c2[base - 1] : 0u;
+                        rs = bst[d] + (b ? c2[b - 1] : 0u) - s0;
+                        re = bst[d] + c2[b] - s0;
+                    } else {
+                        rs = bst[d];
+                        re = bst[d + 1];
+                    }
+                });
+                moved = true;
+                if (tg == 0) atomicAdd(&c.L.ctr[C_DBG2], 1u);
+            }
         } else {
             gsync<NW>();                           // bcur/sc reads done before the LSD passes
         }
     }
+    if (!moved && kdiff && tid % (64 * NW) == 0) atomicAdd(&c.L.ctr[C_DBGL], 1u);
     bool lsd_moved = false;
     for (int dbit = 0; dbit < KEYB && !moved; dbit += 8) {
         if ((kdiff >> dbit & 0xffull) == 0) continue;    // uniform per group
@@ -1008,37 +1185,38 @@ struct GrpIn {                 // one group's inputs, as loaded
     uint64_t k0;
 };
 
+// loads of a group that does not exist (ok false) go to element 0 of slot 0's
+// SA, which always exists; their results are never used
 template <int NW, int E>
 __device__ __forceinline__ void grp_load_vals(const Ctx& c, GrpIn<E>& x, bool ok, int wid, int lane)
 {
-    const uint32_t slot = it_slot(x.item), s = it_start(x.item), m = ok ? it_size(x.item) : 0u,
-                   par = it_par(x.item);
+    if (!ok) x.item = mk_item(0, 0, 1, 0, 0);
+    const uint32_t slot = it_slot(x.item), s = it_start(x.item), m = it_size(x.item), par = it_par(x.item);
     const uint32_t* sv = (par ? c.scr.V : c.scr.SA) + (uint64_t)slot * c.scr.stride + s;
-    if (ok) x.ks = key_src(c, slot, par);
+    x.ks = key_src(c, slot, par);
 #pragma unroll
     for (int e = 0; e < E; ++e) {
         const uint32_t i = (uint32_t)(wid * 64 * E + e * 64 + lane);
-        x.v[e] = i < m ? sv[i] : 0u;
+        x.v[e] = sv[i < m ? i : 0u];
     }
-    x.v0 = m ? sv[0] : 0u;
+    x.v0 = sv[0];
 }
 
-template <int NW, int E>
-__device__ __forceinline__ void grp_load_keys(const Ctx& c, GrpIn<E>& x, bool ok, int wid, int lane)
+template <int NW, int E, bool DBL>
+__device__ __forceinline__ void grp_load_keys(const Ctx& c, GrpIn<E>& x, int wid, int lane)
 {
-    const uint32_t s = it_start(x.item), m = ok ? it_size(x.item) : 0u;
+    const uint32_t s = it_start(x.item), m = it_size(x.item), slot = it_slot(x.item);
 #pragma unroll
     for (int e = 0; e < E; ++e) {
         const uint32_t i = (uint32_t)(wid * 64 * E + e * 64 + lane);
-        x.ls[e] = 0;
-        x.kx[e] = i < m ? x.ks.key_ls(s + i, x.v[e], x.ls[e]) : 0ull;
-        if (i < m && x.ks.usek) x.ls[e] = last_sym(c, it_slot(x.item), x.v[e]);
+        x.kx[e] = elem_key<DBL>(c, x.ks, slot, s + (i < m ? i : 0u), x.v[e], x.ls[e]);
     }
-    x.k0 = m ? x.ks(s, x.v0) : 0ull;
+    x.k0 = elem_key<DBL>(x.ks, s, x.v0);
 }
 
-template <int NW, int E>
-__global__ void __launch_bounds__(256) k3_sort_grp(Ctx c, const uint64_t* __restrict__ items,
+template <int NW, int E, bool DBL>
+__global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(sort_wpe(NW, E))))
+k3_sort_grp(Ctx c, const uint64_t* __restrict__ items,
                                                     uint64_t* __restrict__ hard)
 {
     constexpr int IPW = 4 / NW;                    // groups per workgroup
@@ -1047,7 +1225,7 @@ __global__ void __launch_bounds__(256) k3_sort_grp(Ctx c, const uint64_t* __rest
     constexpr int KEYB = 64 - IDXB;
     constexpr uint64_t KMASK = (1ull << KEYB) - 1ull;
     static_assert(CAP <= (1 << IDXB), "index does not fit");
-    constexpr int DB = CAP <= 256 ? 8 : (CAP <= 1024 ? 10 : 11);   // MSD digit bits
+    constexpr int DB = CAP <= 128 ? 7 : (CAP <= 256 ? 8 : (CAP <= 1024 ? 10 : 11));   // MSD digit bits
     constexpr int NBIN = 1 << DB;
     constexpr int T = NW * 64;
     constexpr int BPT = NBIN / T;                  // bins per thread
@@ -1076,7 +1254,7 @@ __global__ void __launch_bounds__(256) k3_sort_grp(Ctx c, const uint64_t* __rest
     cur.item = it < e_end ? items[it] : 0ull;
     nxt.item = it + nwk < e_end ? items[it + nwk] : 0ull;
     grp_load_vals<NW, E>(c, cur, it < e_end, wid, lane);
-    grp_load_keys<NW, E>(c, cur, it < e_end, wid, lane);
+    grp_load_keys<NW, E, DBL>(c, cur, wid, lane);
     grp_load_vals<NW, E>(c, nxt, it + nwk < e_end, wid, lane);
     uint64_t nitem2 = it + 2 * nwk < e_end ? items[it + 2 * nwk] : 0ull;
     for (; it < e_end; it += nwk) {
@@ -1161,12 +1339,7 @@ __global__ void __launch_bounds__(256) k3_sort_grp(Ctx c, const uint64_t* __rest
                     const uint64_t km = kj & KMASK;
                     const uint32_t d = (uint32_t)((km >> lo) & (uint64_t)(NBIN - 1));
                     const uint32_t bs = bst[d], be = bst[d + 1];
-                    uint32_t r = 0;
-                    for (uint32_t q = bs; q < be; ++q) {
-                        const uint64_t kq = xk[q] & KMASK;
-                        r += (kq < km || (kq == km && q < j)) ? 1u : 0u;
-                    }
-                    pos[e] = bs + r;
+                    pos[e] = bs + rank_in<KMASK>(xk, bs, be, km, j);
                     k[e] = kj;
                 }
             }
@@ -1182,7 +1355,7 @@ __global__ void __launch_bounds__(256) k3_sort_grp(Ctx c, const uint64_t* __rest
         for (int e = 0; e < E; ++e) xk[wid * 64 * E + e * 64 + lane] = k[e];
     }
     // next group's keys (its rotations were loaded one group ago), the item after it
-    grp_load_keys<NW, E>(c, nxt, it + nwk < e_end, wid, lane);
+    grp_load_keys<NW, E, DBL>(c, nxt, wid, lane);
     const uint64_t nitem3 = it + 3 * nwk < e_end ? items[it + 3 * nwk] : 0ull;
     if (!is_hard) {
     gsync<NW>();
@@ -1376,12 +1549,13 @@ void launch_bwt3(BlockDesc* blocks, uint32_t b0, uint32_t nb, const uint8_t* blk
     if (pss_words(scr.stride) * 2 + (uint64_t)(MAXT + 1) * PNB > 2 * scr.stride)
         throw StarchError(-2, "bwt3: block stride too small");
     const uint64_t N = (uint64_t)nb * scr.stride;
-    const uint64_t cap_s = N / (W_MAX + 1) + 64, cap_m1 = N / (S_MAX + 1) + 64, cap_m2 = N / (M1_MAX + 1) + 64,
+    const uint64_t cap_s = N / (W_MAX + 1) + 64, cap_s2 = N / (S1_MAX + 1) + 64, cap_m1 = N / (S_MAX + 1) + 64,
+                   cap_m2 = N / (M1_MAX + 1) + 64,
                    cap_m3 = N / (M2_MAX + 1) + 64, cap_l = N / (M3_MAX + 1) + 64;
     const uint64_t nwg_bin = BIN_MAXWG;
     constexpr uint32_t QSETS = 64, QSET = 32;                   // queue heads + segments per launch
     const uint64_t words = 2 * C_N + 10ull * nb + QSETS * QSET + nwg_bin * nb +
-                           2 * (cap_s + cap_m1 + cap_m2 + cap_m3 + 2 * cap_l) + 64;
+                           2 * (cap_s + cap_s2 + cap_m1 + cap_m2 + cap_m3 + 2 * cap_l) + 64;
     uint32_t* mw = meta.as<uint32_t>(words);
     Ctx c;
     c.blocks = blocks;
@@ -1402,7 +1576,8 @@ void launch_bwt3(BlockDesc* blocks, uint32_t b0, uint32_t nb, const uint8_t* blk
     uintptr_t p = reinterpret_cast<uintptr_t>(binh + nwg_bin * nb);
     p = (p + 7) & ~(uintptr_t)7;
     c.L.s = reinterpret_cast<uint64_t*>(p);
-    c.L.m1 = c.L.s + cap_s;
+    c.L.s2 = c.L.s + cap_s;
+    c.L.m1 = c.L.s2 + cap_s2;
     c.L.m2 = c.L.m1 + cap_m1;
     c.L.m3 = c.L.m2 + cap_m2;
     c.L.l[0] = c.L.m3 + cap_m3;
@@ -1471,13 +1646,19 @@ void launch_bwt3(BlockDesc* blocks, uint32_t b0, uint32_t nb, const uint8_t* blk
             bin(c.L.l[lsel], nl, bout);
             c.lsel = lsel ^ 1u;
             HIP_CHECK(hipMemsetAsync(c.L.ctr + C_L0 + (lsel ^ 1u), 0, sizeof(uint32_t), st));
-            hipLaunchKernelGGL(k3_part_l, dim3(ncu * 2), dim3(LT), 0, st, c, bout);
+            if (c.keysrc) hipLaunchKernelGGL(k3_part_l<true>, dim3(ncu * 2), dim3(LT), 0, st, c, bout);
+            else hipLaunchKernelGGL(k3_part_l<false>, dim3(ncu * 2), dim3(LT), 0, st, c, bout);
             HIP_CHECK(hipGetLastError());
             HIP_CHECK(hipMemsetAsync(c.L.ctr + C_L0 + lsel, 0, sizeof(uint32_t), st));
             lsel ^= 1u;
         }
         c.lsel = 0;
-        const uint32_t nw = hctr[C_W], ns = hctr[C_S], n1 = hctr[C_M1], n2 = hctr[C_M2], n3 = hctr[C_M3];
+        const uint32_t nw = hctr[C_W], ns = hctr[C_S], ns2 = hctr[C_S2], n1 = hctr[C_M1], n2 = hctr[C_M2],
+                       n3 = hctr[C_M3];
+        static const bool dbg = getenv("STARCH_BWT_DEBUG") != nullptr;
+        if (dbg)
+            fprintf(stderr, "[bwt3] rtext %u mode %u: W %u S %u S2 %u M1 %u M2 %u M3 %u | level-2 %u lsd %u (so far)\n",
+                    c.rtext, c.mode, nw, ns, ns2, n1, n2, n3, hctr[C_DBG2], hctr[C_DBGL]);
         // every launch reads its own binned copy; stream order lets them share one buffer
         // grids: a multiple of 8 (static per-XCD segments), about one resident wave of workgroups
         auto g8 = [](uint32_t x) { return dim3((x + 7) / 8 * 8); };
@@ -1488,36 +1669,52 @@ void launch_bwt3(BlockDesc* blocks, uint32_t b0, uint32_t nb, const uint8_t* blk
             HIP_CHECK(hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, f, 256, 0));
             return g8((uint32_t)ncu * (uint32_t)(per_cu > 0 ? per_cu : 1));
         };
-        static const dim3 gm3 = resident(reinterpret_cast<const void*>(&k3_sort_lds<4, 16>));
-        static const dim3 gm2 = resident(reinterpret_cast<const void*>(&k3_sort_lds<4, 8>));
-        static const dim3 gm1 = resident(reinterpret_cast<const void*>(&k3_sort_lds<4, 4>));
-        static const dim3 gs = resident(reinterpret_cast<const void*>(&k3_sort_grp<1, 4>));
-        static const dim3 gw = resident(reinterpret_cast<const void*>(&k3_sort_w));
-        // M classes: k3_sort_lds (MSD digit + compare, LSD fallback); S: k3_sort_grp,
-        // then the groups it listed as hard (k3_sort_lds) from the class list it consumed
+        // M classes: k3_sort_lds (MSD digit(s) + compare, LSD fallback); S: k3_sort_grp,
+        // then the groups it listed as hard (k3_sort_lds) from the class list it consumed.
+        // Doubling rounds (keys in K/K2) run their own instantiations.
         const uint32_t* hard_n = c.L.ctr + C_H;
         auto clear_h = [&]() { HIP_CHECK(hipMemsetAsync(c.L.ctr + C_H, 0, sizeof(uint32_t), st)); };
-        if (n3) {
-            bin(c.L.m3, n3, bout);
-            hipLaunchKernelGGL((k3_sort_lds<4, 16>), gm3, dim3(256), 0, st, c, bout, nullptr);
-        }
-        if (n2) {
-            bin(c.L.m2, n2, bout);
-            hipLaunchKernelGGL((k3_sort_lds<4, 8>), gm2, dim3(256), 0, st, c, bout, nullptr);
-        }
-        if (n1) {
-            bin(c.L.m1, n1, bout);
-            hipLaunchKernelGGL((k3_sort_lds<4, 4>), gm1, dim3(256), 0, st, c, bout, nullptr);
-        }
-        if (ns) {
-            bin(c.L.s, ns, bout);
-            clear_h();
-            hipLaunchKernelGGL((k3_sort_grp<1, 4>), gs, dim3(256), 0, st, c, bout, c.L.s);
-            hipLaunchKernelGGL((k3_sort_lds<1, 4>), dim3(ncu / 2), dim3(256), 0, st, c, c.L.s, hard_n);
-        }
-        if (nw) { bin(c.L.w, nw, bout); hipLaunchKernelGGL(k3_sort_w, gw, dim3(256), 0, st, c, bout); }
+        auto leaf = [&](auto dbl) {
+            constexpr bool D = decltype(dbl)::value;
+            static const dim3 gm3 = resident(reinterpret_cast<const void*>(&k3_sort_lds<4, 16, D>));
+            static const dim3 gm2 = resident(reinterpret_cast<const void*>(&k3_sort_lds<4, 8, D>));
+            static const dim3 gm1 = resident(reinterpret_cast<const void*>(&k3_sort_lds<4, 4, D>));
+            static const dim3 gs = resident(reinterpret_cast<const void*>(&k3_sort_grp<1, 2, D>));
+            static const dim3 gs2 = resident(reinterpret_cast<const void*>(&k3_sort_grp<1, 4, D>));
+            static const dim3 gw = resident(reinterpret_cast<const void*>(&k3_sort_w<D>));
+            if (n3) {
+                bin(c.L.m3, n3, bout);
+                hipLaunchKernelGGL((k3_sort_lds<4, 16, D>), gm3, dim3(256), 0, st, c, bout, nullptr);
+            }
+            if (n2) {
+                bin(c.L.m2, n2, bout);
+                hipLaunchKernelGGL((k3_sort_lds<4, 8, D>), gm2, dim3(256), 0, st, c, bout, nullptr);
+            }
+            if (n1) {
+                bin(c.L.m1, n1, bout);
+                hipLaunchKernelGGL((k3_sort_lds<4, 4, D>), gm1, dim3(256), 0, st, c, bout, nullptr);
+            }
+            if (ns) {
+                bin(c.L.s, ns, bout);
+                clear_h();
+                hipLaunchKernelGGL((k3_sort_grp<1, 2, D>), gs, dim3(256), 0, st, c, bout, c.L.s);
+                hipLaunchKernelGGL((k3_sort_lds<1, 2, D>), dim3(ncu / 2), dim3(256), 0, st, c, c.L.s, hard_n);
+            }
+            if (ns2) {
+                bin(c.L.s2, ns2, bout);
+                clear_h();
+                hipLaunchKernelGGL((k3_sort_grp<1, 4, D>), gs2, dim3(256), 0, st, c, bout, c.L.s2);
+                hipLaunchKernelGGL((k3_sort_lds<1, 4, D>), dim3(ncu / 2), dim3(256), 0, st, c, c.L.s2, hard_n);
+            }
+            if (nw) {
+                bin(c.L.w, nw, bout);
+                hipLaunchKernelGGL(k3_sort_w<D>, gw, dim3(256), 0, st, c, bout);
+            }
+        };
+        if (c.keysrc) leaf(std::true_type{});
+        else leaf(std::false_type{});
         HIP_CHECK(hipGetLastError());
-        HIP_CHECK(hipMemsetAsync(c.L.ctr + C_W, 0, 5 * sizeof(uint32_t), st));
+        HIP_CHECK(hipMemsetAsync(c.L.ctr + C_W, 0, 6 * sizeof(uint32_t), st));
     };
 
     // ---- round 0: packed prefix keys ----

@@ -203,3 +203,60 @@ if __name__ == "__main__" and os.environ.get("RANK_MODEL"):
     for k in range(D):
         key = (key << np.uint64(B)) | ext[k:k + len(blk)]
     rank_cost_model(key, D * B)
+
+
+def two_level_model(key, KB, lim=32, db2s=(4, 5, 6, 8)):
+    """M groups: sum z^2 / m after the first MSD digit, and after a second digit
+    of db2 bits (the bits right below the first) on sub-buckets larger than lim."""
+    order = np.argsort(key, kind="stable")
+    sk = key[order]
+    tops = (sk >> np.uint64(KB - 12)).astype(np.int64)
+    leaves = []
+    for g in np.split(sk, np.flatnonzero(np.diff(tops)) + 1):
+        if len(g) > 4096:
+            d = ((g >> np.uint64(KB - 20)) & np.uint64(255)).astype(np.int64)
+            leaves += [h for h in np.split(g, np.flatnonzero(np.diff(d)) + 1) if len(h) > 256]
+        elif len(g) > 256:
+            leaves.append(g)
+    for DB2 in db2s:
+        r1, r2, mx2 = [], [], []
+        for g in leaves:
+            m = len(g)
+            DB = 10 if m <= 1024 else (11 if m <= 2048 else 11)
+            km = g & np.uint64((1 << 52) - 1)
+            diff = int(np.bitwise_or.reduce(km ^ km[0]))
+            if diff == 0:
+                continue
+            hb = diff.bit_length() - 1
+            lo = max(hb + 1 - DB, 0)
+            d1 = ((km >> np.uint64(lo)) & np.uint64((1 << DB) - 1)).astype(np.int64)
+            z1 = np.bincount(d1)
+            r1.append((z1.astype(np.int64) ** 2).sum() / m)
+            lo2 = max(lo - DB2, 0)
+            d2 = ((km >> np.uint64(lo2)) & np.uint64((1 << (lo - lo2)) - 1)).astype(np.int64) if lo > 0 else np.zeros(m, np.int64)
+            big = z1[d1] > lim
+            comp = np.where(big, (d1 << 16) | d2, d1 << 16)
+            _, z2 = np.unique(comp, return_counts=True)
+            r2.append((z2.astype(np.int64) ** 2).sum() / m)
+            mx2.append(z2.max())
+        print("DB2 %d: groups %d  ratio1 median %.1f mean %.1f | ratio2 median %.1f mean %.1f p95 %.1f | max z2 p50 %d p95 %d" %
+              (DB2, len(r1), np.median(r1), np.mean(r1), np.median(r2), np.mean(r2), np.percentile(r2, 95),
+               np.median(mx2), np.percentile(mx2, 95)))
+
+
+if __name__ == "__main__" and os.environ.get("TWO_LEVEL"):
+    kind = int(sys.argv[1]) if len(sys.argv) > 1 else 0
+    bed = starch_amd.gen_bed(kind, int(os.environ.get("TOTAL", "100000000")), chroms=[0])
+    _, segs = oracle_lib.transform(bytes(bed))
+    blk = np.frombuffer(segs[0][2][:899981], dtype=np.uint8)
+    used = np.unique(blk)
+    B = int(np.ceil(np.log2(len(used))))
+    D = 64 // B
+    mp = np.zeros(256, np.uint64)
+    mp[used] = np.arange(len(used))
+    sym = mp[blk]
+    ext = np.concatenate([sym, sym[:64]])
+    key = np.zeros(len(blk), np.uint64)
+    for k in range(D):
+        key = (key << np.uint64(B)) | ext[k:k + len(blk)]
+    two_level_model(key, D * B)
