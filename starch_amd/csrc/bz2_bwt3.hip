@@ -160,18 +160,38 @@ __device__ __forceinline__ void wave_push(uint32_t* ctr, uint64_t* list, bool pr
     if (pred) list[base + __popcll(m & lanemask_lt())] = item;
 }
 
-// push a group [s, s+m) of slot with key bits [0, shift) still unsorted to its size class
-__device__ __forceinline__ void wave_classify(const Ctx& c, bool pred, uint32_t slot, uint32_t s, uint32_t m,
-                                              uint32_t shift, uint32_t par)
+// push a group [s, s+m) of slot with key bits [0, shift) still unsorted to its
+// size class list (W, S, S2, M1, M2, M3, L).
+// Pushes reserve their slots with LDS atomics and
+// the workgroup takes ONE global atomic per class (the class counters are
+// shared by every workgroup of the launch; per-wave global atomics on them
+// serialise).  Every thread of the workgroup must call it; sh: 16 u32 of LDS.
+__device__ __forceinline__ int size_class(uint32_t m)
 {
-    const uint64_t it = mk_item(slot, s, m, shift, par);
-    wave_push(c.L.ctr + C_W, c.L.w, pred && m <= W_MAX, it);
-    wave_push(c.L.ctr + C_S, c.L.s, pred && m > W_MAX && m <= S1_MAX, it);
-    wave_push(c.L.ctr + C_S2, c.L.s2, pred && m > S1_MAX && m <= S_MAX, it);
-    wave_push(c.L.ctr + C_M1, c.L.m1, pred && m > S_MAX && m <= M1_MAX, it);
-    wave_push(c.L.ctr + C_M2, c.L.m2, pred && m > M1_MAX && m <= M2_MAX, it);
-    wave_push(c.L.ctr + C_M3, c.L.m3, pred && m > M2_MAX && m <= M3_MAX, it);
-    wave_push(c.L.ctr + C_L0 + c.lsel, c.L.l[c.lsel], pred && m > M3_MAX, it);
+    return m <= W_MAX ? 0 : m <= S1_MAX ? 1 : m <= S_MAX ? 2 : m <= M1_MAX ? 3 : m <= M2_MAX ? 4 : m <= M3_MAX ? 5 : 6;
+}
+__device__ __forceinline__ void wg_classify(const Ctx& c, uint32_t* sh, bool pred, uint32_t slot, uint32_t s,
+                                            uint32_t m, uint32_t shift, uint32_t par)
+{
+    const int cls = pred ? size_class(m) : -1;
+    if (threadIdx.x < 8) sh[threadIdx.x] = 0;
+    __syncthreads();
+    uint32_t loff = 0;
+    if (cls >= 0) loff = atomicAdd(&sh[cls], 1u);
+    __syncthreads();
+    if (threadIdx.x < 7 && sh[threadIdx.x]) {
+        const uint32_t k = threadIdx.x;
+        uint32_t* ctr = c.L.ctr + (k == 0 ? C_W : k == 1 ? C_S : k == 2 ? C_S2 : k == 3 ? C_M1 : k == 4 ? C_M2
+                                   : k == 5 ? C_M3 : C_L0 + c.lsel);
+        sh[8 + k] = atomicAdd(ctr, sh[k]);
+    }
+    __syncthreads();
+    if (cls >= 0) {
+        uint64_t* list = cls == 0 ? c.L.w : cls == 1 ? c.L.s : cls == 2 ? c.L.s2 : cls == 3 ? c.L.m1
+                       : cls == 4 ? c.L.m2 : cls == 5 ? c.L.m3 : c.L.l[c.lsel];
+        list[sh[8 + cls] + loff] = mk_item(slot, s, m, shift, par);
+    }
+    __syncthreads();
 }
 
 // bits [bit, bit+nbits) of a packed symbol stream, right-aligned (1 <= nbits <= 64)
@@ -376,8 +396,18 @@ __global__ void __launch_bounds__(PT) k3_hist(Ctx c)
     for (int i = threadIdx.x; i < PNB; i += PT) cnt[i] = 0;
     __syncthreads();
     const uint32_t e = n - t0 < (uint32_t)PTILE ? n - t0 : (uint32_t)PTILE;
-    for (uint32_t k = threadIdx.x; k < e; k += PT)
-        atomicAdd(&cnt[(uint32_t)pss_bits(pss, (uint64_t)(t0 + k) * B, PDIG)], 1u);
+    constexpr int HU = 8;                      // digits of HU rotations in flight per thread
+    for (uint32_t k0 = 0; k0 < e; k0 += HU * PT) {
+        uint32_t d[HU];
+#pragma unroll
+        for (int u = 0; u < HU; ++u) {
+            const uint32_t k = k0 + u * PT + threadIdx.x;
+            d[u] = k < e ? (uint32_t)pss_bits(pss, (uint64_t)(t0 + k) * B, PDIG) : 0xFFFFFFFFu;
+        }
+#pragma unroll
+        for (int u = 0; u < HU; ++u)
+            if (d[u] != 0xFFFFFFFFu) atomicAdd(&cnt[d[u]], 1u);
+    }
     __syncthreads();
     uint32_t* th = tile_hist(c, slot) + (uint64_t)tile * PNB;
     for (int i = threadIdx.x; i < PNB; i += PT) th[i] = cnt[i];
@@ -391,6 +421,7 @@ constexpr int ST = 1024;              // k3_scan threads: 4 buckets each
 __global__ void __launch_bounds__(ST) k3_scan(Ctx c)
 {
     __shared__ uint32_t scan_sh[ST / 64 + 1];
+    __shared__ uint32_t cls_sh[16];
     const int tid = threadIdx.x;
     const uint32_t slot = blockIdx.x, b = c.b0 + slot;
     const uint32_t n = c.blocks[b].n;
@@ -398,6 +429,7 @@ __global__ void __launch_bounds__(ST) k3_scan(Ctx c)
     uint4* th = reinterpret_cast<uint4*>(tile_hist(c, slot));   // [tile][PNB/4]
     uint4* tot = th + (uint64_t)MAXT * (PNB / 4);
     uint4 a = make_uint4(0, 0, 0, 0);
+#pragma unroll 4
     for (uint32_t k = 0; k < ntile; ++k) {
         const uint4 x = th[(uint64_t)k * (PNB / 4) + tid];
         a.x += x.x; a.y += x.y; a.z += x.z; a.w += x.w;
@@ -406,6 +438,7 @@ __global__ void __launch_bounds__(ST) k3_scan(Ctx c)
     const uint32_t sum = a.x + a.y + a.z + a.w;
     const uint32_t pre = block_excl_scan_add<uint32_t>(sum, scan_sh, (uint32_t*)nullptr);
     uint4 run = make_uint4(pre, pre + a.x, pre + a.x + a.y, pre + a.x + a.y + a.z);
+#pragma unroll 4
     for (uint32_t k = 0; k < ntile; ++k) {
         uint4& x = th[(uint64_t)k * (PNB / 4) + tid];
         const uint4 v = x;
@@ -417,7 +450,7 @@ __global__ void __launch_bounds__(ST) k3_scan(Ctx c)
     uint32_t st = pre;
 #pragma unroll
     for (int q = 0; q < 4; ++q) {
-        wave_classify(c, cnt4[q] >= 2, slot, st, cnt4[q], shift, 0);
+        wg_classify(c, cls_sh, cnt4[q] >= 2, slot, st, cnt4[q], shift, 0);
         st += cnt4[q];
     }
 }
@@ -454,14 +487,32 @@ __global__ void __launch_bounds__(SCT) k3_scatter(Ctx c)
         const uint64_t* pss = c.scr.K + so;
         uint32_t* SA = c.scr.SA + so;
         const uint32_t e = n - t0 < (uint32_t)PTILE ? n - t0 : (uint32_t)PTILE;
-        for (uint32_t q = tid; q < e; q += SCT) {
-            const uint32_t r = t0 + q;
-            const uint32_t d = (uint32_t)pss_bits(pss, (uint64_t)r * B, PDIG);
-            const uint32_t p = atomicAdd(&cur[d], 1u);
-            SA[p] = r;
-            if (tot[d] == 1u) {                      // singleton bucket: final
-                c.scr.LL[so + p] = (uint8_t)pss_bits(pss, (uint64_t)(r ? r - 1u : n - 1u) * B, B);
-                if (r == 0) c.blocks[b].orig_ptr = p;
+        // SU rotations per thread per step: digits (PSS loads), then the LDS
+        // cursor atomics, then the stores, so each phase has SU in flight
+        constexpr int SU = 8;
+        for (uint32_t q0 = 0; q0 < e; q0 += SU * SCT) {
+            uint32_t d[SU], p[SU];
+#pragma unroll
+            for (int u = 0; u < SU; ++u) {
+                const uint32_t q = q0 + u * SCT + tid;
+                d[u] = q < e ? (uint32_t)pss_bits(pss, (uint64_t)(t0 + q) * B, PDIG) : 0u;
+            }
+#pragma unroll
+            for (int u = 0; u < SU; ++u) {
+                const uint32_t q = q0 + u * SCT + tid;
+                p[u] = q < e ? atomicAdd(&cur[d[u]], 1u) : 0u;
+            }
+#pragma unroll
+            for (int u = 0; u < SU; ++u) {
+                const uint32_t q = q0 + u * SCT + tid;
+                if (q < e) {
+                    const uint32_t r = t0 + q;
+                    SA[p[u]] = r;
+                    if (tot[d[u]] == 1u) {           // singleton bucket: final
+                        c.scr.LL[so + p[u]] = (uint8_t)pss_bits(pss, (uint64_t)(r ? r - 1u : n - 1u) * B, B);
+                        if (r == 0) c.blocks[b].orig_ptr = p[u];
+                    }
+                }
             }
         }
         __syncthreads();
@@ -562,6 +613,7 @@ __global__ void __launch_bounds__(LT) k3_part_l(Ctx c, const uint64_t* __restric
     __shared__ uint32_t big[257];
     __shared__ uint32_t qs[8];
     __shared__ uint32_t job_sh;
+    __shared__ uint32_t cls_sh[16];
     const int tid = threadIdx.x, wid = tid >> 6;
     const uint32_t x = xcc_id();
     load_qsizes_binned(c, qs);
@@ -617,10 +669,10 @@ __global__ void __launch_bounds__(LT) k3_part_l(Ctx c, const uint64_t* __restric
                 nruns = 1;
             }
         }
-        if (tid < 256) {
-            const uint32_t cc = cntd[tid];
-            const bool push = cc >= 2 && !(cc > M3_MAX && sh2 == 0);
-            wave_classify(c, push, slot, s + st[tid], cc, sh2, par ^ 1u);
+        {
+            const uint32_t cc = tid < 256 ? cntd[tid] : 0u;
+            const bool push = tid < 256 && cc >= 2 && !(cc > M3_MAX && sh2 == 0);
+            wg_classify(c, cls_sh, push, slot, s + (tid < 256 ? st[tid] : 0u), cc, sh2, par ^ 1u);
         }
         if (tid < 256) {
             const uint32_t r = wave_reduce_add(nruns);
@@ -1430,7 +1482,8 @@ __global__ void __launch_bounds__(256) k3_classify_text(Ctx c, const uint64_t* _
     const uint64_t item = active ? items[i] : 0;
     const uint32_t slot = it_slot(item), s = it_start(item), m = it_size(item);
     const Geo g = c.L.geo[active ? slot : 0];
-    wave_classify(c, active, slot, s, m, g.Dp * g.B, 0);
+    __shared__ uint32_t cls_sh[16];
+    wg_classify(c, cls_sh, active, slot, s, m, g.Dp * g.B, 0);
     const uint32_t tied = wave_reduce_add<uint32_t>(active ? m : 0u);
     if (lane == 0 && tied) atomicAdd(&c.L.ctr[C_TIE_ELEMS], tied);
 }
@@ -1480,7 +1533,8 @@ __global__ void __launch_bounds__(256) k3_gather(Ctx c, const uint64_t* __restri
             c.scr.K2[lso + q] = c.scr.RK[lso + t];
         }
     }
-    wave_classify(c, active, slot, s, m, RBITS, 0);
+    __shared__ uint32_t cls_sh[16];
+    wg_classify(c, cls_sh, active, slot, s, m, RBITS, 0);
     if (active) atomicAdd(&c.L.gin[slot], 1u);
     const uint32_t tied = wave_reduce_add<uint32_t>(active ? m : 0u);
     if (lane == 0 && tied) atomicAdd(&c.L.ctr[C_TIE_ELEMS], tied);
@@ -1728,8 +1782,9 @@ void launch_bwt3(BlockDesc* blocks, uint32_t b0, uint32_t nb, const uint8_t* blk
         next_q(head, seg);
         c.qhead = head;
         c.qseg = nullptr;
-        // about one block in flight per XCD: MAXT workgroups of 1024 threads each
-        hipLaunchKernelGGL(k3_scatter, dim3(8 * MAXT), dim3(SCT), 0, st, c);
+        // about one block in flight per XCD: one 1024-thread workgroup per CU,
+        // a block's MAXT tiles spread over its XCD's CUs
+        hipLaunchKernelGGL(k3_scatter, dim3((ncu + 7) / 8 * 8), dim3(SCT), 0, st, c);
         HIP_CHECK(hipGetLastError());
     }
     sort_groups();
