@@ -522,8 +522,8 @@ __global__ void __launch_bounds__(SCT) k3_scatter(Ctx c)
 // ---------------------------------------------------------------------------
 // binning of a work list by block into per-XCD segments (blocks x, x+8, ...)
 // ---------------------------------------------------------------------------
-constexpr uint32_t BIN_CH = 8192;     // items per binning workgroup (at least)
-constexpr uint32_t BIN_MAXWG = 1024;
+constexpr uint32_t BIN_CH = 32768;    // items per binning workgroup (at least)
+constexpr uint32_t BIN_MAXWG = 512;
 
 __global__ void __launch_bounds__(256) k3_bin_hist(const uint64_t* __restrict__ in, uint32_t n, uint32_t nb,
                                                     uint32_t ch, uint32_t* __restrict__ hist)

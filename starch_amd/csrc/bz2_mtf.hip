@@ -135,128 +135,214 @@ __device__ __forceinline__ void put_run(Out16& out, uint32_t z)   // bijective b
     }
 }
 
-__global__ void __launch_bounds__(MT) k_mtf_nib(BlockDesc* __restrict__ blocks, uint32_t b0,
-                                                 const uint8_t* __restrict__ LL, uint64_t ll_stride,
-                                                 uint16_t* __restrict__ mtfv_all, uint64_t mtf_stride)
+// ---- alphabets <= 16: five launches over (block, 512-symbol chunk) ----
+// Per-chunk state lives in the (free) key scratch of the block's batch slot:
+//   [0, 2C)   NibState local recency list          (k_mtf_local)
+//   [2C, 3C)  start list of the chunk              (k_mtf_scan_lists)
+//   [3C, 5C)  RunSum of the chunk's MTF indices    (k_mtf_runs)
+//   [5C, 6C)  (zeros carried in, output offset)    (k_mtf_scan_runs)
+// (u64 words, C = chunks per slot).  The three chunk passes are flat grids,
+// so every CU has work whatever the block count; the two scans are one
+// workgroup per block over <= 2 chunks per thread.
+constexpr uint32_t MCS = 512;                 // symbols per chunk (4 lines)
+constexpr int MCT = 256;                      // threads of the chunk kernels
+constexpr int MST = 1024;                     // threads of the scan kernels
+
+struct MtfScr {
+    uint64_t* base;
+    uint32_t C;
+    __device__ NibState* nst() const { return reinterpret_cast<NibState*>(base); }
+    __device__ uint64_t* l0() const { return base + 2ull * C; }
+    __device__ RunSum* rs() const { return reinterpret_cast<RunSum*>(base + 3ull * C); }
+    __device__ uint2* zo() const { return reinterpret_cast<uint2*>(base + 5ull * C); }
+};
+
+__device__ __forceinline__ MtfScr mtf_scr(uint64_t* K, uint64_t kstride, uint32_t slot, uint32_t C)
 {
-    __shared__ NibState nst[MT];
-    __shared__ RunSum wsum[MT / 64];
-    __shared__ RunSum total_sh;
+    MtfScr m;
+    m.base = K + (uint64_t)slot * kstride;
+    m.C = C;
+    return m;
+}
 
-    const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
-    const uint32_t slot = blockIdx.x;
-    const uint32_t b = b0 + slot;
-    const uint32_t n = blocks[b].n;
-    const uint32_t nin = blocks[b].n_in_use;
-    if (nin > 16) return;                       // uniform per workgroup: k_mtf_big
+// visit symbols [a, e) of a chunk in order: 16-byte pieces, the next piece's
+// load issued before the current one is processed (one load in flight, few
+// registers: the per-symbol chains stay short-lived); the final partial
+// piece is bounds-tested
+template <class F>
+__device__ __forceinline__ void visit_chunk(const uint8_t* ll, uint32_t a, uint32_t e, F&& f)
+{
+    const uint4* q = reinterpret_cast<const uint4*>(ll + a);
+    const uint32_t np = (e - a + 15) / 16;
+    uint4 cur = q[0];
+#pragma unroll 1
+    for (uint32_t i = 0; i < np; ++i) {
+        const uint4 nxt = q[i + 1 < np ? i + 1 : i];
+        const uint32_t lim = e - a - 16 * i;
+        if (lim >= 16) {
+            auto all = [&](int, uint32_t s) { f(s); };
+            piece<true>(cur, 0, all);
+        } else {
+            auto some = [&](int k, uint32_t s) { if ((uint32_t)k < lim) f(s); };
+            piece<true>(cur, 0, some);
+        }
+        cur = nxt;
+    }
+}
+
+// the same, whole 128-byte lines at a time (eight loads in flight): faster
+// for the emit pass, whose branchy per-symbol code keeps few values live
+template <class F>
+__device__ __forceinline__ void visit_chunk_lines(const uint8_t* ll, uint32_t a, uint32_t e, F&& f)
+{
+    const uint32_t full = a + ((e - a) & ~(LINE - 1));
+#pragma unroll 1
+    for (uint32_t j0 = a; j0 < full; j0 += LINE) visit_line<true>(ll + j0, [&](int, uint32_t s) { f(s); });
+    if (full < e) {
+        const uint32_t lim = e - full;
+        visit_line<true>(ll + full, [&](int k, uint32_t s) { if ((uint32_t)k < lim) f(s); });
+    }
+}
+
+__global__ void __launch_bounds__(MCT) k_mtf_local(const BlockDesc* __restrict__ blocks, uint32_t b0,
+                                                   const uint8_t* __restrict__ LL, uint64_t ll_stride,
+                                                   uint64_t* __restrict__ K, uint64_t kstride, uint32_t C)
+{
+    const uint32_t slot = blockIdx.y, b = b0 + slot;
+    const uint32_t n = blocks[b].n, nin = blocks[b].n_in_use;
+    const uint32_t ch = blockIdx.x * MCT + threadIdx.x;
+    const uint32_t a = ch * MCS;
+    if (nin > 16 || a >= n) return;
+    const uint32_t e = a + MCS < n ? a + MCS : n;
     const uint8_t* ll = LL + (uint64_t)slot * ll_stride;
-    uint16_t* mtfv = mtfv_all + (uint64_t)b * mtf_stride;
-    const uint32_t csz = ((n + MT - 1) / MT + LINE - 1) & ~(LINE - 1);
-    const uint32_t a = tid * csz;
-    const uint32_t e = a + csz < n ? a + csz : n;
-    const bool mine = a < e;
-
-    // ---- pass 1: local recency list, backward, stop once every symbol is seen ----
+    // local(c): the chunk's symbols by last occurrence, most recent first;
+    // backward, line by line, until every symbol of the block has been seen
     NibState loc;
     loc.list = 0; loc.set = 0; loc.cnt = 0;
-    if (mine) {
-        for (uint32_t j0 = a + ((e - 1 - a) & ~(LINE - 1));; j0 -= LINE) {
-            const uint32_t lim = e - j0;
-            visit_line<false>(ll + j0, [&](int k, uint32_t byte) {
-                if ((uint32_t)k < lim) {
-                    const uint32_t s = byte;
-                    if (!((loc.set >> s) & 1u)) {
-                        loc.set |= 1u << s;
-                        loc.list |= (uint64_t)s << (4 * loc.cnt);
-                        ++loc.cnt;
-                    }
-                }
-            });
-            if (loc.cnt == nin || j0 == a) break;
-        }
+    const uint32_t full = a + ((e - a) & ~(LINE - 1));
+    auto add = [&](uint32_t s) {
+        if (!((loc.set >> s) & 1u)) { loc.set |= 1u << s; loc.list |= (uint64_t)s << (4 * loc.cnt); ++loc.cnt; }
+    };
+    if (full < e) {
+        const uint32_t lim = e - full;
+        visit_line<false>(ll + full, [&](int k, uint32_t s) { if ((uint32_t)k < lim) add(s); });
     }
-    nst[tid] = loc;
-    __syncthreads();
-    for (int d = 1; d < MT; d <<= 1) {          // inclusive scan of the composition
-        NibState v = (tid >= d) ? nib_compose(nst[tid - d], nst[tid]) : nst[tid];
-        __syncthreads();
-        nst[tid] = v;
-        __syncthreads();
+#pragma unroll 1
+    for (uint32_t j0 = full; j0 > a && loc.cnt < nin;) {
+        j0 -= LINE;
+        visit_line<false>(ll + j0, [&](int, uint32_t s) { add(s); });
     }
-    NibState ident;
-    ident.list = 0;
-    for (uint32_t i = 0; i < nin; ++i) ident.list |= (uint64_t)i << (4 * i);
-    ident.set = (1u << nin) - 1u;
-    ident.cnt = nin;
-    const uint64_t L0 = (tid ? nib_compose(ident, nst[tid - 1]) : ident).list;
+    mtf_scr(K, kstride, slot, C).nst()[ch] = loc;
+}
 
-    // ---- pass 2: zero-run summary of the chunk's MTF indices ----
-    RunSum rs;
-    rs.nz = 0; rs.lz = 0; rs.tz = 0; rs.inner = 0;
-    if (mine) {
-        uint64_t L = L0;
-        uint32_t z = 0;
-        for (uint32_t j0 = a; j0 < e; j0 += LINE) {
-            const uint32_t lim = e - j0;
-            visit_line<true>(ll + j0, [&](int k, uint32_t byte) {
-                if ((uint32_t)k < lim) {
-                    const uint32_t x = nib_mtf(L, byte);
-                    if (x == 0) {
-                        ++z;
-                    } else {
-                        if (!rs.nz) { rs.lz = z; rs.nz = 1; } else { rs.inner += 1 + nsym_run(z); }
-                        z = 0;
-                    }
-                }
-            });
-        }
-        if (!rs.nz) rs.lz = z; else rs.tz = z;
-    }
-    // ---- exclusive scan of the summaries ----
-    RunSum inc = rs;
-#pragma unroll
-    for (int d = 1; d < 64; d <<= 1) {
-        const RunSum o = shfl_up_rs(inc, d);
-        if (lane >= d) inc = run_compose(o, inc);
-    }
-    if (lane == 63) wsum[wid] = inc;
+// start list of every chunk: exclusive scan of the local-list composition
+__global__ void __launch_bounds__(MST) k_mtf_scan_lists(const BlockDesc* __restrict__ blocks, uint32_t b0,
+                                                        uint64_t* __restrict__ K, uint64_t kstride, uint32_t C)
+{
+    __shared__ NibState sh[MST];
+    const int tid = threadIdx.x;
+    const uint32_t slot = blockIdx.x, b = b0 + slot;
+    const uint32_t n = blocks[b].n, nin = blocks[b].n_in_use;
+    if (nin > 16) return;
+    const uint32_t nch = (n + MCS - 1) / MCS;
+    const uint32_t per = (nch + MST - 1) / MST;          // <= 2 for 900 KB blocks
+    const MtfScr ms = mtf_scr(K, kstride, slot, C);
+    const uint32_t c0 = tid * per;
+    NibState agg;
+    agg.list = 0; agg.set = 0; agg.cnt = 0;
+    for (uint32_t q = 0; q < per; ++q)
+        if (c0 + q < nch) agg = nib_compose(agg, ms.nst()[c0 + q]);
+    sh[tid] = agg;
     __syncthreads();
-    RunSum pre;
-    pre.nz = 0; pre.lz = 0; pre.tz = 0; pre.inner = 0;
-    for (int w = 0; w < wid; ++w) pre = run_compose(pre, wsum[w]);
-    RunSum ex = shfl_up_rs(inc, 1);
-    if (lane == 0) { ex.nz = 0; ex.lz = 0; ex.tz = 0; ex.inner = 0; }
-    ex = run_compose(pre, ex);
-    if (tid == MT - 1) total_sh = run_compose(ex, rs);
-    const uint32_t zin = ex.nz ? ex.tz : ex.lz;
-    const uint32_t obase = ex.nz ? nsym_run(ex.lz) + 1 + ex.inner : 0;
+    for (int d = 1; d < MST; d <<= 1) {                 // inclusive scan of the composition
+        const NibState v = (tid >= d) ? nib_compose(sh[tid - d], sh[tid]) : sh[tid];
+        __syncthreads();
+        sh[tid] = v;
+        __syncthreads();
+    }
+    NibState st;
+    st.list = 0;
+    for (uint32_t i = 0; i < nin; ++i) st.list |= (uint64_t)i << (4 * i);
+    st.set = (1u << nin) - 1u;
+    st.cnt = nin;
+    if (tid) st = nib_compose(st, sh[tid - 1]);
+    for (uint32_t q = 0; q < per; ++q) {
+        if (c0 + q >= nch) break;
+        ms.l0()[c0 + q] = st.list;
+        st = nib_compose(st, ms.nst()[c0 + q]);
+    }
+}
 
-    // ---- pass 3: re-run the MTF and emit ----
-    if (mine) {
-        Out16 out;
-        out.init(mtfv, obase);
-        uint64_t L = L0;
-        uint32_t z = zin;
-        for (uint32_t j0 = a; j0 < e; j0 += LINE) {
-            const uint32_t lim = e - j0;
-            visit_line<true>(ll + j0, [&](int k, uint32_t byte) {
-                if ((uint32_t)k < lim) {
-                    const uint32_t x = nib_mtf(L, byte);
-                    if (x == 0) {
-                        ++z;
-                    } else {
-                        put_run(out, z);
-                        out.put(x + 1);
-                        z = 0;
-                    }
-                }
-            });
-        }
-        out.flush();
-    }
+// zero-run summary of each chunk's MTF indices (branch-free per symbol)
+__global__ void __launch_bounds__(MCT) k_mtf_runs(const BlockDesc* __restrict__ blocks, uint32_t b0,
+                                                  const uint8_t* __restrict__ LL, uint64_t ll_stride,
+                                                  uint64_t* __restrict__ K, uint64_t kstride, uint32_t C)
+{
+    const uint32_t slot = blockIdx.y, b = b0 + slot;
+    const uint32_t n = blocks[b].n, nin = blocks[b].n_in_use;
+    const uint32_t ch = blockIdx.x * MCT + threadIdx.x;
+    const uint32_t a = ch * MCS;
+    if (nin > 16 || a >= n) return;
+    const uint32_t e = a + MCS < n ? a + MCS : n;
+    const MtfScr ms = mtf_scr(K, kstride, slot, C);
+    uint64_t L = ms.l0()[ch];
+    uint32_t z = 0, nz = 0, lz = 0, inner = 0;
+    visit_chunk(LL + (uint64_t)slot * ll_stride, a, e, [&](uint32_t s) {
+        const uint32_t x = nib_mtf(L, s);
+        const uint32_t nzf = x != 0 ? 1u : 0u;
+        inner += (nzf & nz) ? 1u + (31u - __clz(z + 1u)) : 0u;
+        lz = (nzf & (nz ^ 1u)) ? z : lz;
+        nz |= nzf;
+        z = nzf ? 0u : z + 1u;
+    });
+    RunSum r;
+    r.nz = nz;
+    r.lz = nz ? lz : z;
+    r.tz = nz ? z : 0u;
+    r.inner = inner;
+    ms.rs()[ch] = r;
+}
+
+// exclusive scan of the run summaries: zeros carried into each chunk and its
+// first output index; the block's trailing run, EOB and n_mtf
+__global__ void __launch_bounds__(MST) k_mtf_scan_runs(BlockDesc* __restrict__ blocks, uint32_t b0,
+                                                       uint64_t* __restrict__ K, uint64_t kstride, uint32_t C,
+                                                       uint16_t* __restrict__ mtfv_all, uint64_t mtf_stride)
+{
+    __shared__ RunSum sh[MST];
+    const int tid = threadIdx.x;
+    const uint32_t slot = blockIdx.x, b = b0 + slot;
+    const uint32_t n = blocks[b].n, nin = blocks[b].n_in_use;
+    if (nin > 16) return;
+    const uint32_t nch = (n + MCS - 1) / MCS;
+    const uint32_t per = (nch + MST - 1) / MST;
+    const MtfScr ms = mtf_scr(K, kstride, slot, C);
+    const uint32_t c0 = tid * per;
+    RunSum agg;
+    agg.nz = 0; agg.lz = 0; agg.tz = 0; agg.inner = 0;
+    for (uint32_t q = 0; q < per; ++q)
+        if (c0 + q < nch) agg = run_compose(agg, ms.rs()[c0 + q]);
+    sh[tid] = agg;
     __syncthreads();
-    if (tid == 0) {
-        const RunSum T = total_sh;
+    for (int d = 1; d < MST; d <<= 1) {
+        const RunSum v = (tid >= d) ? run_compose(sh[tid - d], sh[tid]) : sh[tid];
+        __syncthreads();
+        sh[tid] = v;
+        __syncthreads();
+    }
+    RunSum ex;
+    ex.nz = 0; ex.lz = 0; ex.tz = 0; ex.inner = 0;
+    if (tid) ex = sh[tid - 1];
+    for (uint32_t q = 0; q < per; ++q) {
+        if (c0 + q >= nch) break;
+        const uint32_t zin = ex.nz ? ex.tz : ex.lz;
+        const uint32_t obase = ex.nz ? nsym_run(ex.lz) + 1 + ex.inner : 0;
+        ms.zo()[c0 + q] = make_uint2(zin, obase);
+        ex = run_compose(ex, ms.rs()[c0 + q]);
+    }
+    if (tid == MST - 1) {
+        const RunSum T = sh[MST - 1];
+        uint16_t* mtfv = mtfv_all + (uint64_t)b * mtf_stride;
         uint32_t z = T.nz ? T.tz : T.lz;
         uint32_t o = T.nz ? nsym_run(T.lz) + 1 + T.inner : 0;
         while (z) {
@@ -267,6 +353,37 @@ __global__ void __launch_bounds__(MT) k_mtf_nib(BlockDesc* __restrict__ blocks, 
         mtfv[o++] = (uint16_t)(nin + 1);       // EOB
         blocks[b].n_mtf = o;
     }
+}
+
+// re-run each chunk's MTF and emit RUNA/RUNB + symbols at its offset
+__global__ void __launch_bounds__(MCT) k_mtf_emit(const BlockDesc* __restrict__ blocks, uint32_t b0,
+                                                  const uint8_t* __restrict__ LL, uint64_t ll_stride,
+                                                  const uint64_t* __restrict__ K, uint64_t kstride, uint32_t C,
+                                                  uint16_t* __restrict__ mtfv_all, uint64_t mtf_stride)
+{
+    const uint32_t slot = blockIdx.y, b = b0 + slot;
+    const uint32_t n = blocks[b].n, nin = blocks[b].n_in_use;
+    const uint32_t ch = blockIdx.x * MCT + threadIdx.x;
+    const uint32_t a = ch * MCS;
+    if (nin > 16 || a >= n) return;
+    const uint32_t e = a + MCS < n ? a + MCS : n;
+    const MtfScr ms = mtf_scr(const_cast<uint64_t*>(K), kstride, slot, C);
+    uint64_t L = ms.l0()[ch];
+    const uint2 zo = ms.zo()[ch];
+    Out16 out;
+    out.init(mtfv_all + (uint64_t)b * mtf_stride, zo.y);
+    uint32_t z = zo.x;
+    visit_chunk_lines(LL + (uint64_t)slot * ll_stride, a, e, [&](uint32_t s) {
+        const uint32_t x = nib_mtf(L, s);
+        if (x == 0) {
+            ++z;
+        } else {
+            put_run(out, z);
+            out.put(x + 1);
+            z = 0;
+        }
+    });
+    out.flush();
 }
 
 // ---- alphabets > 16: byte lists in LDS, 256 chunks; also produces mtfFreq ----
@@ -481,7 +598,17 @@ void launch_mtf(BlockDesc* blocks, uint32_t b0, uint32_t nb, const uint8_t* blkb
 {
     (void)blkbytes;
     (void)stride;
-    hipLaunchKernelGGL(k_mtf_nib, dim3(nb), dim3(MT), 0, st, blocks, b0, scr.LL, scr.stride, mtfv, mtf_stride);
+    // alphabets <= 16: chunk passes over the key scratch (free after the sort)
+    const uint32_t C = (uint32_t)((scr.stride + MCS - 1) / MCS);
+    const uint64_t kstride = scr.stride;                     // u64 words per slot
+    const dim3 gch((C + MCT - 1) / MCT, nb);
+    hipLaunchKernelGGL(k_mtf_local, gch, dim3(MCT), 0, st, blocks, b0, scr.LL, scr.stride, scr.K, kstride, C);
+    hipLaunchKernelGGL(k_mtf_scan_lists, dim3(nb), dim3(MST), 0, st, blocks, b0, scr.K, kstride, C);
+    hipLaunchKernelGGL(k_mtf_runs, gch, dim3(MCT), 0, st, blocks, b0, scr.LL, scr.stride, scr.K, kstride, C);
+    hipLaunchKernelGGL(k_mtf_scan_runs, dim3(nb), dim3(MST), 0, st, blocks, b0, scr.K, kstride, C, mtfv,
+                       mtf_stride);
+    hipLaunchKernelGGL(k_mtf_emit, gch, dim3(MCT), 0, st, blocks, b0, scr.LL, scr.stride, scr.K, kstride, C, mtfv,
+                       mtf_stride);
     // large alphabets: index bytes + per-chunk lists in the (free) key scratch
     hipLaunchKernelGGL(k_mtf_big, dim3(nb), dim3(MT), 0, st, blocks, b0, scr.LL, scr.stride,
                        reinterpret_cast<uint8_t*>(scr.K), scr.stride * sizeof(uint64_t), mtfv, mtf_stride, tabs);
