@@ -774,25 +774,25 @@ __global__ void __launch_bounds__(256) k3_sort_w(Ctx c, const uint64_t* __restri
 // k3_sort_lds<NW, E>: groups of <= NW*64*E rotations sorted by NW waves
 // (NW = 1: four independent wave-private sorts per workgroup, no workgroup
 // barrier; NW = 4: one group per workgroup).  Persistent over a binned list.
-// The group-local index rides in the key's constant top bits (every group's
-// keys share at least 12 top bits: the bucket digit, the partition digits, or
-// unused high bits), so each exchange moves one u64 per element through LDS.
+// Every group's keys share at least their top 12 bits (the bucket digit, the
+// partition digits, or unused high bits); dropping them leaves room for the
+// group-local index below the key: (key << IDXB) | index is unique and
+// ordered like the key, so each exchange moves one u64 per element through
+// LDS and ranking is one 64-bit compare per pair.
 // Primary path: one MSD digit (the DB bits below the highest varying bit),
-// then every element ranks itself inside its sub-bucket by comparison.  When
-// a sub-bucket exceeds LIMIT: stable LSD radix over the varying 8-bit digits
-// (8 ballots find a lane's digit peers; one lane per peer set adds the set's
-// size to the wave's counter with a returning LDS atomic).
+// then every element ranks itself inside its sub-bucket by comparison; a
+// second digit for sub-buckets above LIMIT.  Otherwise: stable LSD radix over
+// the varying 8-bit digits (8 ballots find a lane's digit peers; one lane per
+// peer set adds the set's size to the wave's counter with a returning LDS
+// atomic).
 // ---------------------------------------------------------------------------
-// rank of key km (at position j) among positions [rs, re) of xk: keys below
-// it, and equal keys at earlier positions
-template <uint64_t KMASK>
-__device__ __forceinline__ uint32_t rank_in(const uint64_t* xk, uint32_t rs, uint32_t re, uint64_t km, uint32_t j)
+// rank of key kj among positions [rs, re) of xk.  Keys are (key << IDXB) |
+// group index: unique, so one 64-bit compare orders them (ties of the key
+// broken by index)
+__device__ __forceinline__ uint32_t rank_in(const uint64_t* xk, uint32_t rs, uint32_t re, uint64_t kj)
 {
     uint32_t r = 0;
-    for (uint32_t q = rs; q < re; ++q) {
-        const uint64_t a = xk[q] & KMASK;
-        r += (a < km || (a == km && q < j)) ? 1u : 0u;
-    }
+    for (uint32_t q = rs; q < re; ++q) r += xk[q] < kj ? 1u : 0u;
     return r;
 }
 
@@ -881,7 +881,7 @@ k3_sort_lds(Ctx c, const uint64_t* __restrict__ items,
             const uint32_t i = (uint32_t)(wid * 64 * E + e * 64 + lane);
             if (i < m) {
                 diff |= kx[e] ^ k0;
-                k[e] = (kx[e] & KMASK) | ((uint64_t)i << KEYB);
+                k[e] = ((kx[e] & KMASK) << IDXB) | i;
                 vb_all[g][i] = vv[e] | (ls[e] << 24);
             } else {
                 k[e] = ~0ull;                          // pads: max key, last in stable order
@@ -911,7 +911,7 @@ k3_sort_lds(Ctx c, const uint64_t* __restrict__ items,
         uint32_t dg[E];
 #pragma unroll
         for (int e = 0; e < E; ++e) {
-            dg[e] = (uint32_t)(((k[e] & KMASK) >> lo) & (uint64_t)(NBIN - 1));
+            dg[e] = (uint32_t)((k[e] >> (lo + IDXB)) & (uint64_t)(NBIN - 1));
             if ((uint32_t)(wid * 64 * E + e * 64 + lane) < m) atomicAdd(&bcur[dg[e]], 1u);
         }
         gsync<NW>();
@@ -947,10 +947,9 @@ k3_sort_lds(Ctx c, const uint64_t* __restrict__ items,
                 p[e] = j;                          // pads keep the tail
                 if (j < m) {
                     const uint64_t kj = xk[j];
-                    const uint64_t km = kj & KMASK;
                     uint32_t rs, re;
-                    range_of(km, rs, re);
-                    p[e] = rs + rank_in<KMASK>(xk, rs, re, km, j);
+                    range_of(kj, rs, re);
+                    p[e] = rs + rank_in(xk, rs, re, kj);
                     k[e] = kj;
                 }
             }
@@ -970,8 +969,8 @@ k3_sort_lds(Ctx c, const uint64_t* __restrict__ items,
             for (int e = 0; e < E; ++e)
                 if ((uint32_t)(wid * 64 * E + e * 64 + lane) < m) xk[atomicAdd(&bcur[dg[e]], 1u)] = k[e];
             gsync<NW>();
-            rank_place([&](uint64_t km, uint32_t& rs, uint32_t& re) {
-                const uint32_t d = (uint32_t)((km >> lo) & (uint64_t)(NBIN - 1));
+            rank_place([&](uint64_t kj, uint32_t& rs, uint32_t& re) {
+                const uint32_t d = (uint32_t)((kj >> (lo + IDXB)) & (uint64_t)(NBIN - 1));
                 rs = bst[d];
                 re = bst[d + 1];
             });
@@ -1016,7 +1015,7 @@ k3_sort_lds(Ctx c, const uint64_t* __restrict__ items,
                 if ((uint32_t)(wid * 64 * E + e * 64 + lane) < m) {
                     const uint32_t x = bcur[dg[e]];
                     if (x >> 31) {
-                        b2[e] = (x & 0x7FFFFFFFu) + (uint32_t)(((k[e] & KMASK) >> lo2) & ((1ull << w2) - 1ull));
+                        b2[e] = (x & 0x7FFFFFFFu) + (uint32_t)((k[e] >> (lo2 + IDXB)) & ((1ull << w2) - 1ull));
                         atomicAdd(&c2[b2[e]], 1u);
                     }
                 }
@@ -1068,12 +1067,12 @@ k3_sort_lds(Ctx c, const uint64_t* __restrict__ items,
                 gsync<NW>();
                 // after the scatter c2[b] = end of bin b = start of bin b + 1;
                 // big sub-buckets still carry their tag in bcur
-                rank_place([&](uint64_t km, uint32_t& rs, uint32_t& re) {
-                    const uint32_t d = (uint32_t)((km >> lo) & (uint64_t)(NBIN - 1));
+                rank_place([&](uint64_t kj, uint32_t& rs, uint32_t& re) {
+                    const uint32_t d = (uint32_t)((kj >> (lo + IDXB)) & (uint64_t)(NBIN - 1));
                     const uint32_t x = bcur[d];
                     if (x >> 31) {
                         const uint32_t base = x & 0x7FFFFFFFu;
-                        const uint32_t b = base + (uint32_t)((km >> lo2) & ((1ull << w2) - 1ull));
+                        const uint32_t b = base + (uint32_t)((kj >> (lo2 + IDXB)) & ((1ull << w2) - 1ull));
                         const uint32_t s0 = base ? c2[base - 1] : 0u;
                         rs = bst[d] + (b ? c2[b - 1] : 0u) - s0;
                         re = bst[d] + c2[b] - s0;
@@ -1098,7 +1097,7 @@ k3_sort_lds(Ctx c, const uint64_t* __restrict__ items,
         uint32_t dg[E], rk[E], ld[E], ret[E];
 #pragma unroll
         for (int e = 0; e < E; ++e) {
-            const uint32_t d = (uint32_t)(((k[e] & KMASK) >> dbit) & 255u);
+            const uint32_t d = (uint32_t)((k[e] >> (dbit + IDXB)) & 255u);
             uint64_t peers = ~0ull;
 #pragma unroll
             for (int bb = 0; bb < 8; ++bb) {
@@ -1164,7 +1163,7 @@ k3_sort_lds(Ctx c, const uint64_t* __restrict__ items,
 #pragma unroll
     for (int e = 0; e < E; ++e) {
         const uint32_t j = (uint32_t)(wid * 64 * E + e * 64 + lane);
-        if (j > 0 && j < m && ((xk[j - 1] ^ k[e]) & KMASK) == 0) tie_here = true;
+        if (j > 0 && j < m && ((xk[j - 1] ^ k[e]) >> IDXB) == 0) tie_here = true;
     }
     bool ties = __ballot(tie_here) != 0;
     if constexpr (NW > 1) {
@@ -1182,7 +1181,7 @@ k3_sort_lds(Ctx c, const uint64_t* __restrict__ items,
 #pragma unroll
         for (int e = 0; e < E; ++e) {
             const uint32_t j = (uint32_t)(wid * 64 * E + e * 64 + lane);
-            const bool head = j < m && (j == 0 || ((xk[j - 1] ^ k[e]) & KMASK) != 0);
+            const bool head = j < m && (j == 0 || ((xk[j - 1] ^ k[e]) >> IDXB) != 0);
             uint32_t xx = wave_incl_scan_max<uint32_t>(head ? j : 0u);
             xx = xx > carry ? xx : carry;
             hp[e] = xx;
@@ -1205,8 +1204,8 @@ k3_sort_lds(Ctx c, const uint64_t* __restrict__ items,
     for (int e = 0; e < E; ++e) {
         const uint32_t j = (uint32_t)(wid * 64 * E + e * 64 + lane);
         const bool valid = j < m;
-        const uint32_t vb = valid ? vb_all[g][(uint32_t)(k[e] >> KEYB)] : 0u;
-        const bool end = valid && (!ties || j + 1 == m || ((xk[j + 1] ^ k[e]) & KMASK) != 0);
+        const uint32_t vb = valid ? vb_all[g][(uint32_t)(k[e] & ((1u << IDXB) - 1u))] : 0u;
+        const bool end = valid && (!ties || j + 1 == m || ((xk[j + 1] ^ k[e]) >> IDXB) != 0);
         emit_sorted(c, slot, s, j, vb & 0xFFFFFFu, valid, hp[e], end, runs, vb >> 24);
     }
     if (c.mode && lane == 0 && runs) atomicAdd(&c.L.runs[slot], runs);
@@ -1321,7 +1320,7 @@ k3_sort_grp(Ctx c, const uint64_t* __restrict__ items,
         const uint32_t i = (uint32_t)(wid * 64 * E + e * 64 + lane);
         if (i < m) {
             diff |= cur.kx[e] ^ cur.k0;
-            k[e] = (cur.kx[e] & KMASK) | ((uint64_t)i << KEYB);
+            k[e] = ((cur.kx[e] & KMASK) << IDXB) | i;
             vb_all[g][i] = cur.v[e] | (cur.ls[e] << 24);
         } else {
             k[e] = ~0ull;                              // pads: max key, last in order
@@ -1347,7 +1346,7 @@ k3_sort_grp(Ctx c, const uint64_t* __restrict__ items,
         uint32_t dg[E];
 #pragma unroll
         for (int e = 0; e < E; ++e) {
-            dg[e] = (uint32_t)(((k[e] & KMASK) >> lo) & (uint64_t)(NBIN - 1));
+            dg[e] = (uint32_t)((k[e] >> (lo + IDXB)) & (uint64_t)(NBIN - 1));
             if ((uint32_t)(wid * 64 * E + e * 64 + lane) < m) atomicAdd(&bcur[dg[e]], 1u);
         }
         gsync<NW>();
@@ -1388,10 +1387,9 @@ k3_sort_grp(Ctx c, const uint64_t* __restrict__ items,
                 pos[e] = j;
                 if (j < m) {
                     const uint64_t kj = xk[j];
-                    const uint64_t km = kj & KMASK;
-                    const uint32_t d = (uint32_t)((km >> lo) & (uint64_t)(NBIN - 1));
+                    const uint32_t d = (uint32_t)((kj >> (lo + IDXB)) & (uint64_t)(NBIN - 1));
                     const uint32_t bs = bst[d], be = bst[d + 1];
-                    pos[e] = bs + rank_in<KMASK>(xk, bs, be, km, j);
+                    pos[e] = bs + rank_in(xk, bs, be, kj);
                     k[e] = kj;
                 }
             }
@@ -1418,7 +1416,7 @@ k3_sort_grp(Ctx c, const uint64_t* __restrict__ items,
 #pragma unroll
     for (int e = 0; e < E; ++e) {
         const uint32_t j = (uint32_t)(wid * 64 * E + e * 64 + lane);
-        if (j > 0 && j < m && ((xk[j - 1] ^ k[e]) & KMASK) == 0) tie_here = true;
+        if (j > 0 && j < m && ((xk[j - 1] ^ k[e]) >> IDXB) == 0) tie_here = true;
     }
     bool ties = __ballot(tie_here) != 0;
     if constexpr (NW > 1) {
@@ -1436,7 +1434,7 @@ k3_sort_grp(Ctx c, const uint64_t* __restrict__ items,
 #pragma unroll
         for (int e = 0; e < E; ++e) {
             const uint32_t j = (uint32_t)(wid * 64 * E + e * 64 + lane);
-            const bool head = j < m && (j == 0 || ((xk[j - 1] ^ k[e]) & KMASK) != 0);
+            const bool head = j < m && (j == 0 || ((xk[j - 1] ^ k[e]) >> IDXB) != 0);
             uint32_t xx = wave_incl_scan_max<uint32_t>(head ? j : 0u);
             xx = xx > carry ? xx : carry;
             hp[e] = xx;
@@ -1457,8 +1455,8 @@ k3_sort_grp(Ctx c, const uint64_t* __restrict__ items,
     for (int e = 0; e < E; ++e) {
         const uint32_t j = (uint32_t)(wid * 64 * E + e * 64 + lane);
         const bool valid = j < m;
-        const uint32_t vb = valid ? vb_all[g][(uint32_t)(k[e] >> KEYB)] : 0u;
-        const bool end = valid && (!ties || j + 1 == m || ((xk[j + 1] ^ k[e]) & KMASK) != 0);
+        const uint32_t vb = valid ? vb_all[g][(uint32_t)(k[e] & ((1u << IDXB) - 1u))] : 0u;
+        const bool end = valid && (!ties || j + 1 == m || ((xk[j + 1] ^ k[e]) >> IDXB) != 0);
         emit_sorted(c, slot, s, j, vb & 0xFFFFFFu, valid, hp[e], end, runs, vb >> 24);
     }
     if (c.mode && lane == 0 && runs) atomicAdd(&c.L.runs[slot], runs);
