@@ -638,20 +638,43 @@ __global__ void __launch_bounds__(LT) k3_part_l(Ctx c, const uint64_t* __restric
         for (int i = tid; i < LW * 256; i += LT) (&wh[0][0])[i] = 0;
         if (tid == 0) big[256] = 0;
         __syncthreads();
-        for (uint32_t i = tid; i < m; i += LT)
-            atomicAdd(&wh[wid][(uint32_t)((elem_key<DBL>(ks, s + i, sv[i]) >> sh2) & dmask)], 1u);
+        constexpr int PU = 4;                          // elements in flight per thread
+        for (uint32_t i0 = 0; i0 < m; i0 += PU * LT) {
+            uint32_t d[PU];
+#pragma unroll
+            for (int u = 0; u < PU; ++u) {
+                const uint32_t i = i0 + u * LT + tid;
+                const uint32_t ic = i < m ? i : 0u;
+                d[u] = (uint32_t)((elem_key<DBL>(ks, s + ic, sv[ic]) >> sh2) & dmask);
+            }
+#pragma unroll
+            for (int u = 0; u < PU; ++u)
+                if (i0 + u * LT + tid < m) atomicAdd(&wh[wid][d[u]], 1u);
+        }
         __syncthreads();
         uint32_t tcount = 0;
         if (tid < 256) for (int w = 0; w < LW; ++w) tcount += wh[w][tid];
         const uint32_t pre = block_excl_scan_add<uint32_t>(tid < 256 ? tcount : 0u, scan_sh, (uint32_t*)nullptr);
         if (tid < 256) { st[tid] = pre; cur[tid] = pre; cntd[tid] = tcount; }
         __syncthreads();
-        for (uint32_t i = tid; i < m; i += LT) {
-            const uint32_t v = sv[i];
-            const uint64_t k = elem_key<DBL>(ks, s + i, v);
-            const uint32_t p = atomicAdd(&cur[(uint32_t)((k >> sh2) & dmask)], 1u);
-            dv[p] = v;
-            if constexpr (DBL) dk[p] = k;
+        for (uint32_t i0 = 0; i0 < m; i0 += PU * LT) {
+            uint32_t v[PU];
+            uint64_t k[PU];
+#pragma unroll
+            for (int u = 0; u < PU; ++u) {
+                const uint32_t i = i0 + u * LT + tid;
+                const uint32_t ic = i < m ? i : 0u;
+                v[u] = sv[ic];
+                k[u] = elem_key<DBL>(ks, s + ic, v[u]);
+            }
+#pragma unroll
+            for (int u = 0; u < PU; ++u) {
+                if (i0 + u * LT + tid < m) {
+                    const uint32_t p = atomicAdd(&cur[(uint32_t)((k[u] >> sh2) & dmask)], 1u);
+                    dv[p] = v[u];
+                    if constexpr (DBL) dk[p] = k[u];
+                }
+            }
         }
         __syncthreads();
         uint32_t nruns = 0;

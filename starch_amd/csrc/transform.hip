@@ -698,21 +698,25 @@ __device__ __forceinline__ bool tf_parse(const uint8_t* __restrict__ bed, const 
     return true;
 }
 
-constexpr uint32_t kTf1Cap = kParseCap;
-constexpr uint32_t kTf2Cap = 16384;
-constexpr uint32_t kTfOutCap = 16384;
+// LDS staging sizes are chosen per launch from the input's mean line length
+// (and, for pass 2, mean output length): small for BED3, so many workgroups
+// stay resident and their loads overlap; a workgroup whose lines do not fit
+// parses from global memory / writes its output directly.
+constexpr uint32_t kTfCapMax = kParseCap;
+constexpr uint32_t kTfOutCapMax = 16384;
+extern __shared__ uint4 tf_dyn_lds[];
 
 __global__ void __launch_bounds__(kThreads)
 k_tf1(const uint8_t* __restrict__ bed, const uint64_t* __restrict__ line_end, uint64_t nl,
-      uint64_t* __restrict__ wg_len, uint32_t* __restrict__ wg_seg, uint32_t* __restrict__ any_fail)
+      uint64_t* __restrict__ wg_len, uint32_t* __restrict__ wg_seg, uint32_t* __restrict__ any_fail, uint32_t cap)
 {
-    __shared__ uint4 tb4[(kTf1Cap + kStagePad) / 16];
+    uint4* tb4 = tf_dyn_lds;                       // cap + kStagePad bytes
     __shared__ TfShared sh;
     __shared__ uint64_t red[kThreads / 64];
     const uint64_t L0 = (uint64_t)blockIdx.x * kThreads;
     const uint64_t L1 = L0 + kThreads < nl ? L0 + kThreads : nl;
     uint64_t a0 = 0;
-    const bool staged = stage_lines(bed, line_end, L0, L1, tb4, kTf1Cap, a0);
+    const bool staged = stage_lines(bed, line_end, L0, L1, tb4, cap, a0);
     TfLine t;
     uint64_t v = 0;
     if (tf_parse(bed, line_end, nl, L0, staged, reinterpret_cast<const uint8_t*>(tb4), a0, sh, t)) {
@@ -768,17 +772,17 @@ __device__ __forceinline__ void tf_write(const S& src, const TfLine& t, uint8_t*
 __global__ void __launch_bounds__(kThreads)
 k_tf2(const uint8_t* __restrict__ bed, const uint64_t* __restrict__ line_end, uint64_t nl,
       const uint64_t* __restrict__ wg_off, const uint64_t* __restrict__ wg_sego, uint8_t* __restrict__ text,
-      SegInfo* __restrict__ info)
+      SegInfo* __restrict__ info, uint32_t cap, uint32_t ocap)
 {
-    __shared__ uint4 tb4[(kTf2Cap + kStagePad) / 16];
+    uint4* tb4 = tf_dyn_lds;                                                    // cap + kStagePad bytes
+    uint32_t* ob4 = reinterpret_cast<uint32_t*>(tf_dyn_lds + (cap + kStagePad) / 16);   // ocap bytes
     __shared__ TfShared sh;
-    __shared__ uint32_t ob4[kTfOutCap / 4];
     __shared__ uint64_t scan_sh[kThreads / 64 + 1];
     const uint64_t L0 = (uint64_t)blockIdx.x * kThreads;
     const uint64_t L1 = L0 + kThreads < nl ? L0 + kThreads : nl;
     const uint64_t i = L0 + threadIdx.x;
     uint64_t a0 = 0;
-    const bool staged = stage_lines(bed, line_end, L0, L1, tb4, kTf2Cap, a0);
+    const bool staged = stage_lines(bed, line_end, L0, L1, tb4, cap, a0);
     const uint8_t* tb = reinterpret_cast<const uint8_t*>(tb4);
     TfLine t;
     const bool have = tf_parse(bed, line_end, nl, L0, staged, tb, a0, sh, t);
@@ -788,7 +792,7 @@ k_tf2(const uint8_t* __restrict__ bed, const uint64_t* __restrict__ line_end, ui
     const uint64_t ex = block_excl_scan_add<uint64_t>((len << 20) | ns, scan_sh, &tot);
     const uint64_t o0 = wg_off[blockIdx.x];
     const uint64_t loc = ex >> 20, wlen = tot >> 20;
-    const bool in_lds = wlen <= kTfOutCap;
+    const bool in_lds = wlen <= ocap;
     if (have) {
         if (ns) {
             SegInfo& s = info[wg_sego[blockIdx.x] + (ex & 0xFFFFFu)];
@@ -905,7 +909,15 @@ void TransformWorkspace::run(const uint8_t* d_bed, uint64_t n, hipStream_t st, T
     uint64_t* wg_off = wg_len + nb + 1;
     uint32_t* wg_seg = b_seg_flag.as<uint32_t>(nb + 1);
     uint64_t* wg_sego = b_seg_ord.as<uint64_t>(nb + 1);
-    hipLaunchKernelGGL(k_tf1, dim3(nb), dim3(kThreads), 0, st, d_bed, line_end, nl, wg_len, wg_seg, any_fail);
+    auto lds_cap = [](double per_line, uint32_t lo, uint32_t hi) {
+        const double want = 1.3 * (kThreads + 1) * per_line + 256.0;
+        uint32_t c = want > hi ? hi : (uint32_t)want;
+        c = (c + 1023u) & ~1023u;
+        return c < lo ? lo : (c > hi ? hi : c);
+    };
+    const uint32_t cap = lds_cap((double)n / (double)nl, 4096, kTfCapMax);
+    hipLaunchKernelGGL(k_tf1, dim3(nb), dim3(kThreads), cap + kStagePad, st, d_bed, line_end, nl, wg_len, wg_seg,
+                       any_fail, cap);
     scan::excl_sum_u64(wg_len, wg_off, nb, scal + 4, b_tmp, st);
     scan::excl_sum_u32_to_u64(wg_seg, wg_sego, nb, scal + 3, b_tmp, st);
     uint32_t fail = 0;
@@ -917,8 +929,9 @@ void TransformWorkspace::run(const uint8_t* d_bed, uint64_t n, hipStream_t st, T
     if (!fail) {
         info = b_seg_info.as<SegInfo>(nseg + 1);
         text = b_text.as<uint8_t>(ttot + 64);
-        hipLaunchKernelGGL(k_tf2, dim3(nb), dim3(kThreads), 0, st, d_bed, line_end, nl, wg_off, wg_sego, text,
-                           info);
+        const uint32_t ocap = lds_cap((double)ttot / (double)nl, 2048, kTfOutCapMax);
+        hipLaunchKernelGGL(k_tf2, dim3(nb), dim3(kThreads), cap + kStagePad + ocap, st, d_bed, line_end, nl, wg_off,
+                           wg_sego, text, info, cap, ocap);
         hipLaunchKernelGGL(k_seg_close, dim3((unsigned)ceil_div(nseg, 256)), dim3(256), 0, st, info, nseg, nl,
                            ttot);
     } else {
