@@ -55,17 +55,17 @@ constexpr int ET = 1024;
 // One workgroup per block.  Thread 0 writes the fixed header (magic, CRC,
 // origPtr, inUse map, nGroups, nSelectors); the selectors' unary MTF codes
 // are written in parallel (contiguous selector ranges per thread, bit offsets
-// by a block scan); thread 0 writes the delta-coded lengths; then one
-// 50-symbol group per lane.
+// by a block scan); thread 0 writes the delta-coded lengths; then the bit
+// offsets of the data groups (k_emit_data writes them).
 __global__ void __launch_bounds__(ET) k_emit_block(const BlockDesc* __restrict__ blocks,
                                                     const uint16_t* __restrict__ mtfv_all, uint64_t mtf_stride,
                                                     const Tables* __restrict__ tabs, const uint8_t* __restrict__ sel_all,
-                                                    const uint32_t* __restrict__ gbits_all, uint32_t* __restrict__ out32)
+                                                    const uint32_t* __restrict__ gbits_all, uint32_t* __restrict__ gpre_all,
+                                                    uint32_t* __restrict__ out32)
 {
     __shared__ uint8_t len[6][258];
     __shared__ uint32_t code[6][258];
     __shared__ uint32_t scan_sh[ET / 64 + 1];
-    __shared__ unsigned long long carry;
     const int tid = threadIdx.x;
     const uint32_t b = blockIdx.x;
     const BlockDesc bd = blocks[b];
@@ -75,7 +75,6 @@ __global__ void __launch_bounds__(ET) k_emit_block(const BlockDesc* __restrict__
         int t = i / 258, v = i % 258;
         if (t < ng && v < alpha) { len[t][v] = tabs[b].len[t][v]; code[t][v] = tabs[b].code[t][v]; }
     }
-    if (tid == 0) carry = 0;
     const uint16_t* mtfv = mtfv_all + (uint64_t)b * mtf_stride;
     const uint8_t* sel = sel_all + (uint64_t)b * (2 * kMaxSelectors);
     const uint8_t* selmtf = sel + kMaxSelectors;
@@ -139,34 +138,115 @@ __global__ void __launch_bounds__(ET) k_emit_block(const BlockDesc* __restrict__
         }
         o.finish();
     }
-    // coded data, one 50-symbol group per lane
-    const uint64_t data0 = bd.bit_off + bd.hdr_bits;
+    // bit offsets of the coded 50-symbol groups: exclusive scan of their sizes
+    // (k_emit_data writes the groups themselves, flat over all blocks)
+    uint32_t* gpre = gpre_all + (uint64_t)b * kMaxSelectors;
+    uint32_t run = 0;
     for (uint32_t g0 = 0; g0 < bd.n_sel; g0 += ET) {
-        uint32_t g = g0 + tid;
-        uint32_t gb = (g < bd.n_sel) ? gbits[g] : 0u;
+        const uint32_t g = g0 + tid;
+        const uint32_t gb = (g < bd.n_sel) ? gbits[g] : 0u;
         uint32_t tot;
-        uint32_t pre = block_excl_scan_add<uint32_t>(gb, scan_sh, &tot);
-        if (g < bd.n_sel) {
-            BitOut o;
-            o.init(out32, data0 + carry + pre);
-            uint32_t gs = g * 50, ge = gs + 50;
-            if (ge > bd.n_mtf) ge = bd.n_mtf;
-            const int t = sel[g];
-            const uint32_t* m32 = reinterpret_cast<const uint32_t*>(mtfv + gs);   // gs even: 4-B aligned
-            for (uint32_t i = gs; i < ge; i += 2) {
-                const uint32_t w = m32[(i - gs) >> 1];
-                const uint32_t v0 = w & 0xffffu;
-                o.put(len[t][v0], code[t][v0]);
-                if (i + 1 < ge) {
-                    const uint32_t v1 = w >> 16;
-                    o.put(len[t][v1], code[t][v1]);
-                }
-            }
-            o.finish();
+        const uint32_t pre = block_excl_scan_add<uint32_t>(gb, scan_sh, &tot);
+        if (g < bd.n_sel) gpre[g] = run + pre;
+        run += tot;
+    }
+}
+
+// Coded data: one 50-symbol group per lane, over (block, 256-group tile);
+// code lengths and codes packed (len << 24 | code) in LDS, one read per symbol.
+// A lane keeps the first (possibly shared) word of its bit range in a register
+// and plain-stores the words fully inside; the word it shares with the
+// previous lane is completed with that lane's tail bits (a shuffle) and
+// plain-stored, so only the edges of a wave -- and a block's last group --
+// need an atomic OR (every group but a block's last is >= 50 bits long).
+constexpr int DT = 256;
+
+struct BitOutW {
+    uint32_t* w;
+    uint32_t word0, word;
+    uint64_t acc;
+    int nb;
+    bool in_first;
+    uint32_t fw;
+    __device__ __forceinline__ void init(uint32_t* out, uint64_t pos)
+    {
+        w = out;
+        word0 = word = (uint32_t)(pos >> 5);
+        nb = (int)(pos & 31);
+        acc = 0;
+        in_first = true;
+        fw = 0;
+    }
+    __device__ __forceinline__ void put(int len, uint32_t code)
+    {
+        acc = (acc << len) | (uint64_t)code;
+        nb += len;
+        if (nb >= 32) {
+            nb -= 32;
+            const uint32_t v = (uint32_t)(acc >> nb);
+            if (in_first) { fw = v; in_first = false; } else { w[word] = __builtin_bswap32(v); }
+            ++word;
+            acc &= nb ? ((1ull << nb) - 1ull) : 0ull;
         }
-        __syncthreads();
-        if (tid == 0) carry += tot;
-        __syncthreads();
+    }
+};
+
+__global__ void __launch_bounds__(DT) k_emit_data(const BlockDesc* __restrict__ blocks,
+                                                  const uint16_t* __restrict__ mtfv_all, uint64_t mtf_stride,
+                                                  const Tables* __restrict__ tabs, const uint8_t* __restrict__ sel_all,
+                                                  const uint32_t* __restrict__ gpre_all, uint32_t* __restrict__ out32)
+{
+    __shared__ uint32_t lc[6][258];
+    const uint32_t b = blockIdx.y;
+    const uint32_t n_sel = blocks[b].n_sel;
+    const uint32_t g = blockIdx.x * DT + threadIdx.x;
+    const int lane = threadIdx.x & 63;
+    if (blockIdx.x * DT >= n_sel) return;                   // uniform
+    const int alpha = (int)blocks[b].n_in_use + 2;
+    const int ng = (int)blocks[b].n_groups;
+    for (int i = threadIdx.x; i < ng * 258; i += DT) {
+        const int t = i / 258, v = i % 258;
+        if (v < alpha) lc[t][v] = ((uint32_t)tabs[b].len[t][v] << 24) | tabs[b].code[t][v];
+    }
+    __syncthreads();
+    const bool active = g < n_sel;
+    BitOutW o;
+    o.init(out32, blocks[b].bit_off + blocks[b].hdr_bits + (active ? gpre_all[(uint64_t)b * kMaxSelectors + g] : 0u));
+    if (active) {
+        const uint32_t n_mtf = blocks[b].n_mtf;
+        const uint16_t* mtfv = mtfv_all + (uint64_t)b * mtf_stride;
+        const uint32_t gs = g * 50;
+        const uint32_t ge = gs + 50 < n_mtf ? gs + 50 : n_mtf;
+        const uint32_t* row = lc[sel_all[(uint64_t)b * (2 * kMaxSelectors) + g]];
+        const uint32_t* m32 = reinterpret_cast<const uint32_t*>(mtfv + gs);   // gs even: 4-B aligned
+        for (uint32_t i = gs; i < ge; i += 2) {
+            const uint32_t w = m32[(i - gs) >> 1];
+            const uint32_t c0 = row[w & 0xffffu];
+            o.put((int)(c0 >> 24), c0 & 0xFFFFFFu);
+            if (i + 1 < ge) {
+                const uint32_t c1 = row[w >> 16];
+                o.put((int)(c1 >> 24), c1 & 0xFFFFFFu);
+            }
+        }
+    }
+    // tail: the partial last word (bits of this group only); a group that never
+    // completed its first word has only this tail
+    const bool has_tail = active && o.nb > 0;
+    const uint32_t tail = has_tail ? (uint32_t)(o.acc << (32 - o.nb)) : 0u;
+    const uint32_t p_word = (uint32_t)__shfl_up((int)o.word, 1, 64);
+    const uint32_t p_tail = (uint32_t)__shfl_up((int)tail, 1, 64);
+    const bool p_has = __shfl_up((int)has_tail, 1, 64) != 0 && lane > 0;
+    const bool next_takes = lane < 63 && g + 1 < n_sel;   // the next lane completes my tail word
+    if (!active) return;
+    const uint32_t from_prev = (p_has && p_word == o.word0) ? p_tail : 0u;
+    const bool prev_done = lane > 0;                      // the previous group is in this wave
+    if (!o.in_first) {
+        const uint32_t f = o.fw | from_prev;
+        if (prev_done) out32[o.word0] = __builtin_bswap32(f);
+        else atomicOr(&out32[o.word0], __builtin_bswap32(f));
+        if (has_tail && !next_takes) atomicOr(&out32[o.word], __builtin_bswap32(tail));
+    } else if (has_tail) {                                // whole group inside its first word
+        atomicOr(&out32[o.word], __builtin_bswap32(tail | from_prev));
     }
 }
 
@@ -204,7 +284,12 @@ void launch_emit_blocks(const BlockDesc* blocks, uint32_t nb, const uint16_t* mt
                         hipStream_t st)
 {
     if (!nb) return;
-    hipLaunchKernelGGL(k_emit_block, dim3(nb), dim3(ET), 0, st, blocks, mtfv, mtf_stride, tabs, sel, gbits, out32);
+    // gbits holds 2 x nb x kMaxSelectors words: sizes, then their per-block prefix
+    uint32_t* gpre = const_cast<uint32_t*>(gbits) + (uint64_t)nb * kMaxSelectors;
+    hipLaunchKernelGGL(k_emit_block, dim3(nb), dim3(ET), 0, st, blocks, mtfv, mtf_stride, tabs, sel, gbits, gpre,
+                       out32);
+    hipLaunchKernelGGL(k_emit_data, dim3((kMaxSelectors + DT - 1) / DT, nb), dim3(DT), 0, st, blocks, mtfv,
+                       mtf_stride, tabs, sel, gpre, out32);
     HIP_CHECK(hipGetLastError());
 }
 

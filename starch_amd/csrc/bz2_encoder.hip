@@ -154,7 +154,7 @@ void Encoder::plan(const uint8_t* d_text, const std::vector<StreamIn>& streams, 
     uint16_t* d_mtfv = b_mtfv.as<uint16_t>((uint64_t)nb * mtf_stride);
     Tables* d_tabs = b_tabs.as<Tables>(nb);
     uint8_t* d_sel = b_sel.as<uint8_t>((uint64_t)nb * 2 * kMaxSelectors);
-    uint32_t* d_gbits = b_gbits.as<uint32_t>((uint64_t)nb * kMaxSelectors);
+    uint32_t* d_gbits = b_gbits.as<uint32_t>(2ull * nb * kMaxSelectors);   // group sizes, then prefixes (emit)
     HIP_CHECK(hipMemGetInfo(&free_b, &total_b));
     const uint64_t per_slot = blk_stride_ * 41ull;       // 40 B of sort scratch + 1 B last column
     uint64_t max_batch = std::max<uint64_t>(1, (uint64_t)(free_b * 0.45) / per_slot);
