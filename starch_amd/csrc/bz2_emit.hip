@@ -152,30 +152,30 @@ __global__ void __launch_bounds__(ET) k_emit_block(const BlockDesc* __restrict__
     }
 }
 
-// Coded data: one 50-symbol group per lane, over (block, 256-group tile);
-// code lengths and codes packed (len << 24 | code) in LDS, one read per symbol.
-// A lane keeps the first (possibly shared) word of its bit range in a register
-// and plain-stores the words fully inside; the word it shares with the
-// previous lane is completed with that lane's tail bits (a shuffle) and
-// plain-stored, so only the edges of a wave -- and a block's last group --
-// need an atomic OR (every group but a block's last is >= 50 bits long).
+// Coded data: one 50-symbol group per lane, over (block, 256-group tile).
+// The tile's MTF values are staged in LDS with coalesced loads; each lane
+// codes its group (lengths and codes packed len << 24 | code, one LDS read
+// per symbol) into an LDS image of the tile's output words (LDS atomic ORs:
+// neighbouring groups share words), and the image is stored with coalesced
+// writes -- plain stores inside, global atomic ORs for the two edge words
+// shared with the neighbouring tiles / the block header.  A tile whose output
+// does not fit the image writes straight to global memory (BitOut).
 constexpr int DT = 256;
+constexpr uint32_t EI_WORDS = DT * 50 / 2;       // staged MTF values (u16 pairs)
+constexpr uint32_t EO_WORDS = 2048;              // staged output words
 
-struct BitOutW {
-    uint32_t* w;
-    uint32_t word0, word;
+struct BitOutL {                                 // MSB-first bits into LDS words [w0, ...)
+    uint32_t* ob;
+    uint32_t w0, word;
     uint64_t acc;
     int nb;
-    bool in_first;
-    uint32_t fw;
-    __device__ __forceinline__ void init(uint32_t* out, uint64_t pos)
+    __device__ __forceinline__ void init(uint32_t* o, uint32_t wbase, uint64_t pos)
     {
-        w = out;
-        word0 = word = (uint32_t)(pos >> 5);
+        ob = o;
+        w0 = wbase;
+        word = (uint32_t)(pos >> 5);
         nb = (int)(pos & 31);
         acc = 0;
-        in_first = true;
-        fw = 0;
     }
     __device__ __forceinline__ void put(int len, uint32_t code)
     {
@@ -183,70 +183,86 @@ struct BitOutW {
         nb += len;
         if (nb >= 32) {
             nb -= 32;
-            const uint32_t v = (uint32_t)(acc >> nb);
-            if (in_first) { fw = v; in_first = false; } else { w[word] = __builtin_bswap32(v); }
+            atomicOr(&ob[word - w0], (uint32_t)(acc >> nb));
             ++word;
             acc &= nb ? ((1ull << nb) - 1ull) : 0ull;
         }
+    }
+    __device__ __forceinline__ void finish()
+    {
+        if (nb > 0) atomicOr(&ob[word - w0], (uint32_t)(acc << (32 - nb)));
     }
 };
 
 __global__ void __launch_bounds__(DT) k_emit_data(const BlockDesc* __restrict__ blocks,
                                                   const uint16_t* __restrict__ mtfv_all, uint64_t mtf_stride,
                                                   const Tables* __restrict__ tabs, const uint8_t* __restrict__ sel_all,
+                                                  const uint32_t* __restrict__ gbits_all,
                                                   const uint32_t* __restrict__ gpre_all, uint32_t* __restrict__ out32)
 {
     __shared__ uint32_t lc[6][258];
+    __shared__ uint32_t mv[EI_WORDS];
+    __shared__ uint32_t ob[EO_WORDS];
     const uint32_t b = blockIdx.y;
     const uint32_t n_sel = blocks[b].n_sel;
-    const uint32_t g = blockIdx.x * DT + threadIdx.x;
-    const int lane = threadIdx.x & 63;
-    if (blockIdx.x * DT >= n_sel) return;                   // uniform
+    const uint32_t g0 = blockIdx.x * DT;
+    if (g0 >= n_sel) return;                                // uniform
+    const int tid = threadIdx.x;
+    const uint32_t gcnt = n_sel - g0 < (uint32_t)DT ? n_sel - g0 : (uint32_t)DT;
     const int alpha = (int)blocks[b].n_in_use + 2;
     const int ng = (int)blocks[b].n_groups;
-    for (int i = threadIdx.x; i < ng * 258; i += DT) {
+    for (int i = tid; i < ng * 258; i += DT) {
         const int t = i / 258, v = i % 258;
         if (v < alpha) lc[t][v] = ((uint32_t)tabs[b].len[t][v] << 24) | tabs[b].code[t][v];
     }
+    const uint32_t n_mtf = blocks[b].n_mtf;
+    const uint32_t s0 = g0 * 50;
+    const uint32_t s1 = (g0 + gcnt) * 50 < n_mtf ? (g0 + gcnt) * 50 : n_mtf;
+    const uint32_t nwi = (s1 - s0 + 1) / 2;
+    const uint32_t* src = reinterpret_cast<const uint32_t*>(mtfv_all + (uint64_t)b * mtf_stride + s0);
+    for (uint32_t i = tid; i < nwi; i += DT) mv[i] = src[i];
+    const uint32_t* gpre = gpre_all + (uint64_t)b * kMaxSelectors;
+    const uint64_t base = blocks[b].bit_off + blocks[b].hdr_bits;
+    const uint64_t tb0 = base + gpre[g0];
+    const uint64_t tb1 = base + gpre[g0 + gcnt - 1] + gbits_all[(uint64_t)b * kMaxSelectors + g0 + gcnt - 1];
+    const uint32_t w0 = (uint32_t)(tb0 >> 5), nwo = (uint32_t)((tb1 + 31) >> 5) - w0;
+    const bool staged = nwo <= EO_WORDS;                    // uniform
+    if (staged) for (uint32_t i = tid; i < nwo; i += DT) ob[i] = 0;
     __syncthreads();
-    const bool active = g < n_sel;
-    BitOutW o;
-    o.init(out32, blocks[b].bit_off + blocks[b].hdr_bits + (active ? gpre_all[(uint64_t)b * kMaxSelectors + g] : 0u));
-    if (active) {
-        const uint32_t n_mtf = blocks[b].n_mtf;
-        const uint16_t* mtfv = mtfv_all + (uint64_t)b * mtf_stride;
+    if ((uint32_t)tid < gcnt) {
+        const uint32_t g = g0 + tid;
         const uint32_t gs = g * 50;
         const uint32_t ge = gs + 50 < n_mtf ? gs + 50 : n_mtf;
         const uint32_t* row = lc[sel_all[(uint64_t)b * (2 * kMaxSelectors) + g]];
-        const uint32_t* m32 = reinterpret_cast<const uint32_t*>(mtfv + gs);   // gs even: 4-B aligned
-        for (uint32_t i = gs; i < ge; i += 2) {
-            const uint32_t w = m32[(i - gs) >> 1];
-            const uint32_t c0 = row[w & 0xffffu];
-            o.put((int)(c0 >> 24), c0 & 0xFFFFFFu);
-            if (i + 1 < ge) {
-                const uint32_t c1 = row[w >> 16];
-                o.put((int)(c1 >> 24), c1 & 0xFFFFFFu);
+        const uint32_t* m = mv + (gs - s0) / 2;                // gs, s0 even
+        auto code_group = [&](auto& o) {
+            for (uint32_t i = gs; i < ge; i += 2) {
+                const uint32_t w = m[(i - gs) >> 1];
+                const uint32_t c0 = row[w & 0xffffu];
+                o.put((int)(c0 >> 24), c0 & 0xFFFFFFu);
+                if (i + 1 < ge) {
+                    const uint32_t c1 = row[w >> 16];
+                    o.put((int)(c1 >> 24), c1 & 0xFFFFFFu);
+                }
             }
+            o.finish();
+        };
+        if (staged) {
+            BitOutL o;
+            o.init(ob, w0, base + gpre[g]);
+            code_group(o);
+        } else {
+            BitOut o;
+            o.init(out32, base + gpre[g]);
+            code_group(o);
         }
     }
-    // tail: the partial last word (bits of this group only); a group that never
-    // completed its first word has only this tail
-    const bool has_tail = active && o.nb > 0;
-    const uint32_t tail = has_tail ? (uint32_t)(o.acc << (32 - o.nb)) : 0u;
-    const uint32_t p_word = (uint32_t)__shfl_up((int)o.word, 1, 64);
-    const uint32_t p_tail = (uint32_t)__shfl_up((int)tail, 1, 64);
-    const bool p_has = __shfl_up((int)has_tail, 1, 64) != 0 && lane > 0;
-    const bool next_takes = lane < 63 && g + 1 < n_sel;   // the next lane completes my tail word
-    if (!active) return;
-    const uint32_t from_prev = (p_has && p_word == o.word0) ? p_tail : 0u;
-    const bool prev_done = lane > 0;                      // the previous group is in this wave
-    if (!o.in_first) {
-        const uint32_t f = o.fw | from_prev;
-        if (prev_done) out32[o.word0] = __builtin_bswap32(f);
-        else atomicOr(&out32[o.word0], __builtin_bswap32(f));
-        if (has_tail && !next_takes) atomicOr(&out32[o.word], __builtin_bswap32(tail));
-    } else if (has_tail) {                                // whole group inside its first word
-        atomicOr(&out32[o.word], __builtin_bswap32(tail | from_prev));
+    if (!staged) return;
+    __syncthreads();
+    for (uint32_t i = tid; i < nwo; i += DT) {
+        const uint32_t v = __builtin_bswap32(ob[i]);
+        if (i == 0 || i + 1 == nwo) atomicOr(&out32[w0 + i], v);
+        else out32[w0 + i] = v;
     }
 }
 
@@ -289,7 +305,7 @@ void launch_emit_blocks(const BlockDesc* blocks, uint32_t nb, const uint16_t* mt
     hipLaunchKernelGGL(k_emit_block, dim3(nb), dim3(ET), 0, st, blocks, mtfv, mtf_stride, tabs, sel, gbits, gpre,
                        out32);
     hipLaunchKernelGGL(k_emit_data, dim3((kMaxSelectors + DT - 1) / DT, nb), dim3(DT), 0, st, blocks, mtfv,
-                       mtf_stride, tabs, sel, gpre, out32);
+                       mtf_stride, tabs, sel, gbits, gpre, out32);
     HIP_CHECK(hipGetLastError());
 }
 

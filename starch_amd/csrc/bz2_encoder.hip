@@ -130,11 +130,13 @@ void Encoder::plan(const uint8_t* d_text, const std::vector<StreamIn>& streams, 
     uint32_t* d_first = reinterpret_cast<uint32_t*>(b_souts.as<uint64_t>(nstreams_ + 1));
     HIP_CHECK(hipMemcpyAsync(d_first, first.data(), nstreams_ * sizeof(uint32_t), hipMemcpyHostToDevice, st));
     BlockDesc* d_blocks = b_blk.as<BlockDesc>(nb + 1);
-    rle_compact(d_btmp, d_slot0, d_nblk, d_first, nstreams_, d_blocks, st);
+    // tile -> block of its first byte, in the (dead after rle_pos) carry array
+    uint32_t* d_tile_block = d_carry;
+    rle_compact(d_btmp, d_slot0, d_nblk, d_first, nstreams_, d_blocks, d_streams, d_tile0, d_tile_block, st);
     uint8_t* d_blkbytes = b_blkbytes.as<uint8_t>((uint64_t)nb * blk_stride_ + 64);
     if (ntiles) {
-        rle_emit(d_text, d_tiles, ntiles, d_twpre, d_tile0, d_tpos, d_streams, d_first, d_nblk, d_blocks, d_blkbytes,
-                     blk_stride_, st);
+        rle_emit(d_text, d_tiles, ntiles, d_twpre, d_tile0, d_tpos, d_streams, d_first, d_nblk, d_tile_block, d_blocks,
+                 d_blkbytes, blk_stride_, st);
     }
     rle_crc(d_text, d_blocks, nb, b_crc.as<uint32_t>((uint64_t)nb * kCrcMaxChunks), st);
     HIP_CHECK(hipGetLastError());

@@ -118,10 +118,10 @@ void rle_stream_w(const uint64_t* tile0, const uint64_t* wpre, uint32_t ns, uint
 void rle_cut(const StreamIn* streams, const uint64_t* tile0, const uint64_t* wpre, const uint8_t* tpos, uint32_t ns,
              uint32_t nblock_max, const uint64_t* slot0, BlockDesc* tmp, uint32_t* nblk, hipStream_t st);
 void rle_compact(const BlockDesc* tmp, const uint64_t* slot0, const uint32_t* nblk, const uint32_t* first, uint32_t ns,
-                 BlockDesc* out, hipStream_t st);
+                 BlockDesc* out, const StreamIn* streams, const uint64_t* tile0, uint32_t* tile_block, hipStream_t st);
 void rle_emit(const uint8_t* text, const TileDesc* tiles, uint64_t ntiles, const uint64_t* wpre, const uint64_t* tile0,
               const uint8_t* tpos, const StreamIn* streams, const uint32_t* first, const uint32_t* nblk,
-              BlockDesc* blocks, uint8_t* blk, uint64_t stride, hipStream_t st);
+              const uint32_t* tile_block, BlockDesc* blocks, uint8_t* blk, uint64_t stride, hipStream_t st);
 constexpr uint32_t kCrcMaxChunks = 128;       // per block (k_crc_chunks)
 void rle_crc(const uint8_t* text, BlockDesc* blocks, uint32_t nb, uint32_t* creg, hipStream_t st);
 

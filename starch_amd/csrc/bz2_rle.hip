@@ -416,19 +416,42 @@ __global__ void __launch_bounds__(64) k_cut(const StreamIn* __restrict__ streams
     if (lane == 0) nblk[s] = k;
 }
 
+// also maps every tile to the block holding its first byte (tile_block)
 __global__ void k_compact_blocks(const BlockDesc* __restrict__ tmp, const uint64_t* __restrict__ slot0,
                                  const uint32_t* __restrict__ nblk, const uint32_t* __restrict__ first,
-                                 uint32_t nstreams, BlockDesc* __restrict__ out)
+                                 uint32_t nstreams, BlockDesc* __restrict__ out, const StreamIn* __restrict__ streams,
+                                 const uint64_t* __restrict__ seg_tile0, uint32_t* __restrict__ tile_block)
 {
     uint32_t s = blockIdx.x;
     if (s >= nstreams) return;
+    const uint64_t beg = streams[s].text_off, t0 = seg_tile0[s];
     for (uint32_t k = threadIdx.x; k < nblk[s]; k += blockDim.x) {
         BlockDesc b = tmp[slot0[s] + k];
+        const uint64_t ta = (b.in_beg - beg + kTB - 1) / kTB, te = (b.in_end - beg + kTB - 1) / kTB;
+        for (uint64_t t = ta; t < te; ++t) tile_block[t0 + t] = first[s] + k;
         b.bits = 0; b.bit_off = 0; b.crc = 0; b.orig_ptr = 0; b.n_in_use = 0; b.n_mtf = 0; b.flags = 0;
         b.n_groups = 0; b.n_sel = 0;
         for (int j = 0; j < 8; ++j) b.in_use[j] = 0;
         out[first[s] + k] = b;
     }
+}
+
+// cooperative LDS -> global byte copy by the workgroup: head bytes up to a
+// 4-byte aligned destination, 4-byte stores, then the tail (the word stores
+// stay inside [dst, dst + len), so neighbouring tiles never overlap)
+__device__ __forceinline__ void copy_out(uint8_t* dst, const uint8_t* src, uint32_t len)
+{
+    const uint32_t head0 = (uint32_t)((4u - ((uintptr_t)dst & 3u)) & 3u);
+    const uint32_t head = head0 < len ? head0 : len;
+    if (threadIdx.x < head) dst[threadIdx.x] = src[threadIdx.x];
+    const uint32_t nw = (len - head) / 4u;
+    uint32_t* d4 = reinterpret_cast<uint32_t*>(dst + head);
+    for (uint32_t w = threadIdx.x; w < nw; w += blockDim.x) {
+        const uint32_t q = head + 4u * w;
+        d4[w] = (uint32_t)src[q] | ((uint32_t)src[q + 1] << 8) | ((uint32_t)src[q + 2] << 16) |
+                ((uint32_t)src[q + 3] << 24);
+    }
+    for (uint32_t k = head + 4u * nw + threadIdx.x; k < len; k += blockDim.x) dst[k] = src[k];
 }
 
 // materialise RLE1 block bytes (bz:bzlib.c:224-256) + inUse (bz:bzlib.c:232,247)
@@ -437,24 +460,23 @@ __global__ void __launch_bounds__(256) k_rle_emit(const uint8_t* __restrict__ te
                                                    const uint64_t* __restrict__ seg_tile0,
                                                    const uint8_t* __restrict__ tpos, const StreamIn* __restrict__ streams,
                                                    const uint32_t* __restrict__ sfirst, const uint32_t* __restrict__ snblk,
+                                                   const uint32_t* __restrict__ tile_block,
                                                    BlockDesc* __restrict__ blocks, uint8_t* __restrict__ blk,
                                                    uint64_t stride)
 {
     __shared__ uint32_t used[2][8];
     __shared__ uint32_t wsh[5];
-    __shared__ uint32_t bsel;
+    __shared__ uint8_t ob[kTB + kTB / 4 + 16];      // the tile's RLE1 output (<= 5/4 of its bytes)
+    // inUse bits per lane ([slot][word][lane]: no two lanes share a word, so no
+    // serialised LDS atomics on the few words a text's bytes fall in)
+    __shared__ uint32_t ul[2][8][256];
     TileDesc d = tiles[blockIdx.x];
     const uint32_t s = d.stream;
     const uint64_t send = streams[s].text_off + streams[s].text_len;
     if (threadIdx.x < 16) used[threadIdx.x >> 3][threadIdx.x & 7] = 0;
-    if (threadIdx.x == 0) {   // block holding the tile's first byte
-        uint32_t lo = sfirst[s], hi = sfirst[s] + snblk[s];
-        while (hi - lo > 1) {
-            uint32_t mid = (lo + hi) >> 1;
-            if (blocks[mid].in_beg <= d.beg) lo = mid; else hi = mid;
-        }
-        bsel = lo;
-    }
+#pragma unroll
+    for (int q = 0; q < 16; ++q) ul[q >> 3][q & 7][threadIdx.x] = 0;
+    const uint32_t bsel = tile_block[blockIdx.x];   // block holding the tile's first byte
     int off = threadIdx.x * 16;
     int cnt = (int)d.len - off;
     cnt = cnt < 0 ? 0 : (cnt > 16 ? 16 : cnt);
@@ -465,32 +487,46 @@ __global__ void __launch_bounds__(256) k_rle_emit(const uint8_t* __restrict__ te
     uint32_t w = 0;
 #pragma unroll
     for (int k = 0; k < 16; ++k) if (k < cnt) w += rle_w(byte16(tv, k));
-    uint32_t pre = block_excl_scan_add<uint32_t>(w, wsh, (uint32_t*)nullptr);   // contains __syncthreads
+    uint32_t tot = 0;
+    const uint32_t pre = block_excl_scan_add<uint32_t>(w, wsh, &tot);   // contains __syncthreads
     const uint32_t b0 = bsel;
     const uint32_t bl = sfirst[s] + snblk[s];
-    uint64_t W = tile_wpre[blockIdx.x] - tile_wpre[seg_tile0[s]] + pre;
-    uint32_t b = b0;
-    uint64_t bend = blocks[b].in_end, wb = blocks[b].w_beg;
+    // the tile's output is built in LDS at its scan offsets, then copied out
+    // with coalesced stores into at most two blocks (blocks are cut at chunk
+    // starts, so a chunk's bytes never straddle two blocks; a block holds far
+    // more than one tile)
+    const uint64_t Wt = tile_wpre[blockIdx.x] - tile_wpre[seg_tile0[s]];   // stream W of the tile's first byte
+    const uint64_t wb0 = blocks[b0].w_beg;
+    const uint64_t wnext = b0 + 1 < bl ? blocks[b0 + 1].w_beg : ~0ull;
+    uint32_t o = pre;
     for (int k = 0; k < cnt; ++k) {
-        uint64_t i = d.beg + off + k;
-        while (i >= bend && b + 1 < bl) { ++b; bend = blocks[b].in_end; wb = blocks[b].w_beg; }
         const uint32_t t = byte16(tv, k);
         const uint8_t c = (uint8_t)byte16(xv, k);
-        uint8_t* o = blk + (uint64_t)b * stride + (W - wb);
-        int slot = (b == b0) ? 0 : 1;
+        const int slot = (Wt + o >= wnext) ? 1 : 0;
         if (t < 3) {
-            o[0] = c;
-            if (t == 0) atomicOr(&used[slot][c >> 5], 1u << (c & 31));
+            ob[o] = c;
+            if (t == 0) ul[slot][c >> 5][threadIdx.x] |= 1u << (c & 31);
         } else if (t == 3) {
+            const uint64_t i = d.beg + off + k;
             uint64_t j = i + 1;
             while (j < send && tp[j] != 0) ++j;
-            uint32_t L = (uint32_t)(j - i) + 3;
-            uint8_t cnt_byte = (uint8_t)(L - 4);
-            o[0] = c;
-            o[1] = cnt_byte;
-            atomicOr(&used[slot][cnt_byte >> 5], 1u << (cnt_byte & 31));
+            const uint32_t L = (uint32_t)(j - i) + 3;
+            const uint8_t cnt_byte = (uint8_t)(L - 4);
+            ob[o] = c;
+            ob[o + 1] = cnt_byte;
+            ul[slot][cnt_byte >> 5][threadIdx.x] |= 1u << (cnt_byte & 31);
         }
-        W += rle_w(t);
+        o += rle_w(t);
+    }
+    __syncthreads();
+    const uint32_t split = wnext > Wt ? (wnext - Wt < tot ? (uint32_t)(wnext - Wt) : tot) : 0u;
+    copy_out(blk + (uint64_t)b0 * stride + (Wt - wb0), ob, split);
+    if (split < tot) copy_out(blk + (uint64_t)(b0 + 1) * stride, ob + split, tot - split);
+#pragma unroll
+    for (int q = 0; q < 16; ++q) {                  // OR over the wave, one LDS atomic per wave and word
+        const uint32_t v = (uint32_t)__builtin_amdgcn_readlane(
+            (int)wave_incl_scan_or(ul[q >> 3][q & 7][threadIdx.x]), 63);
+        if ((threadIdx.x & 63) == 0 && v) atomicOr(&used[q >> 3][q & 7], v);
     }
     __syncthreads();
     if (threadIdx.x < 16) {
@@ -637,16 +673,17 @@ void rle_cut(const StreamIn* streams, const uint64_t* tile0, const uint64_t* wpr
                        nblk);
 }
 void rle_compact(const BlockDesc* tmp, const uint64_t* slot0, const uint32_t* nblk, const uint32_t* first, uint32_t ns,
-                 BlockDesc* out, hipStream_t st)
+                 BlockDesc* out, const StreamIn* streams, const uint64_t* tile0, uint32_t* tile_block, hipStream_t st)
 {
-    hipLaunchKernelGGL(k_compact_blocks, dim3(ns), dim3(256), 0, st, tmp, slot0, nblk, first, ns, out);
+    hipLaunchKernelGGL(k_compact_blocks, dim3(ns), dim3(256), 0, st, tmp, slot0, nblk, first, ns, out, streams, tile0,
+                       tile_block);
 }
 void rle_emit(const uint8_t* text, const TileDesc* tiles, uint64_t ntiles, const uint64_t* wpre, const uint64_t* tile0,
               const uint8_t* tpos, const StreamIn* streams, const uint32_t* first, const uint32_t* nblk,
-              BlockDesc* blocks, uint8_t* blk, uint64_t stride, hipStream_t st)
+              const uint32_t* tile_block, BlockDesc* blocks, uint8_t* blk, uint64_t stride, hipStream_t st)
 {
     hipLaunchKernelGGL(k_rle_emit, dim3((unsigned)ntiles), dim3(256), 0, st, text, tiles, wpre, tile0, tpos, streams,
-                       first, nblk, blocks, blk, stride);
+                       first, nblk, tile_block, blocks, blk, stride);
 }
 void rle_crc(const uint8_t* text, BlockDesc* blocks, uint32_t nb, uint32_t* creg, hipStream_t st)
 {

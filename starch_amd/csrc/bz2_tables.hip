@@ -21,6 +21,11 @@ struct HuffSmem {
     int32_t weight[6][516];
     int32_t parent[6][516];
 };
+struct HuffSmem32 {                     // alphabets <= 32 (k_tables32)
+    int32_t heap[6][40];
+    int32_t weight[6][72];
+    int32_t parent[6][72];
+};
 
 __device__ void hb_make_lengths(uint8_t* len, const uint32_t* freq, int32_t alpha, int32_t max_len, int32_t* heap,
                                 int32_t* weight, int32_t* parent)
@@ -275,7 +280,9 @@ __global__ void __launch_bounds__(TT) k_tables(BlockDesc* __restrict__ blocks, u
 // wins (bz:compress.c:399-401).  Per-table symbol frequencies go to per-wave
 // LDS copies, one atomic per (group, symbol present).
 // ---------------------------------------------------------------------------
-constexpr int T32 = 1024;
+// 256 threads and small LDS: several blocks per CU, so one block's serial
+// phases (Huffman construction, band setup) overlap other blocks' work
+constexpr int T32 = 256;
 constexpr int NW32 = T32 / 64;
 
 __device__ __forceinline__ uint32_t byte_of(const uint32_t (&h)[8], int v)
@@ -289,7 +296,7 @@ __global__ void __launch_bounds__(T32) k_tables32(BlockDesc* __restrict__ blocks
                                                    uint32_t* __restrict__ gbits_all, uint4* __restrict__ hist_all,
                                                    uint64_t hist_stride)
 {
-    __shared__ HuffSmem hs;
+    __shared__ HuffSmem32 hs;
     __shared__ uint8_t len[6][258];
     __shared__ uint64_t plen[32];
     __shared__ uint32_t rf[NW32][6][32];
@@ -368,7 +375,7 @@ __global__ void __launch_bounds__(T32) k_tables32(BlockDesc* __restrict__ blocks
             rem -= acc;
         }
     }
-    if (tid < 258) tabs[b].freq[tid] = freq[tid];
+    for (int i = tid; i < 258; i += T32) tabs[b].freq[i] = freq[i];
     __syncthreads();
     for (int iter = 0; iter < 4; ++iter) {                         // BZ_N_ITERS
         if (tid < alpha) {
