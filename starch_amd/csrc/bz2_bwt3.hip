@@ -367,6 +367,14 @@ __global__ void __launch_bounds__(256) k3_pss(Ctx c)
     const uint64_t bit0 = (uint64_t)w * 64;
     const uint64_t j0 = bit0 / B, j1 = (bit0 + 63) / B;
     uint64_t word = 0;
+    if (B == 4 && j1 < n) {                      // 16 whole symbols: one aligned 16-B load
+        const uint4 v = *reinterpret_cast<const uint4*>(blk + j0);
+        const uint32_t q[4] = {v.x, v.y, v.z, v.w};
+#pragma unroll
+        for (int k = 0; k < 16; ++k) word = (word << 4) | sym[(q[k >> 2] >> (8 * (k & 3))) & 0xffu];
+        c.scr.K[(uint64_t)slot * c.scr.stride + w] = word;
+        return;
+    }
     for (uint64_t j = j0; j <= j1; ++j) {
         const uint64_t s = sym[blk[j < n ? j : j % n]];
         const int sh = 64 - (int)B - (int)(j * B - bit0);
@@ -396,17 +404,22 @@ __global__ void __launch_bounds__(PT) k3_hist(Ctx c)
     for (int i = threadIdx.x; i < PNB; i += PT) cnt[i] = 0;
     __syncthreads();
     const uint32_t e = n - t0 < (uint32_t)PTILE ? n - t0 : (uint32_t)PTILE;
-    constexpr int HU = 8;                      // digits of HU rotations in flight per thread
-    for (uint32_t k0 = 0; k0 < e; k0 += HU * PT) {
-        uint32_t d[HU];
+    // 16 consecutive rotations per thread and step: their 12-bit digits all
+    // come from four PSS words (funnel shifts), not two loads per rotation
+    for (uint32_t k0 = threadIdx.x * 16u; k0 < e; k0 += PT * 16u) {
+        const uint64_t bit0 = (uint64_t)(t0 + k0) * B;
+        const uint64_t q0 = bit0 >> 6;
+        const uint32_t p0 = (uint32_t)(bit0 & 63u);
+        const uint64_t w[4] = {pss[q0], pss[q0 + 1], pss[q0 + 2], pss[q0 + 3]};
 #pragma unroll
-        for (int u = 0; u < HU; ++u) {
-            const uint32_t k = k0 + u * PT + threadIdx.x;
-            d[u] = k < e ? (uint32_t)pss_bits(pss, (uint64_t)(t0 + k) * B, PDIG) : 0xFFFFFFFFu;
+        for (int k = 0; k < 16; ++k) {
+            const uint32_t bit = p0 + (uint32_t)k * B;      // < 64 + 15 * 8
+            const uint32_t ix = bit >> 6, p = bit & 63u;
+            const uint64_t a = ix == 0 ? w[0] : ix == 1 ? w[1] : w[2];
+            const uint64_t nx = ix == 0 ? w[1] : ix == 1 ? w[2] : w[3];
+            const uint64_t v = (a << p) | ((nx >> 1) >> (63u - p));
+            if (k0 + k < e) atomicAdd(&cnt[(uint32_t)(v >> (64 - PDIG))], 1u);
         }
-#pragma unroll
-        for (int u = 0; u < HU; ++u)
-            if (d[u] != 0xFFFFFFFFu) atomicAdd(&cnt[d[u]], 1u);
     }
     __syncthreads();
     uint32_t* th = tile_hist(c, slot) + (uint64_t)tile * PNB;
