@@ -500,24 +500,34 @@ __global__ void __launch_bounds__(SCT) k3_scatter(Ctx c)
         const uint64_t* pss = c.scr.K + so;
         uint32_t* SA = c.scr.SA + so;
         const uint32_t e = n - t0 < (uint32_t)PTILE ? n - t0 : (uint32_t)PTILE;
-        // SU rotations per thread per step: digits (PSS loads), then the LDS
-        // cursor atomics, then the stores, so each phase has SU in flight
-        constexpr int SU = 8;
-        for (uint32_t q0 = 0; q0 < e; q0 += SU * SCT) {
+        // SU consecutive rotations per thread and step: digits from four PSS
+        // words (funnel shifts), then the LDS cursor atomics, then the stores,
+        // so each phase has SU in flight
+        constexpr int SU = 16;
+        for (uint32_t q0 = tid * SU; q0 < e; q0 += SU * SCT) {
             uint32_t d[SU], p[SU];
+            {
+                const uint64_t bit0 = (uint64_t)(t0 + q0) * B;
+                const uint64_t qw = bit0 >> 6;
+                const uint32_t p0 = (uint32_t)(bit0 & 63u);
+                const uint64_t w[4] = {pss[qw], pss[qw + 1], pss[qw + 2], pss[qw + 3]};
 #pragma unroll
-            for (int u = 0; u < SU; ++u) {
-                const uint32_t q = q0 + u * SCT + tid;
-                d[u] = q < e ? (uint32_t)pss_bits(pss, (uint64_t)(t0 + q) * B, PDIG) : 0u;
+                for (int u = 0; u < SU; ++u) {
+                    const uint32_t bit = p0 + (uint32_t)u * B;  // < 64 + 15 * 8
+                    const uint32_t ix = bit >> 6, pb = bit & 63u;
+                    const uint64_t a = ix == 0 ? w[0] : ix == 1 ? w[1] : w[2];
+                    const uint64_t nx = ix == 0 ? w[1] : ix == 1 ? w[2] : w[3];
+                    d[u] = (uint32_t)(((a << pb) | ((nx >> 1) >> (63u - pb))) >> (64 - PDIG));
+                }
             }
 #pragma unroll
             for (int u = 0; u < SU; ++u) {
-                const uint32_t q = q0 + u * SCT + tid;
+                const uint32_t q = q0 + u;
                 p[u] = q < e ? atomicAdd(&cur[d[u]], 1u) : 0u;
             }
 #pragma unroll
             for (int u = 0; u < SU; ++u) {
-                const uint32_t q = q0 + u * SCT + tid;
+                const uint32_t q = q0 + u;
                 if (q < e) {
                     const uint32_t r = t0 + q;
                     SA[p[u]] = r;

@@ -506,17 +506,16 @@ __device__ __forceinline__ uint32_t next_bit(uint64_t lo, uint64_t hi, uint32_t 
 __device__ __forceinline__ bool dig_fast(const uint8_t* tb, uint32_t b, uint32_t n, int64_t& v)
 {
     if (n - 1u >= 18u) return false;
-    uint32_t x0 = 0, x1 = 0, p = 1, bad = 0;
-#pragma unroll
-    for (uint32_t k = 0; k < 18; ++k) {
+    // trip count = the wave's longest field (coordinates: <= 9 digits), not 18
+    uint64_t acc = 0;
+    uint32_t bad = 0;
+#pragma unroll 3
+    for (uint32_t k = 0; k < n; ++k) {
         const uint32_t d = (uint32_t)tb[b + k] - 48u;
-        if (k < n) {
-            bad |= (d > 9u) ? 1u : 0u;
-            if (k < 9) x0 = x0 * 10u + d;
-            else { x1 = x1 * 10u + d; p *= 10u; }
-        }
+        bad |= (d > 9u) ? 1u : 0u;
+        acc = acc * 10u + d;
     }
-    v = (int64_t)((uint64_t)x0 * p + x1);
+    v = (int64_t)acc;
     return bad == 0;
 }
 
