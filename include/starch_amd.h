@@ -64,6 +64,7 @@ typedef struct {
     uint64_t input_bytes, n_lines, n_segments, text_bytes, archive_bytes;
     uint64_t n_blocks, rle_bytes, bwt_rounds, periodic_blocks;
     uint64_t bwt_tied;       /* rotations re-sorted by prefix-doubling rounds (ties of the packed key) */
+    uint64_t dedup_blocks;   /* blocks that reused a byte-identical block's sort/MTF/tables */
     float ms_transform, ms_rle, ms_bwt, ms_mtf, ms_tables, ms_emit, ms_total;
 } starch_stats;
 

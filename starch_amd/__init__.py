@@ -50,7 +50,7 @@ class Options(ctypes.Structure):
 class Stats(ctypes.Structure):
     _fields_ = [(n, ctypes.c_uint64) for n in ("input_bytes", "n_lines", "n_segments", "text_bytes",
                                                "archive_bytes", "n_blocks", "rle_bytes", "bwt_rounds",
-                                               "periodic_blocks", "bwt_tied")] + \
+                                               "periodic_blocks", "bwt_tied", "dedup_blocks")] + \
                [(n, ctypes.c_float) for n in ("ms_transform", "ms_rle", "ms_bwt", "ms_mtf", "ms_tables",
                                               "ms_emit", "ms_total")]
 

@@ -48,6 +48,7 @@ struct StreamOut {
 struct Stats {                 // per-stage device timings (ms) from HIP events
     float rle = 0, bwt = 0, mtf = 0, tables = 0, emit = 0;
     uint64_t n_blocks = 0, rle_bytes = 0, bwt_rounds = 0, periodic_blocks = 0, bwt_tied = 0;
+    uint64_t dedup_blocks = 0;     // blocks that reused a byte-identical block's results
 };
 
 class Encoder {
@@ -69,7 +70,7 @@ public:
 private:
     DevBuf b_streams, b_tiles, b_tile_sum, b_tile_carry, b_tile_w, b_tile_wpre, b_tpos, b_seg_tile0, b_seg_nblk,
         b_blk_tmp, b_blk, b_blkbytes, b_scal, b_tmp, b_bwt, b_mtfv, b_freq, b_sel, b_tabs, b_gbits, b_souts,
-        b_fallback, b_bwt3, b_crc;
+        b_fallback, b_bwt3, b_crc, b_dedupe, b_rep_bytes, b_rep_blk;
     struct PinnedCtr {
         uint32_t* p = nullptr;
         uint32_t* get();
@@ -79,6 +80,8 @@ private:
     int bs100k_ = 9;
     uint32_t nblocks_ = 0, nstreams_ = 0, ngroups_ = 0;
     uint64_t blk_stride_ = 0;
+    uint64_t gpre_off_ = 0;                 // words: the per-block prefix rows in b_gbits
+    const uint32_t* src_of_dev_ = nullptr;  // block -> data index (null: identity)
     std::vector<StreamIn> streams_;
     std::vector<BlockDesc> host_blocks_;
 };

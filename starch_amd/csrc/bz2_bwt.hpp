@@ -32,9 +32,17 @@ void launch_mtf(BlockDesc* blocks, uint32_t b0, uint32_t nb, const uint8_t* blkb
                 const BwtScratch& scr, uint16_t* mtfv, uint64_t mtf_stride, Tables* tabs, hipStream_t st);
 void launch_tables(BlockDesc* blocks, uint32_t b0, uint32_t nb, const uint16_t* mtfv, uint64_t mtf_stride,
                    Tables* tabs, uint8_t* sel, uint32_t* gbits, const BwtScratch& scr, hipStream_t st);
+// src_of (nullable): block b's MTF values / tables / selectors / group sizes
+// live at data index src_of[b] (exact block reuse, bz2_dedupe.hip); gpre has
+// one kMaxSelectors row per block.
 void launch_emit_blocks(const BlockDesc* blocks, uint32_t nb, const uint16_t* mtfv, uint64_t mtf_stride,
-                        const Tables* tabs, const uint8_t* sel, const uint32_t* gbits, uint32_t* out32,
-                        hipStream_t st);
+                        const Tables* tabs, const uint8_t* sel, const uint32_t* gbits, uint32_t* gpre,
+                        const uint32_t* src_of, uint32_t* out32, hipStream_t st);
+// exact block reuse (bz2_dedupe.hip)
+void launch_block_equal(const uint8_t* blkbytes, uint64_t stride, const uint32_t* pairs, uint32_t npairs,
+                        const BlockDesc* blocks, uint32_t* mismatch, hipStream_t st);
+void launch_gather_blocks(const uint8_t* src, uint64_t stride, const uint32_t* idx, uint32_t n, uint8_t* dst,
+                          hipStream_t st);
 void launch_stream_frame(const StreamOut* souts, const BlockDesc* blocks, uint32_t nstreams, int bs100k,
                          uint64_t out_base, uint32_t* out32, hipStream_t st);
 

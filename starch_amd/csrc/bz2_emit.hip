@@ -61,24 +61,24 @@ __global__ void __launch_bounds__(ET) k_emit_block(const BlockDesc* __restrict__
                                                     const uint16_t* __restrict__ mtfv_all, uint64_t mtf_stride,
                                                     const Tables* __restrict__ tabs, const uint8_t* __restrict__ sel_all,
                                                     const uint32_t* __restrict__ gbits_all, uint32_t* __restrict__ gpre_all,
-                                                    uint32_t* __restrict__ out32)
+                                                    const uint32_t* __restrict__ src_of, uint32_t* __restrict__ out32)
 {
     __shared__ uint8_t len[6][258];
     __shared__ uint32_t code[6][258];
     __shared__ uint32_t scan_sh[ET / 64 + 1];
     const int tid = threadIdx.x;
     const uint32_t b = blockIdx.x;
+    const uint32_t d = src_of ? src_of[b] : b;          // data index (bz2_dedupe.hip)
     const BlockDesc bd = blocks[b];
     const int alpha = (int)bd.n_in_use + 2;
     const int ng = (int)bd.n_groups;
     for (int i = tid; i < 6 * 258; i += ET) {
         int t = i / 258, v = i % 258;
-        if (t < ng && v < alpha) { len[t][v] = tabs[b].len[t][v]; code[t][v] = tabs[b].code[t][v]; }
+        if (t < ng && v < alpha) { len[t][v] = tabs[d].len[t][v]; code[t][v] = tabs[d].code[t][v]; }
     }
-    const uint16_t* mtfv = mtfv_all + (uint64_t)b * mtf_stride;
-    const uint8_t* sel = sel_all + (uint64_t)b * (2 * kMaxSelectors);
+    const uint8_t* sel = sel_all + (uint64_t)d * (2 * kMaxSelectors);
     const uint8_t* selmtf = sel + kMaxSelectors;
-    const uint32_t* gbits = gbits_all + (uint64_t)b * kMaxSelectors;
+    const uint32_t* gbits = gbits_all + (uint64_t)d * kMaxSelectors;
 
     uint32_t used16 = 0;
     for (int i = 0; i < 16; ++i) {
@@ -198,13 +198,15 @@ __global__ void __launch_bounds__(DT) k_emit_data(const BlockDesc* __restrict__ 
                                                   const uint16_t* __restrict__ mtfv_all, uint64_t mtf_stride,
                                                   const Tables* __restrict__ tabs, const uint8_t* __restrict__ sel_all,
                                                   const uint32_t* __restrict__ gbits_all,
-                                                  const uint32_t* __restrict__ gpre_all, uint32_t* __restrict__ out32)
+                                                  const uint32_t* __restrict__ gpre_all,
+                                                  const uint32_t* __restrict__ src_of, uint32_t* __restrict__ out32)
 {
     __shared__ uint32_t lc[6][258];
     __shared__ uint32_t mv[EI_WORDS];
     __shared__ uint32_t ob[EO_WORDS];
     const uint32_t b = blockIdx.y;
     const uint32_t n_sel = blocks[b].n_sel;
+    const uint32_t d = src_of ? src_of[b] : b;          // data index (bz2_dedupe.hip)
     const uint32_t g0 = blockIdx.x * DT;
     if (g0 >= n_sel) return;                                // uniform
     const int tid = threadIdx.x;
@@ -213,18 +215,18 @@ __global__ void __launch_bounds__(DT) k_emit_data(const BlockDesc* __restrict__ 
     const int ng = (int)blocks[b].n_groups;
     for (int i = tid; i < ng * 258; i += DT) {
         const int t = i / 258, v = i % 258;
-        if (v < alpha) lc[t][v] = ((uint32_t)tabs[b].len[t][v] << 24) | tabs[b].code[t][v];
+        if (v < alpha) lc[t][v] = ((uint32_t)tabs[d].len[t][v] << 24) | tabs[d].code[t][v];
     }
     const uint32_t n_mtf = blocks[b].n_mtf;
     const uint32_t s0 = g0 * 50;
     const uint32_t s1 = (g0 + gcnt) * 50 < n_mtf ? (g0 + gcnt) * 50 : n_mtf;
     const uint32_t nwi = (s1 - s0 + 1) / 2;
-    const uint32_t* src = reinterpret_cast<const uint32_t*>(mtfv_all + (uint64_t)b * mtf_stride + s0);
+    const uint32_t* src = reinterpret_cast<const uint32_t*>(mtfv_all + (uint64_t)d * mtf_stride + s0);
     for (uint32_t i = tid; i < nwi; i += DT) mv[i] = src[i];
     const uint32_t* gpre = gpre_all + (uint64_t)b * kMaxSelectors;
     const uint64_t base = blocks[b].bit_off + blocks[b].hdr_bits;
     const uint64_t tb0 = base + gpre[g0];
-    const uint64_t tb1 = base + gpre[g0 + gcnt - 1] + gbits_all[(uint64_t)b * kMaxSelectors + g0 + gcnt - 1];
+    const uint64_t tb1 = base + gpre[g0 + gcnt - 1] + gbits_all[(uint64_t)d * kMaxSelectors + g0 + gcnt - 1];
     const uint32_t w0 = (uint32_t)(tb0 >> 5), nwo = (uint32_t)((tb1 + 31) >> 5) - w0;
     const bool staged = nwo <= EO_WORDS;                    // uniform
     if (staged) for (uint32_t i = tid; i < nwo; i += DT) ob[i] = 0;
@@ -233,7 +235,7 @@ __global__ void __launch_bounds__(DT) k_emit_data(const BlockDesc* __restrict__ 
         const uint32_t g = g0 + tid;
         const uint32_t gs = g * 50;
         const uint32_t ge = gs + 50 < n_mtf ? gs + 50 : n_mtf;
-        const uint32_t* row = lc[sel_all[(uint64_t)b * (2 * kMaxSelectors) + g]];
+        const uint32_t* row = lc[sel_all[(uint64_t)d * (2 * kMaxSelectors) + g]];
         const uint32_t* m = mv + (gs - s0) / 2;                // gs, s0 even
         auto code_group = [&](auto& o) {
             for (uint32_t i = gs; i < ge; i += 2) {
@@ -296,16 +298,14 @@ __global__ void k_stream_frame(const StreamOut* __restrict__ souts, const BlockD
 }
 
 void launch_emit_blocks(const BlockDesc* blocks, uint32_t nb, const uint16_t* mtfv, uint64_t mtf_stride,
-                        const Tables* tabs, const uint8_t* sel, const uint32_t* gbits, uint32_t* out32,
-                        hipStream_t st)
+                        const Tables* tabs, const uint8_t* sel, const uint32_t* gbits, uint32_t* gpre,
+                        const uint32_t* src_of, uint32_t* out32, hipStream_t st)
 {
     if (!nb) return;
-    // gbits holds 2 x nb x kMaxSelectors words: sizes, then their per-block prefix
-    uint32_t* gpre = const_cast<uint32_t*>(gbits) + (uint64_t)nb * kMaxSelectors;
     hipLaunchKernelGGL(k_emit_block, dim3(nb), dim3(ET), 0, st, blocks, mtfv, mtf_stride, tabs, sel, gbits, gpre,
-                       out32);
+                       src_of, out32);
     hipLaunchKernelGGL(k_emit_data, dim3((kMaxSelectors + DT - 1) / DT, nb), dim3(DT), 0, st, blocks, mtfv,
-                       mtf_stride, tabs, sel, gbits, gpre, out32);
+                       mtf_stride, tabs, sel, gbits, gpre, src_of, out32);
     HIP_CHECK(hipGetLastError());
 }
 

@@ -149,18 +149,97 @@ void Encoder::plan(const uint8_t* d_text, const std::vector<StreamIn>& streams, 
         return;
     }
 
-    // ---- per-batch: block sort, MTF, tables ---------------------------------
+    // ---- exact block reuse (bz2_dedupe.hip) ------------------------------------
+    // Group candidate duplicates by (nblock, blockCRC, inUse), confirm each with a
+    // byte compare against its representative, and run the block sort, MTF and
+    // tables once per distinct block.  STARCH_DEDUPE=0 disables it.
+    std::vector<BlockDesc> hb(nb);
+    HIP_CHECK(hipMemcpyAsync(hb.data(), d_blocks, nb * sizeof(BlockDesc), hipMemcpyDeviceToHost, st));
+    HIP_CHECK(hipStreamSynchronize(st));
+    const char* env_d = getenv("STARCH_DEDUPE");
+    const bool dedupe_on = !(env_d && !strcmp(env_d, "0"));
+    // STARCH_DEDUPE_KEY=n groups by nblock only (tests: forces byte-compare rejections)
+    const char* env_k = getenv("STARCH_DEDUPE_KEY");
+    const bool key_n_only = env_k && !strcmp(env_k, "n");
+    std::vector<uint32_t> rep_of(nb);
+    uint32_t ndup = 0;
+    for (uint32_t b = 0; b < nb; ++b) rep_of[b] = b;
+    if (dedupe_on && nb > 1) {
+        std::vector<uint32_t> order(nb);
+        for (uint32_t b = 0; b < nb; ++b) order[b] = b;
+        auto key_less = [&](uint32_t x, uint32_t y) {
+            const BlockDesc &a = hb[x], &c = hb[y];
+            if (a.n != c.n) return a.n < c.n;
+            if (!key_n_only) {
+                if (a.crc != c.crc) return a.crc < c.crc;
+                int m = memcmp(a.in_use, c.in_use, sizeof(a.in_use));
+                if (m) return m < 0;
+            }
+            return x < y;
+        };
+        auto key_eq = [&](uint32_t x, uint32_t y) {
+            const BlockDesc &a = hb[x], &c = hb[y];
+            return a.n == c.n && (key_n_only || (a.crc == c.crc && !memcmp(a.in_use, c.in_use, sizeof(a.in_use))));
+        };
+        std::sort(order.begin(), order.end(), key_less);
+        std::vector<uint32_t> pairs;
+        for (uint32_t i = 1, r = order[0]; i < nb; ++i) {
+            if (key_eq(order[i], r)) { pairs.push_back(order[i]); pairs.push_back(r); }
+            else r = order[i];
+        }
+        const uint32_t npairs = (uint32_t)(pairs.size() / 2);
+        if (npairs) {
+            uint32_t* d_pairs = b_dedupe.as<uint32_t>(3ull * npairs + 2 * nb + 16);
+            uint32_t* d_mis = d_pairs + 2ull * npairs;
+            HIP_CHECK(hipMemcpyAsync(d_pairs, pairs.data(), pairs.size() * sizeof(uint32_t), hipMemcpyHostToDevice,
+                                     st));
+            launch_block_equal(d_blkbytes, blk_stride_, d_pairs, npairs, d_blocks, d_mis, st);
+            std::vector<uint32_t> mis(npairs);
+            HIP_CHECK(hipMemcpyAsync(mis.data(), d_mis, npairs * sizeof(uint32_t), hipMemcpyDeviceToHost, st));
+            HIP_CHECK(hipStreamSynchronize(st));
+            for (uint32_t p = 0; p < npairs; ++p)
+                if (!mis[p]) { rep_of[pairs[2 * p]] = pairs[2 * p + 1]; ++ndup; }
+        }
+    }
+    // data index space: the distinct blocks, in block order
+    const bool reuse = ndup > 0;
+    std::vector<uint32_t> reps, src_of(nb);
+    for (uint32_t b = 0; b < nb; ++b)
+        if (rep_of[b] == b) { src_of[b] = (uint32_t)reps.size(); reps.push_back(b); }
+    for (uint32_t b = 0; b < nb; ++b) src_of[b] = src_of[rep_of[b]];
+    const uint32_t nr = (uint32_t)reps.size();
+    BlockDesc* d_bl = d_blocks;              // blocks the sort / MTF / tables run over
+    const uint8_t* d_bytes = d_blkbytes;
+    src_of_dev_ = nullptr;
+    if (reuse) {
+        uint32_t* d_idx = b_dedupe.as<uint32_t>(2ull * nb + 16);
+        HIP_CHECK(hipMemcpyAsync(d_idx, reps.data(), nr * sizeof(uint32_t), hipMemcpyHostToDevice, st));
+        HIP_CHECK(hipMemcpyAsync(d_idx + nb, src_of.data(), nb * sizeof(uint32_t), hipMemcpyHostToDevice, st));
+        src_of_dev_ = d_idx + nb;
+        uint8_t* d_rbytes = b_rep_bytes.as<uint8_t>((uint64_t)nr * blk_stride_ + 64);
+        launch_gather_blocks(d_blkbytes, blk_stride_, d_idx, nr, d_rbytes, st);
+        std::vector<BlockDesc> hr(nr);
+        for (uint32_t k = 0; k < nr; ++k) hr[k] = hb[reps[k]];
+        d_bl = b_rep_blk.as<BlockDesc>(nr + 1);
+        HIP_CHECK(hipMemcpyAsync(d_bl, hr.data(), nr * sizeof(BlockDesc), hipMemcpyHostToDevice, st));
+        HIP_CHECK(hipStreamSynchronize(st));    // hr leaves scope
+        d_bytes = d_rbytes;
+        if (stats) stats->dedup_blocks += ndup;
+    }
+
+    // ---- per-batch: block sort, MTF, tables (over the distinct blocks) -------
     size_t free_b = 0, total_b = 0;
-    HIP_CHECK(hipMemGetInfo(&free_b, &total_b));
     const uint64_t mtf_stride = blk_stride_ + 16;
-    uint16_t* d_mtfv = b_mtfv.as<uint16_t>((uint64_t)nb * mtf_stride);
-    Tables* d_tabs = b_tabs.as<Tables>(nb);
-    uint8_t* d_sel = b_sel.as<uint8_t>((uint64_t)nb * 2 * kMaxSelectors);
-    uint32_t* d_gbits = b_gbits.as<uint32_t>(2ull * nb * kMaxSelectors);   // group sizes, then prefixes (emit)
+    uint16_t* d_mtfv = b_mtfv.as<uint16_t>((uint64_t)nr * mtf_stride);
+    Tables* d_tabs = b_tabs.as<Tables>(nr);
+    uint8_t* d_sel = b_sel.as<uint8_t>((uint64_t)nr * 2 * kMaxSelectors);
+    // group sizes (one row per distinct block), then their prefixes (one row per block, emit)
+    uint32_t* d_gbits = b_gbits.as<uint32_t>((uint64_t)(nr + nb) * kMaxSelectors);
+    gpre_off_ = (uint64_t)nr * kMaxSelectors;
     HIP_CHECK(hipMemGetInfo(&free_b, &total_b));
     const uint64_t per_slot = blk_stride_ * 41ull;       // 40 B of sort scratch + 1 B last column
     uint64_t max_batch = std::max<uint64_t>(1, (uint64_t)(free_b * 0.45) / per_slot);
-    uint32_t batch = (uint32_t)std::min<uint64_t>({(uint64_t)nb, max_batch, 2048ull});
+    uint32_t batch = (uint32_t)std::min<uint64_t>({(uint64_t)nr, max_batch, 2048ull});
     if (b_bwt.cap < batch * per_slot) {
         // allocate the whole batch scratch once
         b_bwt.get(batch * per_slot + 4096);
@@ -182,48 +261,64 @@ void Encoder::plan(const uint8_t* d_text, const std::vector<StreamIn>& streams, 
     }
     unsigned long long* d_stats = reinterpret_cast<unsigned long long*>(d_scal);
     HIP_CHECK(hipMemsetAsync(d_stats, 0, 4 * sizeof(uint64_t), st));
-    std::vector<BlockDesc> hb(nb);
+    std::vector<BlockDesc> hr(nr);
     uint32_t* d_which = reinterpret_cast<uint32_t*>(b_fallback.as<uint32_t>(batch + 1));
-    for (uint32_t b0 = 0; b0 < nb; b0 += batch) {
-        uint32_t cnt = std::min(batch, nb - b0);
+    for (uint32_t b0 = 0; b0 < nr; b0 += batch) {
+        uint32_t cnt = std::min(batch, nr - b0);
         {
             EvTimer tb(st, stats ? &stats->bwt : nullptr);
             // STARCH_BWT=lsd selects the one-workgroup-per-block prefix-doubling sort of
             // bz2_bwt.hip (kept as an independent implementation for cross-checks)
             static const bool lsd = [] { const char* e = getenv("STARCH_BWT"); return e && !strcmp(e, "lsd"); }();
-            if (lsd) launch_bwt(d_blocks, b0, cnt, d_blkbytes, blk_stride_, scr, d_stats, st);
-            else launch_bwt3(d_blocks, b0, cnt, d_blkbytes, blk_stride_, scr, b_bwt3, h_ctr_.get(), d_stats, st);
-            HIP_CHECK(hipMemcpyAsync(hb.data() + b0, d_blocks + b0, cnt * sizeof(BlockDesc), hipMemcpyDeviceToHost,
+            if (lsd) launch_bwt(d_bl, b0, cnt, d_bytes, blk_stride_, scr, d_stats, st);
+            else launch_bwt3(d_bl, b0, cnt, d_bytes, blk_stride_, scr, b_bwt3, h_ctr_.get(), d_stats, st);
+            HIP_CHECK(hipMemcpyAsync(hr.data() + b0, d_bl + b0, cnt * sizeof(BlockDesc), hipMemcpyDeviceToHost,
                                      st));
             HIP_CHECK(hipStreamSynchronize(st));
             std::vector<uint32_t> which;
             for (uint32_t k = 0; k < cnt; ++k)
-                if (hb[b0 + k].flags & 1u) which.push_back(k);
+                if (hr[b0 + k].flags & 1u) which.push_back(k);
             if (!which.empty()) {
                 HIP_CHECK(hipMemcpyAsync(d_which, which.data(), which.size() * sizeof(uint32_t),
                                          hipMemcpyHostToDevice, st));
-                launch_fallback(d_blocks, b0, d_which, (uint32_t)which.size(), d_blkbytes, blk_stride_, scr, st);
+                launch_fallback(d_bl, b0, d_which, (uint32_t)which.size(), d_bytes, blk_stride_, scr, st);
                 if (stats) stats->periodic_blocks += which.size();
             }
             // the v3 sort writes the last column next to SA; the v1 sort and the
             // fallback (periodic blocks) leave it to the gather kernel
-            if (lsd) launch_last_col(d_blocks, b0, nullptr, cnt, d_blkbytes, blk_stride_, scr, st);
+            if (lsd) launch_last_col(d_bl, b0, nullptr, cnt, d_bytes, blk_stride_, scr, st);
             else if (!which.empty())
-                launch_last_col(d_blocks, b0, d_which, (uint32_t)which.size(), d_blkbytes, blk_stride_, scr, st);
+                launch_last_col(d_bl, b0, d_which, (uint32_t)which.size(), d_bytes, blk_stride_, scr, st);
         }
         {
             EvTimer tm(st, stats ? &stats->mtf : nullptr);
-            launch_mtf(d_blocks, b0, cnt, d_blkbytes, blk_stride_, scr, d_mtfv, mtf_stride, d_tabs, st);
+            launch_mtf(d_bl, b0, cnt, d_bytes, blk_stride_, scr, d_mtfv, mtf_stride, d_tabs, st);
         }
         {
             EvTimer tt(st, stats ? &stats->tables : nullptr);
-            launch_tables(d_blocks, b0, cnt, d_mtfv, mtf_stride, d_tabs, d_sel, d_gbits, scr, st);
+            launch_tables(d_bl, b0, cnt, d_mtfv, mtf_stride, d_tabs, d_sel, d_gbits, scr, st);
         }
     }
-    HIP_CHECK(hipMemcpyAsync(hb.data(), d_blocks, nb * sizeof(BlockDesc), hipMemcpyDeviceToHost, st));
+    HIP_CHECK(hipMemcpyAsync(hr.data(), d_bl, nr * sizeof(BlockDesc), hipMemcpyDeviceToHost, st));
     uint64_t hstats[4] = {0, 0, 0, 0};
     HIP_CHECK(hipMemcpyAsync(hstats, d_stats, sizeof(hstats), hipMemcpyDeviceToHost, st));
     HIP_CHECK(hipStreamSynchronize(st));
+    // every block takes the sort / MTF / table results of its data block; its
+    // position fields (text range, stream, RLE offset) stay its own
+    if (!reuse) hb.swap(hr);
+    else {
+        for (uint32_t b = 0; b < nb; ++b) {
+            BlockDesc o = hr[src_of[b]];
+            o.in_beg = hb[b].in_beg;
+            o.in_end = hb[b].in_end;
+            o.w_beg = hb[b].w_beg;
+            o.bit_off = hb[b].bit_off;
+            o.stream = hb[b].stream;
+            hb[b] = o;
+        }
+        HIP_CHECK(hipMemcpyAsync(d_blocks, hb.data(), nb * sizeof(BlockDesc), hipMemcpyHostToDevice, st));
+        HIP_CHECK(hipStreamSynchronize(st));
+    }
     if (stats) {
         stats->bwt_rounds += hstats[0];
         stats->bwt_tied += hstats[2];
@@ -269,9 +364,10 @@ void Encoder::emit(uint8_t* d_out, uint64_t out_cap, uint64_t out_base, std::vec
     HIP_CHECK(hipMemcpyAsync(d_souts, outs.data(), ngroups_ * sizeof(StreamOut), hipMemcpyHostToDevice, st));
     uint32_t* out32 = reinterpret_cast<uint32_t*>(d_out);
     const uint64_t mtf_stride = blk_stride_ + 16;
+    uint32_t* gbits = static_cast<uint32_t*>(b_gbits.p);
     launch_emit_blocks(d_blocks, nblocks_, static_cast<uint16_t*>(b_mtfv.p), mtf_stride,
-                       static_cast<Tables*>(b_tabs.p), static_cast<uint8_t*>(b_sel.p),
-                       static_cast<uint32_t*>(b_gbits.p), out32, st);
+                       static_cast<Tables*>(b_tabs.p), static_cast<uint8_t*>(b_sel.p), gbits, gbits + gpre_off_,
+                       src_of_dev_, out32, st);
     launch_stream_frame(d_souts, d_blocks, ngroups_, bs100k_, out_base, out32, st);
     for (uint32_t s = 0; s < ngroups_; ++s) {
         uint32_t comb = 0;

@@ -215,6 +215,7 @@ void encode_device(starch_ctx* c, const uint8_t* d_bed, uint64_t n, const starch
     c->stats.bwt_rounds = bst.bwt_rounds;
     c->stats.periodic_blocks = bst.periodic_blocks;
     c->stats.bwt_tied = bst.bwt_tied;
+    c->stats.dedup_blocks = bst.dedup_blocks;
     c->stats.ms_transform = ms_t;
     c->stats.ms_rle = bst.rle;
     c->stats.ms_bwt = bst.bwt;
