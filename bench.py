@@ -32,6 +32,16 @@ TOTAL_LINES = 100_000_000      # cfg2
 SEED = 20261015
 
 
+WORKLOADS = {
+    0: ("cfg2: 100M-interval synthetic hg38 24-chrom BED3, bzip2 -9",
+        "synthetic (seeded hg38 BED3 generator, libstarch_amd starch_gen_bed)"),
+    1: ("cfg4: 50M-row ENCODE-style narrowPeak BED6+4, bzip2 -9",
+        "synthetic (seeded hg38 narrowPeak generator, libstarch_amd starch_gen_bed)"),
+    2: ("cfg5: 3.09G-line single-base per-position hg38 BED (73.6 GB), bzip2 -9",
+        "synthetic (every position of the 24 hg38 chromosomes, libstarch_amd starch_gen_bed)"),
+}
+
+
 def lpt(sizes, n):
     """Longest-processing-time assignment of items to n bins."""
     bins = [[] for _ in range(n)]
@@ -69,14 +79,19 @@ def _chrom_prefixes(data, names, k):
     return out
 
 
-def cpu_baseline(bed_host, names, sample_lines, threads):
+def _perpos_prefixes(names, k):
+    """First k lines of every chromosome of the per-position input (cfg5): the
+    generator writes line p of a chromosome as "<chr>\t<p>\t<p+1>\n"."""
+    return [b"".join(b"%s\t%d\t%d\n" % (nm.encode(), p, p + 1) for p in range(k)) for nm in names]
+
+
+def cpu_baseline(pieces, threads, workload):
     """Reference bzip2 (-9, workFactor 30) + the C transform restatement on a
-    bounded sample of the same input: the first `sample_lines` lines of each
-    chromosome, one chromosome per thread (ctypes releases the GIL)."""
+    bounded sample of the same input: the first lines of each chromosome
+    (`pieces`), one chromosome per thread (ctypes releases the GIL)."""
     from tests import oracle_lib
     ref = oracle_lib.ref()
     kind = "reference" if ref is not None else "port"
-    pieces = _chrom_prefixes(bed_host, names, sample_lines)
     sample_bytes = sum(len(p) for p in pieces)
     todo = list(pieces)
     lock = threading.Lock()
@@ -103,9 +118,9 @@ def cpu_baseline(bed_host, names, sample_lines, threads):
     dt = time.perf_counter() - t0
     return {"value": round(sample_bytes / dt / 1e6, 2), "unit": "MB/s", "cores": threads, "kind": kind,
             "seconds": round(dt, 2),
-            "sample": "first %d lines of each of the %d chromosomes of the same cfg2 input (%.1f MB); transform = "
+            "sample": "first %d lines of each of the %d chromosomes of the same %s input (%.1f MB); transform = "
                       "C restatement (oracle/starch_oracle.c), bzip2 -9 = %s; one chromosome per thread"
-                      % (sample_lines, len(pieces), sample_bytes / 1e6,
+                      % (pieces[0].count(b"\n") if pieces else 0, len(pieces), workload, sample_bytes / 1e6,
                          "the reference's vendored libbz2 1.0.6 (oracle/_ref/libbz2ref.so)" if ref is not None
                          else "oracle restatement")}
 
@@ -116,7 +131,8 @@ def main():
     ap.add_argument("--steps", type=int, default=3)
     ap.add_argument("--warmup", type=int, default=1)
     ap.add_argument("--lines", type=int, default=TOTAL_LINES)
-    ap.add_argument("--kind", type=int, default=0, help="0 BED3 (cfg2), 1 narrowPeak (cfg4)")
+    ap.add_argument("--kind", type=int, default=0,
+                    help="0 BED3 (cfg2), 1 narrowPeak (cfg4), 2 per-position 3.09 G lines (cfg5; --lines ignored)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--cpu-sample-lines", type=int, default=1_000_000)
     ap.add_argument("--cpu-threads", type=int, default=16)
@@ -137,10 +153,7 @@ def main():
     else:
         torch.cuda.set_device(0)
 
-    sizes = [L for L in (248956422, 133797422, 135086622, 133275309, 114364328, 107043718, 101991189, 90338345,
-                         83257441, 80373285, 58617616, 242193529, 64444167, 46709983, 50818468, 198295559,
-                         190214555, 181538259, 170805979, 159345973, 145138636, 138394717, 156040895, 57227415)]
-    shards = lpt(sizes, world)
+    shards = lpt(starch_amd.HG38_LEN, world)
     mine = shards[rank]
 
     t_gen = time.perf_counter()
@@ -148,7 +161,7 @@ def main():
     C = (ctypes.c_int32 * len(mine))(*mine)
     nb = ctypes.c_uint64()
     L.starch_gen_bed(args.kind, SEED, args.lines, C, len(mine), None, 0, ctypes.byref(nb))
-    host = torch.empty(nb.value + 64, dtype=torch.uint8).pin_memory()
+    host = torch.empty(nb.value + 64, dtype=torch.uint8, pin_memory=True)
     L.starch_gen_bed(args.kind, SEED, args.lines, C, len(mine), ctypes.c_void_p(host.data_ptr()), nb.value,
                      ctypes.byref(nb))
     my_bytes = nb.value
@@ -258,26 +271,34 @@ def main():
     st = stats_acc[-1]
     bwt_ms = sum(s["ms_bwt"] for s in stats_acc) / len(stats_acc)
     # algorithmic bytes of the block sort: SURVEY §8(d) BWT work figure,
-    # sum over blocks of (1 + doubling rounds) x n x 16 B (key + index, read + write)
-    rle = st["rle_bytes"]
-    rounds = st["bwt_rounds"]
+    # sum over SORTED blocks of (1 + doubling rounds) x n x 16 B (key + index,
+    # read + write).  Blocks that reuse a byte-identical block's result
+    # (dedup_blocks) are not sorted; their share of rle_bytes is taken as
+    # proportional to their count.
     nblk = max(1, st["n_blocks"])
-    bwt_bytes = 16.0 * rle * (1.0 + rounds / nblk)
+    sorted_blk = max(1, nblk - st["dedup_blocks"])
+    rle_sorted = st["rle_bytes"] * sorted_blk / nblk
+    bwt_bytes = 16.0 * rle_sorted * (1.0 + st["bwt_rounds"] / sorted_blk)
     achieved = bwt_bytes / (bwt_ms / 1e3) / 1e9 if bwt_ms > 0 else 0.0
     pipe_bytes = st["input_bytes"] + 2 * st["text_bytes"] + st["archive_bytes"]
     pipe_achieved = pipe_bytes / (st["ms_total"] / 1e3) / 1e9 if st["ms_total"] > 0 else 0.0
     traffic = None
     pmc = os.path.join(ROOT, "profiles", "pmc_k_bwt.json")
-    if os.path.exists(pmc):
+    # the committed PMC pass was taken on the default workload (cfg2, one GPU)
+    if os.path.exists(pmc) and args.kind == 0 and args.lines == TOTAL_LINES and world == 1:
         try:
             traffic = json.load(open(pmc)).get("hbm_bytes_per_launch")
         except Exception:
             traffic = None
 
     cpu = None
+    names = [starch_amd.HG38[c] for c in mine]
     if not args.no_cpu_baseline and world == 1:
-        cpu = cpu_baseline(host[:my_bytes].numpy().tobytes(), [starch_amd.HG38[c] for c in mine],
-                           args.cpu_sample_lines, args.cpu_threads)
+        if args.kind == 2:
+            pieces = _perpos_prefixes(names, args.cpu_sample_lines)
+        else:
+            pieces = _chrom_prefixes(host[:my_bytes].numpy().tobytes(), names, args.cpu_sample_lines)
+        cpu = cpu_baseline(pieces, args.cpu_threads, WORKLOADS[args.kind][0].split(":")[0])
 
     verify = None
     if args.verify and world == 1:
@@ -285,17 +306,29 @@ def main():
         from tests import oracle_lib
         arch = ctx.archive()
         idx, streams = starch_amd.parse_archive(arch)
-        data = host[:my_bytes].numpy().tobytes()
         verify = {}
-        for nm in ("chr21", "chr22"):
-            k = [m["chromosome"] for m in idx["streams"]].index(nm)
-            piece = _chrom_prefixes(data, [nm], 1 << 40)[0]
-            _, segs = oracle_lib.transform(piece)
-            ref = oracle_lib.ref_bz2(segs[0][2], 9) if oracle_lib.ref() else oracle_lib.bz2(segs[0][2], 9)
-            verify[nm] = (streams[k] == ref)
+        if args.kind == 2:
+            # per-position text of a chromosome of L positions is "p1\n" + "0\n" * L;
+            # check by decompression (libbz2 -9 on 100 MB of it takes minutes)
+            import bz2 as pybz2
+            for nm in ("chr21", "chrY"):
+                k = [m["chromosome"] for m in idx["streams"]].index(nm)
+                L = starch_amd.HG38_LEN[starch_amd.HG38.index(nm)]
+                verify[nm] = pybz2.decompress(streams[k]) == b"p1\n" + b"0\n" * L
+        else:
+            data = host[:my_bytes].numpy().tobytes()
+            for nm in ("chr21", "chr22"):
+                k = [m["chromosome"] for m in idx["streams"]].index(nm)
+                piece = _chrom_prefixes(data, [nm], 1 << 40)[0]
+                _, segs = oracle_lib.transform(piece)
+                ref = oracle_lib.ref_bz2(segs[0][2], 9) if oracle_lib.ref() else oracle_lib.bz2(segs[0][2], 9)
+                verify[nm] = (streams[k] == ref)
 
+    workload, data_desc = WORKLOADS[args.kind]
+    if args.kind != 2 and args.lines != TOTAL_LINES:
+        workload = "kind=%d lines=%d" % (args.kind, args.lines)
     line = {
-        "metric": "input BED MB/s (cfg2, bzip2 -9, archive bit-identical to CPU starch3 path)",
+        "metric": "input BED MB/s (%s, bzip2 -9, archive bit-identical to CPU starch3 path)" % workload.split(":")[0],
         "value": round(value, 2),
         "unit": "MB/s",
         "n_gpus": world,
@@ -306,16 +339,17 @@ def main():
         "scaling": "strong",
         "vs_baseline": None,
         "dtype": "u8",
-        "data": "synthetic (seeded hg38 BED3 generator, libstarch_amd starch_gen_bed)",
-        "config": {"workload": "cfg2: 100M-interval synthetic hg38 24-chrom BED3, bzip2 -9" if args.kind == 0 and
-                   args.lines == TOTAL_LINES else "kind=%d lines=%d" % (args.kind, args.lines),
-                   "input_bytes": total_bytes, "lines": args.lines, "parallelism": "chromosome-shard x%d" % world,
+        "data": data_desc,
+        "config": {"workload": workload,
+                   "input_bytes": total_bytes, "lines": st["n_lines"] if world == 1 else args.lines,
+                   "parallelism": "chromosome-shard x%d" % world,
                    "blocks": st["n_blocks"], "text_bytes": st["text_bytes"], "archive_bytes": st["archive_bytes"]},
         "roofline": {"bound": "hbm", "kernel": "k_bwt (block sort)", "achieved": round(achieved, 1),
                      "peak": HBM_PEAK_GBS, "unit": "GB/s", "frac": round(achieved / HBM_PEAK_GBS, 4),
                      "traffic": traffic, "alg_bytes_per_launch": bwt_bytes, "ms_per_launch": round(bwt_ms, 3)},
         "pipeline_roofline": {"alg_bytes": pipe_bytes, "achieved": round(pipe_achieved, 1), "unit": "GB/s",
                               "frac": round(pipe_achieved / HBM_PEAK_GBS, 4)},
+        "bwt": {k: st[k] for k in ("n_blocks", "dedup_blocks", "bwt_rounds", "bwt_tied", "periodic_blocks")},
         "stage_ms": {k: round(st[k], 3) for k in ("ms_transform", "ms_rle", "ms_bwt", "ms_mtf", "ms_tables",
                                                    "ms_emit", "ms_total")},
         "cpu_baseline": cpu,

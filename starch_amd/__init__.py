@@ -15,7 +15,7 @@ import ctypes
 import json
 import os
 
-__all__ = ["Starch", "StarchError", "load", "gen_bed", "build_index", "parse_archive", "MAGIC", "HG38"]
+__all__ = ["Starch", "StarchError", "load", "gen_bed", "build_index", "parse_archive", "MAGIC", "HG38", "HG38_LEN"]
 
 _HERE = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.path.join(_HERE, "_build", "libstarch_amd.so")
@@ -23,6 +23,11 @@ MAGIC = b"\xca\x5c\xad\x1a"          # hpp:907-910
 HG38 = [  # sort-bed order; index = chromosome id used by gen_bed
     "chr1", "chr10", "chr11", "chr12", "chr13", "chr14", "chr15", "chr16", "chr17", "chr18", "chr19",
     "chr2", "chr20", "chr21", "chr22", "chr3", "chr4", "chr5", "chr6", "chr7", "chr8", "chr9", "chrX", "chrY",
+]
+HG38_LEN = [  # hg38 lengths, same order (per-position input has one line per base)
+    248956422, 133797422, 135086622, 133275309, 114364328, 107043718, 101991189, 90338345, 83257441, 80373285,
+    58617616, 242193529, 64444167, 46709983, 50818468, 198295559, 190214555, 181538259, 170805979, 159345973,
+    145138636, 138394717, 156040895, 57227415,
 ]
 
 # compression methods (hpp:23-27)
