@@ -18,7 +18,7 @@ import os
 __all__ = ["Starch", "StarchError", "load", "gen_bed", "build_index", "parse_archive", "MAGIC", "HG38", "HG38_LEN"]
 
 _HERE = os.path.dirname(os.path.abspath(__file__))
-LIB_PATH = os.path.join(_HERE, "_build", "libstarch_amd.so")
+LIB_PATH = os.environ.get("STARCH_AMD_LIB") or os.path.join(_HERE, "_build", "libstarch_amd.so")
 MAGIC = b"\xca\x5c\xad\x1a"          # hpp:907-910
 HG38 = [  # sort-bed order; index = chromosome id used by gen_bed
     "chr1", "chr10", "chr11", "chr12", "chr13", "chr14", "chr15", "chr16", "chr17", "chr18", "chr19",

@@ -851,7 +851,10 @@ __device__ __forceinline__ void gsync()
 
 // register budget (waves per SIMD) of the sort kernels: keeps a few groups
 // resident per CU while their loads are in flight
-constexpr int sort_wpe(int NW, int E) { return NW == 4 && E == 8 ? 3 : 1; }
+#ifndef STARCH_WPE_GRP
+#define STARCH_WPE_GRP 1
+#endif
+constexpr int sort_wpe(int NW, int E) { return NW == 4 && E == 8 ? 3 : (NW == 1 ? STARCH_WPE_GRP : 1); }
 
 template <int NW, int E, bool DBL>
 __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(sort_wpe(NW, E))))
@@ -1269,7 +1272,10 @@ k3_sort_lds(Ctx c, const uint64_t* __restrict__ items,
 // next group's rotations and keys are already being loaded (software
 // pipeline: item two ahead, rotations and keys one ahead).
 // ---------------------------------------------------------------------------
-constexpr uint32_t HARD_Q = 32;
+#ifndef STARCH_HARD_Q
+#define STARCH_HARD_Q 32
+#endif
+constexpr uint32_t HARD_Q = STARCH_HARD_Q;
 
 template <int E>
 struct GrpIn {                 // one group's inputs, as loaded

@@ -59,8 +59,12 @@ inline size_t put_fix5(char* o, uint64_t micro)   // micro / 1e5 with 5 decimals
 uint64_t lines_of(int kind, int c, uint64_t total)
 {
     if (kind == 2) return kHg38[c].len;
-    long double x = (long double)total * (long double)kHg38[c].len / (long double)kGenome;
-    return (uint64_t)(x + 0.5L);
+    // cumulative rounding: the 24 per-chromosome counts sum to exactly `total`
+    uint64_t before = 0;
+    for (int k = 0; k < c; ++k) before += kHg38[k].len;
+    const uint64_t upto = before + kHg38[c].len;
+    const long double t = (long double)total / (long double)kGenome;
+    return (uint64_t)((long double)upto * t + 0.5L) - (uint64_t)((long double)before * t + 0.5L);
 }
 
 // writes chromosome c's lines (dst may be NULL: size only)
