@@ -282,6 +282,9 @@ __global__ void __launch_bounds__(TT) k_tables(BlockDesc* __restrict__ blocks, u
 // ---------------------------------------------------------------------------
 // 256 threads and small LDS: several blocks per CU, so one block's serial
 // phases (Huffman construction, band setup) overlap other blocks' work
+#ifndef STARCH_TABLES_WPE
+#define STARCH_TABLES_WPE 4
+#endif
 constexpr int T32 = 256;
 constexpr int NW32 = T32 / 64;
 
@@ -290,22 +293,33 @@ __device__ __forceinline__ uint32_t byte_of(const uint32_t (&h)[8], int v)
     return (h[v >> 2] >> (8 * (v & 3))) & 0xffu;
 }
 
-__global__ void __launch_bounds__(T32) k_tables32(BlockDesc* __restrict__ blocks, uint32_t b0,
+__global__ void __launch_bounds__(T32) __attribute__((amdgpu_waves_per_eu(STARCH_TABLES_WPE))) k_tables32(BlockDesc* __restrict__ blocks, uint32_t b0,
                                                    const uint16_t* __restrict__ mtfv_all, uint64_t mtf_stride,
                                                    Tables* __restrict__ tabs, uint8_t* __restrict__ sel_all,
                                                    uint32_t* __restrict__ gbits_all, uint4* __restrict__ hist_all,
                                                    uint64_t hist_stride)
 {
-    __shared__ HuffSmem32 hs;
-    __shared__ uint8_t len[6][258];
+    // phase-disjoint scratch shares one LDS region (histograms, then the four
+    // refinement passes, then the selector MTF) and the per-table rows are
+    // alpha <= 32 wide: ~27 KB, so LDS no longer caps residency; registers do
+    // (STARCH_TABLES_WPE blocks per CU; 4 measured best: 5 spills the hoisted
+    // packed lengths, profiles/r01_v24_tables_wpe.json)
+    union Scratch {
+        uint32_t hl[8][T32];
+        struct { HuffSmem32 hs; uint32_t rf[NW32][6][32]; uint32_t rfreq[6][32]; } it;
+        NibState nst[T32];
+    };
+    __shared__ Scratch u;
+    __shared__ uint8_t len[6][32];
     __shared__ uint64_t plen[32];
-    __shared__ uint32_t rf[NW32][6][32];
-    __shared__ uint32_t rfreq[6][258];
     __shared__ uint32_t freq[258];
-    __shared__ uint32_t hl[8][T32];
     __shared__ uint8_t sel_l[kMaxSelectors];
-    __shared__ NibState nst[T32];
     __shared__ unsigned long long hdr_bits, sbits_sh;
+    auto& hl = u.hl;
+    auto& hs = u.it.hs;
+    auto& rf = u.it.rf;
+    auto& rfreq = u.it.rfreq;
+    auto& nst = u.nst;
 
     const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
     const uint32_t b = b0 + blockIdx.x;
@@ -321,7 +335,7 @@ __global__ void __launch_bounds__(T32) k_tables32(BlockDesc* __restrict__ blocks
     const uint32_t nsel = (n_mtf + 49) / 50;
 
     for (int i = tid; i < 258; i += T32) freq[i] = 0;
-    for (int i = tid; i < 6 * 258; i += T32) (&len[0][0])[i] = 15;   // BZ_GREATER_ICOST
+    for (int i = tid; i < 6 * 32; i += T32) (&len[0][0])[i] = 15;   // BZ_GREATER_ICOST
     __syncthreads();
     // ---- per-group histograms (+ mtfFreq) ----
     for (uint32_t g0 = 0; g0 < nsel; g0 += T32) {
