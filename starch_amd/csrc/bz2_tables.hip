@@ -401,7 +401,11 @@ __global__ void __launch_bounds__(T32) __attribute__((amdgpu_waves_per_eu(STARCH
         __syncthreads();
         uint4 n0 = make_uint4(0, 0, 0, 0), n1 = n0;
         if ((uint32_t)tid < nsel) { n0 = hist[2 * tid]; n1 = hist[2 * tid + 1]; }
-        for (uint32_t g = tid; g < nsel; g += T32) {
+        // wave-uniform trip count: every lane runs every round (the rfreq
+        // reduction below needs the whole wave); lanes past nsel carry h = 0
+        for (uint32_t gb = 0; gb < nsel; gb += T32) {
+            const uint32_t g = gb + (uint32_t)tid;
+            const bool valid = g < nsel;
             const uint4 h0 = n0, h1 = n1;
             if (g + T32 < nsel) { n0 = hist[2 * (g + T32)]; n1 = hist[2 * (g + T32) + 1]; }   // prefetch
             const uint32_t h[8] = {h0.x, h0.y, h0.z, h0.w, h1.x, h1.y, h1.z, h1.w};
@@ -416,13 +420,30 @@ __global__ void __launch_bounds__(T32) __attribute__((amdgpu_waves_per_eu(STARCH
                 const uint32_t ct = (uint32_t)(cost >> (10 * t)) & 1023u;
                 if (ct < bc) { bc = ct; bt = t; }
             }
-            sel_l[g] = (uint8_t)bt;
+            if (valid) sel_l[g] = (uint8_t)bt;
+            // rfreq: once per distinct table chosen in this wave, sum the lanes'
+            // byte histograms as u16 pairs (<= 64 x 50 per field) and let one
+            // lane add them to the wave's private rows -- no same-address LDS
+            // atomics (a wave's 64 groups mostly pick one or two tables)
+            uint32_t rem = valid ? (uint32_t)bt : 7u;
+            for (;;) {
+                const uint64_t act = __ballot(rem != 7u);
+                if (!act) break;
+                const uint32_t t = (uint32_t)__builtin_amdgcn_readlane((int)rem, (int)(__ffsll((long long)act) - 1));
+                const bool mine = rem == t;
 #pragma unroll
-            for (int v = 0; v < 32; ++v) {
-                if (v < alpha) {
-                    const uint32_t cnt = byte_of(h, v);
-                    if (cnt) atomicAdd(&rf[wid][bt][v], cnt);
+                for (int q = 0; q < 8; ++q) {
+                    if (4 * q >= alpha) break;
+                    const uint32_t x = mine ? h[q] : 0u;
+                    const uint32_t ev = wave_reduce_add(x & 0x00ff00ffu), od = wave_reduce_add((x >> 8) & 0x00ff00ffu);
+                    if (lane == 0) {
+                        rf[wid][t][4 * q] += ev & 0xffffu;
+                        rf[wid][t][4 * q + 1] += od & 0xffffu;
+                        rf[wid][t][4 * q + 2] += ev >> 16;
+                        rf[wid][t][4 * q + 3] += od >> 16;
+                    }
                 }
+                if (mine) rem = 7u;
             }
         }
         __syncthreads();
