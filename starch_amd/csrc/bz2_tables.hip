@@ -273,12 +273,10 @@ __global__ void __launch_bounds__(TT) k_tables(BlockDesc* __restrict__ blocks, u
 // ---------------------------------------------------------------------------
 // k_tables32: the same computation for alphabets <= 32 (every BED transform).
 // Each 50-symbol group's histogram (32 u8 counts) is built once and kept in
-// HBM; a group's cost against all six tables is then sum_v count_v * plen[v]
-// where plen packs the six code lengths in 10-bit fields of a u64 (a group
-// costs at most 50 * 17 = 850 per table, so fields never carry) -- the packed
-// cost trick of bz:compress.c:379-398 widened to six tables; the first minimum
-// wins (bz:compress.c:399-401).  Per-table symbol frequencies go to per-wave
-// LDS copies, one atomic per (group, symbol present).
+// HBM; a group's cost against table t is then sum_v count_v * len_t[v], four
+// symbols per v_dot4_u32_u8 (the packed-cost idea of bz:compress.c:379-398
+// applied to byte lanes); the first minimum wins (bz:compress.c:399-401).
+// Per-table symbol frequencies: per-table wave reductions into per-wave rows.
 // ---------------------------------------------------------------------------
 // 256 threads and small LDS: several blocks per CU, so one block's serial
 // phases (Huffman construction, band setup) overlap other blocks' work
@@ -311,7 +309,7 @@ __global__ void __launch_bounds__(T32) __attribute__((amdgpu_waves_per_eu(STARCH
     };
     __shared__ Scratch u;
     __shared__ uint8_t len[6][32];
-    __shared__ uint64_t plen[32];
+    __shared__ uint32_t pl4[6][8];                 // table t's code lengths, 4 symbols per word
     __shared__ uint32_t freq[258];
     __shared__ uint8_t sel_l[kMaxSelectors];
     __shared__ unsigned long long hdr_bits, sbits_sh;
@@ -392,10 +390,12 @@ __global__ void __launch_bounds__(T32) __attribute__((amdgpu_waves_per_eu(STARCH
     for (int i = tid; i < 258; i += T32) tabs[b].freq[i] = freq[i];
     __syncthreads();
     for (int iter = 0; iter < 4; ++iter) {                         // BZ_N_ITERS
-        if (tid < alpha) {
-            uint64_t pl = 0;
-            for (int t = 0; t < 6; ++t) pl |= (uint64_t)len[t][tid] << (10 * t);
-            plen[tid] = pl;
+        if (tid < 48) {
+            const int t = tid >> 3, q = tid & 7;
+            uint32_t w = 0;
+            for (int b = 0; b < 4; ++b)
+                if (4 * q + b < alpha && t < ng) w |= (uint32_t)len[t][4 * q + b] << (8 * b);
+            pl4[t][q] = w;
         }
         for (int i = tid; i < NW32 * 6 * 32; i += T32) (&rf[0][0][0])[i] = 0;
         __syncthreads();
@@ -409,16 +409,20 @@ __global__ void __launch_bounds__(T32) __attribute__((amdgpu_waves_per_eu(STARCH
             const uint4 h0 = n0, h1 = n1;
             if (g + T32 < nsel) { n0 = hist[2 * (g + T32)]; n1 = hist[2 * (g + T32) + 1]; }   // prefetch
             const uint32_t h[8] = {h0.x, h0.y, h0.z, h0.w, h1.x, h1.y, h1.z, h1.w};
-            uint64_t cost = 0;
-#pragma unroll
-            for (int v = 0; v < 32; ++v) {
-                if (v < alpha) cost += (uint64_t)byte_of(h, v) * plen[v];
-            }
+            // cost of the group under table t = sum_v count_v * len_t[v]: byte
+            // counts (<= 50) and lengths (<= 17) packed 4 per word, one
+            // v_dot4_u32_u8 per 4 symbols; first minimum wins (bz:compress.c:399-401)
             int bt = 0;
-            uint32_t bc = (uint32_t)cost & 1023u;
-            for (int t = 1; t < ng; ++t) {
-                const uint32_t ct = (uint32_t)(cost >> (10 * t)) & 1023u;
-                if (ct < bc) { bc = ct; bt = t; }
+            uint32_t bc = ~0u;
+#pragma unroll
+            for (int t = 0; t < 6; ++t) {
+                if (t < ng) {
+                    uint32_t ct = 0;
+#pragma unroll
+                    for (int q = 0; q < 8; ++q)
+                        if (4 * q < alpha) ct = __builtin_amdgcn_udot4(h[q], pl4[t][q], ct, false);
+                    if (ct < bc) { bc = ct; bt = t; }
+                }
             }
             if (valid) sel_l[g] = (uint8_t)bt;
             // rfreq: once per distinct table chosen in this wave, sum the lanes'
