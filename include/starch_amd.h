@@ -58,7 +58,21 @@ typedef struct {
     uint64_t name_len;       /* chromosome name length (starch_segment_name) */
     uint32_t n_blocks;       /* bzip2 blocks in the stream */
     uint32_t combined_crc;   /* bzip2 combined stream CRC */
+    uint64_t unit;           /* input unit the segment came from (archive order = unit order) */
 } starch_segment;
+
+/* A unit: a byte range of the input whose first line starts a chromosome
+ * segment, i.e. its chr token differs from the previous line's (hpp:325-342).
+ * Units are encoded independently and their streams concatenate to the
+ * whole input's.  init_start / init_stop are the sscanf values current before
+ * the unit (a field that fails to parse keeps the previous line's value,
+ * hpp:306-307); 0 for the first unit. */
+typedef struct {
+    uint64_t offset;
+    uint64_t length;
+    int64_t init_start;
+    int64_t init_stop;
+} starch_unit;
 
 typedef struct {
     uint64_t input_bytes, n_lines, n_segments, text_bytes, archive_bytes;
@@ -84,6 +98,34 @@ void starch_options_init(starch_options* opt);
 int starch_encode_device(starch_ctx* ctx, const void* d_bed, uint64_t n, const starch_options* opt);
 /* Same, from host memory (copied to HBM first; the copy is not in ms_total). */
 int starch_encode_host(starch_ctx* ctx, const void* bed, uint64_t n, const starch_options* opt);
+
+/* ---- multi-GPU: per-chromosome units sharded across devices ----
+ * Plan: split host BED bytes (up to the first 0xFF, hpp:181) into at most
+ * max_units units (out must hold max_units entries) by galloping + bisection
+ * over line starts -- the chromosome runs of a sorted BED, never a full scan. */
+int starch_plan_units(const void* bed, uint64_t n, uint64_t max_units, starch_unit* out, uint64_t* nunits);
+/* Longest-processing-time assignment of units to nshards (by byte length). */
+int starch_assign_shards(const starch_unit* units, uint64_t nunits, int nshards, int32_t* shard_of);
+/* One shard: encode units resident in HBM (offsets relative to d_base, in
+ * input order; unit_ids = their global indices, NULL = 0..nunits-1).  The
+ * result is the segments' bzip2 streams back to back (no magic, no index):
+ * starch_streams_device/_copy; starch_segments gives each segment's unit and
+ * stream_offset within the streams. */
+int starch_encode_units_device(starch_ctx* ctx, const void* d_base, const starch_unit* units,
+                               const uint64_t* unit_ids, uint64_t nunits, const starch_options* opt);
+int starch_streams_device(starch_ctx* ctx, const void** d_ptr, uint64_t* n);
+int starch_streams_copy(starch_ctx* ctx, void* dst, uint64_t cap);
+/* Archive order of gathered segments (stable by unit) and their byte offsets
+ * from base; *end = base + total stream bytes (the index offset). */
+int starch_archive_layout(const uint64_t* unit_of, const uint64_t* bytes, uint64_t nseg, uint64_t base,
+                          uint64_t* order, uint64_t* offset, uint64_t* end);
+/* In-process multi-device encode of host bytes over nctx contexts (one host
+ * thread per context; contexts may share a device -- "virtual shards").  The
+ * finished streams are gathered into ctxs[0]'s HBM (hipMemcpyPeerAsync over
+ * xGMI) and the archive is read through ctxs[0] as after starch_encode_host:
+ * byte-identical to the one-context archive. */
+int starch_encode_multi_host(starch_ctx* const* ctxs, int nctx, const void* bed, uint64_t n,
+                             const starch_options* opt);
 
 int starch_archive_size(starch_ctx* ctx, uint64_t* n);
 int starch_archive_device(starch_ctx* ctx, const void** d_ptr);
@@ -118,6 +160,9 @@ int starch_bz2_compress_many_device(starch_ctx* ctx, const void* d_in, const uin
  * size. */
 int starch_gen_bed(int kind, uint64_t seed, uint64_t total_lines, const int32_t* chroms, int nchroms, void* dst,
                    uint64_t cap, uint64_t* len);
+/* Per-chromosome byte counts of starch_gen_bed's output (sizes[k] for chroms[k]). */
+int starch_gen_bed_sizes(int kind, uint64_t seed, uint64_t total_lines, const int32_t* chroms, int nchroms,
+                         uint64_t* sizes);
 
 /* Archive index writer: the JSON index + footer for a set of segments
  * (used by the multi-GPU gather to assemble rank 0's archive). */

@@ -126,16 +126,31 @@ static size_t cstr_len(const uint8_t* p, size_t n)
  * Returns the number of output bytes, or (size_t)-1 when out_cap or seg_cap
  * is too small (the caller retries with larger buffers).
  */
+size_t oracle_transform_init(const uint8_t* in, size_t n,
+                             uint8_t* out, size_t out_cap,
+                             oracle_segment* segs, size_t seg_cap, size_t* nseg_out,
+                             int64_t init_start, int64_t init_stop);
+
 size_t oracle_transform(const uint8_t* in, size_t n,
                         uint8_t* out, size_t out_cap,
                         oracle_segment* segs, size_t seg_cap, size_t* nseg_out)
+{
+    return oracle_transform_init(in, n, out, out_cap, segs, seg_cap, nseg_out, 0, 0);
+}
+
+/* Same, starting from given bed_t.start/stop values: a piece of an input that
+ * begins at a segment boundary, with the sscanf values current before it. */
+size_t oracle_transform_init(const uint8_t* in, size_t n,
+                             uint8_t* out, size_t out_cap,
+                             oracle_segment* segs, size_t seg_cap, size_t* nseg_out,
+                             int64_t init_start, int64_t init_stop)
 {
     /* Framing (hpp:170-191): byte 0xFF reads as EOF (char compared with EOF,
      * hpp:181); a trailing line without '\n' is never transformed. */
     const uint8_t* ff = (const uint8_t*)memchr(in, 0xFF, n);
     size_t lim = ff ? (size_t)(ff - in) : n;
 
-    int64_t start = 0, stop = 0;   /* bed_t.start/stop persist on sscanf failure (hpp:306-307) */
+    int64_t start = init_start, stop = init_stop;   /* bed_t.start/stop persist on sscanf failure (hpp:306-307) */
     int64_t last_cd = 0, last_stop = 0;
     uint64_t line_count = 0;
     size_t o = 0, nseg = 0;

@@ -15,7 +15,8 @@ import ctypes
 import json
 import os
 
-__all__ = ["Starch", "StarchError", "load", "gen_bed", "build_index", "parse_archive", "MAGIC", "HG38", "HG38_LEN"]
+__all__ = ["Starch", "StarchError", "load", "gen_bed", "build_index", "parse_archive", "plan_units", "assign_shards",
+           "archive_layout", "compress_multi", "Unit", "Segment", "MAGIC", "HG38", "HG38_LEN"]
 
 _HERE = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.environ.get("STARCH_AMD_LIB") or os.path.join(_HERE, "_build", "libstarch_amd.so")
@@ -44,7 +45,14 @@ class Segment(ctypes.Structure):
     _fields_ = [("line_count", ctypes.c_uint64), ("text_bytes", ctypes.c_uint64),
                 ("stream_offset", ctypes.c_uint64), ("stream_bytes", ctypes.c_uint64),
                 ("name_len", ctypes.c_uint64), ("n_blocks", ctypes.c_uint32),
-                ("combined_crc", ctypes.c_uint32)]
+                ("combined_crc", ctypes.c_uint32), ("unit", ctypes.c_uint64)]
+
+
+class Unit(ctypes.Structure):
+    """starch_unit: an input byte range starting a chromosome segment, with the
+    sscanf values current before it (hpp:306-307, 325-342)."""
+    _fields_ = [("offset", ctypes.c_uint64), ("length", ctypes.c_uint64),
+                ("init_start", ctypes.c_int64), ("init_stop", ctypes.c_int64)]
 
 
 class Options(ctypes.Structure):
@@ -99,6 +107,18 @@ def load():
                            ctypes.c_int),
         "starch_build_index": ([ctypes.POINTER(Segment), ctypes.POINTER(ctypes.c_char_p), pu64, u64, u64,
                                 ctypes.c_char_p, ctypes.c_int, vp, u64, pu64], ctypes.c_int),
+        "starch_gen_bed_sizes": ([ctypes.c_int, u64, u64, ctypes.POINTER(ctypes.c_int32), ctypes.c_int, pu64],
+                                 ctypes.c_int),
+        "starch_plan_units": ([ctypes.c_char_p, u64, u64, ctypes.POINTER(Unit), pu64], ctypes.c_int),
+        "starch_assign_shards": ([ctypes.POINTER(Unit), u64, ctypes.c_int, ctypes.POINTER(ctypes.c_int32)],
+                                 ctypes.c_int),
+        "starch_encode_units_device": ([vp, vp, ctypes.POINTER(Unit), pu64, u64, ctypes.POINTER(Options)],
+                                       ctypes.c_int),
+        "starch_streams_device": ([vp, ctypes.POINTER(vp), pu64], ctypes.c_int),
+        "starch_streams_copy": ([vp, vp, u64], ctypes.c_int),
+        "starch_archive_layout": ([pu64, pu64, u64, u64, pu64, pu64, pu64], ctypes.c_int),
+        "starch_encode_multi_host": ([ctypes.POINTER(vp), ctypes.c_int, ctypes.c_char_p, u64,
+                                      ctypes.POINTER(Options)], ctypes.c_int),
     }
     for name, (args, res) in sig.items():
         f = getattr(L, name)
@@ -186,10 +206,44 @@ class Starch:
         _check(self._L.starch_encode_host(self._h, bed, len(bed), ctypes.byref(o)), self._h)
         return self.archive()
 
+    def compress_host_ptr(self, ptr: int, n: int, emit_index=True):
+        """BED bytes at a host address (e.g. pinned memory) -> archive in HBM."""
+        o = self._opts(emit_index)
+        _check(self._L.starch_encode_host(self._h, ctypes.cast(ctypes.c_void_p(ptr), ctypes.c_char_p), n,
+                                          ctypes.byref(o)), self._h)
+
+    def archive_into(self, ptr: int, cap: int) -> int:
+        """Copy the archive to a host address; returns its size."""
+        n = self.archive_size()
+        _check(self._L.starch_archive_copy(self._h, ctypes.c_void_p(ptr), cap), self._h)
+        return n
+
     def compress_device(self, d_ptr: int, n: int, emit_index=True):
         """BED bytes already in HBM (device pointer) -> archive stays in HBM."""
         o = self._opts(emit_index)
         _check(self._L.starch_encode_device(self._h, ctypes.c_void_p(d_ptr), n, ctypes.byref(o)), self._h)
+
+    def encode_units_device(self, d_base: int, units, unit_ids=None, emit_index=False):
+        """One shard: units resident in HBM (offsets relative to d_base) -> this
+        context's streams (no magic / index); segments() carry each unit id."""
+        o = self._opts(emit_index)
+        k = len(units)
+        U = (Unit * max(1, k))(*units)
+        ids = (ctypes.c_uint64 * max(1, k))(*(unit_ids if unit_ids is not None else range(k)))
+        _check(self._L.starch_encode_units_device(self._h, ctypes.c_void_p(d_base), U, ids, k, ctypes.byref(o)),
+               self._h)
+
+    def streams_device(self):
+        """(device pointer, bytes) of the last starch_encode_units_device result."""
+        p, n = ctypes.c_void_p(), ctypes.c_uint64()
+        _check(self._L.starch_streams_device(self._h, ctypes.byref(p), ctypes.byref(n)), self._h)
+        return p.value or 0, n.value
+
+    def streams(self) -> bytes:
+        n = self.streams_device()[1]
+        buf = ctypes.create_string_buffer(max(1, n))
+        _check(self._L.starch_streams_copy(self._h, buf, n), self._h)
+        return buf.raw[:n]
 
     def archive_size(self):
         n = ctypes.c_uint64()
@@ -275,6 +329,16 @@ def gen_bed(kind, total_lines, chroms=None, seed=20261015, into=None):
     return buf.raw[:n.value]
 
 
+def gen_bed_sizes(kind, total_lines, chroms=None, seed=20261015):
+    """Byte count of each chromosome's lines in gen_bed's output."""
+    L = load()
+    chroms = list(range(24)) if chroms is None else list(chroms)
+    C = (ctypes.c_int32 * max(1, len(chroms)))(*chroms)
+    out = (ctypes.c_uint64 * max(1, len(chroms)))()
+    _check(L.starch_gen_bed_sizes(kind, seed, total_lines, C, len(chroms), out))
+    return list(out[:len(chroms)])
+
+
 def build_index(segs, names, index_offset, note=None, level=9):
     """JSON index + 32-byte footer for already-placed streams (multi-GPU gather)."""
     L = load()
@@ -288,6 +352,50 @@ def build_index(segs, names, index_offset, note=None, level=9):
     buf = ctypes.create_string_buffer(max(1, n.value))
     _check(L.starch_build_index(arr, nm, nl, k, index_offset, note_b, level, buf, n.value, ctypes.byref(n)))
     return buf.raw[:n.value]
+
+
+def plan_units(bed: bytes, max_units: int):
+    """Split host BED bytes into <= max_units units whose boundaries are segment
+    boundaries (starch_plan_units)."""
+    L = load()
+    out = (Unit * max(1, max_units))()
+    n = ctypes.c_uint64()
+    _check(L.starch_plan_units(bed, len(bed), max_units, out, ctypes.byref(n)))
+    return [Unit(u.offset, u.length, u.init_start, u.init_stop) for u in out[:n.value]]
+
+
+def assign_shards(units, nshards):
+    """LPT assignment of units to shards -> list of shard indices."""
+    L = load()
+    k = len(units)
+    U = (Unit * max(1, k))(*units)
+    out = (ctypes.c_int32 * max(1, k))()
+    _check(L.starch_assign_shards(U, k, nshards, out))
+    return list(out[:k])
+
+
+def archive_layout(unit_of, nbytes, base=4):
+    """Archive order (stable by unit) and byte offsets of gathered segments ->
+    (order, offsets, index offset)."""
+    L = load()
+    k = len(unit_of)
+    A = (ctypes.c_uint64 * max(1, k))(*unit_of)
+    B = (ctypes.c_uint64 * max(1, k))(*nbytes)
+    o = (ctypes.c_uint64 * max(1, k))()
+    f = (ctypes.c_uint64 * max(1, k))()
+    end = ctypes.c_uint64()
+    _check(L.starch_archive_layout(A, B, k, base, o, f, ctypes.byref(end)))
+    return list(o[:k]), list(f[:k]), end.value
+
+
+def compress_multi(ctxs, bed: bytes, emit_index=True, reference_compat=False) -> bytes:
+    """In-process multi-device encode (starch_encode_multi_host): shards over
+    the given contexts (they may share a device), archive read from ctxs[0]."""
+    L = load()
+    o = ctxs[0]._opts(emit_index, reference_compat)
+    H = (ctypes.c_void_p * len(ctxs))(*[c._h.value for c in ctxs])
+    _check(L.starch_encode_multi_host(H, len(ctxs), bed, len(bed), ctypes.byref(o)), ctxs[0]._h)
+    return ctxs[0].archive()
 
 
 def parse_archive(blob: bytes):

@@ -12,7 +12,10 @@
 // full block only when the terminating FLUSH/FINISH call supplied input.
 #include <string.h>
 
+#include <condition_variable>
+#include <memory>
 #include <mutex>
+#include <new>
 #include <string>
 #include <vector>
 
@@ -21,7 +24,7 @@
 
 namespace {
 
-enum Mode { M_IDLE = 1, M_RUNNING = 2, M_FLUSHING = 3, M_FINISHING = 4 };
+enum Mode { M_IDLE = 1, M_RUNNING = 2, M_FLUSHING = 3, M_FINISHING = 4, M_FAILED = 5 };
 
 struct GpuStreamState {
     bz_stream* strm;
@@ -35,14 +38,74 @@ struct GpuStreamState {
     bool encoded = false;
 };
 
-struct Device {
-    std::mutex mu;
-    bool ready = false;
+// Encoder slots: each stream borrows one for its BZ_FINISH encode, so
+// streams of different threads encode concurrently (up to kSlots at once per
+// process) on their own HIP streams.  A slot belongs to one device.
+constexpr int kSlots = 4;
+struct Slot {
+    int device = 0;
+    bool busy = false;
     hipStream_t st = nullptr;
     bz::Encoder enc;
     DevBuf in, out;
 };
-Device g_dev;
+struct Pool {
+    std::mutex mu;
+    std::condition_variable cv;
+    std::vector<std::unique_ptr<Slot>> slots;
+};
+Pool g_pool;
+
+int target_device()
+{
+    const char* e = getenv("STARCH_DEVICE");
+    return e ? atoi(e) : 0;
+}
+
+// device guard: the encode runs on the slot's device; the caller thread's
+// current device is restored afterwards
+struct DeviceGuard {
+    int prev = -1;
+    explicit DeviceGuard(int dev)
+    {
+        if (hipGetDevice(&prev) != hipSuccess) prev = -1;
+        HIP_CHECK(hipSetDevice(dev));
+    }
+    ~DeviceGuard() { if (prev >= 0) (void)hipSetDevice(prev); }
+};
+
+Slot* acquire(int dev)
+{
+    std::unique_lock<std::mutex> lk(g_pool.mu);
+    for (;;) {
+        int n = 0;
+        for (auto& s : g_pool.slots) {
+            if (s->device != dev) continue;
+            ++n;
+            if (!s->busy) { s->busy = true; return s.get(); }
+        }
+        if (n < kSlots) {
+            g_pool.slots.emplace_back(new Slot());
+            Slot* s = g_pool.slots.back().get();
+            s->device = dev;
+            s->busy = true;
+            return s;
+        }
+        g_pool.cv.wait(lk);
+    }
+}
+
+void release(Slot* s)
+{
+    {
+        std::lock_guard<std::mutex> lk(g_pool.mu);
+        s->busy = false;
+    }
+    g_pool.cv.notify_all();
+}
+
+void* default_bzalloc(void*, int items, int size) { return malloc((size_t)items * (size_t)size); }   // bz:bzlib.c:151-156
+void default_bzfree(void*, void* addr) { free(addr); }
 
 void add_in(bz_stream* s, uint64_t n)
 {
@@ -81,29 +144,28 @@ void close_piece(GpuStreamState* g, bool supplied)
 
 int encode_on_gpu(GpuStreamState* g)
 {
-    std::lock_guard<std::mutex> lk(g_dev.mu);
+    Slot* sl = nullptr;
     try {
-        if (!g_dev.ready) {
-            int dev = 0;
-            const char* e = getenv("STARCH_DEVICE");
-            if (e) dev = atoi(e);
-            HIP_CHECK(hipSetDevice(dev));
-            HIP_CHECK(hipStreamCreateWithFlags(&g_dev.st, hipStreamNonBlocking));
-            g_dev.ready = true;
-        }
+        const int dev = target_device();
+        DeviceGuard guard(dev);
+        sl = acquire(dev);
+        if (!sl->st) HIP_CHECK(hipStreamCreateWithFlags(&sl->st, hipStreamNonBlocking));
         uint64_t n = g->input.size();
-        uint8_t* d_in = g_dev.in.as<uint8_t>(n + 64);
-        if (n) HIP_CHECK(hipMemcpyAsync(d_in, g->input.data(), n, hipMemcpyHostToDevice, g_dev.st));
+        uint8_t* d_in = sl->in.as<uint8_t>(n + 64);
+        if (n) HIP_CHECK(hipMemcpyAsync(d_in, g->input.data(), n, hipMemcpyHostToDevice, sl->st));
         std::vector<bz::StreamOut> outs;
-        g_dev.enc.plan(d_in, g->pieces, g->bs100k, g_dev.st, outs, nullptr);
+        sl->enc.plan(d_in, g->pieces, g->bs100k, sl->st, outs, nullptr);
         uint64_t bytes = outs.empty() ? 0 : outs[0].bytes;
         uint64_t cap = (bytes + 64 + 255) / 256 * 256;
-        uint8_t* d_out = g_dev.out.as<uint8_t>(cap);
-        g_dev.enc.emit(d_out, cap, 0, outs, g_dev.st, nullptr);
+        uint8_t* d_out = sl->out.as<uint8_t>(cap);
+        sl->enc.emit(d_out, cap, 0, outs, sl->st, nullptr);
         g->output.resize(bytes);
-        if (bytes) HIP_CHECK(hipMemcpyAsync(g->output.data(), d_out, bytes, hipMemcpyDeviceToHost, g_dev.st));
-        HIP_CHECK(hipStreamSynchronize(g_dev.st));
+        if (bytes) HIP_CHECK(hipMemcpyAsync(g->output.data(), d_out, bytes, hipMemcpyDeviceToHost, sl->st));
+        HIP_CHECK(hipStreamSynchronize(sl->st));
+        release(sl);
     } catch (const std::exception&) {
+        if (sl) release(sl);
+        g->output.clear();
         return BZ_CONFIG_ERROR;
     }
     g->input.clear();
@@ -143,8 +205,11 @@ int BZ2_bzCompressInit(bz_stream* strm, int blockSize100k, int verbosity, int wo
     (void)verbosity;
     if (!strm || blockSize100k < 1 || blockSize100k > 9 || workFactor < 0 || workFactor > 250)
         return BZ_PARAM_ERROR;                                            // bz:bzlib.c:159-162
-    GpuStreamState* g = new (std::nothrow) GpuStreamState();
-    if (!g) return BZ_MEM_ERROR;
+    if (!strm->bzalloc) strm->bzalloc = default_bzalloc;                 // bz:bzlib.c:165-166
+    if (!strm->bzfree) strm->bzfree = default_bzfree;
+    void* mem = strm->bzalloc(strm->opaque, (int)sizeof(GpuStreamState), 1);
+    if (!mem) return BZ_MEM_ERROR;
+    GpuStreamState* g = new (mem) GpuStreamState();
     g->strm = strm;
     g->bs100k = blockSize100k;
     g->mode = M_RUNNING;
@@ -179,15 +244,23 @@ int BZ2_bzCompress(bz_stream* strm, int action)
                 bool supplied = strm->avail_in > 0;
                 consume(g);
                 close_piece(g, supplied);
-                g->mode = M_FINISHING;
                 int rc = encode_on_gpu(g);
-                if (rc != BZ_OK) return rc;
+                if (rc != BZ_OK) {   // never report BZ_STREAM_END for a stream that was not encoded
+                    g->mode = M_FAILED;
+                    return rc;
+                }
+                g->mode = M_FINISHING;
                 break;
             }
             return BZ_PARAM_ERROR;
         case M_FINISHING:
             if (action != BZ_FINISH) return BZ_SEQUENCE_ERROR;
             if (strm->avail_in != 0) return BZ_SEQUENCE_ERROR;          // avail_in_expect mismatch
+            break;
+        case M_FAILED:   // the input is still held: a BZ_FINISH retries the encode
+            if (action != BZ_FINISH || strm->avail_in != 0) return BZ_SEQUENCE_ERROR;
+            if (int rc = encode_on_gpu(g)) return rc;
+            g->mode = M_FINISHING;
             break;
         default:
             return BZ_SEQUENCE_ERROR;
@@ -204,7 +277,8 @@ int BZ2_bzCompressEnd(bz_stream* strm)
 {
     GpuStreamState* g = state_of(strm);
     if (!g) return BZ_PARAM_ERROR;
-    delete g;
+    g->~GpuStreamState();
+    strm->bzfree(strm->opaque, g);                                        // bz:bzlib.c:493-497
     strm->state = nullptr;
     return BZ_OK;
 }

@@ -149,3 +149,19 @@ extern "C" int starch_gen_bed(int kind, uint64_t seed, uint64_t total_lines, con
     run(true, &offs);
     return STARCH_OK;
 }
+
+// per-chromosome byte counts of starch_gen_bed's output (sizes[k] for chroms[k])
+extern "C" int starch_gen_bed_sizes(int kind, uint64_t seed, uint64_t total_lines, const int32_t* chroms, int nchroms,
+                                    uint64_t* sizes)
+{
+    if (kind < 0 || kind > 2 || nchroms < 0 || (nchroms && !sizes)) return STARCH_ERR_ARG;
+    for (int k = 0; k < nchroms; ++k) if (chroms[k] < 0 || chroms[k] >= 24) return STARCH_ERR_ARG;
+    unsigned hw = std::max(1u, std::min(16u, std::thread::hardware_concurrency()));
+    std::vector<std::thread> th;
+    for (unsigned t = 0; t < hw; ++t)
+        th.emplace_back([&, t]() {
+            for (int k = (int)t; k < nchroms; k += (int)hw) sizes[k] = gen_chrom(kind, seed, total_lines, chroms[k], nullptr);
+        });
+    for (auto& x : th) x.join();
+    return STARCH_OK;
+}

@@ -3,11 +3,15 @@
 // of the bzip2 streams is produced by the HIP kernels in this directory.
 #include <string.h>
 
+#include <algorithm>
+#include <chrono>
 #include <string>
+#include <thread>
 #include <vector>
 
 #include "../../include/starch_amd.h"
 #include "bz2.hpp"
+#include "shard.hpp"
 #include "transform.hpp"
 
 struct starch_ctx {
@@ -16,12 +20,14 @@ struct starch_ctx {
     hipStream_t st = nullptr;
     TransformWorkspace tf;
     bz::Encoder enc;
-    DevBuf input, archive, raw_in, raw_out;
+    DevBuf input, archive, part, raw_in, raw_out, text_all;
     std::string err;
     // last result
     bool have = false;
     uint64_t archive_bytes = 0;
+    uint64_t part_bytes = 0;          // streams of a shard (starch_encode_units_device)
     uint64_t text_bytes = 0;
+    const uint8_t* text_dev = nullptr;
     std::vector<starch_segment> segs;
     std::vector<std::string> names;
     starch_stats stats{};
@@ -109,8 +115,133 @@ std::string build_index(const starch_segment* segs, const char* const* names, co
 
 uint64_t align_up(uint64_t x, uint64_t a) { return (x + a - 1) / a * a; }
 
-// transform + bzip2 + archive into ctx->archive (device)
-void encode_device(starch_ctx* c, const uint8_t* d_bed, uint64_t n, const starch_options& opt)
+const uint8_t kMagic[4] = {0xca, 0x5c, 0xad, 0x1a};   // hpp:907-910
+
+struct UnitIn {
+    uint64_t off, len;           // byte range relative to the device base pointer
+    int64_t init_start, init_stop;
+    uint64_t id;                 // global unit index (archive order)
+};
+
+// chr token of the last line before `j` and of the line at `j`, read from small
+// device windows; false when a line does not fit the window (the caller then
+// takes the exact per-unit route)
+bool junction_differs(starch_ctx* c, const uint8_t* d_base, uint64_t lo, uint64_t j, uint64_t hi)
+{
+    const uint64_t W = 1024;
+    uint8_t a[W], b[W];
+    const uint64_t a0 = (j - lo > W) ? j - W : lo, an = j - a0;
+    const uint64_t bn = std::min<uint64_t>(W, hi - j);
+    if (an) HIP_CHECK(hipMemcpyAsync(a, d_base + a0, an, hipMemcpyDeviceToHost, c->st));
+    if (bn) HIP_CHECK(hipMemcpyAsync(b, d_base + j, bn, hipMemcpyDeviceToHost, c->st));
+    HIP_CHECK(hipStreamSynchronize(c->st));
+    if (an == 0 || bn == 0) return false;
+    // previous line: [ls, an) in a (a[an-1] is its '\n')
+    uint64_t ls = an - 1;
+    while (ls > 0 && a[ls - 1] != '\n') --ls;
+    if (ls == 0 && a0 > lo) return false;
+    auto tok = [](const uint8_t* x, uint64_t beg, uint64_t n, bool complete, uint64_t* len) {
+        uint64_t p = beg;
+        while (p < n && x[p] != '\t' && x[p] != '\n') ++p;
+        if (p == n && !complete) return false;
+        uint64_t e = (p < n && x[p] == '\n') ? p + 1 : p;
+        const void* z = memchr(x + beg, 0, e - beg);
+        *len = z ? (uint64_t)(static_cast<const uint8_t*>(z) - (x + beg)) : e - beg;
+        return true;
+    };
+    uint64_t la = 0, lb = 0;
+    if (!tok(a, ls, an, true, &la) || !tok(b, 0, bn, j + bn >= hi, &lb)) return false;
+    return la != lb || memcmp(a + ls, b, la) != 0;
+}
+
+// Transform stage over units.  One launch sequence over the whole range when
+// the units are back to back, every junction changes chromosome (so it is a
+// segment start in the concatenation too) and no sscanf value goes stale;
+// otherwise each unit runs on its own with its initial values.  Fills the host
+// segment table (name_off relative to d_base, text_off into the returned text)
+// and the unit of every segment.
+const uint8_t* transform_units(starch_ctx* c, const uint8_t* d_base, const std::vector<UnitIn>& u,
+                               std::vector<SegInfo>& si, std::vector<uint64_t>& unit_of, uint64_t& text_bytes,
+                               uint64_t& n_lines)
+{
+    si.clear();
+    unit_of.clear();
+    text_bytes = n_lines = 0;
+    if (u.empty()) return nullptr;
+    bool joint = true;
+    for (size_t k = 1; k < u.size() && joint; ++k) joint = u[k].off == u[k - 1].off + u[k - 1].len;
+    for (size_t k = 1; k < u.size() && joint; ++k)
+        if (u[k].len && u[k - 1].len) joint = junction_differs(c, d_base, u[k - 1].off, u[k].off, u[k].off + u[k].len);
+    if (joint) {
+        const uint64_t beg = u[0].off, end = u.back().off + u.back().len;
+        TransformResult tr;
+        c->tf.run(d_base + beg, end - beg, c->st, tr, u[0].init_start, u[0].init_stop);
+        if (u.size() > 1 && tr.ff_pos != ~0ull)
+            throw StarchError(STARCH_ERR_ARG, "a unit contains byte 0xFF (plan units with starch_plan_units)");
+        if (u.size() == 1 || !tr.general) {
+            si.resize(tr.n_segments);
+            if (tr.n_segments)
+                HIP_CHECK(hipMemcpyAsync(si.data(), c->tf.seg_info_dev, tr.n_segments * sizeof(SegInfo),
+                                         hipMemcpyDeviceToHost, c->st));
+            HIP_CHECK(hipStreamSynchronize(c->st));
+            unit_of.resize(si.size());
+            size_t k = 0;
+            for (size_t s = 0; s < si.size(); ++s) {
+                si[s].name_off += beg;
+                while (k + 1 < u.size() && si[s].name_off >= u[k + 1].off) ++k;
+                unit_of[s] = u[k].id;
+            }
+            text_bytes = tr.text_bytes;
+            n_lines = tr.n_lines;
+            return c->tf.text;
+        }
+    }
+    // exact per-unit route: each unit with the sscanf values current before it
+    uint8_t* all = static_cast<uint8_t*>(c->text_all.p);   // staging text of all units
+    uint64_t cap = c->text_all.cap;
+    for (size_t k = 0; k < u.size(); ++k) {
+        TransformResult tr;
+        c->tf.run(d_base + u[k].off, u[k].len, c->st, tr, u[k].init_start, u[k].init_stop);
+        if (tr.ff_pos != ~0ull)
+            throw StarchError(STARCH_ERR_ARG, "a unit contains byte 0xFF (plan units with starch_plan_units)");
+        std::vector<SegInfo> part(tr.n_segments);
+        if (tr.n_segments)
+            HIP_CHECK(hipMemcpyAsync(part.data(), c->tf.seg_info_dev, tr.n_segments * sizeof(SegInfo),
+                                     hipMemcpyDeviceToHost, c->st));
+        if (text_bytes + tr.text_bytes + 64 > cap) {   // grow the staging text, keeping what it holds
+            const uint64_t ncap = std::max<uint64_t>(2 * cap, text_bytes + tr.text_bytes + 64);
+            DevBuf nb;
+            uint8_t* np = nb.as<uint8_t>(ncap);
+            if (text_bytes) HIP_CHECK(hipMemcpyAsync(np, all, text_bytes, hipMemcpyDeviceToDevice, c->st));
+            HIP_CHECK(hipStreamSynchronize(c->st));
+            std::swap(c->text_all.p, nb.p);
+            std::swap(c->text_all.cap, nb.cap);
+            all = np;
+            cap = ncap;
+        }
+        if (tr.text_bytes)
+            HIP_CHECK(hipMemcpyAsync(all + text_bytes, c->tf.text, tr.text_bytes, hipMemcpyDeviceToDevice, c->st));
+        HIP_CHECK(hipStreamSynchronize(c->st));
+        for (auto& g : part) {
+            g.name_off += u[k].off;
+            g.text_off += text_bytes;
+            g.first_line += n_lines;
+            si.push_back(g);
+            unit_of.push_back(u[k].id);
+        }
+        text_bytes += tr.text_bytes;
+        n_lines += tr.n_lines;
+    }
+    return all;
+}
+
+enum Layout { L_ARCHIVE, L_STREAMS };
+
+// transform + bzip2 over units.  L_ARCHIVE: magic + streams + index in
+// c->archive (the whole-input result); L_STREAMS: the streams alone, back to
+// back from offset 0 of c->part (one shard of a multi-GPU run).
+void encode_units(starch_ctx* c, const uint8_t* d_base, const std::vector<UnitIn>& units, const starch_options& opt,
+                  Layout lay)
 {
     hipEvent_t e0, e1, e2;
     HIP_CHECK(hipEventCreate(&e0));
@@ -119,45 +250,47 @@ void encode_device(starch_ctx* c, const uint8_t* d_bed, uint64_t n, const starch
     HIP_CHECK(hipEventRecord(e0, c->st));
     c->have = false;
     c->stats = starch_stats{};
-    c->stats.input_bytes = n;
-    TransformResult tr;
-    c->tf.run(d_bed, n, c->st, tr);
+    for (auto& u : units) c->stats.input_bytes += u.len;
+    std::vector<SegInfo> si;
+    std::vector<uint64_t> unit_of;
+    uint64_t tbytes = 0, nlines = 0;
+    const uint8_t* text = transform_units(c, d_base, units, si, unit_of, tbytes, nlines);
     HIP_CHECK(hipEventRecord(e1, c->st));
-    std::vector<SegInfo> si(tr.n_segments);
-    if (tr.n_segments)
-        HIP_CHECK(hipMemcpyAsync(si.data(), c->tf.seg_info_dev, tr.n_segments * sizeof(SegInfo),
-                                 hipMemcpyDeviceToHost, c->st));
-    HIP_CHECK(hipStreamSynchronize(c->st));
-    c->stats.n_lines = tr.n_lines;
-    c->stats.n_segments = tr.n_segments;
-    c->stats.text_bytes = tr.text_bytes;
-    c->text_bytes = tr.text_bytes;
+    const uint64_t nseg = si.size();
+    c->stats.n_lines = nlines;
+    c->stats.n_segments = nseg;
+    c->stats.text_bytes = tbytes;
+    c->text_bytes = tbytes;
+    c->text_dev = text;
     // segment names (small host copies of the chr tokens)
-    c->names.assign(tr.n_segments, std::string());
-    for (uint64_t s = 0; s < tr.n_segments; ++s) {
+    c->names.assign(nseg, std::string());
+    for (uint64_t s = 0; s < nseg; ++s) {
         c->names[s].resize(si[s].name_len);
         if (si[s].name_len)
-            HIP_CHECK(hipMemcpyAsync(&c->names[s][0], d_bed + si[s].name_off, si[s].name_len, hipMemcpyDeviceToHost,
+            HIP_CHECK(hipMemcpyAsync(&c->names[s][0], d_base + si[s].name_off, si[s].name_len, hipMemcpyDeviceToHost,
                                      c->st));
     }
-    c->segs.assign(tr.n_segments, starch_segment{});
-    const uint64_t magic = 4;
-    if (opt.reference_compat) {   // the reference writes only the magic (hpp:765-769)
+    c->segs.assign(nseg, starch_segment{});
+    for (uint64_t s = 0; s < nseg; ++s) {
+        c->segs[s].line_count = si[s].line_count;
+        c->segs[s].text_bytes = si[s].text_len;
+        c->segs[s].name_len = si[s].name_len;
+        c->segs[s].unit = unit_of[s];
+    }
+    const uint64_t base = (lay == L_ARCHIVE) ? 4 : 0;
+    if (opt.reference_compat && lay == L_ARCHIVE) {   // the reference writes only the magic (hpp:765-769)
         uint8_t* out = c->archive.as<uint8_t>(64);
-        static const uint8_t mb[4] = {0xca, 0x5c, 0xad, 0x1a};
-        HIP_CHECK(hipMemcpyAsync(out, mb, 4, hipMemcpyHostToDevice, c->st));
+        HIP_CHECK(hipMemcpyAsync(out, kMagic, 4, hipMemcpyHostToDevice, c->st));
         HIP_CHECK(hipStreamSynchronize(c->st));
         c->archive_bytes = 4;
-        for (uint64_t s = 0; s < tr.n_segments; ++s) {
-            c->segs[s].line_count = si[s].line_count;
-            c->segs[s].text_bytes = si[s].text_len;
-            c->segs[s].name_len = si[s].name_len;
-        }
         c->have = true;
+        (void)hipEventDestroy(e0);
+        (void)hipEventDestroy(e1);
+        (void)hipEventDestroy(e2);
         return;
     }
-    std::vector<bz::StreamIn> sin(tr.n_segments);
-    for (uint64_t s = 0; s < tr.n_segments; ++s) {
+    std::vector<bz::StreamIn> sin(nseg);
+    for (uint64_t s = 0; s < nseg; ++s) {
         sin[s].text_off = si[s].text_off;
         sin[s].text_len = si[s].text_len;
         sin[s].final_run_joins = 1;
@@ -165,37 +298,32 @@ void encode_device(starch_ctx* c, const uint8_t* d_bed, uint64_t n, const starch
     }
     std::vector<bz::StreamOut> outs;
     bz::Stats bst;
-    c->enc.plan(c->tf.text, sin, opt.block_size_100k, c->st, outs, &bst);
+    c->enc.plan(text, sin, opt.block_size_100k, c->st, outs, &bst);
     uint64_t streams_bytes = 0;
     for (auto& o : outs) streams_bytes = std::max(streams_bytes, o.out_off + o.bytes);
-    for (uint64_t s = 0; s < tr.n_segments; ++s) {
-        starch_segment& g = c->segs[s];
-        g.line_count = si[s].line_count;
-        g.text_bytes = si[s].text_len;
-        g.stream_offset = magic + outs[s].out_off;
-        g.stream_bytes = outs[s].bytes;
-        g.name_len = si[s].name_len;
-        g.n_blocks = outs[s].n_blocks;
+    for (uint64_t s = 0; s < nseg; ++s) {
+        c->segs[s].stream_offset = base + outs[s].out_off;
+        c->segs[s].stream_bytes = outs[s].bytes;
+        c->segs[s].n_blocks = outs[s].n_blocks;
     }
-    // combined CRCs are known after emit; compute the index afterwards
-    const uint64_t index_off = magic + streams_bytes;
-    const uint64_t cap = align_up(index_off + 4 + (opt.emit_index ? 256 + 256 * tr.n_segments + 64 : 0) +
-                                      [&] { uint64_t t = 0; for (auto& nm : c->names) t += 6 * nm.size(); return t; }() +
-                                      (opt.note ? 6 * strlen(opt.note) : 0),
+    const uint64_t index_off = base + streams_bytes;
+    uint64_t names_b = 0;
+    for (auto& nm : c->names) names_b += 6 * nm.size();
+    const bool index = lay == L_ARCHIVE && opt.emit_index;
+    const uint64_t cap = align_up(index_off + 4 + (index ? 256 + 256 * nseg + 64 + names_b : 0) +
+                                      (opt.note && index ? 6 * strlen(opt.note) : 0),
                                   256);
-    uint8_t* out = c->archive.as<uint8_t>(cap);
-    static const uint8_t mb[4] = {0xca, 0x5c, 0xad, 0x1a};
-    HIP_CHECK(hipMemcpyAsync(out, mb, 4, hipMemcpyHostToDevice, c->st));
-    c->enc.emit(out, cap, magic, outs, c->st, &bst);
-    for (uint64_t s = 0; s < tr.n_segments; ++s) c->segs[s].combined_crc = outs[s].combined_crc;
+    uint8_t* out = (lay == L_ARCHIVE ? c->archive : c->part).as<uint8_t>(cap);
+    if (lay == L_ARCHIVE) HIP_CHECK(hipMemcpyAsync(out, kMagic, 4, hipMemcpyHostToDevice, c->st));
+    c->enc.emit(out, cap, base, outs, c->st, &bst);
+    for (uint64_t s = 0; s < nseg; ++s) c->segs[s].combined_crc = outs[s].combined_crc;
     uint64_t total = index_off;
     std::string idx;
-    if (opt.emit_index) {
-        std::vector<const char*> np(tr.n_segments);
-        std::vector<uint64_t> nl(tr.n_segments);
-        for (uint64_t s = 0; s < tr.n_segments; ++s) { np[s] = c->names[s].data(); nl[s] = c->names[s].size(); }
-        idx = build_index(c->segs.data(), np.data(), nl.data(), tr.n_segments, index_off, opt.note,
-                          opt.block_size_100k);
+    if (index) {
+        std::vector<const char*> np(nseg);
+        std::vector<uint64_t> nl(nseg);
+        for (uint64_t s = 0; s < nseg; ++s) { np[s] = c->names[s].data(); nl[s] = c->names[s].size(); }
+        idx = build_index(c->segs.data(), np.data(), nl.data(), nseg, index_off, opt.note, opt.block_size_100k);
         if (index_off + idx.size() > cap) throw StarchError(STARCH_ERR_INTERNAL, "index capacity");
         HIP_CHECK(hipMemcpyAsync(out + index_off, idx.data(), idx.size(), hipMemcpyHostToDevice, c->st));
         total += idx.size();
@@ -208,7 +336,8 @@ void encode_device(starch_ctx* c, const uint8_t* d_bed, uint64_t n, const starch
     (void)hipEventDestroy(e0);
     (void)hipEventDestroy(e1);
     (void)hipEventDestroy(e2);
-    c->archive_bytes = total;
+    if (lay == L_ARCHIVE) c->archive_bytes = total;
+    else c->part_bytes = total;
     c->stats.archive_bytes = total;
     c->stats.n_blocks = bst.n_blocks;
     c->stats.rle_bytes = bst.rle_bytes;
@@ -224,6 +353,157 @@ void encode_device(starch_ctx* c, const uint8_t* d_bed, uint64_t n, const starch
     c->stats.ms_emit = bst.emit;
     c->stats.ms_total = ms_all;
     c->have = true;
+}
+
+// transform + bzip2 + archive of a whole input into ctx->archive (device)
+void encode_device(starch_ctx* c, const uint8_t* d_bed, uint64_t n, const starch_options& opt)
+{
+    std::vector<UnitIn> u(1, UnitIn{0, n, 0, 0, 0});
+    encode_units(c, d_bed, u, opt, L_ARCHIVE);
+}
+
+// Multi-device encode of host bytes: plan units, LPT them over the contexts,
+// encode every shard on its own device in its own host thread, then gather
+// the finished streams into ctxs[0]'s HBM (peer copies over xGMI; a plain
+// device copy when two contexts share a device) and write magic + index.
+void encode_multi(starch_ctx* const* ctxs, int nctx, const uint8_t* bed, uint64_t n, const starch_options& opt)
+{
+    using clk = std::chrono::steady_clock;
+    const auto t0 = clk::now();
+    starch_ctx* c0 = ctxs[0];
+    std::vector<shard::Unit> plan;
+    shard::plan_units(bed, n, 64ull * (uint64_t)nctx, plan);
+    std::vector<int32_t> shard_of;
+    shard::assign_lpt(plan, nctx, shard_of);
+    std::vector<std::vector<UnitIn>> mine(nctx);
+    std::vector<uint64_t> dev_bytes(nctx, 0);
+    for (size_t k = 0; k < plan.size(); ++k) {
+        const int s = shard_of[k];
+        mine[s].push_back(UnitIn{dev_bytes[s], plan[k].length, plan[k].init_start, plan[k].init_stop, k});
+        dev_bytes[s] += plan[k].length;
+    }
+    std::vector<std::string> errs(nctx);
+    std::vector<int> codes(nctx, 0);
+    auto work = [&](int s) {
+        starch_ctx* c = ctxs[s];
+        try {
+            Ctx g(c);
+            uint8_t* d = c->input.as<uint8_t>(dev_bytes[s] + 64);
+            for (auto& u : mine[s]) {
+                const uint64_t src = plan[u.id].offset;
+                if (u.len) HIP_CHECK(hipMemcpyAsync(d + u.off, bed + src, u.len, hipMemcpyHostToDevice, c->st));
+            }
+            encode_units(c, d, mine[s], opt, L_STREAMS);
+        } catch (const StarchError& e) {
+            codes[s] = e.code;
+            errs[s] = e.what();
+        } catch (const std::exception& e) {
+            codes[s] = STARCH_ERR_INTERNAL;
+            errs[s] = e.what();
+        }
+    };
+    {
+        std::vector<std::thread> th;
+        for (int s = 1; s < nctx; ++s) th.emplace_back(work, s);
+        work(0);
+        for (auto& t : th) t.join();
+    }
+    for (int s = 0; s < nctx; ++s)
+        if (codes[s]) throw StarchError(codes[s], "shard " + std::to_string(s) + ": " + errs[s]);
+    // gather: archive order = unit order
+    std::vector<uint64_t> unit_of, bytes;
+    std::vector<std::pair<int, uint64_t>> src;   // (shard, segment) of each gathered segment
+    for (int s = 0; s < nctx; ++s)
+        for (uint64_t j = 0; j < ctxs[s]->segs.size(); ++j) {
+            unit_of.push_back(ctxs[s]->segs[j].unit);
+            bytes.push_back(ctxs[s]->segs[j].stream_bytes);
+            src.emplace_back(s, j);
+        }
+    const uint64_t nseg = unit_of.size();
+    std::vector<uint64_t> order, offset;
+    uint64_t end = 4;
+    shard::layout(unit_of.data(), bytes.data(), nseg, 4, order, offset, &end);
+    std::vector<starch_segment> segs(nseg);
+    std::vector<std::string> names(nseg);
+    for (uint64_t k = 0; k < nseg; ++k) {
+        const auto& sj = src[order[k]];
+        segs[k] = ctxs[sj.first]->segs[sj.second];
+        segs[k].stream_offset = offset[order[k]];
+        names[k] = ctxs[sj.first]->names[sj.second];
+    }
+    std::string idx;
+    if (opt.emit_index && !opt.reference_compat) {
+        std::vector<const char*> np(nseg);
+        std::vector<uint64_t> nl(nseg);
+        for (uint64_t s = 0; s < nseg; ++s) { np[s] = names[s].data(); nl[s] = names[s].size(); }
+        idx = build_index(segs.data(), np.data(), nl.data(), nseg, end, opt.note, opt.block_size_100k);
+    }
+    Ctx g(c0);
+    const uint64_t total = opt.reference_compat ? 4 : end + idx.size();
+    uint8_t* out = c0->archive.as<uint8_t>(align_up(total + 64, 256));
+    HIP_CHECK(hipMemcpyAsync(out, kMagic, 4, hipMemcpyHostToDevice, c0->st));
+    if (!opt.reference_compat) {
+        for (int s = 0; s < nctx; ++s) {
+            starch_ctx* c = ctxs[s];
+            if (c->device != c0->device) (void)hipDeviceEnablePeerAccess(c->device, 0);
+            (void)hipGetLastError();   // already enabled / not supported: the copy still works
+        }
+        // one copy per run of segments that are adjacent both in the part and in the archive
+        for (uint64_t k = 0; k < nseg;) {
+            const auto& sj = src[order[k]];
+            starch_ctx* c = ctxs[sj.first];
+            const uint64_t s_off = c->segs[sj.second].stream_offset, d_off = offset[order[k]];
+            uint64_t len = bytes[order[k]], k2 = k + 1;
+            while (k2 < nseg) {
+                const auto& sn = src[order[k2]];
+                if (sn.first != sj.first || c->segs[sn.second].stream_offset != s_off + len ||
+                    offset[order[k2]] != d_off + len)
+                    break;
+                len += bytes[order[k2]];
+                ++k2;
+            }
+            if (len) {
+                if (c->device == c0->device)
+                    HIP_CHECK(hipMemcpyAsync(out + d_off, static_cast<uint8_t*>(c->part.p) + s_off, len,
+                                             hipMemcpyDeviceToDevice, c0->st));
+                else
+                    HIP_CHECK(hipMemcpyPeerAsync(out + d_off, c0->device, static_cast<uint8_t*>(c->part.p) + s_off,
+                                                 c->device, len, c0->st));
+            }
+            k = k2;
+        }
+        if (!idx.empty()) HIP_CHECK(hipMemcpyAsync(out + end, idx.data(), idx.size(), hipMemcpyHostToDevice, c0->st));
+    }
+    HIP_CHECK(hipStreamSynchronize(c0->st));
+    starch_stats st{};
+    st.input_bytes = n;
+    for (int s = 0; s < nctx; ++s) {
+        const starch_stats& x = ctxs[s]->stats;
+        st.n_lines += x.n_lines;
+        st.n_segments += x.n_segments;
+        st.text_bytes += x.text_bytes;
+        st.n_blocks += x.n_blocks;
+        st.rle_bytes += x.rle_bytes;
+        st.bwt_rounds += x.bwt_rounds;
+        st.periodic_blocks += x.periodic_blocks;
+        st.bwt_tied += x.bwt_tied;
+        st.dedup_blocks += x.dedup_blocks;
+        st.ms_transform = std::max(st.ms_transform, x.ms_transform);
+        st.ms_rle = std::max(st.ms_rle, x.ms_rle);
+        st.ms_bwt = std::max(st.ms_bwt, x.ms_bwt);
+        st.ms_mtf = std::max(st.ms_mtf, x.ms_mtf);
+        st.ms_tables = std::max(st.ms_tables, x.ms_tables);
+        st.ms_emit = std::max(st.ms_emit, x.ms_emit);
+    }
+    st.archive_bytes = total;
+    st.ms_total = std::chrono::duration<float, std::milli>(clk::now() - t0).count();
+    c0->segs.swap(segs);
+    c0->names.swap(names);
+    c0->stats = st;
+    c0->text_bytes = 0;
+    c0->text_dev = nullptr;
+    c0->archive_bytes = total;
+    c0->have = true;
 }
 
 }  // namespace
@@ -332,6 +612,118 @@ int starch_encode_host(starch_ctx* c, const void* bed, uint64_t n, const starch_
     END_GUARD(c)
 }
 
+static int units_in(const starch_unit* units, const uint64_t* ids, uint64_t nunits, std::vector<UnitIn>& u)
+{
+    if (nunits && !units) return STARCH_ERR_ARG;
+    u.resize(nunits);
+    for (uint64_t k = 0; k < nunits; ++k)
+        u[k] = UnitIn{units[k].offset, units[k].length, units[k].init_start, units[k].init_stop, ids ? ids[k] : k};
+    for (uint64_t k = 1; k < nunits; ++k)
+        if (u[k].id <= u[k - 1].id) return STARCH_ERR_ARG;   // units in input order
+    return STARCH_OK;
+}
+
+int starch_encode_units_device(starch_ctx* c, const void* d_base, const starch_unit* units, const uint64_t* unit_ids,
+                               uint64_t nunits, const starch_options* opt)
+{
+    GUARD(c)
+    starch_options o;
+    starch_options_init(&o);
+    if (opt) o = *opt;
+    if (o.block_size_100k < 1 || o.block_size_100k > 9 || (nunits && !d_base)) return STARCH_ERR_ARG;
+    std::vector<UnitIn> u;
+    int rc = units_in(units, unit_ids, nunits, u);
+    if (rc) return rc;
+    encode_units(c, static_cast<const uint8_t*>(d_base), u, o, L_STREAMS);
+    return STARCH_OK;
+    END_GUARD(c)
+}
+
+int starch_streams_device(starch_ctx* c, const void** d_ptr, uint64_t* n)
+{
+    if (!c || !d_ptr || !n) return STARCH_ERR_ARG;
+    if (!c->have) return STARCH_ERR_STATE;
+    *d_ptr = c->part.p;
+    *n = c->part_bytes;
+    return STARCH_OK;
+}
+
+int starch_streams_copy(starch_ctx* c, void* dst, uint64_t cap)
+{
+    GUARD(c)
+    if (!c->have) return STARCH_ERR_STATE;
+    if (cap < c->part_bytes || (c->part_bytes && !dst)) return STARCH_ERR_MEM;
+    if (c->part_bytes) HIP_CHECK(hipMemcpyAsync(dst, c->part.p, c->part_bytes, hipMemcpyDeviceToHost, c->st));
+    HIP_CHECK(hipStreamSynchronize(c->st));
+    return STARCH_OK;
+    END_GUARD(c)
+}
+
+int starch_encode_multi_host(starch_ctx* const* ctxs, int nctx, const void* bed, uint64_t n, const starch_options* opt)
+{
+    if (!ctxs || nctx < 1 || (n && !bed)) return STARCH_ERR_ARG;
+    for (int i = 0; i < nctx; ++i) {
+        if (!ctxs[i]) return STARCH_ERR_ARG;
+        for (int j = 0; j < i; ++j)
+            if (ctxs[j] == ctxs[i]) return STARCH_ERR_ARG;   // one context per shard
+    }
+    starch_ctx* c = ctxs[0];
+    GUARD(c)
+    starch_options o;
+    starch_options_init(&o);
+    if (opt) o = *opt;
+    if (o.block_size_100k < 1 || o.block_size_100k > 9) return STARCH_ERR_ARG;
+    if (nctx == 1) {
+        uint8_t* d = c->input.as<uint8_t>(n + 64);
+        if (n) HIP_CHECK(hipMemcpyAsync(d, bed, n, hipMemcpyHostToDevice, c->st));
+        encode_device(c, d, n, o);
+    } else {
+        encode_multi(ctxs, nctx, static_cast<const uint8_t*>(bed), n, o);
+    }
+    return STARCH_OK;
+    END_GUARD(c)
+}
+
+int starch_plan_units(const void* bed, uint64_t n, uint64_t max_units, starch_unit* out, uint64_t* nunits)
+{
+    if (!nunits || !out || max_units < 1 || (n && !bed)) return STARCH_ERR_ARG;
+    try {
+        std::vector<shard::Unit> u;
+        shard::plan_units(static_cast<const uint8_t*>(bed), n, max_units, u);
+        for (size_t k = 0; k < u.size(); ++k)
+            out[k] = starch_unit{u[k].offset, u[k].length, u[k].init_start, u[k].init_stop};
+        *nunits = u.size();
+    } catch (const std::exception&) {
+        return STARCH_ERR_MEM;
+    }
+    return STARCH_OK;
+}
+
+int starch_assign_shards(const starch_unit* units, uint64_t nunits, int nshards, int32_t* shard_of)
+{
+    if ((nunits && (!units || !shard_of)) || nshards < 1) return STARCH_ERR_ARG;
+    std::vector<shard::Unit> u(nunits);
+    for (uint64_t k = 0; k < nunits; ++k)
+        u[k] = shard::Unit{units[k].offset, units[k].length, units[k].init_start, units[k].init_stop};
+    std::vector<int32_t> s;
+    shard::assign_lpt(u, nshards, s);
+    if (nunits) memcpy(shard_of, s.data(), nunits * sizeof(int32_t));
+    return STARCH_OK;
+}
+
+int starch_archive_layout(const uint64_t* unit_of, const uint64_t* bytes, uint64_t nseg, uint64_t base,
+                          uint64_t* order, uint64_t* offset, uint64_t* end)
+{
+    if (!end || (nseg && (!unit_of || !bytes || !order || !offset))) return STARCH_ERR_ARG;
+    std::vector<uint64_t> o, f;
+    shard::layout(unit_of, bytes, nseg, base, o, f, end);
+    if (nseg) {
+        memcpy(order, o.data(), nseg * sizeof(uint64_t));
+        memcpy(offset, f.data(), nseg * sizeof(uint64_t));
+    }
+    return STARCH_OK;
+}
+
 int starch_archive_size(starch_ctx* c, uint64_t* n)
 {
     if (!c || !n) return STARCH_ERR_ARG;
@@ -422,6 +814,7 @@ int starch_transform_host(starch_ctx* c, const void* bed, uint64_t n)
         c->names[s].assign(reinterpret_cast<const char*>(hb + si[s].name_off), si[s].name_len);
     }
     c->text_bytes = tr.text_bytes;
+    c->text_dev = c->tf.text;
     c->archive_bytes = 0;
     c->have = true;
     return STARCH_OK;
@@ -441,7 +834,7 @@ int starch_text_copy(starch_ctx* c, void* dst, uint64_t cap)
     GUARD(c)
     if (!c->have) return STARCH_ERR_STATE;
     if (cap < c->text_bytes) return STARCH_ERR_MEM;
-    if (c->text_bytes) HIP_CHECK(hipMemcpyAsync(dst, c->tf.text, c->text_bytes, hipMemcpyDeviceToHost, c->st));
+    if (c->text_bytes) HIP_CHECK(hipMemcpyAsync(dst, c->text_dev, c->text_bytes, hipMemcpyDeviceToHost, c->st));
     HIP_CHECK(hipStreamSynchronize(c->st));
     return STARCH_OK;
     END_GUARD(c)

@@ -345,13 +345,16 @@ __global__ void k_ok_index(const uint8_t* __restrict__ flags, uint64_t nl, uint8
     uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
     if (i < nl) idx[i] = (flags[i] & bit) ? i + 1 : 0;
 }
+// `init` is the value before the first line: 0 for a whole input (uninitialised
+// malloc memory was observed as 0), the previous unit's
+// last parsed value for a shard that starts mid-input.
 __global__ void k_gather_stale(const int64_t* __restrict__ cp, const uint64_t* __restrict__ idx, uint64_t nl,
-                               int64_t* __restrict__ v)
+                               int64_t init, int64_t* __restrict__ v)
 {
     uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
     if (i < nl) {
         uint64_t j = idx[i];
-        v[i] = j ? cp[j - 1] : 0;   // uninitialised malloc memory was observed as 0
+        v[i] = j ? cp[j - 1] : init;
     }
 }
 
@@ -869,7 +872,8 @@ __global__ void k_seg_info(const uint64_t* __restrict__ seg_first, uint64_t nseg
 // ---------------------------------------------------------------------------
 using namespace tf;
 
-void TransformWorkspace::run(const uint8_t* d_bed, uint64_t n, hipStream_t st, TransformResult& res)
+void TransformWorkspace::run(const uint8_t* d_bed, uint64_t n, hipStream_t st, TransformResult& res, int64_t init_start,
+                             int64_t init_stop)
 {
     res = TransformResult();
     uint64_t ntile = ceil_div(n, kTileBytes);
@@ -935,6 +939,7 @@ void TransformWorkspace::run(const uint8_t* d_bed, uint64_t n, hipStream_t st, T
                            ttot);
     } else {
         // general path: some start/stop does not parse (stale values, hpp:306-316)
+        res.general = true;
         int64_t* start = b_start.as<int64_t>(nl);
         int64_t* stop = b_stop.as<int64_t>(nl);
         uint8_t* flags = b_flags.as<uint8_t>(nl);
@@ -952,7 +957,8 @@ void TransformWorkspace::run(const uint8_t* d_bed, uint64_t n, hipStream_t st, T
             int64_t* v = (w == 0) ? start : stop;
             int64_t* cp = b_vcopy.as<int64_t>(nl);
             HIP_CHECK(hipMemcpyAsync(cp, v, nl * sizeof(int64_t), hipMemcpyDeviceToDevice, st));
-            hipLaunchKernelGGL(k_gather_stale, dim3(nb), dim3(kThreads), 0, st, cp, idx, nl, v);
+            hipLaunchKernelGGL(k_gather_stale, dim3(nb), dim3(kThreads), 0, st, cp, idx, nl, w == 0 ? init_start : init_stop,
+                               v);
         }
         uint32_t* out_len = b_out_len.as<uint32_t>(nl);
         uint32_t* seg_flag = b_seg_flag.as<uint32_t>(nl);

@@ -13,6 +13,7 @@ struct SegInfo {            // one chromosome segment (hpp:393-407 flush unit)
 
 struct TransformResult {
     uint64_t n_lines = 0, n_segments = 0, text_bytes = 0, ff_pos = ~0ull;
+    bool general = false;   // some start/stop failed to parse: stale values were propagated
 };
 
 struct TransformWorkspace {
@@ -20,5 +21,8 @@ struct TransformWorkspace {
         b_chr_len, b_idx, b_vcopy, b_out_len, b_seg_flag, b_out_off, b_seg_ord, b_seg_first, b_seg_info, b_text;
     uint8_t* text = nullptr;          // device: transformed text (valid after run)
     SegInfo* seg_info_dev = nullptr;  // device: n_segments entries
-    void run(const uint8_t* d_bed, uint64_t n, hipStream_t st, TransformResult& res);
+    // init_start/init_stop: bed_t.start/stop before the first line (stale sscanf
+    // values carried into a shard that starts mid-input, hpp:306-307)
+    void run(const uint8_t* d_bed, uint64_t n, hipStream_t st, TransformResult& res, int64_t init_start = 0,
+             int64_t init_stop = 0);
 };

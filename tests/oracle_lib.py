@@ -32,6 +32,7 @@ def lib():
                                    os.path.join(ROOT, "oracle", "_build", "libstarch_oracle.so")])
         L = ctypes.CDLL(ORACLE_SO)
         L.oracle_transform.restype = ctypes.c_size_t
+        L.oracle_transform_init.restype = ctypes.c_size_t
         L.oracle_bz2_compress.restype = ctypes.c_size_t
         L.oracle_crc32_bzip2.restype = ctypes.c_uint32
         L.oracle_block_sort.restype = ctypes.c_int32
@@ -51,16 +52,18 @@ def ref():
     return _ref
 
 
-def transform(data: bytes):
-    """-> (text bytes, [(chr bytes, line_count, text bytes)])"""
+def transform(data: bytes, init_start=0, init_stop=0):
+    """-> (text bytes, [(chr bytes, line_count, text bytes)]); init_* are the
+    sscanf values current before the first line (0 for a whole input)."""
     L = lib()
     cap = 2 * len(data) + 64 * (data.count(b"\n") + 1) + 1024
     seg_cap = data.count(b"\n") + 2
     out = ctypes.create_string_buffer(cap)
     segs = (Seg * seg_cap)()
     nseg = ctypes.c_size_t(0)
-    n = L.oracle_transform(data, ctypes.c_size_t(len(data)), out, ctypes.c_size_t(cap),
-                           segs, ctypes.c_size_t(seg_cap), ctypes.byref(nseg))
+    n = L.oracle_transform_init(data, ctypes.c_size_t(len(data)), out, ctypes.c_size_t(cap),
+                                segs, ctypes.c_size_t(seg_cap), ctypes.byref(nseg),
+                                ctypes.c_int64(init_start), ctypes.c_int64(init_stop))
     assert n != ctypes.c_size_t(-1).value
     text = out.raw[:n]
     res = []

@@ -135,3 +135,36 @@ def test_param_and_sequence_errors():
     assert L.BZ2_bzCompress(ctypes.byref(s), BZ_FINISH) == -1              # IDLE -> sequence error
     assert L.BZ2_bzCompressEnd(ctypes.byref(s)) == 0
     assert L.BZ2_bzCompressEnd(ctypes.byref(s)) == -2
+
+
+def test_threads_encode_concurrently_and_keep_their_device():
+    """Streams of several threads (the encode must not depend on or
+    change the calling thread's current HIP device)."""
+    import threading
+    import torch
+    r = random.Random(17)
+    inputs = [bytes(r.choice(b"0123456789\np-") for _ in range(r.randint(1000, 400000))) for _ in range(6)]
+    results, devs = [None] * len(inputs), [None] * len(inputs)
+
+    def work(i):
+        results[i] = run_script(inputs[i], [(BZ_FINISH, len(inputs[i]))])[0]
+        devs[i] = torch.cuda.current_device()
+
+    ths = [threading.Thread(target=work, args=(i,)) for i in range(len(inputs))]
+    for t in ths:
+        t.start()
+    for t in ths:
+        t.join()
+    for i, d in enumerate(inputs):
+        assert results[i] == oracle_lib.bz2(d, 9), i
+    assert devs == [0] * len(inputs)
+
+
+def test_default_allocators_installed():
+    """bzalloc / bzfree default to malloc / free like bz:bzlib.c:165-166."""
+    L = _lib()
+    s = BzStream()
+    assert L.BZ2_bzCompressInit(ctypes.byref(s), 9, 0, 30) == 0
+    assert s.bzalloc and s.bzfree and s.state
+    assert L.BZ2_bzCompressEnd(ctypes.byref(s)) == 0
+    assert not s.state

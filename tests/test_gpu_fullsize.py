@@ -1,0 +1,39 @@
+"""Full-size parity (north_star's target): every one of the 24 chromosome
+streams of cfg2 (100 M-line hg38 BED3) and cfg4 (50 M-row narrowPeak) equals
+the CPU path's stream -- the oracle transform followed by the reference's own
+libbz2 1.0.6 at -9 -- by SHA-256 (tests/golden/fullsize_cfg*.json, made in the
+CPU container by tools/make_fullsize_goldens.py)."""
+import hashlib
+import json
+import os
+
+import pytest
+
+pytestmark = pytest.mark.gpu
+
+GOLDEN = os.path.join(os.path.dirname(os.path.abspath(__file__)), "golden")
+
+
+@pytest.mark.parametrize("cfg", ["cfg2", "cfg4"])
+def test_fullsize_streams_match_cpu_path(cfg):
+    import torch
+    import starch_amd
+    g = json.load(open(os.path.join(GOLDEN, "fullsize_%s.json" % cfg)))
+    n = sum(starch_amd.gen_bed_sizes(g["kind"], g["total_lines"], seed=g["seed"]))
+    assert n == g["input_bytes"]
+    host = torch.empty(n, dtype=torch.uint8, pin_memory=True)
+    import ctypes
+    starch_amd.gen_bed(g["kind"], g["total_lines"], seed=g["seed"], into=ctypes.c_void_p(host.data_ptr()))
+    dev = host.to("cuda")
+    del host
+    c = starch_amd.Starch(0)
+    c.compress_device(dev.data_ptr(), n)
+    idx, streams = starch_amd.parse_archive(c.archive())
+    assert len(streams) == 24
+    for st, meta, want in zip(streams, idx["streams"], g["streams"]):
+        assert meta["chromosome"] == want["chromosome"]
+        assert meta["uncompressedLineCount"] == want["lines"]
+        assert meta["transformedBytes"] == want["text_bytes"]
+        assert len(st) == want["stream_bytes"], want["chromosome"]
+        assert hashlib.sha256(st).hexdigest() == want["sha256"], want["chromosome"]
+    c.close()

@@ -12,7 +12,7 @@ PASSES=${PASSES:-sq1 sq2 fetch write}
 run() {   # name, counters...
   local name=$1; shift
   timeout -s KILL ${TP:-120} rocprofv3 --kernel-trace --pmc "$@" -d $ROOT/gpurun_out/pmc/$name -o run \
-      --output-format csv -- python3 $ROOT/bench.py --steps 1 --warmup 0 --lines $LINES --no-cpu-baseline \
+      --output-format csv -- python3 $ROOT/bench.py --steps 1 --warmup 0 --lines $LINES --no-cpu-baseline --no-verify --no-e2e \
       > $ROOT/gpurun_out/pmc/$name.log 2>&1
 }
 rc=0

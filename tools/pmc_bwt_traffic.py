@@ -17,6 +17,9 @@ import json
 import os
 import sys
 
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+from bench import src_stamp  # noqa: E402
+
 
 def is_bwt(name):
     n = name.replace("(anonymous namespace)::", "")
@@ -40,6 +43,8 @@ def main():
     fetch_b = 2.0 * sum(f.values()) * 1024.0
     write_b = sum(w.values()) * 1024.0
     res = {
+        "src_stamp": src_stamp(),
+        "lines": int(os.environ.get("LINES", "100000000")),
         "hbm_bytes_per_launch": fetch_b + write_b,
         "fetch_bytes": fetch_b,
         "write_bytes": write_b,

@@ -8,7 +8,9 @@
 // The archive goes to stdout: magic ca5cad1a, one bzip2 stream per chromosome,
 // JSON index + footer.  Build-only flags: --level N, --no-index,
 // --reference-compat (stdout exactly as the reference: the 4 magic bytes),
-// --device N, --stats.
+// --device N, --gpus N (shard chromosomes over devices 0..N-1 in one process),
+// --devices LIST (explicit device list, e.g. 0,1 or 0,0 for virtual shards),
+// --stats.
 #include <errno.h>
 #include <getopt.h>
 #include <stdio.h>
@@ -39,6 +41,8 @@ static void usage(FILE* f)
             "  --no-index            streams only, no JSON index/footer\n"
             "  --reference-compat    write exactly what the reference writes (magic bytes only)\n"
             "  --device N            GPU ordinal (default 0)\n"
+            "  --gpus N              shard chromosomes over GPUs 0..N-1 (archive identical to one GPU)\n"
+            "  --devices LIST        comma-separated GPU ordinals to shard over (may repeat)\n"
             "  --stats               print per-stage timings to stderr\n"
             "  --help | -h           this message\n"
             "  --version | -v        version\n",
@@ -49,12 +53,14 @@ int main(int argc, char** argv)
 {
     std::string note, input;
     int methods = 0, gzip = 0, level = 9, emit_index = 1, compat = 0, device = 0, stats = 0;
+    std::vector<int> devices;
     static struct option longs[] = {
         {"note", required_argument, nullptr, 'n'}, {"bzip2", no_argument, nullptr, 'b'},
         {"gzip", no_argument, nullptr, 'g'},       {"help", no_argument, nullptr, 'h'},
         {"version", no_argument, nullptr, 'v'},    {"level", required_argument, nullptr, 'L'},
         {"no-index", no_argument, nullptr, 'I'},   {"reference-compat", no_argument, nullptr, 'R'},
         {"device", required_argument, nullptr, 'D'}, {"stats", no_argument, nullptr, 'S'},
+        {"gpus", required_argument, nullptr, 'G'},   {"devices", required_argument, nullptr, 'E'},
         {nullptr, 0, nullptr, 0}};
     opterr = 0;
     int c, li;
@@ -71,6 +77,20 @@ int main(int argc, char** argv)
             case 'R': compat = 1; break;
             case 'D': device = atoi(optarg); break;
             case 'S': stats = 1; break;
+            case 'G': {
+                devices.clear();
+                for (int i = 0, k = atoi(optarg); i < k; ++i) devices.push_back(i);
+                break;
+            }
+            case 'E': {
+                devices.clear();
+                for (const char* p = optarg; *p;) {
+                    devices.push_back(atoi(p));
+                    while (*p && *p != ',') ++p;
+                    if (*p == ',') ++p;
+                }
+                break;
+            }
             default: break;
         }
     }
@@ -119,22 +139,29 @@ int main(int argc, char** argv)
         while ((k = fread(buf.data(), 1, buf.size(), in)) > 0) data.insert(data.end(), buf.begin(), buf.begin() + k);
         if (in != stdin) fclose(in);
     }
-    starch_ctx* ctx = nullptr;
-    int rc = starch_create(device, &ctx);
-    if (rc != STARCH_OK) {
-        fprintf(stderr, "Error: could not open MI355X device %d (%s)\n", device, starch_strerror(rc));
-        return EINVAL;
+    if (devices.empty()) devices.push_back(device);
+    std::vector<starch_ctx*> ctxs(devices.size(), nullptr);
+    int rc = STARCH_OK;
+    for (size_t i = 0; i < devices.size(); ++i) {
+        rc = starch_create(devices[i], &ctxs[i]);
+        if (rc != STARCH_OK) {
+            fprintf(stderr, "Error: could not open MI355X device %d (%s)\n", devices[i], starch_strerror(rc));
+            for (size_t j = 0; j < i; ++j) starch_destroy(ctxs[j]);
+            return EINVAL;
+        }
     }
+    starch_ctx* ctx = ctxs[0];
     starch_options opt;
     starch_options_init(&opt);
     opt.block_size_100k = level;
     opt.emit_index = emit_index;
     opt.reference_compat = compat;
     opt.note = note.empty() ? nullptr : note.c_str();
-    rc = starch_encode_host(ctx, data.data(), data.size(), &opt);
+    rc = ctxs.size() > 1 ? starch_encode_multi_host(ctxs.data(), (int)ctxs.size(), data.data(), data.size(), &opt)
+                         : starch_encode_host(ctx, data.data(), data.size(), &opt);
     if (rc != STARCH_OK) {
         fprintf(stderr, "Error: encode failed (%s: %s)\n", starch_strerror(rc), starch_last_error(ctx));
-        starch_destroy(ctx);
+        for (auto* c : ctxs) starch_destroy(c);
         return rc == STARCH_ERR_MEM ? ENOMEM : EINVAL;
     }
     uint64_t n = 0;
@@ -154,6 +181,6 @@ int main(int argc, char** argv)
                 (unsigned long long)s.text_bytes, (unsigned long long)s.archive_bytes, (unsigned long long)s.n_blocks,
                 s.ms_total, s.ms_transform, s.ms_rle, s.ms_bwt, s.ms_mtf, s.ms_tables, s.ms_emit);
     }
-    starch_destroy(ctx);
+    for (auto* c : ctxs) starch_destroy(c);
     return 0;
 }
