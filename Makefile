@@ -10,7 +10,7 @@ OBJS := $(patsubst $(CSRC)/%.hip,$(BUILD)/%.o,$(HIPSRC)) $(patsubst $(CSRC)/%.cp
 HDRS := $(wildcard $(CSRC)/*.hpp) include/starch_amd.h include/starch_bzlib.h
 FLAGS := -O3 -std=c++17 -fPIC -Wall -Wno-unused-function -Wno-unused-variable --offload-arch=$(ARCH)
 
-all: $(BUILD)/libstarch_amd.so $(BUILD)/starch3 oracle
+all: $(BUILD)/libstarch_amd.so $(BUILD)/starch3 $(BUILD)/starch3_hpp_example oracle
 
 $(BUILD)/%.o: $(CSRC)/%.hip $(HDRS)
 	@mkdir -p $(BUILD)
@@ -25,6 +25,9 @@ $(BUILD)/libstarch_amd.so: $(OBJS)
 
 $(BUILD)/starch3: tools/starch3_cli.cpp $(BUILD)/libstarch_amd.so include/starch_amd.h
 	$(HIPCC) -O2 -std=c++17 -o $@ tools/starch3_cli.cpp -L$(BUILD) -lstarch_amd -Wl,-rpath,'$$ORIGIN'
+
+$(BUILD)/starch3_hpp_example: tools/starch3_hpp_example.cpp $(BUILD)/libstarch_amd.so include/starch3_amd.hpp include/starch_amd.h
+	g++ -O2 -std=c++11 -Wall -o $@ tools/starch3_hpp_example.cpp -L$(BUILD) -lstarch_amd -Wl,-rpath,'$$ORIGIN'
 
 oracle:
 	$(MAKE) -C oracle

@@ -144,6 +144,9 @@ int starch_text_copy(starch_ctx* ctx, void* dst, uint64_t cap);
 /* One bzip2 stream (BZ_FINISH semantics) of n bytes; result to host. */
 int starch_bz2_compress_host(starch_ctx* ctx, const void* in, uint64_t n, int block_size_100k, void* out,
                              uint64_t cap, uint64_t* out_len);
+/* Block count and combined CRC of the (first) stream of the last
+ * starch_bz2_compress_* call (the index fields of a process_tf_buffer hook). */
+int starch_bz2_stream_info(starch_ctx* ctx, uint32_t* n_blocks, uint32_t* combined_crc);
 
 /* Several independent bzip2 streams in one launch sequence (device memory):
  * stream k = d_in[offs[k] .. offs[k]+lens[k]); results packed back to back in

@@ -28,6 +28,7 @@ struct starch_ctx {
     uint64_t part_bytes = 0;          // streams of a shard (starch_encode_units_device)
     uint64_t text_bytes = 0;
     const uint8_t* text_dev = nullptr;
+    uint32_t bz_nblocks = 0, bz_crc = 0;    // first stream of the last starch_bz2_compress_* call
     std::vector<starch_segment> segs;
     std::vector<std::string> names;
     starch_stats stats{};
@@ -858,6 +859,8 @@ int starch_bz2_compress_many_device(starch_ctx* c, const void* d_in, const uint6
                            c->st, nullptr);
     HIP_CHECK(hipStreamSynchronize(c->st));
     for (uint64_t s = 0; s < nstreams; ++s) { out_offs[s] = outs[s].out_off; out_lens[s] = outs[s].bytes; }
+    c->bz_nblocks = nstreams ? outs[0].n_blocks : 0;
+    c->bz_crc = nstreams ? outs[0].combined_crc : 0;
     return STARCH_OK;
     END_GUARD(c)
 }
@@ -880,6 +883,14 @@ int starch_bz2_compress_host(starch_ctx* c, const void* in, uint64_t n, int bs, 
     HIP_CHECK(hipStreamSynchronize(c->st));
     return STARCH_OK;
     END_GUARD(c)
+}
+
+int starch_bz2_stream_info(starch_ctx* c, uint32_t* n_blocks, uint32_t* combined_crc)
+{
+    if (!c || !n_blocks || !combined_crc) return STARCH_ERR_ARG;
+    *n_blocks = c->bz_nblocks;
+    *combined_crc = c->bz_crc;
+    return STARCH_OK;
 }
 
 int starch_build_index(const starch_segment* segs, const char* const* names, const uint64_t* name_lens,
