@@ -138,6 +138,7 @@ int starch_get_stats(starch_ctx* ctx, starch_stats* out);
 /* Transform stage only: afterwards starch_text_size/starch_text_copy give the
  * concatenated segment texts and starch_segments the per-segment counts. */
 int starch_transform_host(starch_ctx* ctx, const void* bed, uint64_t n);
+int starch_transform_device(starch_ctx* ctx, const void* d_bed, uint64_t n);   /* BED bytes in HBM */
 int starch_text_size(starch_ctx* ctx, uint64_t* n);
 int starch_text_copy(starch_ctx* ctx, void* dst, uint64_t cap);
 

@@ -98,6 +98,7 @@ def load():
         "starch_segment_name": ([vp, u64, vp, u64, pu64], ctypes.c_int),
         "starch_get_stats": ([vp, ctypes.POINTER(Stats)], ctypes.c_int),
         "starch_transform_host": ([vp, ctypes.c_char_p, u64], ctypes.c_int),
+        "starch_transform_device": ([vp, vp, u64], ctypes.c_int),
         "starch_text_size": ([vp, pu64], ctypes.c_int),
         "starch_text_copy": ([vp, vp, u64], ctypes.c_int),
         "starch_bz2_compress_host": ([vp, ctypes.c_char_p, u64, ctypes.c_int, vp, u64, pu64], ctypes.c_int),
@@ -292,6 +293,11 @@ class Starch:
         for name, s in self.segments():
             segs.append((name, s.line_count, text[s.stream_offset:s.stream_offset + s.text_bytes]))
         return text, segs
+
+    def transform_device(self, d_ptr: int, n: int):
+        """Transform stage only on BED bytes in HBM; the text stays in HBM
+        (text_size / segments(); stats()["ms_transform"])."""
+        _check(self._L.starch_transform_device(self._h, ctypes.c_void_p(d_ptr), n), self._h)
 
     def bz2_compress(self, data: bytes, level: int = 9) -> bytes:
         """One bzip2 stream, byte-identical to libbz2 BZ2_bzCompress(BZ_FINISH)."""

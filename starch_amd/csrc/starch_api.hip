@@ -791,14 +791,17 @@ int starch_get_stats(starch_ctx* c, starch_stats* out)
     return STARCH_OK;
 }
 
-int starch_transform_host(starch_ctx* c, const void* bed, uint64_t n)
+// transform stage only on device-resident BED bytes (segments: stream_offset =
+// offset of the segment's text in the text buffer)
+static void transform_only(starch_ctx* c, const uint8_t* d, uint64_t n)
 {
-    GUARD(c)
-    if (n && !bed) return STARCH_ERR_ARG;
-    uint8_t* d = c->input.as<uint8_t>(n + 64);
-    if (n) HIP_CHECK(hipMemcpyAsync(d, bed, n, hipMemcpyHostToDevice, c->st));
+    hipEvent_t e0, e1;
+    HIP_CHECK(hipEventCreate(&e0));
+    HIP_CHECK(hipEventCreate(&e1));
+    HIP_CHECK(hipEventRecord(e0, c->st));
     TransformResult tr;
     c->tf.run(d, n, c->st, tr);
+    HIP_CHECK(hipEventRecord(e1, c->st));
     std::vector<SegInfo> si(tr.n_segments);
     if (tr.n_segments)
         HIP_CHECK(hipMemcpyAsync(si.data(), c->tf.seg_info_dev, tr.n_segments * sizeof(SegInfo),
@@ -806,18 +809,49 @@ int starch_transform_host(starch_ctx* c, const void* bed, uint64_t n)
     HIP_CHECK(hipStreamSynchronize(c->st));
     c->segs.assign(tr.n_segments, starch_segment{});
     c->names.assign(tr.n_segments, std::string());
-    const uint8_t* hb = static_cast<const uint8_t*>(bed);
     for (uint64_t s = 0; s < tr.n_segments; ++s) {
         c->segs[s].line_count = si[s].line_count;
         c->segs[s].text_bytes = si[s].text_len;
         c->segs[s].stream_offset = si[s].text_off;   // transform-only: offset into the text
         c->segs[s].name_len = si[s].name_len;
-        c->names[s].assign(reinterpret_cast<const char*>(hb + si[s].name_off), si[s].name_len);
+        c->names[s].resize(si[s].name_len);
+        if (si[s].name_len)
+            HIP_CHECK(hipMemcpyAsync(&c->names[s][0], d + si[s].name_off, si[s].name_len, hipMemcpyDeviceToHost, c->st));
     }
+    HIP_CHECK(hipStreamSynchronize(c->st));
+    float ms = 0;
+    HIP_CHECK(hipEventElapsedTime(&ms, e0, e1));
+    (void)hipEventDestroy(e0);
+    (void)hipEventDestroy(e1);
+    c->stats = starch_stats{};
+    c->stats.input_bytes = n;
+    c->stats.n_lines = tr.n_lines;
+    c->stats.n_segments = tr.n_segments;
+    c->stats.text_bytes = tr.text_bytes;
+    c->stats.ms_transform = ms;
+    c->stats.ms_total = ms;
     c->text_bytes = tr.text_bytes;
     c->text_dev = c->tf.text;
     c->archive_bytes = 0;
     c->have = true;
+}
+
+int starch_transform_host(starch_ctx* c, const void* bed, uint64_t n)
+{
+    GUARD(c)
+    if (n && !bed) return STARCH_ERR_ARG;
+    uint8_t* d = c->input.as<uint8_t>(n + 64);
+    if (n) HIP_CHECK(hipMemcpyAsync(d, bed, n, hipMemcpyHostToDevice, c->st));
+    transform_only(c, d, n);
+    return STARCH_OK;
+    END_GUARD(c)
+}
+
+int starch_transform_device(starch_ctx* c, const void* d_bed, uint64_t n)
+{
+    GUARD(c)
+    if (n && !d_bed) return STARCH_ERR_ARG;
+    transform_only(c, static_cast<const uint8_t*>(d_bed), n);
     return STARCH_OK;
     END_GUARD(c)
 }

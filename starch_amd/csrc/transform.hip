@@ -15,6 +15,10 @@
 //   rem_beg u64[L], rem_len u32[L], chr_len u32[L], flags u8[L]
 //   out_off u64[L]          exclusive scan of per-line output lengths
 //   text     u8[T]          transformed text, segments back to back
+#include <string.h>
+
+#include <algorithm>
+
 #include "common.hpp"
 #include "transform.hpp"
 
@@ -865,6 +869,426 @@ __global__ void k_seg_info(const uint64_t* __restrict__ seg_first, uint64_t nseg
     info[s] = r;
 }
 
+
+// --- single-pass transform (default) -----------------------------------------
+// One workgroup per 8 KiB byte tile, taken in order from an atomic counter.  A
+// line belongs to the tile holding its '\n'; the tile is staged in LDS with a
+// 1 KiB halo before it (the start of its first line and the whole previous
+// line, whose chromosome and start/stop the first line depends on).  The
+// workgroup finds its newlines, parses its lines 256 at a time (parse_fast /
+// the byte-serial parser), builds their output in LDS, and learns where it
+// goes from a decoupled look-back over the tiles before it: a tile publishes
+// its (bytes, lines, segments, saw 0xFF) aggregate, then its inclusive prefix;
+// the combine operator stops at the first tile holding a 0xFF (hpp:181: 0xFF
+// reads as EOF), so lines after it vanish.  Input is read once; no per-line
+// array exists in HBM.  Anything outside this shape sets a flag and the host
+// takes the two-pass path: a stale sscanf value (FX_FAIL: general path), a
+// line longer than the halo or a tile of > 2048 lines (FX_FALLBACK), or text /
+// segment capacity (FX_TEXT_CAP / FX_SEG_CAP: grow, rerun).
+constexpr uint32_t kFT = 8192;                 // tile bytes
+constexpr uint32_t kFH = 1024;                 // halo bytes before the tile
+constexpr uint32_t kFMaxLines = 2048;
+constexpr uint32_t kFOut = 10240;              // LDS output bytes per tile
+constexpr uint32_t kFSeg = 64;                 // segment records per tile in LDS
+enum : uint32_t { FX_FAIL = 1, FX_FALLBACK = 2, FX_TEXT_CAP = 4, FX_SEG_CAP = 8 };
+
+struct TileAgg { uint64_t bytes, lines, segs, ff; };
+
+__device__ __forceinline__ TileAgg agg_combine(const TileAgg& x, const TileAgg& y)   // x precedes y
+{
+    if (x.ff) return x;
+    return TileAgg{x.bytes + y.bytes, x.lines + y.lines, x.segs + y.segs, y.ff};
+}
+
+__device__ __forceinline__ TileAgg agg_shfl_up(const TileAgg& v, int d)
+{
+    TileAgg r;
+    r.bytes = __shfl_up(v.bytes, d, 64);
+    r.lines = __shfl_up(v.lines, d, 64);
+    r.segs = __shfl_up(v.segs, d, 64);
+    r.ff = __shfl_up(v.ff, d, 64);
+    return r;
+}
+
+template <class S>
+__device__ __forceinline__ LineVals parse_line_at(const S& bed, uint64_t ls, uint64_t le)
+{
+    LineVals r;
+    const Fields f = tokenize(bed, ls, le);
+    uint64_t len[4];
+#pragma unroll
+    for (int t = 0; t < 4; ++t) len[t] = cstr_len(bed, f.b[t], f.e[t] - f.b[t]);
+    r.a = 0;
+    r.b = 0;
+    r.aok = scan_i64(bed, f.b[1], len[1], r.a);
+    r.bok = scan_i64(bed, f.b[2], len[2], r.b);
+    r.newseg = true;
+    r.rem_b = f.b[3];
+    r.rem_len = (uint32_t)len[3];
+    r.chr_len = (uint32_t)len[0];
+    return r;
+}
+
+struct FusedSeg { uint32_t line, name_ls, name_len, text; };
+struct LineKey { int64_t a, b; uint32_t cls, clen; };   // what the next line needs of its predecessor
+
+struct FusedShared {
+    uint4 tb4[(kFH + kFT + 32 + kStagePad) / 16];
+    uint16_t nlp[kFMaxLines];                  // LDS position of each line's '\n'
+    uint32_t ob4[kFOut / 4];
+    uint64_t scan[kThreads / 64 + 1];
+    FusedSeg seg[kFSeg];
+    LineKey wlast[kThreads / 64 + 1];          // [0]: carry into the chunk; [w+1]: wave w's last line
+    uint32_t tile, ffpos, p1, p2, over;
+    TileAgg excl;
+};
+
+__device__ __forceinline__ LineKey shfl_up_key(const LineKey& k)
+{
+    LineKey r;
+    r.a = __shfl_up(k.a, 1, 64);
+    r.b = __shfl_up(k.b, 1, 64);
+    r.cls = __shfl_up(k.cls, 1, 64);
+    r.clen = __shfl_up(k.clen, 1, 64);
+    return r;
+}
+
+// The tile's lines, 512 at a time, two consecutive lines per thread: parse,
+// output length, one block scan, output and segment records into LDS at
+// tile-relative offsets.  A line's predecessor comes by shuffle (wave
+// boundaries and chunk starts through LDS).  Returns (bytes, segments).
+__device__ __forceinline__ void fused_lines(FusedShared& S, const uint8_t* tb, uint64_t a0, uint32_t nl,
+                                            uint32_t first_ls, bool input_start, uint32_t* __restrict__ xflags,
+                                            uint64_t& bytes_out, uint32_t& segs_out)
+{
+    const uint32_t tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+    const LSrc lsrc{tb, a0};
+    uint8_t* ob = reinterpret_cast<uint8_t*>(S.ob4);
+    uint64_t run = 0;
+    uint32_t segrun = 0;
+    for (uint32_t c0 = 0; c0 < nl; c0 += 2 * kThreads) {
+        TfLine t[2];
+        uint32_t ls[2] = {0, 0};
+        LineKey key[2];
+        bool have[2];
+#pragma unroll
+        for (int u = 0; u < 2; ++u) {
+            const uint32_t k = c0 + 2 * tid + u;
+            have[u] = k < nl;
+            key[u] = LineKey{0, 0, 0, 0};
+            if (have[u]) {
+                ls[u] = k ? (uint32_t)S.nlp[k - 1] + 1u : first_ls;
+                const uint32_t le = (uint32_t)S.nlp[k] + 1u;
+                t[u].ls = a0 + ls[u];
+                if (!parse_fast(tb, ls[u], le - ls[u], t[u].ls, t[u].r))
+                    t[u].r = parse_line_at(lsrc, a0 + ls[u], a0 + le);
+                if (!t[u].r.aok || !t[u].r.bok) atomicOr(xflags, FX_FAIL);
+                key[u] = LineKey{t[u].r.a, t[u].r.b, ls[u], t[u].r.chr_len};
+            }
+        }
+        if (lane == 63) S.wlast[wave + 1] = key[1];
+        const LineKey up = shfl_up_key(key[1]);
+        __syncthreads();
+        const LineKey prev0 = lane ? up : S.wlast[wave];
+        uint64_t len[2] = {0, 0}, ns[2] = {0, 0};
+#pragma unroll
+        for (int u = 0; u < 2; ++u) {
+            if (!have[u]) continue;
+            const LineKey& p = u ? key[0] : prev0;
+            t[u].pa = p.a;
+            t[u].pb = p.b;
+            bool newseg = true;
+            if (!(c0 + 2 * tid + u == 0 && input_start)) {
+                const uint32_t cl = t[u].r.chr_len;
+                bool same = (p.clen == cl);
+                for (uint32_t q = 0; same && q < cl; q += 8) {
+#pragma unroll
+                    for (uint32_t j = 0; j < 8; ++j) {
+                        const bool e = tb[p.cls + q + j] == tb[ls[u] + q + j];
+                        if (q + j < cl) same = same && e;
+                    }
+                }
+                newseg = !same;
+            }
+            t[u].r.newseg = newseg;
+            len[u] = out_desc(t[u].r, t[u].pa, t[u].pb).len;
+            ns[u] = newseg ? 1u : 0u;
+        }
+        uint64_t tot = 0;
+        const uint64_t ex = block_excl_scan_add<uint64_t>(((len[0] + len[1]) << 20) | (ns[0] + ns[1]), S.scan, &tot);
+        uint64_t off = run + (ex >> 20);
+        uint32_t sl = segrun + (uint32_t)(ex & 0xFFFFFu);
+#pragma unroll
+        for (int u = 0; u < 2; ++u) {
+            if (!have[u]) continue;
+            if (off + len[u] <= kFOut) tf_write(lsrc, t[u], ob + off);
+            else S.over = 1;
+            if (ns[u]) {
+                if (sl < kFSeg) S.seg[sl] = FusedSeg{c0 + 2 * tid + u, ls[u], t[u].r.chr_len, (uint32_t)off};
+                else S.over = 1;
+                ++sl;
+            }
+            off += len[u];
+        }
+        run += tot >> 20;
+        segrun += (uint32_t)(tot & 0xFFFFFu);
+        // carry: the chunk's last line is the next chunk's first predecessor
+        const uint32_t last = (nl - c0 < 2 * kThreads ? nl - c0 : 2 * kThreads) - 1;
+        if (2 * tid == last) S.wlast[0] = key[0];
+        if (2 * tid + 1 == last) S.wlast[0] = key[1];
+        __syncthreads();
+    }
+    bytes_out = run;
+    segs_out = segrun;
+}
+
+__global__ void __launch_bounds__(kThreads)
+k_tf_fused(const uint8_t* __restrict__ bed, uint64_t n, uint32_t* __restrict__ tile_ctr,
+           uint64_t* __restrict__ aw, uint64_t* __restrict__ iw,
+           uint8_t* __restrict__ text, uint64_t text_cap, SegInfo* __restrict__ info, uint64_t seg_cap,
+           uint32_t* __restrict__ xflags, uint64_t* __restrict__ totals, uint32_t ntiles, uint32_t dbg_mode)
+{
+    __shared__ FusedShared S;
+    const uint32_t tid = threadIdx.x, lane = tid & 63;
+    if (tid == 0) {
+        S.tile = atomicAdd(tile_ctr, 1u);
+        S.ffpos = 0xFFFFFFFFu;
+        S.p1 = 0;
+        S.p2 = 0;
+        S.over = 0;
+    }
+    __syncthreads();
+    const uint32_t tile = S.tile;
+    const uint64_t t0 = (uint64_t)tile * kFT;
+    const uint64_t tend = t0 + kFT < n ? t0 + kFT : n;
+    const uint64_t s0 = t0 > kFH ? t0 - kFH : 0;
+    const uintptr_t abs0 = reinterpret_cast<uintptr_t>(bed + s0) & ~(uintptr_t)15;
+    const uint64_t a0 = (uint64_t)(abs0 - reinterpret_cast<uintptr_t>(bed));   // bed-relative (may wrap)
+    const uint32_t nw = (uint32_t)((reinterpret_cast<uintptr_t>(bed + tend) - abs0 + 15) / 16);
+    {
+        const uint4* src = reinterpret_cast<const uint4*>(abs0);
+        for (uint32_t w = tid; w < nw; w += kThreads) S.tb4[w] = src[w];
+    }
+    __syncthreads();
+    const uint8_t* tb = reinterpret_cast<const uint8_t*>(S.tb4);
+    const uint32_t Lt0 = (uint32_t)(t0 - a0), Lend = (uint32_t)(tend - a0), Ls0 = (uint32_t)(s0 - a0);
+    // newline / 0xFF masks of 32-byte LDS chunks covering [Lt0, Lend); a thread
+    // owns two consecutive chunks, so scan order is byte order
+    const uint32_t cbeg = Lt0 >> 5, cend = (Lend + 31) >> 5;
+    uint32_t nlm[2] = {0, 0};
+#pragma unroll
+    for (uint32_t it = 0; it < 2; ++it) {
+        const uint32_t ch = cbeg + 2 * tid + it;
+        if (ch >= cend) continue;
+        const uint4* q = reinterpret_cast<const uint4*>(tb + ch * 32);
+        const uint4 x = q[0], y = q[1];
+        const uint32_t w[8] = {x.x, x.y, x.z, x.w, y.x, y.y, y.z, y.w};
+        uint32_t nm = 0, fm = 0;
+#pragma unroll
+        for (int j = 0; j < 8; ++j) {
+            nm |= eq4(w[j], 0x0a0a0a0au) << (4 * j);
+            fm |= eq4(w[j], 0xffffffffu) << (4 * j);
+        }
+        const uint32_t lo = ch * 32 < Lt0 ? Lt0 - ch * 32 : 0u;
+        const uint32_t hi = Lend - ch * 32 < 32u ? Lend - ch * 32 : 32u;
+        const uint32_t keep = (hi >= 32u ? 0xFFFFFFFFu : ((1u << hi) - 1u)) & ~((1u << lo) - 1u);
+        nlm[it] = nm & keep;
+        fm &= keep;
+        if (fm) atomicMin(&S.ffpos, ch * 32 + (uint32_t)__builtin_ctz(fm));
+    }
+    // the halo's last two newlines (wave 0, 64 bytes at a time, backwards):
+    // the previous line is [p2, p1), the first line starts at p1
+    if (tid < 64 && Lt0 > Ls0) {
+        uint32_t found = 0, p1 = 0, p2 = 0;
+        for (uint32_t e = Lt0; e > Ls0 && found < 2;) {
+            const uint32_t b0 = e - Ls0 > 64u ? e - 64u : Ls0;
+            const uint32_t j = b0 + lane;
+            uint64_t m = __ballot(j < e && tb[j] == '\n');
+            while (m && found < 2) {
+                const uint32_t pos = b0 + (uint32_t)(63 - __clzll((long long)m));
+                if (found == 0) p1 = pos + 1; else p2 = pos + 1;
+                ++found;
+                m &= ~(1ull << (pos - b0));
+            }
+            e = b0;
+        }
+        if (lane == 0) { S.p1 = p1; S.p2 = p2; }
+    }
+    __syncthreads();
+    const uint32_t ffpos = S.ffpos;
+    uint32_t cnt = 0;
+#pragma unroll
+    for (uint32_t it = 0; it < 2; ++it) {
+        const uint32_t ch = cbeg + 2 * tid + it;
+        if (ffpos != 0xFFFFFFFFu && ch * 32 + 32 > ffpos) {   // lines ending after the 0xFF are dropped
+            const uint32_t lim = ffpos > ch * 32 ? ffpos - ch * 32 : 0u;
+            nlm[it] &= lim >= 32u ? 0xFFFFFFFFu : ((1u << lim) - 1u);
+        }
+        cnt += __popc(nlm[it]);
+    }
+    uint32_t nl_tile = 0;
+    const uint32_t pre = block_excl_scan_add<uint32_t>(cnt, reinterpret_cast<uint32_t*>(S.scan), &nl_tile);
+    bool fallback = nl_tile > kFMaxLines;
+    if (!fallback) {
+        uint32_t o = pre;
+#pragma unroll
+        for (uint32_t it = 0; it < 2; ++it) {
+            const uint32_t ch = cbeg + 2 * tid + it;
+            uint32_t m = nlm[it];
+            while (m) {
+                S.nlp[o++] = (uint16_t)(ch * 32 + (uint32_t)__builtin_ctz(m));
+                m &= m - 1;
+            }
+        }
+    }
+    // first line start and the previous line
+    bool input_start = false;
+    uint32_t first_ls = Lt0, prev_ls = 0;
+    if (t0 == 0) {
+        input_start = true;
+    } else if (S.p1) {
+        first_ls = S.p1;
+        if (S.p2) prev_ls = S.p2;
+        else if (s0 == 0) prev_ls = Ls0;
+        else fallback = true;                      // previous line longer than the halo
+    } else if (s0 == 0) {
+        first_ls = Ls0;                            // no line ended before the tile: the input's first line
+        input_start = true;
+    } else {
+        fallback = fallback || nl_tile > 0;        // first line longer than the halo
+    }
+    if (tid == 0) {
+        LineKey pk{0, 0, 0, 0};
+        if (!fallback && !input_start && nl_tile > 0) {
+            LineVals pr;
+            const uint32_t ple = first_ls;         // one past the previous line's '\n'
+            if (!parse_fast(tb, prev_ls, ple - prev_ls, a0 + prev_ls, pr))
+                pr = parse_line_at(LSrc{tb, a0}, a0 + prev_ls, a0 + ple);
+            pk = LineKey{pr.a, pr.b, prev_ls, pr.chr_len};
+        }
+        S.wlast[0] = pk;
+    }
+    __syncthreads();
+    uint64_t bytes = 0;
+    uint32_t segs = 0;
+    if (!fallback && nl_tile > 0) fused_lines(S, tb, a0, nl_tile, first_ls, input_start, xflags, bytes, segs);
+    fallback = fallback || S.over;
+    if (fallback && tid == 0) atomicOr(xflags, FX_FALLBACK);
+    const TileAgg local{bytes, fallback ? 0ull : nl_tile, segs, ffpos != 0xFFFFFFFFu ? 1ull : 0ull};
+    if (dbg_mode == 1) return;                      // timing experiment: parse only
+    // decoupled look-back (wave 0).  Every published word carries its own
+    // valid bit (bit 63), so no fence orders separate stores: aggregates go to
+    // aw[3*tile..], inclusive prefixes to iw[3*tile..], each read and written
+    // with relaxed agent-scope atomics (no cache-wide invalidate per poll).
+    if (tid < 64) {
+        constexpr uint64_t V = 1ull << 63;
+        if (lane < 3) {
+            const uint64_t w = lane == 0 ? local.bytes : lane == 1 ? local.lines : (local.segs | (local.ff << 62));
+            __hip_atomic_store(aw + 3ull * tile + lane, w | V, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        }
+        TileAgg excl{0, 0, 0, 0};
+        int64_t j = (int64_t)tile - 1;
+        while (j >= 0) {
+            const int64_t idx = j - (63 - (int64_t)lane);
+            bool incl_here = true;
+            TileAgg v{0, 0, 0, 0};
+            if (idx >= 0) {
+                for (;;) {
+                    const uint64_t* ip = iw + 3ull * (uint64_t)idx;
+                    const uint64_t x0 = __hip_atomic_load(ip, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                    const uint64_t x1 = __hip_atomic_load(ip + 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                    const uint64_t x2 = __hip_atomic_load(ip + 2, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                    if (x0 & x1 & x2 & V) {
+                        v = TileAgg{x0 & ~V, x1 & ~V, x2 & ((1ull << 62) - 1), (x2 >> 62) & 1ull};
+                        break;
+                    }
+                    const uint64_t* ap = aw + 3ull * (uint64_t)idx;
+                    const uint64_t y0 = __hip_atomic_load(ap, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                    const uint64_t y1 = __hip_atomic_load(ap + 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                    const uint64_t y2 = __hip_atomic_load(ap + 2, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                    if (y0 & y1 & y2 & V) {
+                        v = TileAgg{y0 & ~V, y1 & ~V, y2 & ((1ull << 62) - 1), (y2 >> 62) & 1ull};
+                        incl_here = false;
+                        break;
+                    }
+                    __builtin_amdgcn_s_sleep(1);
+                }
+            }
+            const uint64_t pm = __ballot(incl_here);
+            const int hp = pm ? 63 - __clzll((long long)pm) : -1;   // nearest tile with its inclusive prefix
+            if ((int)lane < hp) v = TileAgg{0, 0, 0, 0};
+#pragma unroll
+            for (int d = 1; d < 64; d <<= 1) {
+                const TileAgg u = agg_shfl_up(v, d);
+                if ((int)lane >= d) v = agg_combine(u, v);
+            }
+            TileAgg w;
+            w.bytes = __shfl(v.bytes, 63, 64);
+            w.lines = __shfl(v.lines, 63, 64);
+            w.segs = __shfl(v.segs, 63, 64);
+            w.ff = __shfl(v.ff, 63, 64);
+            excl = agg_combine(w, excl);
+            if (pm) break;
+            j -= 64;
+        }
+        const TileAgg inc = agg_combine(excl, local);
+        if (lane < 3) {
+            const uint64_t w = lane == 0 ? inc.bytes : lane == 1 ? inc.lines : (inc.segs | (inc.ff << 62));
+            __hip_atomic_store(iw + 3ull * tile + lane, w | V, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        }
+        if (lane == 0) {
+            S.excl = excl;
+            if (tile == ntiles - 1) {
+                totals[0] = inc.lines;
+                totals[1] = inc.segs;
+                totals[2] = inc.bytes;
+                totals[3] = inc.ff;
+            }
+        }
+    }
+    __syncthreads();
+    const TileAgg excl = S.excl;
+    if (excl.ff || fallback || nl_tile == 0) return;   // dropped after an earlier 0xFF, or nothing here
+    const uint64_t o0 = excl.bytes;
+    if (o0 + bytes > text_cap || excl.segs + segs > seg_cap) {
+        if (tid == 0) atomicOr(xflags, o0 + bytes > text_cap ? FX_TEXT_CAP : FX_SEG_CAP);
+        return;
+    }
+    for (uint32_t q = tid; q < segs; q += kThreads) {
+        const FusedSeg f = S.seg[q];
+        SegInfo& g = info[excl.segs + q];
+        g.first_line = excl.lines + f.line;
+        g.name_off = a0 + f.name_ls;
+        g.name_len = f.name_len;
+        g.text_off = o0 + f.text;
+    }
+    const uint8_t* ob = reinterpret_cast<const uint8_t*>(S.ob4);
+    const uint32_t wl = (uint32_t)bytes;
+    uint32_t head = (uint32_t)((4u - (o0 & 3u)) & 3u);
+    head = head < wl ? head : wl;
+    if (tid < head) text[o0 + tid] = ob[tid];
+    const uint32_t nw4 = (wl - head) / 4u;
+    uint32_t* dst = reinterpret_cast<uint32_t*>(text + o0 + head);
+    for (uint32_t w = tid; w < nw4; w += kThreads) {
+        const uint32_t q = head + 4u * w;
+        dst[w] = (uint32_t)ob[q] | ((uint32_t)ob[q + 1] << 8) | ((uint32_t)ob[q + 2] << 16) | ((uint32_t)ob[q + 3] << 24);
+    }
+    for (uint32_t k = head + 4u * nw4 + tid; k < wl; k += kThreads) text[o0 + k] = ob[k];
+}
+
+// line_count / text_len of each segment from its successor; totals on the device
+__global__ void k_seg_close_dev(SegInfo* __restrict__ info, const uint64_t* __restrict__ totals, uint64_t seg_cap)
+{
+    const uint64_t nseg = totals[1], nl = totals[0], ttot = totals[2];
+    for (uint64_t s = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; s < nseg && s < seg_cap;
+         s += (uint64_t)gridDim.x * blockDim.x) {
+        const uint64_t nf = (s + 1 < nseg) ? info[s + 1].first_line : nl;
+        const uint64_t nt = (s + 1 < nseg) ? info[s + 1].text_off : ttot;
+        info[s].line_count = nf - info[s].first_line;
+        info[s].text_len = nt - info[s].text_off;
+    }
+}
+
 }  // namespace tf
 
 // ---------------------------------------------------------------------------
@@ -874,6 +1298,72 @@ using namespace tf;
 
 void TransformWorkspace::run(const uint8_t* d_bed, uint64_t n, hipStream_t st, TransformResult& res, int64_t init_start,
                              int64_t init_stop)
+{
+    res = TransformResult();
+    // STARCH_TF=2pass / fused forces a path; by default the single pass runs
+    // unless the last input produced more than 0.6 text bytes per input byte
+    // (long remainder columns, e.g. narrowPeak: there the two-pass kernels,
+    // which stage exactly 256 lines per workgroup, measured faster)
+    static const int force = [] {
+        const char* e = getenv("STARCH_TF");
+        return !e ? 0 : !strcmp(e, "2pass") ? 2 : !strcmp(e, "fused") ? 1 : 0;
+    }();
+    if (n == 0 || force == 2 || (force == 0 && ratio_seen && text_ratio > 0.6))
+        return run_two_pass(d_bed, n, st, res, init_start, init_stop);
+    const uint32_t ntiles = (uint32_t)ceil_div(n, kFT);
+    uint64_t* aw = b_faggs.as<uint64_t>(6ull * ntiles + 8);   // tagged look-back words: aggregates, prefixes
+    uint64_t* iw = aw + 3ull * ntiles + 4;
+    uint64_t* fx = b_fx.as<uint64_t>(16);     // [0..3] totals (lines, segments, bytes, saw 0xFF), [4] flags, [5] tile counter
+    uint64_t tcap = std::max<uint64_t>(1u << 20, (uint64_t)(text_ratio * 1.05 * (double)n) + 4096);
+    uint64_t scap = std::max<uint64_t>(4096, 2 * seg_hint);
+    static const uint32_t dbg_mode = [] { const char* e = getenv("STARCH_TF_MODE"); return e ? (uint32_t)atoi(e) : 0u; }();
+    if (dbg_mode == 1) {   // timing experiment: the parse phase alone, then the normal path
+        HIP_CHECK(hipMemsetAsync(fx, 0, 8 * sizeof(uint64_t), st));
+        hipLaunchKernelGGL(k_tf_fused, dim3(ntiles), dim3(kThreads), 0, st, d_bed, n,
+                           reinterpret_cast<uint32_t*>(fx + 5), aw, iw, b_text.as<uint8_t>(tcap + 64),
+                           tcap, b_seg_info.as<SegInfo>(scap + 1), scap, reinterpret_cast<uint32_t*>(fx + 4), fx,
+                           ntiles, 1u);
+    }
+    for (int attempt = 0; attempt < 3; ++attempt) {
+        uint8_t* txt = b_text.as<uint8_t>(tcap + 64);
+        SegInfo* info = b_seg_info.as<SegInfo>(scap + 1);
+        HIP_CHECK(hipMemsetAsync(aw, 0, (6ull * ntiles + 8) * sizeof(uint64_t), st));
+        HIP_CHECK(hipMemsetAsync(fx, 0, 8 * sizeof(uint64_t), st));
+        hipLaunchKernelGGL(k_tf_fused, dim3(ntiles), dim3(kThreads), 0, st, d_bed, n,
+                           reinterpret_cast<uint32_t*>(fx + 5), aw, iw, txt, tcap, info, scap,
+                           reinterpret_cast<uint32_t*>(fx + 4), fx, ntiles, 0u);
+        const uint32_t cg = (uint32_t)std::min<uint64_t>(1024, ceil_div(scap, 256));
+        hipLaunchKernelGGL(k_seg_close_dev, dim3(cg), dim3(256), 0, st, info, fx, scap);
+        HIP_CHECK(hipGetLastError());
+        uint64_t h[5];
+        HIP_CHECK(hipMemcpyAsync(h, fx, sizeof(h), hipMemcpyDeviceToHost, st));
+        HIP_CHECK(hipStreamSynchronize(st));
+        const uint32_t flags = (uint32_t)h[4];
+        static const bool dbg = getenv("STARCH_TF_DEBUG") != nullptr;
+        if (dbg) fprintf(stderr, "[tf] attempt %d flags %u lines %llu segs %llu bytes %llu\n", attempt, flags,
+                         (unsigned long long)h[0], (unsigned long long)h[1], (unsigned long long)h[2]);
+        if (flags & (FX_FAIL | FX_FALLBACK)) break;                 // stale values / long lines: two-pass path
+        if (flags & (FX_TEXT_CAP | FX_SEG_CAP)) {                     // grow to the exact totals and rerun
+            tcap = std::max(tcap, h[2] + 64);
+            scap = std::max(scap, h[1] + 1);
+            continue;
+        }
+        res.n_lines = h[0];
+        res.n_segments = h[1];
+        res.text_bytes = h[2];
+        res.ff_pos = h[3] ? 0 : ~0ull;                                 // (a 0xFF was met; its offset is not kept)
+        text_ratio = (double)h[2] / (double)n;
+        ratio_seen = true;
+        seg_hint = h[1];
+        text = txt;
+        seg_info_dev = info;
+        return;
+    }
+    run_two_pass(d_bed, n, st, res, init_start, init_stop);
+}
+
+void TransformWorkspace::run_two_pass(const uint8_t* d_bed, uint64_t n, hipStream_t st, TransformResult& res,
+                                      int64_t init_start, int64_t init_stop)
 {
     res = TransformResult();
     uint64_t ntile = ceil_div(n, kTileBytes);
@@ -985,4 +1475,8 @@ void TransformWorkspace::run(const uint8_t* d_bed, uint64_t n, hipStream_t st, T
     res.n_segments = nseg;
     res.text_bytes = ttot;
     seg_info_dev = info;
+    if (n) {
+        text_ratio = (double)ttot / (double)n;
+        ratio_seen = true;
+    }
 }

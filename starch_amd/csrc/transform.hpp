@@ -18,11 +18,18 @@ struct TransformResult {
 
 struct TransformWorkspace {
     DevBuf b_tile_cnt, b_tile_off, b_scal, b_tmp, b_line_end, b_start, b_stop, b_flags, b_rem_beg, b_rem_len,
-        b_chr_len, b_idx, b_vcopy, b_out_len, b_seg_flag, b_out_off, b_seg_ord, b_seg_first, b_seg_info, b_text;
+        b_chr_len, b_idx, b_vcopy, b_out_len, b_seg_flag, b_out_off, b_seg_ord, b_seg_first, b_seg_info, b_text,
+        b_fstatus, b_faggs, b_fx;
+    double text_ratio = 1.0;          // text bytes per input byte of the last run (single-pass capacity, path choice)
+    bool ratio_seen = false;
+    uint64_t seg_hint = 0;
     uint8_t* text = nullptr;          // device: transformed text (valid after run)
     SegInfo* seg_info_dev = nullptr;  // device: n_segments entries
     // init_start/init_stop: bed_t.start/stop before the first line (stale sscanf
     // values carried into a shard that starts mid-input, hpp:306-307)
     void run(const uint8_t* d_bed, uint64_t n, hipStream_t st, TransformResult& res, int64_t init_start = 0,
              int64_t init_stop = 0);
+    // line-index based path (k_count_nl / k_index_nl, then k_tf1 + k_tf2 or the general path)
+    void run_two_pass(const uint8_t* d_bed, uint64_t n, hipStream_t st, TransformResult& res, int64_t init_start,
+                      int64_t init_stop);
 };

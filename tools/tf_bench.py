@@ -1,0 +1,36 @@
+#!/usr/bin/env python3
+"""Transform-stage micro-benchmark on the GPU (dev tool): cfg2/cfg4 input in
+HBM, starch_transform_device repeated, HIP-event ms per call."""
+import argparse
+import ctypes
+import os
+import sys
+
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--kind", type=int, default=0)
+    ap.add_argument("--lines", type=int, default=100_000_000)
+    ap.add_argument("--reps", type=int, default=5)
+    a = ap.parse_args()
+    import torch
+    import starch_amd
+    n = sum(starch_amd.gen_bed_sizes(a.kind, a.lines))
+    host = torch.empty(n + 64, dtype=torch.uint8, pin_memory=True)
+    starch_amd.gen_bed(a.kind, a.lines, into=ctypes.c_void_p(host.data_ptr()))
+    dev = host.to("cuda")
+    c = starch_amd.Starch(0)
+    ms = []
+    for _ in range(a.reps):
+        c.transform_device(dev.data_ptr(), n)
+        ms.append(c.stats()["ms_transform"])
+    st = c.stats()
+    print("kind %d bytes %d lines %d text %d segs %d  ms %s  best %.3f ms = %.1f GB/s" % (
+        a.kind, n, st["n_lines"], st["text_bytes"], st["n_segments"], " ".join("%.3f" % x for x in ms), min(ms),
+        n / min(ms) / 1e6))
+
+
+if __name__ == "__main__":
+    main()
