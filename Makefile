@@ -2,13 +2,13 @@
 # here; the built .so/binary travel to the GPU box with the repo snapshot.
 HIPCC ?= /opt/rocm/bin/hipcc
 ARCH ?= gfx950
-BUILD := starch_amd/_build
+BUILD ?= starch_amd/_build
 CSRC := starch_amd/csrc
 HIPSRC := $(wildcard $(CSRC)/*.hip)
 CPPSRC := $(wildcard $(CSRC)/*.cpp)
 OBJS := $(patsubst $(CSRC)/%.hip,$(BUILD)/%.o,$(HIPSRC)) $(patsubst $(CSRC)/%.cpp,$(BUILD)/%.o,$(CPPSRC))
 HDRS := $(wildcard $(CSRC)/*.hpp) include/starch_amd.h include/starch_bzlib.h
-FLAGS := -O3 -std=c++17 -fPIC -Wall -Wno-unused-function -Wno-unused-variable --offload-arch=$(ARCH)
+FLAGS := -O3 -std=c++17 -fPIC -Wall -Wno-unused-function -Wno-unused-variable --offload-arch=$(ARCH) $(EXTRA)
 
 all: $(BUILD)/libstarch_amd.so $(BUILD)/starch3 $(BUILD)/starch3_hpp_example oracle
 

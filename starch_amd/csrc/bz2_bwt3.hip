@@ -661,7 +661,10 @@ __global__ void __launch_bounds__(LT) k3_part_l(Ctx c, const uint64_t* __restric
         for (int i = tid; i < LW * 256; i += LT) (&wh[0][0])[i] = 0;
         if (tid == 0) big[256] = 0;
         __syncthreads();
-        constexpr int PU = 4;                          // elements in flight per thread
+#ifndef STARCH_PART_PU
+#define STARCH_PART_PU 4
+#endif
+        constexpr int PU = STARCH_PART_PU;             // elements in flight per thread
         for (uint32_t i0 = 0; i0 < m; i0 += PU * LT) {
             uint32_t d[PU];
 #pragma unroll

@@ -135,35 +135,155 @@ __device__ __forceinline__ void put_run(Out16& out, uint32_t z)   // bijective b
     }
 }
 
-// ---- alphabets <= 16: five launches over (block, 512-symbol chunk) ----
+// ---- alphabets <= 32: five launches over (block, 512-symbol chunk) ----
 // Per-chunk state lives in the (free) key scratch of the block's batch slot:
-//   [0, 2C)   NibState local recency list          (k_mtf_local)
-//   [2C, 3C)  start list of the chunk              (k_mtf_scan_lists)
-//   [3C, 5C)  RunSum of the chunk's MTF indices    (k_mtf_runs)
-//   [5C, 6C)  (zeros carried in, output offset)    (k_mtf_scan_runs)
+//   [0, SW*C)          local recency list + set    (k_mtf_local)
+//   [SW*C, (SW+LW)*C)  start list of the chunk     (k_mtf_scan_lists)
+//   then RunSum (2 words) and (zeros carried in, output offset) (1 word)
 // (u64 words, C = chunks per slot).  The three chunk passes are flat grids,
 // so every CU has work whatever the block count; the two scans are one
-// workgroup per block over <= 2 chunks per thread.
+// workgroup per block over <= 2 chunks per thread.  The list lives in
+// registers: 16 nibbles of a u64 for <= 16 symbols (NibP, BED3 text), 32
+// bytes in four u64 for 17..32 symbols (ByteP, narrowPeak and other BED6+
+// text); both do the move-to-front branch-free with SWAR compares.
 constexpr uint32_t MCS = 512;                 // symbols per chunk (4 lines)
 constexpr int MCT = 256;                      // threads of the chunk kernels
 constexpr int MST = 1024;                     // threads of the scan kernels
 
+struct NibP {
+    using State = NibState;
+    using List = uint64_t;
+    static constexpr uint32_t LO = 1, HI = 16;        // nInUse range handled
+    static constexpr uint32_t SW = 2, LW = 1;         // u64 words per State / List
+    __device__ static State empty() { State r; r.list = 0; r.set = 0; r.cnt = 0; return r; }
+    __device__ static void add(State& st, uint32_t s)
+    {
+        if (!((st.set >> s) & 1u)) { st.set |= 1u << s; st.list |= (uint64_t)s << (4 * st.cnt); ++st.cnt; }
+    }
+    __device__ static State compose(const State& c, const State& d) { return nib_compose(c, d); }
+    __device__ static State identity(uint32_t nin)
+    {
+        State st;
+        st.list = 0;
+        for (uint32_t i = 0; i < nin; ++i) st.list |= (uint64_t)i << (4 * i);
+        st.set = nin >= 32 ? ~0u : (1u << nin) - 1u;
+        st.cnt = nin;
+        return st;
+    }
+    __device__ static List list_of(const State& st) { return st.list; }
+    __device__ static uint32_t mtf(List& L, uint32_t s) { return nib_mtf(L, s); }
+};
+
+struct ByteState {        // transform L -> list ++ (L \ set); list byte i = i-th symbol, unused bytes 0xFF
+    uint64_t w[4];
+    uint32_t set;         // 32-bit symbol set
+    uint32_t cnt;
+};
+struct ByteList { uint64_t w[4]; };
+
+struct ByteP {
+    using State = ByteState;
+    using List = ByteList;
+    static constexpr uint32_t LO = 17, HI = 32;
+    static constexpr uint32_t SW = 5, LW = 4;
+    __device__ static void put(uint64_t* w, uint32_t i, uint32_t s)
+    {
+        const uint32_t j = i >> 3, sh = 8 * (i & 7);
+#pragma unroll
+        for (uint32_t q = 0; q < 4; ++q)
+            if (q == j) w[q] = (w[q] & ~(0xFFull << sh)) | ((uint64_t)s << sh);
+    }
+    __device__ static uint32_t get(const uint64_t* w, uint32_t i)
+    {
+        const uint32_t j = i >> 3;
+        const uint64_t x = j == 0 ? w[0] : j == 1 ? w[1] : j == 2 ? w[2] : w[3];
+        return (uint32_t)(x >> (8 * (i & 7))) & 0xFFu;
+    }
+    __device__ static State empty()
+    {
+        State r;
+        r.w[0] = r.w[1] = r.w[2] = r.w[3] = ~0ull;
+        r.set = 0;
+        r.cnt = 0;
+        return r;
+    }
+    __device__ static void add(State& st, uint32_t s)
+    {
+        if (!((st.set >> s) & 1u)) { st.set |= 1u << s; put(st.w, st.cnt, s); ++st.cnt; }
+    }
+    __device__ static State compose(const State& c, const State& d)   // apply c, then d
+    {
+        State r = d;
+        for (uint32_t i = 0; i < c.cnt; ++i) {
+            const uint32_t sym = get(c.w, i);
+            if (!((d.set >> sym) & 1u)) { put(r.w, r.cnt, sym); ++r.cnt; }
+        }
+        r.set = c.set | d.set;
+        return r;
+    }
+    __device__ static State identity(uint32_t nin)
+    {
+        State st = empty();
+        for (uint32_t i = 0; i < nin; ++i) put(st.w, i, i);
+        st.set = nin >= 32 ? ~0u : (1u << nin) - 1u;
+        st.cnt = nin;
+        return st;
+    }
+    __device__ static List list_of(const State& st)
+    {
+        List l;
+        l.w[0] = st.w[0]; l.w[1] = st.w[1]; l.w[2] = st.w[2]; l.w[3] = st.w[3];
+        return l;
+    }
+    // one MTF step: index of s (s must be in the list); zero-byte search per
+    // word (the lowest flagged byte is exact), then bytes 0..k-1 move up one
+    __device__ static uint32_t mtf(List& L, uint32_t s)
+    {
+        const uint64_t pat = (uint64_t)s * 0x0101010101010101ull;
+        uint64_t z[4];
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+            const uint64_t x = L.w[j] ^ pat;
+            z[j] = (x - 0x0101010101010101ull) & ~x & 0x8080808080808080ull;
+        }
+        const uint32_t k = z[0] ? ((uint32_t)__builtin_ctzll(z[0]) >> 3)
+                         : z[1] ? 8u + ((uint32_t)__builtin_ctzll(z[1]) >> 3)
+                         : z[2] ? 16u + ((uint32_t)__builtin_ctzll(z[2]) >> 3)
+                                : 24u + ((uint32_t)__builtin_ctzll(z[3]) >> 3);
+        const uint32_t jk = k >> 3, kb = k & 7u;
+        const uint64_t m = kb == 7u ? ~0ull : ((1ull << (8u * kb + 8u)) - 1ull);   // bytes [0, kb]
+        uint64_t carry = s;
+#pragma unroll
+        for (uint32_t j = 0; j < 4; ++j) {
+            const uint64_t nv = (L.w[j] << 8) | carry;
+            carry = L.w[j] >> 56;
+            L.w[j] = j < jk ? nv : (j == jk ? ((nv & m) | (L.w[j] & ~m)) : L.w[j]);
+        }
+        return k;
+    }
+};
+
+template <class P>
 struct MtfScr {
     uint64_t* base;
     uint32_t C;
-    __device__ NibState* nst() const { return reinterpret_cast<NibState*>(base); }
-    __device__ uint64_t* l0() const { return base + 2ull * C; }
-    __device__ RunSum* rs() const { return reinterpret_cast<RunSum*>(base + 3ull * C); }
-    __device__ uint2* zo() const { return reinterpret_cast<uint2*>(base + 5ull * C); }
+    __device__ typename P::State* st() const { return reinterpret_cast<typename P::State*>(base); }
+    __device__ typename P::List* l0() const { return reinterpret_cast<typename P::List*>(base + (uint64_t)P::SW * C); }
+    __device__ RunSum* rs() const { return reinterpret_cast<RunSum*>(base + (uint64_t)(P::SW + P::LW) * C); }
+    __device__ uint2* zo() const { return reinterpret_cast<uint2*>(base + (uint64_t)(P::SW + P::LW + 2) * C); }
 };
 
-__device__ __forceinline__ MtfScr mtf_scr(uint64_t* K, uint64_t kstride, uint32_t slot, uint32_t C)
+template <class P>
+__device__ __forceinline__ MtfScr<P> mtf_scr(uint64_t* K, uint64_t kstride, uint32_t slot, uint32_t C)
 {
-    MtfScr m;
+    MtfScr<P> m;
     m.base = K + (uint64_t)slot * kstride;
     m.C = C;
     return m;
 }
+
+template <class P>
+__device__ __forceinline__ bool mtf_mine(uint32_t nin) { return nin >= P::LO && nin <= P::HI; }
 
 // visit symbols [a, e) of a chunk in order: 16-byte pieces, the next piece's
 // load issued before the current one is processed (one load in flight, few
@@ -204,6 +324,7 @@ __device__ __forceinline__ void visit_chunk_lines(const uint8_t* ll, uint32_t a,
     }
 }
 
+template <class P>
 __global__ void __launch_bounds__(MCT) k_mtf_local(const BlockDesc* __restrict__ blocks, uint32_t b0,
                                                    const uint8_t* __restrict__ LL, uint64_t ll_stride,
                                                    uint64_t* __restrict__ K, uint64_t kstride, uint32_t C)
@@ -212,17 +333,14 @@ __global__ void __launch_bounds__(MCT) k_mtf_local(const BlockDesc* __restrict__
     const uint32_t n = blocks[b].n, nin = blocks[b].n_in_use;
     const uint32_t ch = blockIdx.x * MCT + threadIdx.x;
     const uint32_t a = ch * MCS;
-    if (nin > 16 || a >= n) return;
+    if (!mtf_mine<P>(nin) || a >= n) return;
     const uint32_t e = a + MCS < n ? a + MCS : n;
     const uint8_t* ll = LL + (uint64_t)slot * ll_stride;
     // local(c): the chunk's symbols by last occurrence, most recent first;
     // backward, line by line, until every symbol of the block has been seen
-    NibState loc;
-    loc.list = 0; loc.set = 0; loc.cnt = 0;
+    typename P::State loc = P::empty();
     const uint32_t full = a + ((e - a) & ~(LINE - 1));
-    auto add = [&](uint32_t s) {
-        if (!((loc.set >> s) & 1u)) { loc.set |= 1u << s; loc.list |= (uint64_t)s << (4 * loc.cnt); ++loc.cnt; }
-    };
+    auto add = [&](uint32_t s) { P::add(loc, s); };
     if (full < e) {
         const uint32_t lim = e - full;
         visit_line<false>(ll + full, [&](int k, uint32_t s) { if ((uint32_t)k < lim) add(s); });
@@ -232,48 +350,45 @@ __global__ void __launch_bounds__(MCT) k_mtf_local(const BlockDesc* __restrict__
         j0 -= LINE;
         visit_line<false>(ll + j0, [&](int, uint32_t s) { add(s); });
     }
-    mtf_scr(K, kstride, slot, C).nst()[ch] = loc;
+    mtf_scr<P>(K, kstride, slot, C).st()[ch] = loc;
 }
 
 // start list of every chunk: exclusive scan of the local-list composition
+template <class P>
 __global__ void __launch_bounds__(MST) k_mtf_scan_lists(const BlockDesc* __restrict__ blocks, uint32_t b0,
                                                         uint64_t* __restrict__ K, uint64_t kstride, uint32_t C)
 {
-    __shared__ NibState sh[MST];
+    __shared__ typename P::State sh[MST];
     const int tid = threadIdx.x;
     const uint32_t slot = blockIdx.x, b = b0 + slot;
     const uint32_t n = blocks[b].n, nin = blocks[b].n_in_use;
-    if (nin > 16) return;
+    if (!mtf_mine<P>(nin)) return;
     const uint32_t nch = (n + MCS - 1) / MCS;
     const uint32_t per = (nch + MST - 1) / MST;          // <= 2 for 900 KB blocks
-    const MtfScr ms = mtf_scr(K, kstride, slot, C);
+    const MtfScr<P> ms = mtf_scr<P>(K, kstride, slot, C);
     const uint32_t c0 = tid * per;
-    NibState agg;
-    agg.list = 0; agg.set = 0; agg.cnt = 0;
+    typename P::State agg = P::empty();
     for (uint32_t q = 0; q < per; ++q)
-        if (c0 + q < nch) agg = nib_compose(agg, ms.nst()[c0 + q]);
+        if (c0 + q < nch) agg = P::compose(agg, ms.st()[c0 + q]);
     sh[tid] = agg;
     __syncthreads();
     for (int d = 1; d < MST; d <<= 1) {                 // inclusive scan of the composition
-        const NibState v = (tid >= d) ? nib_compose(sh[tid - d], sh[tid]) : sh[tid];
+        const typename P::State v = (tid >= d) ? P::compose(sh[tid - d], sh[tid]) : sh[tid];
         __syncthreads();
         sh[tid] = v;
         __syncthreads();
     }
-    NibState st;
-    st.list = 0;
-    for (uint32_t i = 0; i < nin; ++i) st.list |= (uint64_t)i << (4 * i);
-    st.set = (1u << nin) - 1u;
-    st.cnt = nin;
-    if (tid) st = nib_compose(st, sh[tid - 1]);
+    typename P::State st = P::identity(nin);
+    if (tid) st = P::compose(st, sh[tid - 1]);
     for (uint32_t q = 0; q < per; ++q) {
         if (c0 + q >= nch) break;
-        ms.l0()[c0 + q] = st.list;
-        st = nib_compose(st, ms.nst()[c0 + q]);
+        ms.l0()[c0 + q] = P::list_of(st);
+        st = P::compose(st, ms.st()[c0 + q]);
     }
 }
 
 // zero-run summary of each chunk's MTF indices (branch-free per symbol)
+template <class P>
 __global__ void __launch_bounds__(MCT) k_mtf_runs(const BlockDesc* __restrict__ blocks, uint32_t b0,
                                                   const uint8_t* __restrict__ LL, uint64_t ll_stride,
                                                   uint64_t* __restrict__ K, uint64_t kstride, uint32_t C)
@@ -282,13 +397,13 @@ __global__ void __launch_bounds__(MCT) k_mtf_runs(const BlockDesc* __restrict__ 
     const uint32_t n = blocks[b].n, nin = blocks[b].n_in_use;
     const uint32_t ch = blockIdx.x * MCT + threadIdx.x;
     const uint32_t a = ch * MCS;
-    if (nin > 16 || a >= n) return;
+    if (!mtf_mine<P>(nin) || a >= n) return;
     const uint32_t e = a + MCS < n ? a + MCS : n;
-    const MtfScr ms = mtf_scr(K, kstride, slot, C);
-    uint64_t L = ms.l0()[ch];
+    const MtfScr<P> ms = mtf_scr<P>(K, kstride, slot, C);
+    typename P::List L = ms.l0()[ch];
     uint32_t z = 0, nz = 0, lz = 0, inner = 0;
     visit_chunk(LL + (uint64_t)slot * ll_stride, a, e, [&](uint32_t s) {
-        const uint32_t x = nib_mtf(L, s);
+        const uint32_t x = P::mtf(L, s);
         const uint32_t nzf = x != 0 ? 1u : 0u;
         inner += (nzf & nz) ? 1u + (31u - __clz(z + 1u)) : 0u;
         lz = (nzf & (nz ^ 1u)) ? z : lz;
@@ -305,6 +420,7 @@ __global__ void __launch_bounds__(MCT) k_mtf_runs(const BlockDesc* __restrict__ 
 
 // exclusive scan of the run summaries: zeros carried into each chunk and its
 // first output index; the block's trailing run, EOB and n_mtf
+template <class P>
 __global__ void __launch_bounds__(MST) k_mtf_scan_runs(BlockDesc* __restrict__ blocks, uint32_t b0,
                                                        uint64_t* __restrict__ K, uint64_t kstride, uint32_t C,
                                                        uint16_t* __restrict__ mtfv_all, uint64_t mtf_stride)
@@ -313,10 +429,10 @@ __global__ void __launch_bounds__(MST) k_mtf_scan_runs(BlockDesc* __restrict__ b
     const int tid = threadIdx.x;
     const uint32_t slot = blockIdx.x, b = b0 + slot;
     const uint32_t n = blocks[b].n, nin = blocks[b].n_in_use;
-    if (nin > 16) return;
+    if (!mtf_mine<P>(nin)) return;
     const uint32_t nch = (n + MCS - 1) / MCS;
     const uint32_t per = (nch + MST - 1) / MST;
-    const MtfScr ms = mtf_scr(K, kstride, slot, C);
+    const MtfScr<P> ms = mtf_scr<P>(K, kstride, slot, C);
     const uint32_t c0 = tid * per;
     RunSum agg;
     agg.nz = 0; agg.lz = 0; agg.tz = 0; agg.inner = 0;
@@ -356,6 +472,7 @@ __global__ void __launch_bounds__(MST) k_mtf_scan_runs(BlockDesc* __restrict__ b
 }
 
 // re-run each chunk's MTF and emit RUNA/RUNB + symbols at its offset
+template <class P>
 __global__ void __launch_bounds__(MCT) k_mtf_emit(const BlockDesc* __restrict__ blocks, uint32_t b0,
                                                   const uint8_t* __restrict__ LL, uint64_t ll_stride,
                                                   const uint64_t* __restrict__ K, uint64_t kstride, uint32_t C,
@@ -365,16 +482,16 @@ __global__ void __launch_bounds__(MCT) k_mtf_emit(const BlockDesc* __restrict__ 
     const uint32_t n = blocks[b].n, nin = blocks[b].n_in_use;
     const uint32_t ch = blockIdx.x * MCT + threadIdx.x;
     const uint32_t a = ch * MCS;
-    if (nin > 16 || a >= n) return;
+    if (!mtf_mine<P>(nin) || a >= n) return;
     const uint32_t e = a + MCS < n ? a + MCS : n;
-    const MtfScr ms = mtf_scr(const_cast<uint64_t*>(K), kstride, slot, C);
-    uint64_t L = ms.l0()[ch];
+    const MtfScr<P> ms = mtf_scr<P>(const_cast<uint64_t*>(K), kstride, slot, C);
+    typename P::List L = ms.l0()[ch];
     const uint2 zo = ms.zo()[ch];
     Out16 out;
     out.init(mtfv_all + (uint64_t)b * mtf_stride, zo.y);
     uint32_t z = zo.x;
     visit_chunk_lines(LL + (uint64_t)slot * ll_stride, a, e, [&](uint32_t s) {
-        const uint32_t x = nib_mtf(L, s);
+        const uint32_t x = P::mtf(L, s);
         if (x == 0) {
             ++z;
         } else {
@@ -410,7 +527,7 @@ __global__ void __launch_bounds__(MT) k_mtf_big(BlockDesc* __restrict__ blocks, 
     const uint32_t b = b0 + slot;
     const uint32_t n = blocks[b].n;
     const uint32_t nin = blocks[b].n_in_use;
-    if (nin <= 16) return;
+    if (nin <= ByteP::HI) return;                    // <= 32 symbols: the register-list kernels
     for (int i = tid; i < NF * 258; i += MT) (&freq[0][0])[i] = 0;
     const uint8_t* ll = LL + (uint64_t)slot * ll_stride;
     uint8_t* idx = scratch + (uint64_t)slot * scratch_stride;            // MTF indices
@@ -598,17 +715,22 @@ void launch_mtf(BlockDesc* blocks, uint32_t b0, uint32_t nb, const uint8_t* blkb
 {
     (void)blkbytes;
     (void)stride;
-    // alphabets <= 16: chunk passes over the key scratch (free after the sort)
+    // alphabets <= 32: chunk passes over the key scratch (free after the sort)
     const uint32_t C = (uint32_t)((scr.stride + MCS - 1) / MCS);
     const uint64_t kstride = scr.stride;                     // u64 words per slot
     const dim3 gch((C + MCT - 1) / MCT, nb);
-    hipLaunchKernelGGL(k_mtf_local, gch, dim3(MCT), 0, st, blocks, b0, scr.LL, scr.stride, scr.K, kstride, C);
-    hipLaunchKernelGGL(k_mtf_scan_lists, dim3(nb), dim3(MST), 0, st, blocks, b0, scr.K, kstride, C);
-    hipLaunchKernelGGL(k_mtf_runs, gch, dim3(MCT), 0, st, blocks, b0, scr.LL, scr.stride, scr.K, kstride, C);
-    hipLaunchKernelGGL(k_mtf_scan_runs, dim3(nb), dim3(MST), 0, st, blocks, b0, scr.K, kstride, C, mtfv,
-                       mtf_stride);
-    hipLaunchKernelGGL(k_mtf_emit, gch, dim3(MCT), 0, st, blocks, b0, scr.LL, scr.stride, scr.K, kstride, C, mtfv,
-                       mtf_stride);
+    auto run = [&](auto pol) {
+        using P = decltype(pol);
+        hipLaunchKernelGGL(k_mtf_local<P>, gch, dim3(MCT), 0, st, blocks, b0, scr.LL, scr.stride, scr.K, kstride, C);
+        hipLaunchKernelGGL(k_mtf_scan_lists<P>, dim3(nb), dim3(MST), 0, st, blocks, b0, scr.K, kstride, C);
+        hipLaunchKernelGGL(k_mtf_runs<P>, gch, dim3(MCT), 0, st, blocks, b0, scr.LL, scr.stride, scr.K, kstride, C);
+        hipLaunchKernelGGL(k_mtf_scan_runs<P>, dim3(nb), dim3(MST), 0, st, blocks, b0, scr.K, kstride, C, mtfv,
+                           mtf_stride);
+        hipLaunchKernelGGL(k_mtf_emit<P>, gch, dim3(MCT), 0, st, blocks, b0, scr.LL, scr.stride, scr.K, kstride, C,
+                           mtfv, mtf_stride);
+    };
+    run(NibP{});
+    run(ByteP{});
     // large alphabets: index bytes + per-chunk lists in the (free) key scratch
     hipLaunchKernelGGL(k_mtf_big, dim3(nb), dim3(MT), 0, st, blocks, b0, scr.LL, scr.stride,
                        reinterpret_cast<uint8_t*>(scr.K), scr.stride * sizeof(uint64_t), mtfv, mtf_stride, tabs);

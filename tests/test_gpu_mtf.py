@@ -1,0 +1,49 @@
+"""MTF/RUNA-RUNB (bz:compress.c:119-231) across the alphabet-size paths: <= 16
+symbols (nibble lists), 17..32 (byte lists in registers), > 32 (LDS lists),
+each against the reference libbz2 stream, including runs of zeros that cross
+512-symbol chunks and multi-block inputs."""
+import random
+
+import pytest
+
+from tests import oracle_lib
+
+pytestmark = pytest.mark.gpu
+
+
+def _ref(data, bs=9):
+    return oracle_lib.ref_bz2(data, bs) if oracle_lib.ref() is not None else oracle_lib.bz2(data, bs)
+
+
+@pytest.fixture(scope="module")
+def ctx():
+    import starch_amd
+    c = starch_amd.Starch(0)
+    yield c
+    c.close()
+
+
+@pytest.mark.parametrize("nsym", [2, 15, 16, 17, 18, 24, 31, 32, 33, 40, 200])
+def test_alphabet_sizes(ctx, nsym):
+    r = random.Random(nsym)
+    alpha = bytes(r.sample(range(256), nsym))
+    out = bytearray()
+    while len(out) < 300_000:
+        k = r.random()
+        if k < 0.2:
+            out += bytes([r.choice(alpha)]) * r.randint(1, 3000)     # long runs: zero runs across chunks
+        elif k < 0.5:
+            w = bytes(r.choice(alpha) for _ in range(r.randint(2, 12)))
+            out += w * r.randint(1, 40)
+        else:
+            out += bytes(r.choice(alpha) for _ in range(r.randint(1, 200)))
+    data = bytes(out)
+    assert ctx.bz2_compress(data, 9) == _ref(data, 9)
+    assert ctx.bz2_compress(data[:150_000], 1) == _ref(data[:150_000], 1)
+
+
+def test_narrowpeak_text_multiblock(ctx):
+    import starch_amd
+    data = starch_amd.gen_bed(1, 300_000, chroms=[13])
+    text, segs = ctx.transform(data)
+    assert ctx.bz2_compress(segs[0][2], 9) == _ref(segs[0][2], 9)
