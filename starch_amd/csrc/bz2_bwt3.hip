@@ -69,6 +69,11 @@ constexpr int MAXT = (900064 + PTILE - 1) / PTILE;   // tiles per block (bs <= 9
 // size classes: W rank-by-compare (one wave), S wave-private LDS sort,
 // M1..M3 workgroup LDS sort, L MSD partition
 constexpr uint32_t W_MAX = 64, S1_MAX = 128, S_MAX = 256, M1_MAX = 1024, M2_MAX = 2048, M3_MAX = 4096;
+// groups above L_MIN are MSD-partitioned (k3_part_l) instead of sorted whole
+#ifndef STARCH_L_MIN
+#define STARCH_L_MIN 4096
+#endif
+constexpr uint32_t L_MIN = STARCH_L_MIN;
 constexpr uint32_t RBITS = 20;          // rank bits (n <= 899,985 < 2^20)
 constexpr uint32_t TEXT_ROUNDS = 4;     // max text-extension rounds before doubling
 
@@ -168,7 +173,8 @@ __device__ __forceinline__ void wave_push(uint32_t* ctr, uint64_t* list, bool pr
 // serialise).  Every thread of the workgroup must call it; sh: 16 u32 of LDS.
 __device__ __forceinline__ int size_class(uint32_t m)
 {
-    return m <= W_MAX ? 0 : m <= S1_MAX ? 1 : m <= S_MAX ? 2 : m <= M1_MAX ? 3 : m <= M2_MAX ? 4 : m <= M3_MAX ? 5 : 6;
+    return m <= W_MAX ? 0 : m <= S1_MAX ? 1 : m <= S_MAX ? 2 : m > L_MIN ? 6 : m <= M1_MAX ? 3 : m <= M2_MAX ? 4
+         : m <= M3_MAX ? 5 : 6;
 }
 __device__ __forceinline__ void wg_classify(const Ctx& c, uint32_t* sh, bool pred, uint32_t slot, uint32_t s,
                                             uint32_t m, uint32_t shift, uint32_t par)
@@ -221,6 +227,9 @@ struct KeySrc {
     {
         uint32_t rr = r + off;
         rr = rr >= n ? rr - n : rr;
+#ifdef STARCH_EXP_NOGATHER   // timing experiment only: keys from a cache-resident window (wrong order)
+        rr &= 4095u;
+#endif
         const uint64_t bit = (uint64_t)rr * B;
         const uint64_t q = bit >> 6;
         const uint32_t p = (uint32_t)(bit & 63u);
@@ -230,7 +239,11 @@ struct KeySrc {
     // ... and the last-column symbol of r (the symbol before it), also branch-free
     __device__ __forceinline__ uint64_t key_pss(uint32_t r, uint32_t& ls) const
     {
+#ifdef STARCH_EXP_NOGATHER
+        const uint32_t pr = r & 4095u;
+#else
         const uint32_t pr = r ? r - 1u : n - 1u;
+#endif
         const uint64_t pbit = (uint64_t)pr * B;
         const uint64_t pq = pbit >> 6;
         const uint32_t pp = (uint32_t)(pbit & 63u);
@@ -713,14 +726,14 @@ __global__ void __launch_bounds__(LT) k3_part_l(Ctx c, const uint64_t* __restric
                 if (c.mode) RK[v] = s + ss;
                 if (v == 0) c.blocks[b].orig_ptr = s + ss;
                 nruns = 1;
-            } else if (cc > M3_MAX && sh2 == 0) {
+            } else if (size_class(cc) == 6 && sh2 == 0) {
                 big[atomicAdd(&big[256], 1u)] = tid;   // all keys equal: one group
                 nruns = 1;
             }
         }
         {
             const uint32_t cc = tid < 256 ? cntd[tid] : 0u;
-            const bool push = tid < 256 && cc >= 2 && !(cc > M3_MAX && sh2 == 0);
+            const bool push = tid < 256 && cc >= 2 && !(size_class(cc) == 6 && sh2 == 0);
             wg_classify(c, cls_sh, push, slot, s + (tid < 256 ? st[tid] : 0u), cc, sh2, par ^ 1u);
         }
         if (tid < 256) {
@@ -875,7 +888,13 @@ k3_sort_lds(Ctx c, const uint64_t* __restrict__ items,
     constexpr int NBIN = 1 << DB;
     constexpr int T = NW * 64;
     constexpr int BPT = NBIN / T;                  // bins per thread
-    constexpr uint32_t LIMIT = 256 / E;            // largest sub-bucket ranked by comparison
+#ifndef STARCH_LIM_NUM
+#define STARCH_LIM_NUM 256
+#endif
+#ifndef STARCH_LIM2_NUM
+#define STARCH_LIM2_NUM 512
+#endif
+    constexpr uint32_t LIMIT = STARCH_LIM_NUM / E; // largest sub-bucket ranked by comparison
     __shared__ uint64_t xk_all[IPW][CAP];
     __shared__ uint32_t vb_all[IPW][CAP];          // rotations by group index
     __shared__ uint32_t bst_all[IPW][NBIN + 1];   // sub-bucket starts
@@ -883,7 +902,7 @@ k3_sort_lds(Ctx c, const uint64_t* __restrict__ items,
     __shared__ uint32_t cnt_all[4][256];
     __shared__ uint32_t sc_all[IPW][NW + 1];
     constexpr int NB2 = NW == 1 ? 256 : 1024;      // second-digit bins
-    constexpr uint32_t LIMIT2 = 512 / E;           // largest second-level sub-bucket ranked by comparison
+    constexpr uint32_t LIMIT2 = STARCH_LIM2_NUM / E;   // largest second-level sub-bucket ranked by comparison
     __shared__ uint32_t c2_all[IPW][NB2 + 1];
     __shared__ uint32_t sc2_all[IPW][NW + 1];
     __shared__ uint64_t red_all[4];
@@ -1658,7 +1677,7 @@ void launch_bwt3(BlockDesc* blocks, uint32_t b0, uint32_t nb, const uint8_t* blk
     const uint64_t N = (uint64_t)nb * scr.stride;
     const uint64_t cap_s = N / (W_MAX + 1) + 64, cap_s2 = N / (S1_MAX + 1) + 64, cap_m1 = N / (S_MAX + 1) + 64,
                    cap_m2 = N / (M1_MAX + 1) + 64,
-                   cap_m3 = N / (M2_MAX + 1) + 64, cap_l = N / (M3_MAX + 1) + 64;
+                   cap_m3 = N / (M2_MAX + 1) + 64, cap_l = N / ((L_MIN < M3_MAX ? L_MIN : M3_MAX) + 1) + 64;
     const uint64_t nwg_bin = BIN_MAXWG;
     constexpr uint32_t QSETS = 64, QSET = 32;                   // queue heads + segments per launch
     const uint64_t words = 2 * C_N + 10ull * nb + QSETS * QSET + nwg_bin * nb +
@@ -1714,7 +1733,9 @@ void launch_bwt3(BlockDesc* blocks, uint32_t b0, uint32_t nb, const uint8_t* blk
     auto read_ctr = [&]() {
         HIP_CHECK(hipMemcpyAsync(hctr, c.L.ctr, C_N * sizeof(uint32_t), hipMemcpyDeviceToHost, st));
         HIP_CHECK(hipStreamSynchronize(st));
+#ifndef STARCH_EXP_NOGATHER
         if (hctr[C_ERR]) throw StarchError(-11, "bwt3: group keys do not share 12 top bits");
+#endif
     };
     int dev = 0;
     HIP_CHECK(hipGetDevice(&dev));
