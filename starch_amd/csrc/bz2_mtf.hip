@@ -184,7 +184,9 @@ struct ByteList { uint64_t w[4]; };
 struct ByteP {
     using State = ByteState;
     using List = ByteList;
-    static constexpr uint32_t LO = 17, HI = 32;
+    // <= 30 symbols: the alphabet (nInUse + 2) stays within k_tables32, which
+    // counts mtfFreq itself (k_tables reads the counts k_mtf_big leaves)
+    static constexpr uint32_t LO = 17, HI = 30;
     static constexpr uint32_t SW = 5, LW = 4;
     __device__ static void put(uint64_t* w, uint32_t i, uint32_t s)
     {
@@ -527,7 +529,7 @@ __global__ void __launch_bounds__(MT) k_mtf_big(BlockDesc* __restrict__ blocks, 
     const uint32_t b = b0 + slot;
     const uint32_t n = blocks[b].n;
     const uint32_t nin = blocks[b].n_in_use;
-    if (nin <= ByteP::HI) return;                    // <= 32 symbols: the register-list kernels
+    if (nin <= ByteP::HI) return;                    // <= 30 symbols: the register-list kernels
     for (int i = tid; i < NF * 258; i += MT) (&freq[0][0])[i] = 0;
     const uint8_t* ll = LL + (uint64_t)slot * ll_stride;
     uint8_t* idx = scratch + (uint64_t)slot * scratch_stride;            // MTF indices

@@ -359,6 +359,28 @@ __global__ void __launch_bounds__(64) k_cut(const StreamIn* __restrict__ streams
         uint64_t block_end = end, wblock_end = wend;
         if (wend >= target) {
             uint64_t lo = t0 + (bs - beg) / kTB, hi = t1;   // Wstart(lo) <= wbs < target <= Wstart(hi)
+            // RLE1 sizes run close to text sizes (a byte weighs 0..2), so the
+            // crossing tile sits near lo + (target - W(lo)) / kTB: one window of
+            // 64 tiles around that guess, one round trip; bisection otherwise
+            {
+                const uint64_t wl = tile_wpre[lo] - w0;
+                uint64_t g = lo + (target > wl ? (target - wl) / kTB : 0);
+                uint64_t a = g > lo + 32 ? g - 32 : lo;
+                if (a + 64 > hi) a = hi > lo + 64 ? hi - 64 : lo;
+                const uint64_t t = a + (uint64_t)lane;
+                const bool ge = t < hi && tile_wpre[t] - w0 >= target;
+                const uint64_t ball = __ballot(ge);
+                const bool below_all = (tile_wpre[a] - w0) < target;   // the window starts below the target
+                if (ball && below_all) {         // crossing inside the window: adjacent (lo, hi)
+                    const uint64_t f = a + (uint64_t)(__ffsll((unsigned long long)ball) - 1);
+                    hi = f;
+                    lo = f - 1;
+                } else if (ball) {               // W(a) >= target: before the window (a > lo)
+                    hi = a;
+                } else if (a + 63 < hi) {        // after the window
+                    lo = a + 63;
+                }
+            }
             while (hi - lo > 1) {
                 uint64_t mid = (lo + hi) >> 1;
                 if (tile_wpre[mid] - w0 < target) lo = mid; else hi = mid;

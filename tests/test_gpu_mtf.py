@@ -42,6 +42,23 @@ def test_alphabet_sizes(ctx, nsym):
     assert ctx.bz2_compress(data[:150_000], 1) == _ref(data[:150_000], 1)
 
 
+@pytest.mark.parametrize("nsym", [29, 30, 31, 32])
+def test_alphabet_edges_without_runs(ctx, nsym):
+    """No run of 4 (no RLE1 count bytes): nInUse is exactly nsym, at the
+    boundary between the register-list path (<= 30) and the LDS path."""
+    r = random.Random(100 + nsym)
+    alpha = list(range(65, 65 + nsym))
+    out, prev = [], None
+    while len(out) < 200_000:
+        c = r.choice(alpha)
+        if c == prev:
+            continue
+        out.append(c)
+        prev = c
+    data = bytes(out)
+    assert ctx.bz2_compress(data, 9) == _ref(data, 9)
+
+
 def test_narrowpeak_text_multiblock(ctx):
     import starch_amd
     data = starch_amd.gen_bed(1, 300_000, chroms=[13])
