@@ -236,7 +236,9 @@ struct KeySrc {
         const uint64_t v = (pss[q] << p) | ((pss[q + 1] >> 1) >> (63u - p));
         return v >> (64u - kbits);
     }
-    // ... and the last-column symbol of r (the symbol before it), also branch-free
+    // ... and the last-column symbol of r (the symbol before it): its B bits sit
+    // right before the key window, so three consecutive words cover both
+    // (rotation 0 wraps: its symbol is the block's last)
     __device__ __forceinline__ uint64_t key_pss(uint32_t r, uint32_t& ls) const
     {
 #ifdef STARCH_EXP_NOGATHER
@@ -244,6 +246,20 @@ struct KeySrc {
 #else
         const uint32_t pr = r ? r - 1u : n - 1u;
 #endif
+        uint32_t rr = r + off;
+        rr = rr >= n ? rr - n : rr;
+        if (off == 0 && r != 0) {
+            const uint64_t bit0 = (uint64_t)pr * B;
+            const uint64_t q0 = bit0 >> 6;
+            const uint32_t p0 = (uint32_t)(bit0 & 63u);
+            const uint64_t w0 = pss[q0], w1 = pss[q0 + 1], w2 = pss[q0 + 2];
+            ls = (uint32_t)(((w0 << p0) | ((w1 >> 1) >> (63u - p0))) >> (64u - B));
+            const uint32_t ps = p0 + B;                      // key start, relative to word q0
+            const uint64_t a = ps >= 64 ? w1 : w0, b = ps >= 64 ? w2 : w1;
+            const uint32_t p = ps & 63u;
+            const uint64_t v = (a << p) | ((b >> 1) >> (63u - p));
+            return v >> (64u - kbits);
+        }
         const uint64_t pbit = (uint64_t)pr * B;
         const uint64_t pq = pbit >> 6;
         const uint32_t pp = (uint32_t)(pbit & 63u);
