@@ -127,6 +127,24 @@ int starch_archive_layout(const uint64_t* unit_of, const uint64_t* bytes, uint64
 int starch_encode_multi_host(starch_ctx* const* ctxs, int nctx, const void* bed, uint64_t n,
                              const starch_options* opt);
 
+/* Streaming ingestion (replaces the reference's line-at-a-time
+ * produce_line / consume_line hand-off, include/starch3api.hpp:158-345, and
+ * the per-chromosome flush, hpp:393-407).  Feed host BED bytes in pieces of
+ * any size (lines may straddle pieces); whenever at least batch_bytes
+ * (0 = 256 MiB) are held, everything before the last chromosome change among
+ * the complete lines is encoded on the GPU and its finished streams become
+ * readable with starch_stream_read (the magic is readable at once).
+ * starch_stream_end encodes the rest and appends the index.  The bytes read
+ * out, in order, are exactly the archive starch_encode_host gives for the
+ * concatenated input.  A 0xFF byte ends the input (hpp:181): later bytes are
+ * ignored.  After end, segments/stats describe the whole stream; the archive
+ * accessors below report STARCH_ERR_STATE (the bytes went out by read). */
+int starch_stream_begin(starch_ctx* ctx, const starch_options* opt, uint64_t batch_bytes);
+int starch_stream_feed(starch_ctx* ctx, const void* bed, uint64_t n);
+int starch_stream_end(starch_ctx* ctx);
+int starch_stream_available(starch_ctx* ctx, uint64_t* n);
+int starch_stream_read(starch_ctx* ctx, void* dst, uint64_t cap, uint64_t* len);
+
 int starch_archive_size(starch_ctx* ctx, uint64_t* n);
 int starch_archive_device(starch_ctx* ctx, const void** d_ptr);
 int starch_archive_copy(starch_ctx* ctx, void* dst, uint64_t cap);

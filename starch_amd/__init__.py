@@ -120,6 +120,11 @@ def load():
         "starch_archive_layout": ([pu64, pu64, u64, u64, pu64, pu64, pu64], ctypes.c_int),
         "starch_encode_multi_host": ([ctypes.POINTER(vp), ctypes.c_int, ctypes.c_char_p, u64,
                                       ctypes.POINTER(Options)], ctypes.c_int),
+        "starch_stream_begin": ([vp, ctypes.POINTER(Options), u64], ctypes.c_int),
+        "starch_stream_feed": ([vp, vp, u64], ctypes.c_int),
+        "starch_stream_end": ([vp], ctypes.c_int),
+        "starch_stream_available": ([vp, pu64], ctypes.c_int),
+        "starch_stream_read": ([vp, vp, u64, pu64], ctypes.c_int),
     }
     for name, (args, res) in sig.items():
         f = getattr(L, name)
@@ -212,6 +217,47 @@ class Starch:
         o = self._opts(emit_index)
         _check(self._L.starch_encode_host(self._h, ctypes.cast(ctypes.c_void_p(ptr), ctypes.c_char_p), n,
                                           ctypes.byref(o)), self._h)
+
+    # -- streaming ingestion (starch_stream_*) ----------------------------------
+    def stream_begin(self, batch_bytes=0, emit_index=True, reference_compat=False):
+        """Start a streamed encode; feed pieces, read archive bytes as they finish."""
+        self._stream_opts = self._opts(emit_index, reference_compat)
+        _check(self._L.starch_stream_begin(self._h, ctypes.byref(self._stream_opts), batch_bytes), self._h)
+
+    def stream_feed(self, piece, n=None):
+        """Feed host bytes (bytes-like, or an address with n)."""
+        if n is None:
+            buf = ctypes.c_char_p(bytes(piece)) if not isinstance(piece, bytes) else ctypes.c_char_p(piece)
+            _check(self._L.starch_stream_feed(self._h, ctypes.cast(buf, ctypes.c_void_p), len(piece)), self._h)
+        else:
+            _check(self._L.starch_stream_feed(self._h, ctypes.c_void_p(piece), n), self._h)
+
+    def stream_end(self):
+        _check(self._L.starch_stream_end(self._h), self._h)
+
+    def stream_read(self, into=None, cap=None) -> bytes:
+        """Drain the archive bytes ready so far (or copy up to cap into an address; returns the count)."""
+        if into is not None:
+            k = ctypes.c_uint64()
+            _check(self._L.starch_stream_read(self._h, ctypes.c_void_p(into), cap, ctypes.byref(k)), self._h)
+            return k.value
+        n = ctypes.c_uint64()
+        _check(self._L.starch_stream_available(self._h, ctypes.byref(n)), self._h)
+        buf = ctypes.create_string_buffer(max(1, n.value))
+        k = ctypes.c_uint64()
+        _check(self._L.starch_stream_read(self._h, buf, n.value, ctypes.byref(k)), self._h)
+        return buf.raw[:k.value]
+
+    def compress_stream(self, pieces, batch_bytes=0, emit_index=True, reference_compat=False) -> bytes:
+        """Iterable of BED byte pieces -> the archive (streamed encode)."""
+        self.stream_begin(batch_bytes, emit_index, reference_compat)
+        out = [self.stream_read()]
+        for p in pieces:
+            self.stream_feed(p)
+            out.append(self.stream_read())
+        self.stream_end()
+        out.append(self.stream_read())
+        return b"".join(out)
 
     def archive_into(self, ptr: int, cap: int) -> int:
         """Copy the archive to a host address; returns its size."""

@@ -121,7 +121,8 @@ uint64_t input_limit(const uint8_t* b, uint64_t n)
     return ff ? (uint64_t)(static_cast<const uint8_t*>(ff) - b) : n;
 }
 
-void plan_units(const uint8_t* b, uint64_t n, uint64_t max_units, std::vector<Unit>& out)
+void plan_units(const uint8_t* b, uint64_t n, uint64_t max_units, std::vector<Unit>& out, int64_t init_start0,
+                int64_t init_stop0)
 {
     out.clear();
     const uint64_t lim = input_limit(b, n);
@@ -165,6 +166,7 @@ void plan_units(const uint8_t* b, uint64_t n, uint64_t max_units, std::vector<Un
         out.push_back(Unit{s, hi - s, 0, 0});
         s = hi;
     }
+    if (!out.empty()) { out[0].init_start = init_start0; out[0].init_stop = init_stop0; }
     // sscanf values current before each unit: those of the last line before it
     // whose field parses; scanning back stops at the previous unit's start
     // (older lines are summarised by that unit's own initial values)

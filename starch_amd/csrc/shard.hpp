@@ -13,8 +13,10 @@ struct Unit {              // same layout as starch_unit (include/starch_amd.h)
 
 // bytes before the first 0xFF (which reads as EOF, hpp:181)
 uint64_t input_limit(const uint8_t* b, uint64_t n);
-// split [0, input_limit) into at most max_units units whose boundaries are segment boundaries
-void plan_units(const uint8_t* b, uint64_t n, uint64_t max_units, std::vector<Unit>& out);
+// split [0, input_limit) into at most max_units units whose boundaries are segment boundaries;
+// (init_start0, init_stop0) = the sscanf values current before byte 0 (0, 0 at the input start)
+void plan_units(const uint8_t* b, uint64_t n, uint64_t max_units, std::vector<Unit>& out, int64_t init_start0 = 0,
+                int64_t init_stop0 = 0);
 // longest-processing-time assignment of units to shards by byte length
 void assign_lpt(const std::vector<Unit>& units, int nshards, std::vector<int32_t>& shard_of);
 // archive order of gathered segments (stable by unit) and their byte offsets from `base`

@@ -32,6 +32,24 @@ struct starch_ctx {
     std::vector<starch_segment> segs;
     std::vector<std::string> names;
     starch_stats stats{};
+    bool streamed = false;            // the last result went out through starch_stream_read
+    struct Streaming {                // starch_stream_* session
+        bool active = false, eof = false;
+        starch_options opt{};
+        std::string note;
+        uint8_t* held = nullptr;      // pinned: input not yet encoded, from a segment boundary on
+        uint64_t held_n = 0, held_cap = 0, try_at = 0, batch = 0, batches = 0;
+        int64_t init_start = 0, init_stop = 0;   // sscanf values current before held[0]
+        std::vector<uint8_t> ready;   // archive bytes not yet read, from ready_off on
+        uint64_t ready_off = 0, stream_end = 4;  // archive offset of the next stream
+        std::vector<starch_segment> segs;
+        std::vector<std::string> names;
+        starch_stats stats{};
+    } sm;
+    ~starch_ctx()
+    {
+        if (sm.held) (void)hipHostFree(sm.held);
+    }
 };
 
 namespace {
@@ -250,6 +268,7 @@ void encode_units(starch_ctx* c, const uint8_t* d_base, const std::vector<UnitIn
     HIP_CHECK(hipEventCreate(&e2));
     HIP_CHECK(hipEventRecord(e0, c->st));
     c->have = false;
+    c->streamed = false;
     c->stats = starch_stats{};
     for (auto& u : units) c->stats.input_bytes += u.len;
     std::vector<SegInfo> si;
@@ -505,6 +524,102 @@ void encode_multi(starch_ctx* const* ctxs, int nctx, const uint8_t* bed, uint64_
     c0->text_dev = nullptr;
     c0->archive_bytes = total;
     c0->have = true;
+    c0->streamed = false;
+}
+
+// ---- streaming ingestion (starch_stream_*) ---------------------------------
+// The input arrives in pieces of any size.  Bytes not yet encoded are held in
+// pinned host memory from a segment boundary on, together with the sscanf
+// values current before them (shard.cpp: a unit boundary is any line start
+// where the chr token changes, and a unit encoded on its own with those
+// values gives exactly the streams of the whole input).  When at least a batch
+// of input is held, the planner finds the last segment boundary among the
+// complete lines; everything before it is encoded as one unit (H2D, transform,
+// bzip2 on the GPU) and its finished streams are appended to the archive
+// bytes ready for reading.  The held tail -- the last chromosome run, which may
+// continue in the next piece -- moves to the front.  end() encodes the rest
+// and appends the index.
+
+void stream_reserve(starch_ctx* c, uint64_t need)
+{
+    auto& m = c->sm;
+    if (need <= m.held_cap) return;
+    const uint64_t cap = align_up(std::max<uint64_t>(need, 2 * m.held_cap), 1ull << 20);
+    void* p = nullptr;
+    HIP_CHECK(hipHostMalloc(&p, cap, hipHostMallocDefault));
+    if (m.held_n) memcpy(p, m.held, m.held_n);
+    if (m.held) (void)hipHostFree(m.held);
+    m.held = static_cast<uint8_t*>(p);
+    m.held_cap = cap;
+}
+
+// encode held[0, cut) (from a segment boundary to one, or to the end) and
+// append its streams to the ready bytes
+void stream_encode(starch_ctx* c, uint64_t cut)
+{
+    auto& m = c->sm;
+    if (cut == 0) return;
+    m.stats.input_bytes += cut;
+    if (m.opt.reference_compat) return;   // the reference writes only the magic (hpp:765-769)
+    uint8_t* d = c->input.as<uint8_t>(cut + 64);
+    HIP_CHECK(hipMemcpyAsync(d, m.held, cut, hipMemcpyHostToDevice, c->st));
+    std::vector<UnitIn> u(1, UnitIn{0, cut, m.init_start, m.init_stop, 0});
+    encode_units(c, d, u, m.opt, L_STREAMS);
+    const uint64_t old = m.ready.size();
+    m.ready.resize(old + c->part_bytes);
+    if (c->part_bytes)
+        HIP_CHECK(hipMemcpyAsync(m.ready.data() + old, c->part.p, c->part_bytes, hipMemcpyDeviceToHost, c->st));
+    HIP_CHECK(hipStreamSynchronize(c->st));
+    for (size_t s = 0; s < c->segs.size(); ++s) {
+        starch_segment g = c->segs[s];
+        g.stream_offset += m.stream_end;
+        g.unit = m.batches;
+        m.segs.push_back(g);
+        m.names.push_back(c->names[s]);
+    }
+    m.stream_end += c->part_bytes;
+    ++m.batches;
+    const starch_stats& x = c->stats;
+    starch_stats& t = m.stats;
+    t.n_lines += x.n_lines;
+    t.n_segments += x.n_segments;
+    t.text_bytes += x.text_bytes;
+    t.n_blocks += x.n_blocks;
+    t.rle_bytes += x.rle_bytes;
+    t.bwt_rounds += x.bwt_rounds;
+    t.periodic_blocks += x.periodic_blocks;
+    t.bwt_tied += x.bwt_tied;
+    t.dedup_blocks += x.dedup_blocks;
+    t.ms_transform += x.ms_transform;
+    t.ms_rle += x.ms_rle;
+    t.ms_bwt += x.ms_bwt;
+    t.ms_mtf += x.ms_mtf;
+    t.ms_tables += x.ms_tables;
+    t.ms_emit += x.ms_emit;
+    t.ms_total += x.ms_total;
+}
+
+// encode everything before the last segment boundary among the complete lines
+void stream_cut(starch_ctx* c)
+{
+    auto& m = c->sm;
+    const void* nl = memrchr(m.held, '\n', m.held_n);
+    std::vector<shard::Unit> u;
+    if (nl) {
+        const uint64_t lim = (uint64_t)(static_cast<const uint8_t*>(nl) - m.held) + 1;
+        shard::plan_units(m.held, lim, 4096, u, m.init_start, m.init_stop);
+    }
+    if (u.size() < 2) {   // no boundary yet: the held run continues
+        m.try_at = m.held_n + m.batch / 2;
+        return;
+    }
+    const uint64_t cut = u.back().offset;
+    stream_encode(c, cut);
+    memmove(m.held, m.held + cut, m.held_n - cut);
+    m.held_n -= cut;
+    m.init_start = u.back().init_start;
+    m.init_stop = u.back().init_stop;
+    m.try_at = std::max(m.batch, m.held_n + m.batch / 2);
 }
 
 }  // namespace
@@ -728,7 +843,7 @@ int starch_archive_layout(const uint64_t* unit_of, const uint64_t* bytes, uint64
 int starch_archive_size(starch_ctx* c, uint64_t* n)
 {
     if (!c || !n) return STARCH_ERR_ARG;
-    if (!c->have) return STARCH_ERR_STATE;
+    if (!c->have || c->streamed) return STARCH_ERR_STATE;
     *n = c->archive_bytes;
     return STARCH_OK;
 }
@@ -736,7 +851,7 @@ int starch_archive_size(starch_ctx* c, uint64_t* n)
 int starch_archive_device(starch_ctx* c, const void** p)
 {
     if (!c || !p) return STARCH_ERR_ARG;
-    if (!c->have) return STARCH_ERR_STATE;
+    if (!c->have || c->streamed) return STARCH_ERR_STATE;
     *p = c->archive.p;
     return STARCH_OK;
 }
@@ -744,7 +859,7 @@ int starch_archive_device(starch_ctx* c, const void** p)
 int starch_archive_copy(starch_ctx* c, void* dst, uint64_t cap)
 {
     GUARD(c)
-    if (!c->have) return STARCH_ERR_STATE;
+    if (!c->have || c->streamed) return STARCH_ERR_STATE;
     if (cap < c->archive_bytes || !dst) return STARCH_ERR_MEM;
     if (c->archive_bytes)
         HIP_CHECK(hipMemcpyAsync(dst, c->archive.p, c->archive_bytes, hipMemcpyDeviceToHost, c->st));
@@ -924,6 +1039,109 @@ int starch_bz2_stream_info(starch_ctx* c, uint32_t* n_blocks, uint32_t* combined
     if (!c || !n_blocks || !combined_crc) return STARCH_ERR_ARG;
     *n_blocks = c->bz_nblocks;
     *combined_crc = c->bz_crc;
+    return STARCH_OK;
+}
+
+int starch_stream_begin(starch_ctx* c, const starch_options* opt, uint64_t batch_bytes)
+{
+    GUARD(c)
+    starch_options o;
+    starch_options_init(&o);
+    if (opt) o = *opt;
+    if (o.block_size_100k < 1 || o.block_size_100k > 9) return STARCH_ERR_ARG;
+    auto& m = c->sm;
+    m.active = true;
+    m.eof = false;
+    m.note = o.note ? o.note : "";
+    m.opt = o;
+    m.opt.note = o.note ? m.note.c_str() : nullptr;
+    m.held_n = 0;
+    m.batch = batch_bytes ? batch_bytes : (256ull << 20);
+    m.try_at = m.batch;
+    m.batches = 0;
+    m.init_start = m.init_stop = 0;
+    m.ready.assign(kMagic, kMagic + 4);
+    m.ready_off = 0;
+    m.stream_end = 4;
+    m.segs.clear();
+    m.names.clear();
+    m.stats = starch_stats{};
+    c->have = false;
+    c->streamed = false;
+    return STARCH_OK;
+    END_GUARD(c)
+}
+
+int starch_stream_feed(starch_ctx* c, const void* bed, uint64_t n)
+{
+    GUARD(c)
+    auto& m = c->sm;
+    if (!m.active) return STARCH_ERR_STATE;
+    if (n && !bed) return STARCH_ERR_ARG;
+    if (m.eof || n == 0) return STARCH_OK;
+    const uint8_t* b = static_cast<const uint8_t*>(bed);
+    const uint64_t k = shard::input_limit(b, n);   // 0xFF reads as EOF (hpp:181): the rest is never read
+    if (k < n) m.eof = true;
+    stream_reserve(c, m.held_n + k);
+    memcpy(m.held + m.held_n, b, k);
+    m.held_n += k;
+    if (m.held_n >= m.try_at) stream_cut(c);
+    return STARCH_OK;
+    END_GUARD(c)
+}
+
+int starch_stream_end(starch_ctx* c)
+{
+    GUARD(c)
+    auto& m = c->sm;
+    if (!m.active) return STARCH_ERR_STATE;
+    m.active = false;
+    stream_encode(c, m.held_n);
+    m.held_n = 0;
+    if (m.opt.emit_index && !m.opt.reference_compat) {
+        std::vector<const char*> np(m.segs.size());
+        std::vector<uint64_t> nl(m.segs.size());
+        for (size_t s = 0; s < m.segs.size(); ++s) { np[s] = m.names[s].data(); nl[s] = m.names[s].size(); }
+        const std::string idx = build_index(m.segs.data(), np.data(), nl.data(), m.segs.size(), m.stream_end,
+                                            m.opt.note, m.opt.block_size_100k);
+        m.ready.insert(m.ready.end(), idx.begin(), idx.end());
+        m.stats.archive_bytes = m.stream_end + idx.size();
+    } else {
+        m.stats.archive_bytes = m.opt.reference_compat ? 4 : m.stream_end;
+    }
+    m.stats.n_segments = m.segs.size();
+    c->segs = m.segs;
+    c->names = m.names;
+    c->stats = m.stats;
+    c->archive_bytes = m.stats.archive_bytes;
+    c->have = true;
+    c->streamed = true;
+    return STARCH_OK;
+    END_GUARD(c)
+}
+
+int starch_stream_available(starch_ctx* c, uint64_t* n)
+{
+    if (!c || !n) return STARCH_ERR_ARG;
+    *n = c->sm.ready.size() - c->sm.ready_off;
+    return STARCH_OK;
+}
+
+int starch_stream_read(starch_ctx* c, void* dst, uint64_t cap, uint64_t* len)
+{
+    if (!c || !len || (cap && !dst)) return STARCH_ERR_ARG;
+    auto& m = c->sm;
+    const uint64_t k = std::min<uint64_t>(cap, m.ready.size() - m.ready_off);
+    if (k) memcpy(dst, m.ready.data() + m.ready_off, k);
+    m.ready_off += k;
+    if (m.ready_off == m.ready.size()) {
+        m.ready.clear();
+        m.ready_off = 0;
+    } else if (m.ready_off > (64ull << 20) && 2 * m.ready_off > m.ready.size()) {
+        m.ready.erase(m.ready.begin(), m.ready.begin() + (std::ptrdiff_t)m.ready_off);
+        m.ready_off = 0;
+    }
+    *len = k;
     return STARCH_OK;
 }
 

@@ -1,0 +1,136 @@
+"""Streaming ingestion: BED bytes fed in pieces of any size
+through starch_stream_begin/feed/end, finished chromosome runs encoded on the
+GPU as the input passes them, archive bytes read out as they finish.  The
+concatenated output must equal the one-call archive of the whole input byte
+for byte (the same bar as the multi-GPU shard path), whatever the piece sizes
+and batch thresholds, including pieces that split lines, tokens and CRLF-free
+tails, stale sscanf values across a cut, revisited chromosomes, NUL bytes and
+a 0xFF that ends the input mid-piece."""
+import os
+import subprocess
+
+import pytest
+
+from tests import corpus
+
+pytestmark = pytest.mark.gpu
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+
+
+def _one_call(data, **kw):
+    import starch_amd
+    c = starch_amd.Starch(0)
+    a = c.compress(data, **kw)
+    c.close()
+    return a
+
+
+def _pieces(data, size):
+    return [data[i:i + size] for i in range(0, len(data), size)]
+
+
+def _streamed(data, piece, batch, **kw):
+    import starch_amd
+    c = starch_amd.Starch(0)
+    a = c.compress_stream(_pieces(data, piece), batch_bytes=batch, **kw)
+    st = c.stats()
+    c.close()
+    return a, st
+
+
+@pytest.mark.parametrize("piece,batch", [(1 << 20, 1), (65_537, 300_000), (4_093, 1 << 20), (10 ** 9, 0)])
+def test_stream_hg38_identical(piece, batch):
+    import starch_amd
+    data = starch_amd.gen_bed(0, 400_000)
+    ref = _one_call(data)
+    got, st = _streamed(data, piece, batch)
+    assert got == ref
+    assert st["input_bytes"] == len(data)
+    assert st["n_segments"] == 24
+
+
+@pytest.mark.parametrize("seed", range(4))
+def test_stream_quirky_inputs(seed):
+    data = (corpus.fuzz_bed(seed, 3000) + corpus.multi_chrom_bed(5, 400, seed, "bed6") +
+            corpus.parseable_fuzz_bed(seed, 2000) + b"chr9\tx\ty\nchr9\t1")
+    ref = _one_call(data)
+    for piece, batch in ((997, 1), (7, 5000), (1 << 16, 1 << 16)):
+        got, _ = _streamed(data, piece, batch)
+        assert got == ref, (piece, batch)
+
+
+def test_stream_stale_values_across_cut():
+    """A chromosome whose first lines do not parse keeps the previous
+    chromosome's last values (hpp:306-307): the streamed cut must carry them."""
+    data = (b"chrA\t10\t20\nchrA\t30\t45\n" + b"chrB\tq\tz\nchrB\t7\tw\n" * 50 +
+            b"chrC\t5\t9\nchrC\tx\t12\n" + b"chrD\tx\ty\n" * 30)
+    ref = _one_call(data)
+    for piece in (1, 3, 16, 31):
+        got, _ = _streamed(data, piece, 1)
+        assert got == ref, piece
+
+
+def test_stream_ff_ends_input():
+    import starch_amd
+    head = starch_amd.gen_bed(0, 20_000)
+    data = head + b"chrZ\t1\t2\n\xffchrZ\t3\t4\n" + head
+    ref = _one_call(data)
+    got, st = _streamed(data, 4096, 1)
+    assert got == ref
+    assert st["input_bytes"] == data.index(b"\xff")
+
+
+@pytest.mark.parametrize("kw", [dict(emit_index=False), dict(reference_compat=True)])
+def test_stream_options(kw):
+    import starch_amd
+    data = starch_amd.gen_bed(1, 50_000)
+    assert _streamed(data, 10_000, 100_000, **kw)[0] == _one_call(data, **kw)
+
+
+def test_stream_empty_and_tiny():
+    assert _streamed(b"", 1, 1)[0] == _one_call(b"")
+    assert _streamed(b"chr1\t1\t2", 1, 1)[0] == _one_call(b"chr1\t1\t2")
+
+
+def test_stream_segments_and_reads_interleaved():
+    """Streams become readable before end(); segments() after end() describe
+    the whole archive (offsets into the streamed bytes)."""
+    import starch_amd
+    data = starch_amd.gen_bed(0, 200_000)
+    c = starch_amd.Starch(0)
+    c.stream_begin(batch_bytes=1 << 20)
+    out = [c.stream_read()]
+    assert out[0] == starch_amd.MAGIC
+    early = 0
+    for p in _pieces(data, 1 << 20):
+        c.stream_feed(p)
+        out.append(c.stream_read())
+        early += len(out[-1])
+    assert early > 0                      # streams came out while input was still arriving
+    c.stream_end()
+    out.append(c.stream_read())
+    arch = b"".join(out)
+    assert arch == _one_call(data)
+    idx, streams = starch_amd.parse_archive(arch)
+    segs = c.segments()
+    assert [n.decode() for n, _ in segs] == starch_amd.HG38
+    for (n, s), st in zip(segs, streams):
+        assert arch[s.stream_offset:s.stream_offset + s.stream_bytes] == st
+    with pytest.raises(starch_amd.StarchError):
+        c.archive()                       # the bytes went out through stream_read
+    c.close()
+
+
+def test_cli_streams_stdin(tmp_path):
+    """starch3 < file (streamed, small batches) == starch3 --slurp == one call."""
+    import starch_amd
+    data = starch_amd.gen_bed(0, 300_000) + corpus.fuzz_bed(3, 500)
+    f = tmp_path / "in.bed"
+    f.write_bytes(data)
+    exe = os.path.join(ROOT, "starch_amd", "_build", "starch3")
+    with open(f, "rb") as fin:
+        a = subprocess.run([exe, "--batch-mb", "1"], stdin=fin, capture_output=True, timeout=120)
+    b = subprocess.run([exe, "--slurp", str(f)], capture_output=True, timeout=120)
+    assert a.returncode == 0 and b.returncode == 0, (a.stderr, b.stderr)
+    assert a.stdout == b.stdout == _one_call(data)

@@ -10,7 +10,15 @@
 // --reference-compat (stdout exactly as the reference: the 4 magic bytes),
 // --device N, --gpus N (shard chromosomes over devices 0..N-1 in one process),
 // --devices LIST (explicit device list, e.g. 0,1 or 0,0 for virtual shards),
-// --stats.
+// --stats, --batch-mb N, --slurp.
+//
+// One device (the default): streaming ingestion -- a reader
+// thread reads the input in 64 MiB pieces while the main thread feeds them to
+// starch_stream_feed, which encodes every finished chromosome run on the GPU
+// as the input passes its end; finished streams are written to stdout as they
+// come, so reading, H2D + encode and writing overlap and host memory holds
+// only the unfinished chromosome run.  --slurp (and --gpus/--devices) read the
+// whole input first and encode it in one call.
 #include <errno.h>
 #include <getopt.h>
 #include <stdio.h>
@@ -19,7 +27,12 @@
 #include <sys/stat.h>
 #include <unistd.h>
 
+#include <chrono>
+#include <condition_variable>
+#include <deque>
+#include <mutex>
 #include <string>
+#include <thread>
 #include <vector>
 
 #include "../include/starch_amd.h"
@@ -44,6 +57,8 @@ static void usage(FILE* f)
             "  --gpus N              shard chromosomes over GPUs 0..N-1 (archive identical to one GPU)\n"
             "  --devices LIST        comma-separated GPU ordinals to shard over (may repeat)\n"
             "  --stats               print per-stage timings to stderr\n"
+            "  --batch-mb N          streamed encode: encode once N MiB are held (default 256)\n"
+            "  --slurp               read the whole input, then encode it in one call\n"
             "  --help | -h           this message\n"
             "  --version | -v        version\n",
             kName, kVersion, kName, kName);
@@ -52,7 +67,8 @@ static void usage(FILE* f)
 int main(int argc, char** argv)
 {
     std::string note, input;
-    int methods = 0, gzip = 0, level = 9, emit_index = 1, compat = 0, device = 0, stats = 0;
+    int methods = 0, gzip = 0, level = 9, emit_index = 1, compat = 0, device = 0, stats = 0, slurp = 0;
+    uint64_t batch_mb = 256;
     std::vector<int> devices;
     static struct option longs[] = {
         {"note", required_argument, nullptr, 'n'}, {"bzip2", no_argument, nullptr, 'b'},
@@ -61,6 +77,7 @@ int main(int argc, char** argv)
         {"no-index", no_argument, nullptr, 'I'},   {"reference-compat", no_argument, nullptr, 'R'},
         {"device", required_argument, nullptr, 'D'}, {"stats", no_argument, nullptr, 'S'},
         {"gpus", required_argument, nullptr, 'G'},   {"devices", required_argument, nullptr, 'E'},
+        {"batch-mb", required_argument, nullptr, 'M'}, {"slurp", no_argument, nullptr, 'U'},
         {nullptr, 0, nullptr, 0}};
     opterr = 0;
     int c, li;
@@ -77,6 +94,8 @@ int main(int argc, char** argv)
             case 'R': compat = 1; break;
             case 'D': device = atoi(optarg); break;
             case 'S': stats = 1; break;
+            case 'M': batch_mb = strtoull(optarg, nullptr, 10); break;
+            case 'U': slurp = 1; break;
             case 'G': {
                 devices.clear();
                 for (int i = 0, k = atoi(optarg); i < k; ++i) devices.push_back(i);
@@ -132,13 +151,7 @@ int main(int argc, char** argv)
         fprintf(stderr, "Error: This method is unsupported at this time\n");
         return ENOSYS;
     }
-    std::vector<char> data;
-    {
-        std::vector<char> buf(1 << 24);
-        size_t k;
-        while ((k = fread(buf.data(), 1, buf.size(), in)) > 0) data.insert(data.end(), buf.begin(), buf.begin() + k);
-        if (in != stdin) fclose(in);
-    }
+    const auto t0 = std::chrono::steady_clock::now();
     if (devices.empty()) devices.push_back(device);
     std::vector<starch_ctx*> ctxs(devices.size(), nullptr);
     int rc = STARCH_OK;
@@ -157,29 +170,89 @@ int main(int argc, char** argv)
     opt.emit_index = emit_index;
     opt.reference_compat = compat;
     opt.note = note.empty() ? nullptr : note.c_str();
-    rc = ctxs.size() > 1 ? starch_encode_multi_host(ctxs.data(), (int)ctxs.size(), data.data(), data.size(), &opt)
-                         : starch_encode_host(ctx, data.data(), data.size(), &opt);
+    if (ctxs.size() == 1 && !slurp) {
+        // streamed: reader thread -> bounded queue of pieces -> feed; drain to stdout
+        const size_t kPiece = 64u << 20, kQueue = 3;
+        std::mutex mu;
+        std::condition_variable cv;
+        std::deque<std::vector<char>> q;
+        bool done = false;
+        std::thread reader([&] {
+            for (;;) {
+                std::vector<char> b(kPiece);
+                size_t k = fread(b.data(), 1, b.size(), in);
+                b.resize(k);
+                std::unique_lock<std::mutex> lk(mu);
+                cv.wait(lk, [&] { return q.size() < kQueue; });
+                if (k == 0) { done = true; cv.notify_all(); return; }
+                q.push_back(std::move(b));
+                cv.notify_all();
+            }
+        });
+        std::vector<char> out(1u << 20);
+        auto drain = [&]() {
+            uint64_t k = 0;
+            do {
+                if (starch_stream_read(ctx, out.data(), out.size(), &k) != STARCH_OK) break;
+                if (k) fwrite(out.data(), 1, k, stdout);
+            } while (k == out.size());
+        };
+        rc = starch_stream_begin(ctx, &opt, batch_mb << 20);
+        drain();
+        for (;;) {
+            std::vector<char> b;
+            {
+                std::unique_lock<std::mutex> lk(mu);
+                cv.wait(lk, [&] { return !q.empty() || done; });
+                if (q.empty()) break;
+                b = std::move(q.front());
+                q.pop_front();
+                cv.notify_all();
+            }
+            if (rc == STARCH_OK) rc = starch_stream_feed(ctx, b.data(), b.size());
+            drain();
+        }
+        reader.join();
+        if (in != stdin) fclose(in);
+        if (rc == STARCH_OK) rc = starch_stream_end(ctx);
+        drain();
+    } else {
+        std::vector<char> data;
+        {
+            std::vector<char> buf(1 << 24);
+            size_t k;
+            while ((k = fread(buf.data(), 1, buf.size(), in)) > 0) data.insert(data.end(), buf.begin(), buf.begin() + k);
+            if (in != stdin) fclose(in);
+        }
+        rc = ctxs.size() > 1 ? starch_encode_multi_host(ctxs.data(), (int)ctxs.size(), data.data(), data.size(), &opt)
+                             : starch_encode_host(ctx, data.data(), data.size(), &opt);
+        if (rc == STARCH_OK) {
+            uint64_t n = 0;
+            starch_archive_size(ctx, &n);
+            std::vector<char> out(n);
+            starch_archive_copy(ctx, out.data(), n);
+            fwrite(out.data(), 1, n, stdout);
+        }
+    }
     if (rc != STARCH_OK) {
         fprintf(stderr, "Error: encode failed (%s: %s)\n", starch_strerror(rc), starch_last_error(ctx));
         for (auto* c : ctxs) starch_destroy(c);
         return rc == STARCH_ERR_MEM ? ENOMEM : EINVAL;
     }
-    uint64_t n = 0;
-    starch_archive_size(ctx, &n);
-    std::vector<char> out(n);
-    starch_archive_copy(ctx, out.data(), n);
-    fwrite(out.data(), 1, n, stdout);
     fflush(stdout);
     if (stats) {
+        const double wall = std::chrono::duration<double>(std::chrono::steady_clock::now() - t0).count();
         starch_stats s;
         starch_get_stats(ctx, &s);
         fprintf(stderr,
                 "{\"input_bytes\": %llu, \"lines\": %llu, \"segments\": %llu, \"text_bytes\": %llu, "
                 "\"archive_bytes\": %llu, \"blocks\": %llu, \"ms_total\": %.3f, \"ms_transform\": %.3f, "
-                "\"ms_rle\": %.3f, \"ms_bwt\": %.3f, \"ms_mtf\": %.3f, \"ms_tables\": %.3f, \"ms_emit\": %.3f}\n",
+                "\"ms_rle\": %.3f, \"ms_bwt\": %.3f, \"ms_mtf\": %.3f, \"ms_tables\": %.3f, \"ms_emit\": %.3f, "
+                "\"wall_s\": %.3f, \"e2e_mb_s\": %.1f}\n",
                 (unsigned long long)s.input_bytes, (unsigned long long)s.n_lines, (unsigned long long)s.n_segments,
                 (unsigned long long)s.text_bytes, (unsigned long long)s.archive_bytes, (unsigned long long)s.n_blocks,
-                s.ms_total, s.ms_transform, s.ms_rle, s.ms_bwt, s.ms_mtf, s.ms_tables, s.ms_emit);
+                s.ms_total, s.ms_transform, s.ms_rle, s.ms_bwt, s.ms_mtf, s.ms_tables, s.ms_emit, wall,
+                wall > 0 ? s.input_bytes / wall / 1e6 : 0.0);
     }
     for (auto* c : ctxs) starch_destroy(c);
     return 0;
