@@ -51,7 +51,9 @@ public:
         k_compression_method_undefined
     } compression_method_t;
 
-    Starch() : _in_stream(NULL), _out_stream(NULL), _block_size(9), _reference_compat(false), _emit_index(true)
+    Starch()
+        : _in_stream(NULL), _out_stream(NULL), _block_size(9), _reference_compat(false), _emit_index(true),
+          _base_counts(false)
     {
         set_note(std::string());
         set_compression_method(k_compression_method_undefined);   // hpp:912-916
@@ -143,6 +145,8 @@ public:
     void set_block_size(int bs100k) { _block_size = bs100k; }
     void set_reference_compat(bool on) { _reference_compat = on; }
     void set_emit_index(bool on) { _emit_index = on; }
+    // per-segment base_count_unique / base_count_nonunique (hpp:61-62) in the index
+    void set_base_counts(bool on) { _base_counts = on; }
     starch_ctx* context(void) { return _ctx.empty() ? NULL : _ctx[0]; }
 
     // ---- the hot path -------------------------------------------------------
@@ -270,6 +274,7 @@ private:
         o.emit_index = _emit_index ? 1 : 0;
         o.reference_compat = _reference_compat ? 1 : 0;
         o.note = _note.empty() ? NULL : _note.c_str();
+        o.base_counts = _base_counts ? 1 : 0;
         return o;
     }
 
@@ -284,6 +289,7 @@ private:
     int _block_size;
     bool _reference_compat;
     bool _emit_index;
+    bool _base_counts;
     std::vector<Pending> _pending;
 };
 }  // namespace starch3

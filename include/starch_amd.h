@@ -48,6 +48,7 @@ typedef struct {
     int emit_index;          /* 1: append JSON index + footer after the streams */
     int reference_compat;    /* 1: archive is exactly the reference's stdout (magic only) */
     const char* note;        /* --note text for the index (may be NULL) */
+    int base_counts;         /* 1: per-segment base counts (hpp:61-62) in the segments and the index */
 } starch_options;
 
 typedef struct {
@@ -59,6 +60,13 @@ typedef struct {
     uint32_t n_blocks;       /* bzip2 blocks in the stream */
     uint32_t combined_crc;   /* bzip2 combined stream CRC */
     uint64_t unit;           /* input unit the segment came from (archive order = unit order) */
+    /* transform_state_t.base_count_unique / _nonunique (hpp:61-62; declared,
+     * never computed by the reference), filled when starch_options.base_counts:
+     * nonunique = sum of (stop - start) over the segment's lines, unique = sum
+     * of max(0, stop - max(start, largest earlier stop)) = size of the union
+     * of the intervals for a BED sorted by start; modulo 2^64. */
+    int64_t base_count_unique;
+    int64_t base_count_nonunique;
 } starch_segment;
 
 /* A unit: a byte range of the input whose first line starts a chromosome
@@ -132,8 +140,11 @@ int starch_encode_multi_host(starch_ctx* const* ctxs, int nctx, const void* bed,
  * the per-chromosome flush, hpp:393-407).  Feed host BED bytes in pieces of
  * any size (lines may straddle pieces); whenever at least batch_bytes
  * (0 = 256 MiB) are held, everything before the last chromosome change among
- * the complete lines is encoded on the GPU and its finished streams become
- * readable with starch_stream_read (the magic is readable at once).
+ * the complete lines is handed to the session's encoder thread (H2D, GPU
+ * encode, D2H) while the caller keeps feeding into the other of two pinned
+ * buffers; finished streams become readable with starch_stream_read (the
+ * magic is readable at once).  Make no other calls on the context while a
+ * session is open.
  * starch_stream_end encodes the rest and appends the index.  The bytes read
  * out, in order, are exactly the archive starch_encode_host gives for the
  * concatenated input.  A 0xFF byte ends the input (hpp:181): later bytes are
@@ -141,6 +152,11 @@ int starch_encode_multi_host(starch_ctx* const* ctxs, int nctx, const void* bed,
  * accessors below report STARCH_ERR_STATE (the bytes went out by read). */
 int starch_stream_begin(starch_ctx* ctx, const starch_options* opt, uint64_t batch_bytes);
 int starch_stream_feed(starch_ctx* ctx, const void* bed, uint64_t n);
+/* Zero-copy feed: a window of >= min_bytes in the session's pinned buffer to
+ * read input into directly (e.g. read(2) from a file or pipe), then commit the
+ * n bytes written there.  feed() = window + memcpy + commit. */
+int starch_stream_window(starch_ctx* ctx, uint64_t min_bytes, void** ptr, uint64_t* cap);
+int starch_stream_commit(starch_ctx* ctx, uint64_t n);
 int starch_stream_end(starch_ctx* ctx);
 int starch_stream_available(starch_ctx* ctx, uint64_t* n);
 int starch_stream_read(starch_ctx* ctx, void* dst, uint64_t cap, uint64_t* len);
@@ -191,6 +207,10 @@ int starch_gen_bed_sizes(int kind, uint64_t seed, uint64_t total_lines, const in
 int starch_build_index(const starch_segment* segs, const char* const* names, const uint64_t* name_lens,
                        uint64_t nseg, uint64_t index_offset, const char* note, int block_size_100k, char* dst,
                        uint64_t cap, uint64_t* len);
+/* Same, with the index options taken from opt (note, block size, base counts). */
+int starch_build_index_opt(const starch_segment* segs, const char* const* names, const uint64_t* name_lens,
+                           uint64_t nseg, uint64_t index_offset, const starch_options* opt, char* dst, uint64_t cap,
+                           uint64_t* len);
 
 #ifdef __cplusplus
 }

@@ -140,10 +140,41 @@ size_t oracle_transform(const uint8_t* in, size_t n,
 
 /* Same, starting from given bed_t.start/stop values: a piece of an input that
  * begins at a segment boundary, with the sscanf values current before it. */
+static size_t transform_core(const uint8_t* in, size_t n, uint8_t* out, size_t out_cap, oracle_segment* segs,
+                             size_t seg_cap, size_t* nseg_out, int64_t init_start, int64_t init_stop,
+                             uint64_t* base_unique, uint64_t* base_nonunique);
+
 size_t oracle_transform_init(const uint8_t* in, size_t n,
                              uint8_t* out, size_t out_cap,
                              oracle_segment* segs, size_t seg_cap, size_t* nseg_out,
                              int64_t init_start, int64_t init_stop)
+{
+    return transform_core(in, n, out, out_cap, segs, seg_cap, nseg_out, init_start, init_stop, NULL, NULL);
+}
+
+/* Per-segment base counts (the reference declares
+ * transform_state_t.base_count_unique / base_count_nonunique, hpp:61-62, and
+ * zeroes them at every segment start, hpp:516-532, but never computes them).
+ * Over the lines of a segment, with start/stop as the transform uses them
+ * (stale sscanf values included): nonunique = sum of (stop - start); unique =
+ * sum of max(0, stop - max(start, M)), M = the largest stop of the segment's
+ * earlier lines -- the size of the union of the intervals for a BED sorted by
+ * start.  Arithmetic is modulo 2^64 (read as int64).  No text is produced;
+ * returns 0, or (size_t)-1 when seg_cap is too small. */
+size_t oracle_base_counts(const uint8_t* in, size_t n, int64_t init_start, int64_t init_stop,
+                          uint64_t* base_unique, uint64_t* base_nonunique, size_t seg_cap, size_t* nseg_out)
+{
+    oracle_segment* segs = (oracle_segment*)malloc((seg_cap ? seg_cap : 1) * sizeof(oracle_segment));
+    if (!segs) return (size_t)-1;
+    size_t r = transform_core(in, n, NULL, 0, segs, seg_cap, nseg_out, init_start, init_stop, base_unique,
+                              base_nonunique);
+    free(segs);
+    return r == (size_t)-1 ? r : 0;
+}
+
+static size_t transform_core(const uint8_t* in, size_t n, uint8_t* out, size_t out_cap, oracle_segment* segs,
+                             size_t seg_cap, size_t* nseg_out, int64_t init_start, int64_t init_stop,
+                             uint64_t* base_unique, uint64_t* base_nonunique)
 {
     /* Framing (hpp:170-191): byte 0xFF reads as EOF (char compared with EOF,
      * hpp:181); a trailing line without '\n' is never transformed. */
@@ -156,6 +187,8 @@ size_t oracle_transform_init(const uint8_t* in, size_t n,
     size_t o = 0, nseg = 0;
     size_t cur_name_off = 0, cur_name_len = 0; int have_cur = 0;
     size_t seg_text_start = 0;
+    uint64_t bu = 0, bn = 0;           /* base counts of the current segment */
+    int64_t run_max = 0; int have_max = 0;
 
     size_t pos = 0;
     while (pos < lim) {
@@ -193,16 +226,27 @@ size_t oracle_transform_init(const uint8_t* in, size_t n,
                 segs[nseg].name_off = cur_name_off; segs[nseg].name_len = cur_name_len;
                 segs[nseg].line_count = line_count;
                 segs[nseg].text_off = seg_text_start; segs[nseg].text_len = o - seg_text_start;
+                if (base_unique) { base_unique[nseg] = bu; base_nonunique[nseg] = bn; }
                 ++nseg;
             }
             have_cur = 1; cur_name_off = f_beg[0]; cur_name_len = len[0];
             last_cd = 0; last_stop = 0; line_count = 0;          /* hpp:523-536 */
             seg_text_start = o;
+            bu = bn = 0; have_max = 0;
         }
+
+        int64_t cd = (int64_t)((uint64_t)stop - (uint64_t)start);
+        if (base_unique) {
+            const int64_t lo = (have_max && run_max > start) ? run_max : start;
+            bn += (uint64_t)cd;
+            if (stop > lo) bu += (uint64_t)stop - (uint64_t)lo;
+            run_max = (have_max && run_max > stop) ? run_max : stop;
+            have_max = 1;
+        }
+        if (!out) { last_stop = stop; ++line_count; continue; }
 
         /* Transform (hpp:428-504) */
         if (o + 64 + len[3] > out_cap) return (size_t)-1;
-        int64_t cd = (int64_t)((uint64_t)stop - (uint64_t)start);
         if (cd != last_cd) {
             last_cd = cd;
             size_t keep = (size_t)(2 + n_digits_ref(cd));      /* tf_line[len]='\0' (hpp:452) */
@@ -223,6 +267,7 @@ size_t oracle_transform_init(const uint8_t* in, size_t n,
         segs[nseg].name_off = cur_name_off; segs[nseg].name_len = cur_name_len;
         segs[nseg].line_count = line_count;
         segs[nseg].text_off = seg_text_start; segs[nseg].text_len = o - seg_text_start;
+        if (base_unique) { base_unique[nseg] = bu; base_nonunique[nseg] = bn; }
         ++nseg;
     }
     *nseg_out = nseg;

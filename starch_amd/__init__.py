@@ -45,7 +45,8 @@ class Segment(ctypes.Structure):
     _fields_ = [("line_count", ctypes.c_uint64), ("text_bytes", ctypes.c_uint64),
                 ("stream_offset", ctypes.c_uint64), ("stream_bytes", ctypes.c_uint64),
                 ("name_len", ctypes.c_uint64), ("n_blocks", ctypes.c_uint32),
-                ("combined_crc", ctypes.c_uint32), ("unit", ctypes.c_uint64)]
+                ("combined_crc", ctypes.c_uint32), ("unit", ctypes.c_uint64),
+                ("base_count_unique", ctypes.c_int64), ("base_count_nonunique", ctypes.c_int64)]
 
 
 class Unit(ctypes.Structure):
@@ -57,7 +58,7 @@ class Unit(ctypes.Structure):
 
 class Options(ctypes.Structure):
     _fields_ = [("block_size_100k", ctypes.c_int), ("emit_index", ctypes.c_int),
-                ("reference_compat", ctypes.c_int), ("note", ctypes.c_char_p)]
+                ("reference_compat", ctypes.c_int), ("note", ctypes.c_char_p), ("base_counts", ctypes.c_int)]
 
 
 class Stats(ctypes.Structure):
@@ -78,6 +79,16 @@ def load():
         return _lib
     if not os.path.exists(LIB_PATH):
         raise StarchError(-10, "native library missing: %s (run __graft_entry__.build())" % LIB_PATH)
+    # One HIP runtime per process: PyTorch-ROCm ships its own libamdhip64
+    # (same soname as /opt/rocm's).  Loading torch first makes this library
+    # bind to torch's copy, so the two share devices, streams and memory;
+    # loading ours first and torch later leaves the process with a runtime
+    # torch's device setup then breaks for this library (seen as
+    # hipErrorNoDevice from starch_create).
+    try:
+        import torch  # noqa: F401
+    except ImportError:
+        pass
     L = ctypes.CDLL(LIB_PATH)
     vp, u64, pu64 = ctypes.c_void_p, ctypes.c_uint64, ctypes.POINTER(ctypes.c_uint64)
     sig = {
@@ -108,6 +119,8 @@ def load():
                            ctypes.c_int),
         "starch_build_index": ([ctypes.POINTER(Segment), ctypes.POINTER(ctypes.c_char_p), pu64, u64, u64,
                                 ctypes.c_char_p, ctypes.c_int, vp, u64, pu64], ctypes.c_int),
+        "starch_build_index_opt": ([ctypes.POINTER(Segment), ctypes.POINTER(ctypes.c_char_p), pu64, u64, u64,
+                                    ctypes.POINTER(Options), vp, u64, pu64], ctypes.c_int),
         "starch_gen_bed_sizes": ([ctypes.c_int, u64, u64, ctypes.POINTER(ctypes.c_int32), ctypes.c_int, pu64],
                                  ctypes.c_int),
         "starch_plan_units": ([ctypes.c_char_p, u64, u64, ctypes.POINTER(Unit), pu64], ctypes.c_int),
@@ -122,6 +135,8 @@ def load():
                                       ctypes.POINTER(Options)], ctypes.c_int),
         "starch_stream_begin": ([vp, ctypes.POINTER(Options), u64], ctypes.c_int),
         "starch_stream_feed": ([vp, vp, u64], ctypes.c_int),
+        "starch_stream_window": ([vp, u64, ctypes.POINTER(vp), pu64], ctypes.c_int),
+        "starch_stream_commit": ([vp, u64], ctypes.c_int),
         "starch_stream_end": ([vp], ctypes.c_int),
         "starch_stream_available": ([vp, pu64], ctypes.c_int),
         "starch_stream_read": ([vp, vp, u64, pu64], ctypes.c_int),
@@ -156,6 +171,7 @@ class Starch:
         self._note = ""
         self._method = K_BZIP2
         self.block_size_100k = 9
+        self.base_counts = False       # per-segment base counts in segments() and the index (hpp:61-62)
         self._magic = MAGIC
 
     def close(self):
@@ -202,6 +218,7 @@ class Starch:
         o.block_size_100k = self.block_size_100k
         o.emit_index = 1 if emit_index else 0
         o.reference_compat = 1 if reference_compat else 0
+        o.base_counts = 1 if self.base_counts else 0
         self._note_b = self._note.encode() if self._note else None
         o.note = self._note_b
         return o
@@ -391,7 +408,7 @@ def gen_bed_sizes(kind, total_lines, chroms=None, seed=20261015):
     return list(out[:len(chroms)])
 
 
-def build_index(segs, names, index_offset, note=None, level=9):
+def build_index(segs, names, index_offset, note=None, level=9, base_counts=False):
     """JSON index + 32-byte footer for already-placed streams (multi-GPU gather)."""
     L = load()
     k = len(segs)
@@ -400,9 +417,12 @@ def build_index(segs, names, index_offset, note=None, level=9):
     nl = (ctypes.c_uint64 * max(1, k))(*[len(x) for x in names])
     n = ctypes.c_uint64()
     note_b = note.encode() if note else None
-    _check(L.starch_build_index(arr, nm, nl, k, index_offset, note_b, level, None, 0, ctypes.byref(n)))
+    o = Options()
+    L.starch_options_init(ctypes.byref(o))
+    o.block_size_100k, o.note, o.base_counts = level, note_b, 1 if base_counts else 0
+    _check(L.starch_build_index_opt(arr, nm, nl, k, index_offset, ctypes.byref(o), None, 0, ctypes.byref(n)))
     buf = ctypes.create_string_buffer(max(1, n.value))
-    _check(L.starch_build_index(arr, nm, nl, k, index_offset, note_b, level, buf, n.value, ctypes.byref(n)))
+    _check(L.starch_build_index_opt(arr, nm, nl, k, index_offset, ctypes.byref(o), buf, n.value, ctypes.byref(n)))
     return buf.raw[:n.value]
 
 

@@ -5,6 +5,8 @@
 
 #include <algorithm>
 #include <chrono>
+#include <condition_variable>
+#include <mutex>
 #include <string>
 #include <thread>
 #include <vector>
@@ -37,18 +39,48 @@ struct starch_ctx {
         bool active = false, eof = false;
         starch_options opt{};
         std::string note;
-        uint8_t* held = nullptr;      // pinned: input not yet encoded, from a segment boundary on
-        uint64_t held_n = 0, held_cap = 0, try_at = 0, batch = 0, batches = 0;
-        int64_t init_start = 0, init_stop = 0;   // sscanf values current before held[0]
+        // two pinned buffers: the caller's bytes go into buf[cur] (from a
+        // segment boundary on); a finished prefix is handed to the encoder
+        // thread while the tail moves to the other buffer (double buffering)
+        uint8_t* buf[2] = {nullptr, nullptr};
+        uint64_t cap[2] = {0, 0};
+        int cur = 0;
+        uint64_t held_n = 0, try_at = 0, batch = 0, batches = 0;
+        int64_t init_start = 0, init_stop = 0;   // sscanf values current before buf[cur][0]
+        // encoder thread and its one job slot
+        std::thread worker;
+        std::mutex mu;                // guards the job slot, ready, segs/names/stats, err
+        std::condition_variable cv;
+        bool job = false, busy = false, stop = false;
+        const uint8_t* job_buf = nullptr;
+        uint64_t job_n = 0;
+        int64_t job_is = 0, job_ip = 0;
+        int err = 0;
+        std::string err_msg;
         std::vector<uint8_t> ready;   // archive bytes not yet read, from ready_off on
         uint64_t ready_off = 0, stream_end = 4;  // archive offset of the next stream
         std::vector<starch_segment> segs;
         std::vector<std::string> names;
         starch_stats stats{};
     } sm;
+    void stream_shutdown()
+    {
+        if (sm.worker.joinable()) {
+            {
+                std::lock_guard<std::mutex> lk(sm.mu);
+                sm.stop = true;
+            }
+            sm.cv.notify_all();
+            sm.worker.join();
+        }
+        sm.stop = false;
+        sm.active = false;
+    }
     ~starch_ctx()
     {
-        if (sm.held) (void)hipHostFree(sm.held);
+        stream_shutdown();
+        for (int i = 0; i < 2; ++i)
+            if (sm.buf[i]) (void)hipHostFree(sm.buf[i]);
     }
 };
 
@@ -101,7 +133,7 @@ void json_str(std::string& o, const char* p, size_t n, bool keep_utf8 = false)
 }
 
 std::string build_index(const starch_segment* segs, const char* const* names, const uint64_t* nlens, uint64_t nseg,
-                        uint64_t index_off, const char* note, int bs)
+                        uint64_t index_off, const char* note, int bs, bool base_counts = false)
 {
     std::string j;
     j += "{\"archive\":{\"type\":\"starch\",\"format\":\"starch3-mi355x\",\"version\":{\"major\":3,\"minor\":0,"
@@ -120,6 +152,10 @@ std::string build_index(const starch_segment* segs, const char* const* names, co
         j += ",\"transformedBytes\":" + std::to_string(segs[s].text_bytes);
         j += ",\"blocks\":" + std::to_string(segs[s].n_blocks);
         j += ",\"combinedCRC\":" + std::to_string(segs[s].combined_crc);
+        if (base_counts) {   // hpp:61-62
+            j += ",\"uniqueBaseCount\":" + std::to_string(segs[s].base_count_unique);
+            j += ",\"nonUniqueBaseCount\":" + std::to_string(segs[s].base_count_nonunique);
+        }
         j += '}';
     }
     j += "]}";
@@ -275,6 +311,16 @@ void encode_units(starch_ctx* c, const uint8_t* d_base, const std::vector<UnitIn
     std::vector<uint64_t> unit_of;
     uint64_t tbytes = 0, nlines = 0;
     const uint8_t* text = transform_units(c, d_base, units, si, unit_of, tbytes, nlines);
+    std::vector<uint64_t> bc_u, bc_n;
+    if (opt.base_counts) {   // per unit (units start segments), in segment order
+        std::vector<uint64_t> uu, nn;
+        for (auto& u : units) {
+            c->tf.base_counts(d_base + u.off, u.len, c->st, u.init_start, u.init_stop, uu, nn);
+            bc_u.insert(bc_u.end(), uu.begin(), uu.end());
+            bc_n.insert(bc_n.end(), nn.begin(), nn.end());
+        }
+        if (bc_u.size() != si.size()) throw StarchError(STARCH_ERR_INTERNAL, "base counts: segment count mismatch");
+    }
     HIP_CHECK(hipEventRecord(e1, c->st));
     const uint64_t nseg = si.size();
     c->stats.n_lines = nlines;
@@ -296,6 +342,10 @@ void encode_units(starch_ctx* c, const uint8_t* d_base, const std::vector<UnitIn
         c->segs[s].text_bytes = si[s].text_len;
         c->segs[s].name_len = si[s].name_len;
         c->segs[s].unit = unit_of[s];
+        if (opt.base_counts) {
+            c->segs[s].base_count_unique = (int64_t)bc_u[s];
+            c->segs[s].base_count_nonunique = (int64_t)bc_n[s];
+        }
     }
     const uint64_t base = (lay == L_ARCHIVE) ? 4 : 0;
     if (opt.reference_compat && lay == L_ARCHIVE) {   // the reference writes only the magic (hpp:765-769)
@@ -343,7 +393,8 @@ void encode_units(starch_ctx* c, const uint8_t* d_base, const std::vector<UnitIn
         std::vector<const char*> np(nseg);
         std::vector<uint64_t> nl(nseg);
         for (uint64_t s = 0; s < nseg; ++s) { np[s] = c->names[s].data(); nl[s] = c->names[s].size(); }
-        idx = build_index(c->segs.data(), np.data(), nl.data(), nseg, index_off, opt.note, opt.block_size_100k);
+        idx = build_index(c->segs.data(), np.data(), nl.data(), nseg, index_off, opt.note, opt.block_size_100k,
+                          opt.base_counts != 0);
         if (index_off + idx.size() > cap) throw StarchError(STARCH_ERR_INTERNAL, "index capacity");
         HIP_CHECK(hipMemcpyAsync(out + index_off, idx.data(), idx.size(), hipMemcpyHostToDevice, c->st));
         total += idx.size();
@@ -456,7 +507,8 @@ void encode_multi(starch_ctx* const* ctxs, int nctx, const uint8_t* bed, uint64_
         std::vector<const char*> np(nseg);
         std::vector<uint64_t> nl(nseg);
         for (uint64_t s = 0; s < nseg; ++s) { np[s] = names[s].data(); nl[s] = names[s].size(); }
-        idx = build_index(segs.data(), np.data(), nl.data(), nseg, end, opt.note, opt.block_size_100k);
+        idx = build_index(segs.data(), np.data(), nl.data(), nseg, end, opt.note, opt.block_size_100k,
+                          opt.base_counts != 0);
     }
     Ctx g(c0);
     const uint64_t total = opt.reference_compat ? 4 : end + idx.size();
@@ -534,42 +586,41 @@ void encode_multi(starch_ctx* const* ctxs, int nctx, const uint8_t* bed, uint64_
 // where the chr token changes, and a unit encoded on its own with those
 // values gives exactly the streams of the whole input).  When at least a batch
 // of input is held, the planner finds the last segment boundary among the
-// complete lines; everything before it is encoded as one unit (H2D, transform,
-// bzip2 on the GPU) and its finished streams are appended to the archive
-// bytes ready for reading.  The held tail -- the last chromosome run, which may
-// continue in the next piece -- moves to the front.  end() encodes the rest
-// and appends the index.
+// complete lines; the prefix before it goes to the session's encoder thread
+// (H2D, transform, bzip2 on the GPU, streams D2H into the ready bytes) while
+// the held tail -- the last chromosome run, which may continue in the next
+// piece -- moves to the other pinned buffer and the caller keeps feeding.
+// end() encodes the rest and appends the index.
 
-void stream_reserve(starch_ctx* c, uint64_t need)
+void stream_reserve(starch_ctx* c, int i, uint64_t need)
 {
     auto& m = c->sm;
-    if (need <= m.held_cap) return;
-    const uint64_t cap = align_up(std::max<uint64_t>(need, 2 * m.held_cap), 1ull << 20);
+    if (need <= m.cap[i]) return;
+    const uint64_t cap = align_up(std::max<uint64_t>(need, 2 * m.cap[i]), 1ull << 20);
     void* p = nullptr;
     HIP_CHECK(hipHostMalloc(&p, cap, hipHostMallocDefault));
-    if (m.held_n) memcpy(p, m.held, m.held_n);
-    if (m.held) (void)hipHostFree(m.held);
-    m.held = static_cast<uint8_t*>(p);
-    m.held_cap = cap;
+    if (i == m.cur && m.held_n) memcpy(p, m.buf[i], m.held_n);
+    if (m.buf[i]) (void)hipHostFree(m.buf[i]);
+    m.buf[i] = static_cast<uint8_t*>(p);
+    m.cap[i] = cap;
 }
 
-// encode held[0, cut) (from a segment boundary to one, or to the end) and
-// append its streams to the ready bytes
-void stream_encode(starch_ctx* c, uint64_t cut)
+// encoder thread: encode b[0, n) (segment boundary to segment boundary, or to
+// the end) with the given initial values and append its streams
+void stream_encode(starch_ctx* c, const uint8_t* b, uint64_t n, int64_t is, int64_t ip)
 {
     auto& m = c->sm;
-    if (cut == 0) return;
-    m.stats.input_bytes += cut;
     if (m.opt.reference_compat) return;   // the reference writes only the magic (hpp:765-769)
-    uint8_t* d = c->input.as<uint8_t>(cut + 64);
-    HIP_CHECK(hipMemcpyAsync(d, m.held, cut, hipMemcpyHostToDevice, c->st));
-    std::vector<UnitIn> u(1, UnitIn{0, cut, m.init_start, m.init_stop, 0});
+    uint8_t* d = c->input.as<uint8_t>(n + 64);
+    HIP_CHECK(hipMemcpyAsync(d, b, n, hipMemcpyHostToDevice, c->st));
+    std::vector<UnitIn> u(1, UnitIn{0, n, is, ip, 0});
     encode_units(c, d, u, m.opt, L_STREAMS);
-    const uint64_t old = m.ready.size();
-    m.ready.resize(old + c->part_bytes);
+    std::vector<uint8_t> part(c->part_bytes);
     if (c->part_bytes)
-        HIP_CHECK(hipMemcpyAsync(m.ready.data() + old, c->part.p, c->part_bytes, hipMemcpyDeviceToHost, c->st));
+        HIP_CHECK(hipMemcpyAsync(part.data(), c->part.p, c->part_bytes, hipMemcpyDeviceToHost, c->st));
     HIP_CHECK(hipStreamSynchronize(c->st));
+    std::lock_guard<std::mutex> lk(m.mu);
+    m.ready.insert(m.ready.end(), part.begin(), part.end());
     for (size_t s = 0; s < c->segs.size(); ++s) {
         starch_segment g = c->segs[s];
         g.stream_offset += m.stream_end;
@@ -582,7 +633,6 @@ void stream_encode(starch_ctx* c, uint64_t cut)
     const starch_stats& x = c->stats;
     starch_stats& t = m.stats;
     t.n_lines += x.n_lines;
-    t.n_segments += x.n_segments;
     t.text_bytes += x.text_bytes;
     t.n_blocks += x.n_blocks;
     t.rle_bytes += x.rle_bytes;
@@ -599,27 +649,97 @@ void stream_encode(starch_ctx* c, uint64_t cut)
     t.ms_total += x.ms_total;
 }
 
-// encode everything before the last segment boundary among the complete lines
+void stream_worker(starch_ctx* c)
+{
+    auto& m = c->sm;
+    (void)hipSetDevice(c->device);
+    for (;;) {
+        const uint8_t* b;
+        uint64_t n;
+        int64_t is, ip;
+        {
+            std::unique_lock<std::mutex> lk(m.mu);
+            m.cv.wait(lk, [&] { return m.job || m.stop; });
+            if (!m.job) return;
+            b = m.job_buf;
+            n = m.job_n;
+            is = m.job_is;
+            ip = m.job_ip;
+            m.job = false;
+            m.busy = true;
+        }
+        int code = 0;
+        std::string msg;
+        try {
+            stream_encode(c, b, n, is, ip);
+        } catch (const StarchError& e) {
+            code = e.code;
+            msg = e.what();
+        } catch (const std::exception& e) {
+            code = STARCH_ERR_INTERNAL;
+            msg = e.what();
+        }
+        {
+            std::lock_guard<std::mutex> lk(m.mu);
+            m.busy = false;
+            if (code && !m.err) { m.err = code; m.err_msg = msg; }
+        }
+        m.cv.notify_all();
+    }
+}
+
+// wait until the encoder thread is idle; rethrow its error
+void stream_wait(starch_ctx* c)
+{
+    auto& m = c->sm;
+    std::unique_lock<std::mutex> lk(m.mu);
+    m.cv.wait(lk, [&] { return !m.job && !m.busy; });
+    if (m.err) throw StarchError(m.err, m.err_msg);
+}
+
+// hand buf[cur][0, n) to the encoder thread (the caller has waited for idle)
+void stream_submit(starch_ctx* c, uint64_t n)
+{
+    auto& m = c->sm;
+    m.stats.input_bytes += n;
+    {
+        std::lock_guard<std::mutex> lk(m.mu);
+        m.job = true;
+        m.job_buf = m.buf[m.cur];
+        m.job_n = n;
+        m.job_is = m.init_start;
+        m.job_ip = m.init_stop;
+    }
+    m.cv.notify_all();
+}
+
+// hand everything before the last segment boundary among the complete lines
+// to the encoder thread; the tail moves to the other buffer
 void stream_cut(starch_ctx* c)
 {
     auto& m = c->sm;
-    const void* nl = memrchr(m.held, '\n', m.held_n);
+    uint8_t* h = m.buf[m.cur];
+    const void* nl = memrchr(h, '\n', m.held_n);
     std::vector<shard::Unit> u;
     if (nl) {
-        const uint64_t lim = (uint64_t)(static_cast<const uint8_t*>(nl) - m.held) + 1;
-        shard::plan_units(m.held, lim, 4096, u, m.init_start, m.init_stop);
+        const uint64_t lim = (uint64_t)(static_cast<const uint8_t*>(nl) - h) + 1;
+        shard::plan_units(h, lim, 4096, u, m.init_start, m.init_stop);
     }
     if (u.size() < 2) {   // no boundary yet: the held run continues
         m.try_at = m.held_n + m.batch / 2;
         return;
     }
-    const uint64_t cut = u.back().offset;
-    stream_encode(c, cut);
-    memmove(m.held, m.held + cut, m.held_n - cut);
-    m.held_n -= cut;
+    const uint64_t cut = u.back().offset, tail = m.held_n - cut;
+    stream_wait(c);                                   // the other buffer is free again
+    const int o = 1 - m.cur;
+    stream_reserve(c, o, std::max<uint64_t>(tail + m.batch + (m.batch >> 2), 1ull << 20));
+    memcpy(m.buf[o], h + cut, tail);
+    stream_submit(c, cut);
+    m.cur = o;
+    m.held_n = tail;
     m.init_start = u.back().init_start;
     m.init_stop = u.back().init_stop;
-    m.try_at = std::max(m.batch, m.held_n + m.batch / 2);
+    m.try_at = std::max(m.batch, tail + m.batch / 2);
 }
 
 }  // namespace
@@ -677,6 +797,7 @@ int starch_create(int device, starch_ctx** out)
 void starch_destroy(starch_ctx* c)
 {
     if (!c) return;
+    c->stream_shutdown();
     (void)hipSetDevice(c->device);
     (void)hipStreamSynchronize(c->st);
     if (c->own) (void)hipStreamDestroy(c->own);
@@ -697,6 +818,7 @@ void starch_options_init(starch_options* o)
     o->emit_index = 1;
     o->reference_compat = 0;
     o->note = nullptr;
+    o->base_counts = 0;
 }
 
 int starch_encode_device(starch_ctx* c, const void* d_bed, uint64_t n, const starch_options* opt)
@@ -1049,17 +1171,22 @@ int starch_stream_begin(starch_ctx* c, const starch_options* opt, uint64_t batch
     starch_options_init(&o);
     if (opt) o = *opt;
     if (o.block_size_100k < 1 || o.block_size_100k > 9) return STARCH_ERR_ARG;
+    c->stream_shutdown();                       // a session left open is abandoned
     auto& m = c->sm;
     m.active = true;
     m.eof = false;
     m.note = o.note ? o.note : "";
     m.opt = o;
     m.opt.note = o.note ? m.note.c_str() : nullptr;
+    m.cur = 0;
     m.held_n = 0;
     m.batch = batch_bytes ? batch_bytes : (256ull << 20);
     m.try_at = m.batch;
     m.batches = 0;
     m.init_start = m.init_stop = 0;
+    m.job = m.busy = false;
+    m.err = 0;
+    m.err_msg.clear();
     m.ready.assign(kMagic, kMagic + 4);
     m.ready_off = 0;
     m.stream_end = 4;
@@ -1068,26 +1195,58 @@ int starch_stream_begin(starch_ctx* c, const starch_options* opt, uint64_t batch
     m.stats = starch_stats{};
     c->have = false;
     c->streamed = false;
+    // both pinned buffers sized once for a batch plus a long held run (kept
+    // across sessions: pinning is paid on the context's first session only)
+    stream_reserve(c, 0, 2 * m.batch);
+    stream_reserve(c, 1, 2 * m.batch);
+    m.worker = std::thread(stream_worker, c);
+    return STARCH_OK;
+    END_GUARD(c)
+}
+
+int starch_stream_window(starch_ctx* c, uint64_t min_bytes, void** ptr, uint64_t* cap)
+{
+    GUARD(c)
+    auto& m = c->sm;
+    if (!m.active) return STARCH_ERR_STATE;
+    if (!ptr || !cap) return STARCH_ERR_ARG;
+    {
+        std::lock_guard<std::mutex> lk(m.mu);
+        if (m.err) throw StarchError(m.err, m.err_msg);
+    }
+    stream_reserve(c, m.cur, m.held_n + std::max<uint64_t>(min_bytes, 1));
+    *ptr = m.buf[m.cur] + m.held_n;
+    *cap = m.cap[m.cur] - m.held_n;
+    return STARCH_OK;
+    END_GUARD(c)
+}
+
+int starch_stream_commit(starch_ctx* c, uint64_t n)
+{
+    GUARD(c)
+    auto& m = c->sm;
+    if (!m.active) return STARCH_ERR_STATE;
+    if (m.held_n + n > m.cap[m.cur]) return STARCH_ERR_ARG;
+    if (m.eof || n == 0) return STARCH_OK;
+    const uint64_t k = shard::input_limit(m.buf[m.cur] + m.held_n, n);   // 0xFF reads as EOF (hpp:181)
+    if (k < n) m.eof = true;
+    m.held_n += k;
+    if (m.held_n >= m.try_at) stream_cut(c);
     return STARCH_OK;
     END_GUARD(c)
 }
 
 int starch_stream_feed(starch_ctx* c, const void* bed, uint64_t n)
 {
-    GUARD(c)
-    auto& m = c->sm;
-    if (!m.active) return STARCH_ERR_STATE;
+    if (!c) return STARCH_ERR_ARG;
     if (n && !bed) return STARCH_ERR_ARG;
-    if (m.eof || n == 0) return STARCH_OK;
-    const uint8_t* b = static_cast<const uint8_t*>(bed);
-    const uint64_t k = shard::input_limit(b, n);   // 0xFF reads as EOF (hpp:181): the rest is never read
-    if (k < n) m.eof = true;
-    stream_reserve(c, m.held_n + k);
-    memcpy(m.held + m.held_n, b, k);
-    m.held_n += k;
-    if (m.held_n >= m.try_at) stream_cut(c);
-    return STARCH_OK;
-    END_GUARD(c)
+    if (c->sm.eof || n == 0) return c->sm.active ? STARCH_OK : STARCH_ERR_STATE;
+    void* w = nullptr;
+    uint64_t cap = 0;
+    int rc = starch_stream_window(c, n, &w, &cap);
+    if (rc) return rc;
+    memcpy(w, bed, n);
+    return starch_stream_commit(c, n);
 }
 
 int starch_stream_end(starch_ctx* c)
@@ -1095,15 +1254,24 @@ int starch_stream_end(starch_ctx* c)
     GUARD(c)
     auto& m = c->sm;
     if (!m.active) return STARCH_ERR_STATE;
-    m.active = false;
-    stream_encode(c, m.held_n);
+    try {
+        stream_wait(c);
+        if (m.held_n) {
+            stream_submit(c, m.held_n);
+            stream_wait(c);
+        }
+    } catch (...) {
+        c->stream_shutdown();
+        throw;
+    }
+    c->stream_shutdown();
     m.held_n = 0;
     if (m.opt.emit_index && !m.opt.reference_compat) {
         std::vector<const char*> np(m.segs.size());
         std::vector<uint64_t> nl(m.segs.size());
         for (size_t s = 0; s < m.segs.size(); ++s) { np[s] = m.names[s].data(); nl[s] = m.names[s].size(); }
         const std::string idx = build_index(m.segs.data(), np.data(), nl.data(), m.segs.size(), m.stream_end,
-                                            m.opt.note, m.opt.block_size_100k);
+                                            m.opt.note, m.opt.block_size_100k, m.opt.base_counts != 0);
         m.ready.insert(m.ready.end(), idx.begin(), idx.end());
         m.stats.archive_bytes = m.stream_end + idx.size();
     } else {
@@ -1123,6 +1291,7 @@ int starch_stream_end(starch_ctx* c)
 int starch_stream_available(starch_ctx* c, uint64_t* n)
 {
     if (!c || !n) return STARCH_ERR_ARG;
+    std::lock_guard<std::mutex> lk(c->sm.mu);
     *n = c->sm.ready.size() - c->sm.ready_off;
     return STARCH_OK;
 }
@@ -1131,6 +1300,7 @@ int starch_stream_read(starch_ctx* c, void* dst, uint64_t cap, uint64_t* len)
 {
     if (!c || !len || (cap && !dst)) return STARCH_ERR_ARG;
     auto& m = c->sm;
+    std::lock_guard<std::mutex> lk(m.mu);
     const uint64_t k = std::min<uint64_t>(cap, m.ready.size() - m.ready_off);
     if (k) memcpy(dst, m.ready.data() + m.ready_off, k);
     m.ready_off += k;
@@ -1151,6 +1321,20 @@ int starch_build_index(const starch_segment* segs, const char* const* names, con
 {
     if (!len || (nseg && (!segs || !names || !name_lens))) return STARCH_ERR_ARG;
     std::string s = build_index(segs, names, name_lens, nseg, index_offset, note, bs);
+    *len = s.size();
+    if (!dst) return STARCH_OK;
+    if (cap < s.size()) return STARCH_ERR_MEM;
+    memcpy(dst, s.data(), s.size());
+    return STARCH_OK;
+}
+
+int starch_build_index_opt(const starch_segment* segs, const char* const* names, const uint64_t* name_lens,
+                           uint64_t nseg, uint64_t index_offset, const starch_options* opt, char* dst, uint64_t cap,
+                           uint64_t* len)
+{
+    if (!len || !opt || (nseg && (!segs || !names || !name_lens))) return STARCH_ERR_ARG;
+    std::string s = build_index(segs, names, name_lens, nseg, index_offset, opt->note, opt->block_size_100k,
+                                opt->base_counts != 0);
     *len = s.size();
     if (!dst) return STARCH_OK;
     if (cap < s.size()) return STARCH_ERR_MEM;

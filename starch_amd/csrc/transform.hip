@@ -1289,6 +1289,132 @@ __global__ void k_seg_close_dev(SegInfo* __restrict__ info, const uint64_t* __re
     }
 }
 
+// ---------------------------------------------------------------------------
+// Base counts per segment (transform_state_t.base_count_unique /
+// base_count_nonunique, hpp:61-62, declared and zeroed by the reference but
+// never computed).  Over a segment's lines, with the start / stop values the
+// transform uses (stale sscanf values included): nonunique = sum of (stop -
+// start); unique = sum of max(0, stop - max(start, M)), M = the largest stop
+// of the segment's earlier lines (INT64_MIN before the first) -- the size of
+// the union of the intervals for a BED sorted by start.  Modulo 2^64, as the
+// oracle (oracle/starch_oracle.c oracle_base_counts).
+//
+// M is a segmented max-scan: elements (reset, max) with
+// (a, b) -> (a.reset | b.reset, b.reset ? b.max : max(a.max, b.max)).
+// Three passes: per-workgroup aggregates, one workgroup scanning them, then
+// every line's contribution, reduced per segment in LDS (a workgroup's 256
+// lines touch at most 256 segments) and added to the segment's totals.
+// ---------------------------------------------------------------------------
+struct SegMax { uint32_t r; int64_t m; };
+__device__ __forceinline__ SegMax segmax(SegMax a, SegMax b)
+{
+    return SegMax{a.r | b.r, b.r ? b.m : (a.m > b.m ? a.m : b.m)};
+}
+
+// in-workgroup inclusive segmented max-scan over 256 elements (one per thread)
+__device__ __forceinline__ SegMax segmax_scan(SegMax x, uint32_t* sr, int64_t* sm)
+{
+    const int t = threadIdx.x;
+    for (int d = 1; d < kThreads; d <<= 1) {
+        sr[t] = x.r;
+        sm[t] = x.m;
+        __syncthreads();
+        if (t >= d) x = segmax(SegMax{sr[t - d], sm[t - d]}, x);
+        __syncthreads();
+    }
+    return x;
+}
+
+__global__ void __launch_bounds__(kThreads)
+k_bc_agg(const int64_t* __restrict__ stop, const uint8_t* __restrict__ flags, uint64_t nl, uint32_t* __restrict__ agg_r,
+         int64_t* __restrict__ agg_m)
+{
+    __shared__ uint32_t sr[kThreads];
+    __shared__ int64_t sm[kThreads];
+    const uint64_t i = (uint64_t)blockIdx.x * kThreads + threadIdx.x;
+    SegMax x{0u, INT64_MIN};
+    if (i < nl) x = SegMax{(flags[i] & F_NEW_SEG) ? 1u : 0u, stop[i]};
+    x = segmax_scan(x, sr, sm);
+    if (threadIdx.x == kThreads - 1) { agg_r[blockIdx.x] = x.r; agg_m[blockIdx.x] = x.m; }
+}
+
+// one workgroup: exclusive scan of the workgroup aggregates -> incoming max
+__global__ void __launch_bounds__(1024)
+k_bc_scan(const uint32_t* __restrict__ agg_r, const int64_t* __restrict__ agg_m, uint64_t nb, int64_t* __restrict__ pre_m)
+{
+    __shared__ uint32_t cr[1024];
+    __shared__ int64_t cm[1024];
+    const uint64_t per = (nb + 1023) / 1024, b0 = threadIdx.x * per, b1 = b0 + per < nb ? b0 + per : nb;
+    SegMax a{0u, INT64_MIN};
+    for (uint64_t b = b0; b < b1; ++b) a = segmax(a, SegMax{agg_r[b], agg_m[b]});
+    cr[threadIdx.x] = a.r;
+    cm[threadIdx.x] = a.m;
+    __syncthreads();
+    if (threadIdx.x == 0) {   // exclusive over the 1024 chunk aggregates
+        SegMax run{0u, INT64_MIN};
+        for (int t = 0; t < 1024; ++t) {
+            const SegMax v{cr[t], cm[t]};
+            cr[t] = run.r;
+            cm[t] = run.m;
+            run = segmax(run, v);
+        }
+    }
+    __syncthreads();
+    SegMax run{cr[threadIdx.x], cm[threadIdx.x]};
+    for (uint64_t b = b0; b < b1; ++b) {
+        pre_m[b] = run.m;
+        run = segmax(run, SegMax{agg_r[b], agg_m[b]});
+    }
+}
+
+__global__ void __launch_bounds__(kThreads)
+k_bc_final(const int64_t* __restrict__ start, const int64_t* __restrict__ stop, const uint8_t* __restrict__ flags,
+           const uint64_t* __restrict__ seg_ord, uint64_t nl, const int64_t* __restrict__ pre_m,
+           unsigned long long* __restrict__ out_u, unsigned long long* __restrict__ out_n)
+{
+    __shared__ uint32_t sr[kThreads];
+    __shared__ int64_t sm[kThreads];
+    __shared__ unsigned long long lu[kThreads], ln[kThreads];
+    const int t = threadIdx.x;
+    const uint64_t L0 = (uint64_t)blockIdx.x * kThreads, i = L0 + t;
+    const bool valid = i < nl;
+    const uint32_t f = valid && (flags[i] & F_NEW_SEG) ? 1u : 0u;
+    const int64_t a = valid ? start[i] : 0, b = valid ? stop[i] : INT64_MIN;
+    lu[t] = 0;
+    ln[t] = 0;
+    const SegMax incl = segmax_scan(SegMax{f, b}, sr, sm);   // (ends with __syncthreads)
+    sr[t] = incl.r;
+    sm[t] = incl.m;
+    __syncthreads();
+    // the max over the segment's earlier lines: the previous line's inclusive
+    // value, after the workgroup's incoming one; nothing for a segment's first line
+    SegMax prev{0u, pre_m[blockIdx.x]};
+    if (t > 0) prev = segmax(prev, SegMax{sr[t - 1], sm[t - 1]});
+    if (valid) {
+        const int64_t M = f ? INT64_MIN : prev.m;
+        const int64_t lo = M > a ? M : a;
+        const unsigned long long u = b > lo ? (unsigned long long)((uint64_t)b - (uint64_t)lo) : 0ull;
+        const unsigned long long cd = (unsigned long long)((uint64_t)b - (uint64_t)a);
+        const uint64_t seg = seg_ord[i] + f - 1, sb = seg_ord[L0] + ((flags[L0] & F_NEW_SEG) ? 1u : 0u) - 1;
+        atomicAdd(&lu[seg - sb], u);
+        atomicAdd(&ln[seg - sb], cd);
+    }
+    __syncthreads();
+    const uint64_t Lm = (L0 + kThreads < nl ? L0 + kThreads : nl) - 1;
+    const uint64_t sb = seg_ord[L0] + ((flags[L0] & F_NEW_SEG) ? 1u : 0u) - 1;
+    const uint64_t se = seg_ord[Lm] + ((flags[Lm] & F_NEW_SEG) ? 1u : 0u) - 1;
+    if ((uint64_t)t <= se - sb) {
+        atomicAdd(out_u + sb + t, lu[t]);
+        atomicAdd(out_n + sb + t, ln[t]);
+    }
+}
+
+__global__ void k_bc_flag(const uint8_t* __restrict__ flags, uint64_t nl, uint32_t* __restrict__ seg_flag)
+{
+    const uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (i < nl) seg_flag[i] = (flags[i] & F_NEW_SEG) ? 1u : 0u;
+}
+
 }  // namespace tf
 
 // ---------------------------------------------------------------------------
@@ -1360,6 +1486,91 @@ void TransformWorkspace::run(const uint8_t* d_bed, uint64_t n, hipStream_t st, T
         return;
     }
     run_two_pass(d_bed, n, st, res, init_start, init_stop);
+}
+
+uint64_t TransformWorkspace::index_lines(const uint8_t* d_bed, uint64_t n, hipStream_t st, uint64_t* ff_pos)
+{
+    uint64_t ntile = ceil_div(n, kTileBytes);
+    uint32_t* tile_cnt = b_tile_cnt.as<uint32_t>(ntile + 1);
+    uint64_t* tile_off = b_tile_off.as<uint64_t>(ntile + 1);
+    uint64_t* scal = b_scal.as<uint64_t>(16);
+    HIP_CHECK(hipMemsetAsync(scal, 0, 16 * sizeof(uint64_t), st));
+    HIP_CHECK(hipMemsetAsync(scal + 1, 0xff, sizeof(uint64_t), st));
+    if (n > 0) {
+        hipLaunchKernelGGL(k_count_nl, dim3((unsigned)ntile), dim3(kThreads), 0, st, d_bed, n, tile_cnt,
+                           (unsigned long long*)(scal + 1));
+        scan::excl_sum_u32_to_u64(tile_cnt, tile_off, ntile, scal + 0, b_tmp, st);
+    }
+    uint64_t h[2];
+    HIP_CHECK(hipMemcpyAsync(h, scal, 2 * sizeof(uint64_t), hipMemcpyDeviceToHost, st));
+    HIP_CHECK(hipStreamSynchronize(st));
+    uint64_t nl = h[0];
+    uint64_t* line_end = b_line_end.as<uint64_t>(nl + 1);
+    if (nl) {
+        hipLaunchKernelGGL(k_index_nl, dim3((unsigned)ntile), dim3(kThreads), 0, st, d_bed, n, tile_off, line_end);
+        if (h[1] != ~0ull) {
+            hipLaunchKernelGGL(k_lines_before, dim3(1), dim3(1), 0, st, line_end, nl,
+                               (const unsigned long long*)(scal + 1), scal + 2);
+            HIP_CHECK(hipMemcpyAsync(&nl, scal + 2, sizeof(uint64_t), hipMemcpyDeviceToHost, st));
+            HIP_CHECK(hipStreamSynchronize(st));
+        }
+    }
+    if (ff_pos) *ff_pos = h[1];
+    return nl;
+}
+
+void TransformWorkspace::base_counts(const uint8_t* d_bed, uint64_t n, hipStream_t st, int64_t init_start,
+                                     int64_t init_stop, std::vector<uint64_t>& unique, std::vector<uint64_t>& nonunique)
+{
+    unique.clear();
+    nonunique.clear();
+    const uint64_t nl = index_lines(d_bed, n, st, nullptr);
+    if (nl == 0) return;
+    const uint64_t* line_end = static_cast<const uint64_t*>(b_line_end.p);
+    const unsigned nb = (unsigned)ceil_div(nl, kThreads);
+    uint64_t* scal = b_scal.as<uint64_t>(16);
+    uint32_t* any_fail = reinterpret_cast<uint32_t*>(scal + 5);
+    int64_t* start = b_start.as<int64_t>(nl);
+    int64_t* stop = b_stop.as<int64_t>(nl);
+    uint8_t* flags = b_flags.as<uint8_t>(nl);
+    hipLaunchKernelGGL(k_parse, dim3(nb), dim3(kThreads), 0, st, d_bed, line_end, nl, start, stop, flags,
+                       b_rem_beg.as<uint64_t>(nl), b_rem_len.as<uint32_t>(nl), b_chr_len.as<uint32_t>(nl), any_fail);
+    uint64_t* idx = b_idx.as<uint64_t>(nl);
+    for (int w = 0; w < 2; ++w) {   // stale values, as the general path (hpp:306-316)
+        hipLaunchKernelGGL(k_ok_index, dim3(nb), dim3(kThreads), 0, st, flags, nl,
+                           (uint8_t)(w == 0 ? F_START_OK : F_STOP_OK), idx);
+        scan::incl_max_u64(idx, nl, b_tmp, st);
+        int64_t* v = (w == 0) ? start : stop;
+        int64_t* cp = b_vcopy.as<int64_t>(nl);
+        HIP_CHECK(hipMemcpyAsync(cp, v, nl * sizeof(int64_t), hipMemcpyDeviceToDevice, st));
+        hipLaunchKernelGGL(k_gather_stale, dim3(nb), dim3(kThreads), 0, st, cp, idx, nl, w == 0 ? init_start : init_stop,
+                           v);
+    }
+    uint32_t* seg_flag = b_seg_flag.as<uint32_t>(nl);
+    uint64_t* seg_ord = b_seg_ord.as<uint64_t>(nl);
+    hipLaunchKernelGGL(k_bc_flag, dim3(nb), dim3(kThreads), 0, st, flags, nl, seg_flag);
+    scan::excl_sum_u32_to_u64(seg_flag, seg_ord, nl, scal + 3, b_tmp, st);
+    uint64_t nseg = 0;
+    HIP_CHECK(hipMemcpyAsync(&nseg, scal + 3, sizeof(uint64_t), hipMemcpyDeviceToHost, st));
+    // aggregates / incoming maxima live in the (now free) index buffers
+    uint32_t* agg_r = b_out_len.as<uint32_t>(nb + 1);
+    int64_t* agg_m = reinterpret_cast<int64_t*>(b_vcopy.as<int64_t>(nl > 2ull * nb ? nl : 2ull * nb));
+    int64_t* pre_m = agg_m + nb;
+    hipLaunchKernelGGL(k_bc_agg, dim3(nb), dim3(kThreads), 0, st, stop, flags, nl, agg_r, agg_m);
+    hipLaunchKernelGGL(k_bc_scan, dim3(1), dim3(1024), 0, st, agg_r, agg_m, (uint64_t)nb, pre_m);
+    HIP_CHECK(hipStreamSynchronize(st));
+    unsigned long long* out = reinterpret_cast<unsigned long long*>(b_seg_first.as<uint64_t>(2 * nseg + 2));
+    HIP_CHECK(hipMemsetAsync(out, 0, (2 * nseg + 2) * sizeof(uint64_t), st));
+    hipLaunchKernelGGL(k_bc_final, dim3(nb), dim3(kThreads), 0, st, start, stop, flags, seg_ord, nl, pre_m, out,
+                       out + nseg);
+    HIP_CHECK(hipGetLastError());
+    unique.resize(nseg);
+    nonunique.resize(nseg);
+    if (nseg) {
+        HIP_CHECK(hipMemcpyAsync(unique.data(), out, nseg * sizeof(uint64_t), hipMemcpyDeviceToHost, st));
+        HIP_CHECK(hipMemcpyAsync(nonunique.data(), out + nseg, nseg * sizeof(uint64_t), hipMemcpyDeviceToHost, st));
+    }
+    HIP_CHECK(hipStreamSynchronize(st));
 }
 
 void TransformWorkspace::run_two_pass(const uint8_t* d_bed, uint64_t n, hipStream_t st, TransformResult& res,

@@ -1,5 +1,7 @@
 // starch_amd/csrc/transform.hpp -- host interface of the transform stage.
 #pragma once
+#include <vector>
+
 #include "common.hpp"
 
 struct SegInfo {            // one chromosome segment (hpp:393-407 flush unit)
@@ -32,4 +34,9 @@ struct TransformWorkspace {
     // line-index based path (k_count_nl / k_index_nl, then k_tf1 + k_tf2 or the general path)
     void run_two_pass(const uint8_t* d_bed, uint64_t n, hipStream_t st, TransformResult& res, int64_t init_start,
                       int64_t init_stop);
+    // line ends of the input up to the first 0xFF (b_line_end); returns the line count
+    uint64_t index_lines(const uint8_t* d_bed, uint64_t n, hipStream_t st, uint64_t* ff_pos);
+    // per-segment base counts, modulo 2^64; leaves text / seg_info_dev untouched
+    void base_counts(const uint8_t* d_bed, uint64_t n, hipStream_t st, int64_t init_start, int64_t init_stop,
+                     std::vector<uint64_t>& unique, std::vector<uint64_t>& nonunique);
 };

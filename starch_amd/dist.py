@@ -16,7 +16,8 @@ starch_archive_layout / starch_build_index); this module only moves bytes.
 import starch_amd
 
 # metadata columns exchanged per segment
-_COLS = ("unit", "stream_offset", "stream_bytes", "line_count", "text_bytes", "n_blocks", "combined_crc", "name_len")
+_COLS = ("unit", "stream_offset", "stream_bytes", "line_count", "text_bytes", "n_blocks", "combined_crc", "name_len",
+         "base_count_unique", "base_count_nonunique")
 
 
 class TorchTransport:
@@ -61,7 +62,7 @@ def local_segments(ctx):
     return rec, [n for n, _ in segs]
 
 
-def gather_archive(tr, records, names, streams, note=None, level=9, emit_index=True):
+def gather_archive(tr, records, names, streams, note=None, level=9, emit_index=True, base_counts=False):
     """Gather every rank's streams to rank 0 in archive (unit) order.
 
     records / names: this rank's segments (``local_segments``); streams: a
@@ -117,9 +118,12 @@ def gather_archive(tr, records, names, streams, note=None, level=9, emit_index=T
         out_segs.append(starch_amd.Segment(line_count=d["line_count"], text_bytes=d["text_bytes"],
                                            stream_offset=offset[g], stream_bytes=d["stream_bytes"],
                                            name_len=len(name), n_blocks=d["n_blocks"],
-                                           combined_crc=d["combined_crc"] & 0xFFFFFFFF, unit=d["unit"]))
+                                           combined_crc=d["combined_crc"] & 0xFFFFFFFF, unit=d["unit"],
+                                           base_count_unique=d["base_count_unique"],
+                                           base_count_nonunique=d["base_count_nonunique"]))
         out_names.append(name)
-    idx = starch_amd.build_index(out_segs, out_names, end, note=note, level=level) if emit_index else b""
+    idx = (starch_amd.build_index(out_segs, out_names, end, note=note, level=level, base_counts=base_counts)
+           if emit_index else b"")
     arch = torch.empty(end + len(idx), dtype=torch.uint8, device=dev)
     arch[0:4] = torch.frombuffer(bytearray(starch_amd.MAGIC), dtype=torch.uint8)
     for r, s, d, ln in runs:

@@ -36,6 +36,7 @@ def lib():
         L.oracle_bz2_compress.restype = ctypes.c_size_t
         L.oracle_crc32_bzip2.restype = ctypes.c_uint32
         L.oracle_block_sort.restype = ctypes.c_int32
+        L.oracle_base_counts.restype = ctypes.c_size_t
         _lib = L
     return _lib
 
@@ -71,6 +72,21 @@ def transform(data: bytes, init_start=0, init_stop=0):
         res.append((data[s.name_off:s.name_off + s.name_len], s.line_count,
                     text[s.text_off:s.text_off + s.text_len]))
     return text, res
+
+
+def base_counts(data: bytes, init_start=0, init_stop=0):
+    """-> [(unique, nonunique)] per segment (int64; oracle/starch_oracle.c
+    oracle_base_counts)."""
+    L = lib()
+    seg_cap = data.count(b"\n") + 2
+    bu = (ctypes.c_uint64 * seg_cap)()
+    bn = (ctypes.c_uint64 * seg_cap)()
+    nseg = ctypes.c_size_t(0)
+    r = L.oracle_base_counts(data, ctypes.c_size_t(len(data)), ctypes.c_int64(init_start), ctypes.c_int64(init_stop),
+                             bu, bn, ctypes.c_size_t(seg_cap), ctypes.byref(nseg))
+    assert r == 0
+    s64 = lambda v: v - (1 << 64) if v >= 1 << 63 else v
+    return [(s64(bu[i]), s64(bn[i])) for i in range(nseg.value)]
 
 
 def bz2(data: bytes, bs: int = 9) -> bytes:

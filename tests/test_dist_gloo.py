@@ -30,11 +30,13 @@ def _inputs(world):
         for k, u in enumerate(units):
             if shard_of[k] != r:
                 continue
-            _, segs = oracle_lib.transform(data[u.offset:u.offset + u.length], u.init_start, u.init_stop)
-            for chr_, lines, text in segs:
+            piece = data[u.offset:u.offset + u.length]
+            _, segs = oracle_lib.transform(piece, u.init_start, u.init_stop)
+            bcs = oracle_lib.base_counts(piece, u.init_start, u.init_stop)
+            for (chr_, lines, text), (bu, bn) in zip(segs, bcs):
                 st = oracle_lib.bz2(text, 9)
                 recs.append([k, len(blob), len(st), lines, len(text), 1 + len(st) % 5, len(text) * 7919 % (1 << 32),
-                             len(chr_)])
+                             len(chr_), bu, bn])
                 names.append(chr_)
                 blob += st
         parts.append((recs, names, blob))
@@ -46,11 +48,14 @@ def _inputs(world):
         rec, name, blob = parts[r][0][i], parts[r][1][i], parts[r][2]
         segs.append(starch_amd.Segment(line_count=rec[3], text_bytes=rec[4], stream_offset=len(body),
                                        stream_bytes=rec[2], name_len=len(name), n_blocks=rec[5],
-                                       combined_crc=rec[6], unit=rec[0]))
+                                       combined_crc=rec[6], unit=rec[0], base_count_unique=rec[8],
+                                       base_count_nonunique=rec[9]))
         names.append(name)
         body += blob[rec[1]:rec[1] + rec[2]]
     assert [n for n in names] == [c for c, _, _ in whole]
-    expect = bytes(body) + starch_amd.build_index(segs, names, len(body), note="gloo")
+    # base counts of the units, in archive order, are the whole input's
+    assert [(s.base_count_unique, s.base_count_nonunique) for s in segs] == oracle_lib.base_counts(data)
+    expect = bytes(body) + starch_amd.build_index(segs, names, len(body), note="gloo", base_counts=True)
     return parts, expect
 
 
@@ -63,7 +68,7 @@ def _rank_main(rank, world, port, parts, out_path):
     recs, names, blob = parts[rank]
     tr = dist.TorchTransport(torch.device("cpu"))
     streams = torch.frombuffer(bytearray(blob or b"\0"), dtype=torch.uint8)
-    arch = dist.gather_archive(tr, recs, names, streams, note="gloo")
+    arch = dist.gather_archive(tr, recs, names, streams, note="gloo", base_counts=True)
     if rank == 0:
         with open(out_path, "wb") as f:
             f.write(arch.numpy().tobytes())

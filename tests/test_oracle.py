@@ -88,3 +88,43 @@ def test_oracle_crc():
     L = oracle_lib.lib()
     # CRC-32/BZIP2 check value of "123456789"
     assert L.oracle_crc32_bzip2(b"123456789", 9) == 0xFC891918
+
+
+# ---- base counts (hpp:61-62 declared, never computed) --------
+@pytest.mark.parametrize("bed,want", [
+    # union of [10,20) [15,30) [40,45) = 25; sum of lengths 30
+    (b"chr1\t10\t20\nchr1\t15\t30\nchr1\t40\t45\n", [(25, 30)]),
+    # nested interval adds nothing unique
+    (b"chr1\t0\t100\nchr1\t10\t20\nchr1\t50\t150\n", [(150, 210)]),
+    # a new segment resets the running maximum
+    (b"chr1\t0\t100\nchr2\t0\t100\nchr1\t50\t60\n", [(100, 100), (100, 100), (10, 10)]),
+    # stale start (x does not parse): the line is [5, 12)
+    (b"chr2\t5\t9\nchr2\tx\t12\n", [(7, 11)]),
+    # stop < start: nonunique goes negative, unique adds nothing
+    (b"chr1\t50\t40\nchr1\t60\t70\n", [(10, 0)]),
+    # the unterminated tail and everything after 0xFF are not lines
+    (b"chr1\t1\t3\nchr1\t2\t9", [(2, 2)]),
+    (b"chr1\t1\t3\n\xffchr1\t2\t9\n", [(2, 2)]),
+    (b"", []),
+])
+def test_oracle_base_counts_known(bed, want):
+    from tests import oracle_lib
+    assert oracle_lib.base_counts(bed) == want
+
+
+def test_oracle_base_counts_match_interval_union():
+    """For sorted BED the unique count is the size of the union of the
+    intervals (checked against a set of covered positions)."""
+    import random
+    from tests import oracle_lib
+    rng = random.Random(7)
+    for _ in range(20):
+        lines, pos = [], 0
+        for _ in range(rng.randint(1, 60)):
+            pos += rng.randint(0, 30)
+            lines.append((pos, pos + rng.randint(1, 50)))
+        bed = b"".join(b"chrR\t%d\t%d\n" % (a, b) for a, b in lines)
+        cover = set()
+        for a, b in lines:
+            cover.update(range(a, b))
+        assert oracle_lib.base_counts(bed) == [(len(cover), sum(b - a for a, b in lines))]

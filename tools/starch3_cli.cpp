@@ -12,12 +12,12 @@
 // --devices LIST (explicit device list, e.g. 0,1 or 0,0 for virtual shards),
 // --stats, --batch-mb N, --slurp.
 //
-// One device (the default): streaming ingestion -- a reader
-// thread reads the input in 64 MiB pieces while the main thread feeds them to
-// starch_stream_feed, which encodes every finished chromosome run on the GPU
-// as the input passes its end; finished streams are written to stdout as they
-// come, so reading, H2D + encode and writing overlap and host memory holds
-// only the unfinished chromosome run.  --slurp (and --gpus/--devices) read the
+// One device (the default): streaming ingestion -- the input
+// is read(2) in 64 MiB pieces straight into the session's pinned buffer
+// (starch_stream_window / _commit); every finished chromosome run goes to the
+// library's encoder thread (H2D + GPU encode) while reading continues into the
+// other buffer, and finished streams are written to stdout as they come, so
+// host memory holds only the unfinished chromosome run.  --slurp (and --gpus/--devices) read the
 // whole input first and encode it in one call.
 #include <errno.h>
 #include <getopt.h>
@@ -28,11 +28,7 @@
 #include <unistd.h>
 
 #include <chrono>
-#include <condition_variable>
-#include <deque>
-#include <mutex>
 #include <string>
-#include <thread>
 #include <vector>
 
 #include "../include/starch_amd.h"
@@ -59,6 +55,7 @@ static void usage(FILE* f)
             "  --stats               print per-stage timings to stderr\n"
             "  --batch-mb N          streamed encode: encode once N MiB are held (default 256)\n"
             "  --slurp               read the whole input, then encode it in one call\n"
+            "  --base-counts         per-chromosome unique / non-unique base counts in the index\n"
             "  --help | -h           this message\n"
             "  --version | -v        version\n",
             kName, kVersion, kName, kName);
@@ -67,7 +64,7 @@ static void usage(FILE* f)
 int main(int argc, char** argv)
 {
     std::string note, input;
-    int methods = 0, gzip = 0, level = 9, emit_index = 1, compat = 0, device = 0, stats = 0, slurp = 0;
+    int methods = 0, gzip = 0, level = 9, emit_index = 1, compat = 0, device = 0, stats = 0, slurp = 0, bases = 0;
     uint64_t batch_mb = 256;
     std::vector<int> devices;
     static struct option longs[] = {
@@ -78,6 +75,7 @@ int main(int argc, char** argv)
         {"device", required_argument, nullptr, 'D'}, {"stats", no_argument, nullptr, 'S'},
         {"gpus", required_argument, nullptr, 'G'},   {"devices", required_argument, nullptr, 'E'},
         {"batch-mb", required_argument, nullptr, 'M'}, {"slurp", no_argument, nullptr, 'U'},
+        {"base-counts", no_argument, nullptr, 'B'},
         {nullptr, 0, nullptr, 0}};
     opterr = 0;
     int c, li;
@@ -96,6 +94,7 @@ int main(int argc, char** argv)
             case 'S': stats = 1; break;
             case 'M': batch_mb = strtoull(optarg, nullptr, 10); break;
             case 'U': slurp = 1; break;
+            case 'B': bases = 1; break;
             case 'G': {
                 devices.clear();
                 for (int i = 0, k = atoi(optarg); i < k; ++i) devices.push_back(i);
@@ -170,25 +169,11 @@ int main(int argc, char** argv)
     opt.emit_index = emit_index;
     opt.reference_compat = compat;
     opt.note = note.empty() ? nullptr : note.c_str();
+    opt.base_counts = bases;
     if (ctxs.size() == 1 && !slurp) {
-        // streamed: reader thread -> bounded queue of pieces -> feed; drain to stdout
-        const size_t kPiece = 64u << 20, kQueue = 3;
-        std::mutex mu;
-        std::condition_variable cv;
-        std::deque<std::vector<char>> q;
-        bool done = false;
-        std::thread reader([&] {
-            for (;;) {
-                std::vector<char> b(kPiece);
-                size_t k = fread(b.data(), 1, b.size(), in);
-                b.resize(k);
-                std::unique_lock<std::mutex> lk(mu);
-                cv.wait(lk, [&] { return q.size() < kQueue; });
-                if (k == 0) { done = true; cv.notify_all(); return; }
-                q.push_back(std::move(b));
-                cv.notify_all();
-            }
-        });
+        // streamed: read(2) straight into the session's pinned buffer while the
+        // encoder thread works on the previous batch; drain finished streams
+        const uint64_t kPiece = 64ull << 20;
         std::vector<char> out(1u << 20);
         auto drain = [&]() {
             uint64_t k = 0;
@@ -197,22 +182,20 @@ int main(int argc, char** argv)
                 if (k) fwrite(out.data(), 1, k, stdout);
             } while (k == out.size());
         };
+        const int fd = fileno(in);
         rc = starch_stream_begin(ctx, &opt, batch_mb << 20);
         drain();
-        for (;;) {
-            std::vector<char> b;
-            {
-                std::unique_lock<std::mutex> lk(mu);
-                cv.wait(lk, [&] { return !q.empty() || done; });
-                if (q.empty()) break;
-                b = std::move(q.front());
-                q.pop_front();
-                cv.notify_all();
-            }
-            if (rc == STARCH_OK) rc = starch_stream_feed(ctx, b.data(), b.size());
+        while (rc == STARCH_OK) {
+            void* w = nullptr;
+            uint64_t cap = 0;
+            rc = starch_stream_window(ctx, kPiece, &w, &cap);
+            if (rc != STARCH_OK) break;
+            ssize_t k = read(fd, w, cap < kPiece ? cap : kPiece);
+            if (k < 0 && errno == EINTR) continue;
+            if (k <= 0) break;
+            rc = starch_stream_commit(ctx, (uint64_t)k);
             drain();
         }
-        reader.join();
         if (in != stdin) fclose(in);
         if (rc == STARCH_OK) rc = starch_stream_end(ctx);
         drain();
