@@ -906,11 +906,26 @@ __global__ void __launch_bounds__(256) k3_sort_w(Ctx c, const uint64_t* __restri
     __shared__ uint64_t skey[4][W_MAX + 1];
     __shared__ uint32_t sval[4][W_MAX];
     const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
-    // static assignment: workgroup L works XCD segment L mod 8 (the XCD it runs
-    // on under round-robin dealing), its waves striding over the segment
-    const uint32_t xs = blockIdx.x & 7u, nwk = (gridDim.x >> 3) * 4u;
-    const uint32_t e_end = c.qseg[xs + 1];
-    for (uint32_t it = c.qseg[xs] + (blockIdx.x >> 3) * 4u + wid; it < e_end; it += nwk) {
+    // dynamic assignment: every wave pops groups from its XCD's queue (list
+    // order per XCD: neighbouring groups share a block's PSS in its L2)
+#ifndef STARCH_W_DYN
+#define STARCH_W_DYN 0
+#endif
+    __shared__ uint32_t qs[8];
+    const uint32_t xs = xcc_id();
+    load_qsizes_binned(c, qs);
+    WaveQueue<4> wq;
+    const uint32_t xs8 = blockIdx.x & 7u, s_nwk = (gridDim.x >> 3) * 4u, s_end = c.qseg[xs8 + 1];
+    uint32_t it_s = c.qseg[xs8] + (blockIdx.x >> 3) * 4u + wid;
+    auto next_item = [&]() -> uint32_t {
+        if (!STARCH_W_DYN) {
+            const uint32_t r = it_s < s_end ? it_s : 0xFFFFFFFFu;
+            it_s += s_nwk;
+            return r;
+        }
+        return wq.next(c.qhead, qs, c.qseg, xs);
+    };
+    for (uint32_t it = next_item(); it != 0xFFFFFFFFu; it = next_item()) {
         const uint64_t item = items[it];
         const uint32_t slot = it_slot(item), s = it_start(item), m = it_size(item), par = it_par(item);
         const uint64_t base = (uint64_t)slot * c.scr.stride + s;
@@ -1025,15 +1040,40 @@ k3_sort_lds(Ctx c, const uint64_t* __restrict__ items,
     uint32_t* wcnt = cnt_all[wave];
     uint32_t* sc = sc_all[g];
     const uint64_t lt = lanemask_lt();
-    // static assignment: workgroup L works XCD segment L mod 8 (the XCD it runs
-    // on under round-robin dealing); its IPW groups stride over the segment
-    // (hard_n: an unbinned list of *hard_n groups, grid-strided)
-    const uint32_t xs = blockIdx.x & 7u;
-    const uint32_t nwk = hard_n ? gridDim.x * (uint32_t)IPW : (gridDim.x >> 3) * (uint32_t)IPW;
-    const uint32_t e_end = hard_n ? *hard_n : c.qseg[xs + 1];
-    const uint32_t it0 = hard_n ? blockIdx.x * (uint32_t)IPW + (uint32_t)g
-                                : c.qseg[xs] + (blockIdx.x >> 3) * (uint32_t)IPW + (uint32_t)g;
-    for (uint32_t it = it0; it < e_end; it += nwk) {
+    // binned list: dynamic pops from the XCD's queue (a workgroup per group for
+    // NW = 4, a wave per group for NW = 1), so an XCD's groups are worked in
+    // list order (neighbouring groups share a block's PSS in its L2).
+    // hard_n: an unbinned list of *hard_n groups, grid-strided.
+    constexpr uint32_t NONE = 0xFFFFFFFFu;
+    __shared__ uint32_t qs[8];
+    __shared__ uint32_t job_sh;
+    const uint32_t xs = xcc_id();
+    if (!hard_n) load_qsizes_binned(c, qs);
+    const uint32_t nwk = gridDim.x * (uint32_t)IPW;
+    const uint32_t e_end = hard_n ? *hard_n : 0u;
+    WaveQueue<1> wq;
+    uint32_t it_s = blockIdx.x * (uint32_t)IPW + (uint32_t)g;   // hard_n walk
+#ifndef STARCH_LDS_DYN
+#define STARCH_LDS_DYN 0
+#endif
+    const uint32_t xs8 = blockIdx.x & 7u;                        // static: segment L mod 8
+    const uint32_t s_end = hard_n ? e_end : c.qseg[xs8 + 1];
+    const uint32_t s_nwk = hard_n ? nwk : (gridDim.x >> 3) * (uint32_t)IPW;
+    if (!hard_n) it_s = c.qseg[xs8] + (blockIdx.x >> 3) * (uint32_t)IPW + (uint32_t)g;
+    auto next_item = [&]() -> uint32_t {
+        if (hard_n || !STARCH_LDS_DYN) {
+            const uint32_t r = it_s < s_end ? it_s : NONE;
+            it_s += s_nwk;
+            return r;
+        }
+        if constexpr (NW == 1) {
+            return wq.next(c.qhead, qs, c.qseg, xs);
+        } else {
+            const uint32_t j = wg_pop(c, qs, &job_sh, xs);
+            return j == NONE ? NONE : c.qseg[j >> 28] + (j & 0x0FFFFFFFu);
+        }
+    };
+    for (uint32_t it = next_item(); it != NONE; it = next_item()) {
     const uint64_t item = items[it];
     const uint32_t slot = it_slot(item), s = it_start(item), m = it_size(item), par = it_par(item);
     const uint64_t base = (uint64_t)slot * c.scr.stride + s;
@@ -1481,19 +1521,30 @@ k3_sort_grp(Ctx c, const uint64_t* __restrict__ items,
     uint32_t* bst = bst_all[g];
     uint32_t* bcur = bcur_all[g];
     const int tg = wid * 64 + lane;
-    // static assignment: workgroup L works XCD segment L mod 8 (the XCD it runs
-    // on under round-robin dealing); its IPW groups stride over the segment
-    const uint32_t xs = blockIdx.x & 7u, nwk = (gridDim.x >> 3) * (uint32_t)IPW;
-    const uint32_t e_end = c.qseg[xs + 1];
-    uint32_t it = c.qseg[xs] + (blockIdx.x >> 3) * (uint32_t)IPW + (uint32_t)g;
+#ifndef STARCH_GRP_CHUNK
+#define STARCH_GRP_CHUNK 16
+#endif
+    // dynamic assignment (NW == 1): each wave pops groups, STARCH_GRP_CHUNK at a time,
+    // from its XCD's queue, so the XCD's waves stay on neighbouring groups (one block's
+    // PSS in its L2) however uneven the groups' costs; static striding drifted
+    // apart by many blocks over a launch (a third of the key loads missed L2)
+    static_assert(NW == 1, "k3_sort_grp: one wave per group");
+    __shared__ uint32_t qs[8];
+    const uint32_t xs = xcc_id();
+    load_qsizes_binned(c, qs);
+    WaveQueue<STARCH_GRP_CHUNK> wq;
+    constexpr uint32_t NONE = 0xFFFFFFFFu;
+    uint32_t it = wq.next(c.qhead, qs, c.qseg, xs);
+    uint32_t it1 = it != NONE ? wq.next(c.qhead, qs, c.qseg, xs) : NONE;
+    uint32_t it2 = it1 != NONE ? wq.next(c.qhead, qs, c.qseg, xs) : NONE;
     GrpIn<E> cur, nxt;
-    cur.item = it < e_end ? items[it] : 0ull;
-    nxt.item = it + nwk < e_end ? items[it + nwk] : 0ull;
-    grp_load_vals<NW, E>(c, cur, it < e_end, wid, lane);
+    cur.item = it != NONE ? items[it] : 0ull;
+    nxt.item = it1 != NONE ? items[it1] : 0ull;
+    grp_load_vals<NW, E>(c, cur, it != NONE, wid, lane);
     grp_load_keys<NW, E, DBL>(c, cur, wid, lane);
-    grp_load_vals<NW, E>(c, nxt, it + nwk < e_end, wid, lane);
-    uint64_t nitem2 = it + 2 * nwk < e_end ? items[it + 2 * nwk] : 0ull;
-    for (; it < e_end; it += nwk) {
+    grp_load_vals<NW, E>(c, nxt, it1 != NONE, wid, lane);
+    uint64_t nitem2 = it2 != NONE ? items[it2] : 0ull;
+    while (it != NONE) {
     const uint64_t item = cur.item;
     const uint32_t slot = it_slot(item), s = it_start(item), m = it_size(item);
     gsync<NW>();                                   // the previous group's LDS reads are done
@@ -1591,7 +1642,8 @@ k3_sort_grp(Ctx c, const uint64_t* __restrict__ items,
     }
     // next group's keys (its rotations were loaded one group ago), the item after it
     grp_load_keys<NW, E, DBL>(c, nxt, wid, lane);
-    const uint64_t nitem3 = it + 3 * nwk < e_end ? items[it + 3 * nwk] : 0ull;
+    const uint32_t it3 = it2 != NONE ? wq.next(c.qhead, qs, c.qseg, xs) : NONE;
+    const uint64_t nitem3 = it3 != NONE ? items[it3] : 0ull;
     if (!is_hard) {
     gsync<NW>();
 #pragma unroll
@@ -1650,7 +1702,10 @@ k3_sort_grp(Ctx c, const uint64_t* __restrict__ items,
     cur = nxt;
     nxt.item = nitem2;
     nitem2 = nitem3;
-    grp_load_vals<NW, E>(c, nxt, it + 2 * nwk < e_end, wid, lane);
+    grp_load_vals<NW, E>(c, nxt, it2 != NONE, wid, lane);
+    it = it1;
+    it1 = it2;
+    it2 = it3;
     }
 }
 
@@ -1790,7 +1845,7 @@ void launch_bwt3(BlockDesc* blocks, uint32_t b0, uint32_t nb, const uint8_t* blk
                    cap_m2 = N / (M1_MAX + 1) + 64,
                    cap_m3 = N / (M2_MAX + 1) + 64, cap_l = N / ((L_MIN < M3_MAX ? L_MIN : M3_MAX) + 1) + 64;
     const uint64_t nwg_bin = BIN_MAXWG;
-    constexpr uint32_t QSETS = 64, QSET = 32;                   // queue heads + segments per launch
+    constexpr uint32_t QSETS = 64, QSET = 8 * XQ_STRIDE + 32;   // queue heads (a line each) + segments per launch
     const uint64_t words = 2 * C_N + 10ull * nb + QSETS * QSET + nwg_bin * nb +
                            2 * (cap_s + cap_s2 + cap_m1 + cap_m2 + cap_m3 + 2 * cap_l) + 64;
     uint32_t* mw = meta.as<uint32_t>(words);
@@ -1838,7 +1893,7 @@ void launch_bwt3(BlockDesc* blocks, uint32_t b0, uint32_t nb, const uint8_t* blk
             qnext = 0;
         }
         head = qpool + qnext * QSET;
-        seg = head + 16;
+        seg = head + 8 * XQ_STRIDE;
         ++qnext;
     };
     auto read_ctr = [&]() {

@@ -47,6 +47,10 @@ __device__ __forceinline__ uint32_t xcc_id()
     return (uint32_t)__builtin_amdgcn_s_getreg(20 | (0 << 6) | (3 << 11)) & 7u;   // hwreg(HW_REG_XCC_ID, 0, 4)
 }
 
+// Queue y's head word sits at head[y * XQ_STRIDE]: one 128-B line per head, so
+// the XCDs' atomics never share a line.
+constexpr uint32_t XQ_STRIDE = 32;
+
 // qsize[y] = items in queue y; returns (y << 28) | index, or ~0u when all are
 // drained.  Called by one lane.
 __device__ __forceinline__ uint32_t xq_pop(uint32_t* head, const uint32_t* qsize, uint32_t x)
@@ -54,12 +58,53 @@ __device__ __forceinline__ uint32_t xq_pop(uint32_t* head, const uint32_t* qsize
     for (uint32_t t = 0; t < 8; ++t) {
         const uint32_t y = (x + t) & 7u;
         const uint32_t sz = qsize[y];
-        if (__hip_atomic_load(head + y, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) >= sz) continue;
-        const uint32_t i = atomicAdd(head + y, 1u);
+        if (__hip_atomic_load(head + y * XQ_STRIDE, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) >= sz) continue;
+        const uint32_t i = atomicAdd(head + y * XQ_STRIDE, 1u);
         if (i < sz) return (y << 28) | i;
     }
     return 0xFFFFFFFFu;
 }
+
+// Chunked pop: up to k consecutive items; cnt = how many.  Called by one lane.
+__device__ __forceinline__ uint32_t xq_pop_n(uint32_t* head, const uint32_t* qsize, uint32_t x, uint32_t k,
+                                             uint32_t& cnt)
+{
+    for (uint32_t t = 0; t < 8; ++t) {
+        const uint32_t y = (x + t) & 7u;
+        const uint32_t sz = qsize[y];
+        if (__hip_atomic_load(head + y * XQ_STRIDE, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) >= sz) continue;
+        const uint32_t i = atomicAdd(head + y * XQ_STRIDE, k);
+        if (i < sz) {
+            cnt = sz - i < k ? sz - i : k;
+            return (y << 28) | i;
+        }
+    }
+    cnt = 0;
+    return 0xFFFFFFFFu;
+}
+
+// A wave's walk over per-XCD queues of a segmented list (seg[y] = start of
+// queue y in the list): items come in list order per XCD, so the waves of one
+// XCD stay on neighbouring items (one block's data in that XCD's L2) however
+// uneven the items' costs.  next() is wave-uniform; ~0u when drained.
+template <uint32_t K>
+struct WaveQueue {
+    uint32_t a = 0, r = 0;
+    __device__ __forceinline__ uint32_t next(uint32_t* head, const uint32_t* qsize, const uint32_t* seg, uint32_t x)
+    {
+        if (r == 0) {
+            uint32_t j = 0, cnt = 0;
+            if ((threadIdx.x & 63) == 0) j = xq_pop_n(head, qsize, x, K, cnt);
+            j = (uint32_t)__shfl((int)j, 0, 64);
+            cnt = (uint32_t)__shfl((int)cnt, 0, 64);
+            if (j == 0xFFFFFFFFu) return 0xFFFFFFFFu;
+            a = seg[j >> 28] + (j & 0x0FFFFFFFu);
+            r = cnt;
+        }
+        --r;
+        return a++;
+    }
+};
 
 // ---- move-to-front on a list of <= 16 symbols kept as nibbles of a u64 ----
 struct NibState {          // transform L -> list ++ (L \ set)

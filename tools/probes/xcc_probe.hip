@@ -1,5 +1,6 @@
 // Probe: which XCD does workgroup L run on?  (placement check for the per-XCD
 // queues; prints a histogram of (L mod 8, XCC_ID) pairs)
+//   hipcc -O3 --offload-arch=gfx950 tools/probes/xcc_probe.hip -o starch_amd/_build/xcc_probe
 #include <hip/hip_runtime.h>
 #include <stdio.h>
 __global__ void k(unsigned* o)
