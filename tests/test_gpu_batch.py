@@ -1,0 +1,36 @@
+"""Block-sort batches after the first: the encoder sorts the
+distinct blocks in batches sized by free HBM (bz2_encoder.hip); every test
+input fits one batch, so STARCH_BWT_BATCH caps it in a child process and the
+archive must equal the one-batch archive byte for byte (per-batch scratch
+reuse, k_tables32's batch-relative indexing, the host block-descriptor round
+trips).  Reference behaviour: each block's stream bytes depend on that block
+alone (bz:compress.c:602-667)."""
+import os
+import subprocess
+import sys
+
+import pytest
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+
+CHILD = ("import sys; sys.path.insert(0, %r); import starch_amd; "
+         "d = open(sys.argv[1], 'rb').read(); c = starch_amd.Starch(0); "
+         "sys.stdout.buffer.write(c.compress(d)); c.close()" % ROOT)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("cap", [1, 3])
+def test_small_bwt_batches_bit_identical(tmp_path, cap):
+    import starch_amd
+    data = starch_amd.gen_bed(0, 600_000)
+    c = starch_amd.Starch(0)
+    arch = c.compress(data)
+    nb = c.stats()["n_blocks"]
+    c.close()
+    assert nb > 2 * cap
+    f = tmp_path / "in.bed"
+    f.write_bytes(data)
+    env = dict(os.environ, STARCH_BWT_BATCH=str(cap))
+    out = subprocess.run([sys.executable, "-c", CHILD, str(f)], env=env, capture_output=True, timeout=300)
+    assert out.returncode == 0, out.stderr.decode()[-2000:]
+    assert out.stdout == arch
