@@ -19,6 +19,12 @@
  *   starch_transform_*   hpp:158-504 alone (the stderr "Content" text)
  *   starch_bz2_compress_* one BZ2_bzCompressInit + BZ2_bzCompress(BZ_FINISH)
  *                        stream (bz:bzlib.c:148-474), byte-identical
+ *   starch_bz2_decompress_* / starch_unstarch_host
+ *                        the decompression side: bzip2-1.0.6's
+ *                        BZ2_bzDecompress (bz:decompress.c:106-646,
+ *                        bz:bzlib.c:621-708) over concatenated streams, and the
+ *                        inverse of hpp:428-504 (segment text -> BED lines),
+ *                        which the reference does not ship (BEDOPS unstarch)
  *   the archive layout   magic bytes ca 5c ad 1a (hpp:765-769, 907-910), then
  *                        one bzip2 stream per chromosome segment, then a JSON
  *                        index and a 32-byte footer (DESIGN.md "Archive")
@@ -40,6 +46,7 @@ extern "C" {
 #define STARCH_ERR_STATE (-4)      /* no result yet */
 #define STARCH_ERR_DEVICE (-10)    /* HIP runtime error or no MI355X */
 #define STARCH_ERR_INTERNAL (-11)
+#define STARCH_ERR_DATA (-12)       /* malformed / corrupt compressed data (bz: BZ_DATA_ERROR, BZ_DATA_ERROR_MAGIC) */
 
 typedef struct starch_ctx starch_ctx;
 
@@ -211,6 +218,36 @@ int starch_build_index(const starch_segment* segs, const char* const* names, con
 int starch_build_index_opt(const starch_segment* segs, const char* const* names, const uint64_t* name_lens,
                            uint64_t nseg, uint64_t index_offset, const starch_options* opt, char* dst, uint64_t cap,
                            uint64_t* len);
+
+/* ---- decompression / unstarch -------------------------------
+ * Results stay in the context: starch_output_size / _copy / _device. */
+typedef struct {
+    uint64_t in_beg, in_end;     /* the stream's bytes in the input */
+    uint64_t out_off, out_len;   /* its decompressed bytes in the output */
+    uint32_t level;              /* blockSize100k of its "BZh" header */
+    uint32_t n_blocks;
+    uint32_t combined_crc;       /* stored = recomputed (checked) */
+} starch_dec_stream;
+
+/* Every bzip2 stream of in[0, n) (concatenated streams, as bzip2 -d), decoded
+ * on the GPU with every block CRC and stream CRC checked; STARCH_ERR_DATA on
+ * malformed input or a CRC mismatch (bz: BZ_DATA_ERROR).  Randomised blocks
+ * (bzip2 < 0.9.5) are refused. */
+int starch_bz2_decompress_host(starch_ctx* ctx, const void* in, uint64_t n);
+int starch_bz2_decompress_device(starch_ctx* ctx, const void* d_in, uint64_t n);
+int starch_bz2_stream_count(starch_ctx* ctx, uint64_t* n);
+int starch_bz2_streams(starch_ctx* ctx, starch_dec_stream* out, uint64_t cap);
+/* Inverse transform of one segment's text: "chr\tstart\tstop[\trem]\n" lines.
+ * Exact for canonical BED (decimal coordinates, stop >= start); a negative
+ * p-value (whose newline the forward transform drops, hpp:440,452) or a
+ * malformed line gives STARCH_ERR_DATA. */
+int starch_untransform_host(starch_ctx* ctx, const void* text, uint64_t n, const char* chr, uint64_t chr_len);
+/* A whole archive of this library (magic, streams, index, footer) back to BED:
+ * every stream decoded and inverse-transformed on the GPU, in index order. */
+int starch_unstarch_host(starch_ctx* ctx, const void* archive, uint64_t n);
+int starch_output_size(starch_ctx* ctx, uint64_t* n);
+int starch_output_copy(starch_ctx* ctx, void* dst, uint64_t cap);
+int starch_output_device(starch_ctx* ctx, const void** d_ptr);
 
 #ifdef __cplusplus
 }

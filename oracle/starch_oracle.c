@@ -724,3 +724,77 @@ size_t oracle_bz2_compress(const uint8_t* in, size_t n, int bs100k, uint8_t* out
     if (s.bw.overflow) return (size_t)-1;
     return s.bw.nbytes;
 }
+
+/* -------------------------------------------------------------------------
+ * (3) The inverse transform (unstarch): one segment's text ->
+ * BED lines "chr\tstart\tstop[\trem]\n", walking the forward transform's state
+ * (hpp:428-504) line by line: "p<cd>" sets cd; "<v>[\t<rem>]" gives
+ * start = last_stop ? last_stop + v : v, stop = start + cd, last_stop = stop.
+ * Arithmetic modulo 2^64 like the forward int64 differences.  Returns the
+ * output length, or (size_t)-1 for text the forward transform cannot produce
+ * in an invertible way (a negative p-value: its newline was dropped,
+ * hpp:440,452; a malformed line; a final line without its newline).
+ * ------------------------------------------------------------------------- */
+static int ut_parse(const uint8_t* t, size_t b, size_t e, int64_t* v)
+{
+    int neg = 0;
+    uint64_t a = 0;
+    if (b < e && t[b] == '-') { neg = 1; ++b; }
+    if (b >= e || e - b > 19) return 0;
+    for (size_t k = b; k < e; ++k) {
+        if (t[k] < '0' || t[k] > '9') return 0;
+        a = a * 10u + (uint64_t)(t[k] - '0');
+    }
+    *v = neg ? (int64_t)(0ull - a) : (int64_t)a;
+    return 1;
+}
+
+static size_t ut_put(uint8_t* o, int64_t v)
+{
+    char buf[24];
+    uint64_t u = v < 0 ? 0ull - (uint64_t)v : (uint64_t)v;
+    int k = 0;
+    do { buf[k++] = (char)('0' + u % 10u); u /= 10u; } while (u);
+    size_t n = 0;
+    if (v < 0) o[n++] = '-';
+    while (k) o[n++] = (uint8_t)buf[--k];
+    return n;
+}
+
+size_t oracle_untransform(const uint8_t* t, size_t n, const uint8_t* chr, size_t chr_len, uint8_t* out, size_t cap)
+{
+    uint64_t last_stop = 0;
+    int64_t cd = 0;
+    size_t o = 0, pos = 0;
+    while (pos < n) {
+        const uint8_t* nl = (const uint8_t*)memchr(t + pos, '\n', n - pos);
+        if (!nl) return (size_t)-1;
+        size_t ls = pos, le = (size_t)(nl - t);                 /* le: the '\n' */
+        pos = le + 1;
+        if (t[ls] == 'p') {
+            if (!ut_parse(t, ls + 1, le, &cd) || cd < 0) return (size_t)-1;
+            continue;
+        }
+        size_t e = ls;
+        while (e < le && t[e] != '\t') ++e;
+        int64_t v;
+        if (!ut_parse(t, ls, e, &v)) return (size_t)-1;
+        const uint64_t start = last_stop ? last_stop + (uint64_t)v : (uint64_t)v;
+        const uint64_t stop = start + (uint64_t)cd;
+        if (o + chr_len + 48 + (le - e) > cap) return (size_t)-1;
+        memcpy(out + o, chr, chr_len);
+        o += chr_len;
+        out[o++] = '\t';
+        o += ut_put(out + o, (int64_t)start);
+        out[o++] = '\t';
+        o += ut_put(out + o, (int64_t)stop);
+        if (e < le) {
+            out[o++] = '\t';
+            memcpy(out + o, t + e + 1, le - e - 1);
+            o += le - e - 1;
+        }
+        out[o++] = '\n';
+        last_stop = stop;
+    }
+    return o;
+}

@@ -72,6 +72,13 @@ class Stats(ctypes.Structure):
 _lib = None
 
 
+class DecStream(ctypes.Structure):
+    """starch_dec_stream: one decoded bzip2 stream."""
+    _fields_ = [("in_beg", ctypes.c_uint64), ("in_end", ctypes.c_uint64), ("out_off", ctypes.c_uint64),
+                ("out_len", ctypes.c_uint64), ("level", ctypes.c_uint32), ("n_blocks", ctypes.c_uint32),
+                ("combined_crc", ctypes.c_uint32)]
+
+
 def load():
     """Load libstarch_amd.so (raises if it was not built)."""
     global _lib
@@ -140,6 +147,15 @@ def load():
         "starch_stream_end": ([vp], ctypes.c_int),
         "starch_stream_available": ([vp, pu64], ctypes.c_int),
         "starch_stream_read": ([vp, vp, u64, pu64], ctypes.c_int),
+        "starch_bz2_decompress_host": ([vp, ctypes.c_char_p, u64], ctypes.c_int),
+        "starch_bz2_decompress_device": ([vp, vp, u64], ctypes.c_int),
+        "starch_bz2_stream_count": ([vp, pu64], ctypes.c_int),
+        "starch_bz2_streams": ([vp, ctypes.POINTER(DecStream), u64], ctypes.c_int),
+        "starch_untransform_host": ([vp, ctypes.c_char_p, u64, ctypes.c_char_p, u64], ctypes.c_int),
+        "starch_unstarch_host": ([vp, ctypes.c_char_p, u64], ctypes.c_int),
+        "starch_output_size": ([vp, pu64], ctypes.c_int),
+        "starch_output_copy": ([vp, vp, u64], ctypes.c_int),
+        "starch_output_device": ([vp, ctypes.POINTER(vp)], ctypes.c_int),
     }
     for name, (args, res) in sig.items():
         f = getattr(L, name)
@@ -380,6 +396,49 @@ class Starch:
         _check(self._L.starch_bz2_compress_many_device(self._h, ctypes.c_void_p(d_in), O, N, k, level,
                                                        ctypes.c_void_p(d_out), cap, oo, ol), self._h)
         return list(oo[:k]), list(ol[:k])
+
+
+    # ---- decompression / unstarch ----
+    def _output(self) -> bytes:
+        n = ctypes.c_uint64()
+        _check(self._L.starch_output_size(self._h, ctypes.byref(n)), self._h)
+        buf = ctypes.create_string_buffer(max(1, n.value))
+        _check(self._L.starch_output_copy(self._h, buf, n.value), self._h)
+        return buf.raw[:n.value]
+
+    def bz2_decompress(self, data: bytes) -> bytes:
+        """Concatenated bzip2 streams -> their bytes (GPU decode, CRCs checked)."""
+        _check(self._L.starch_bz2_decompress_host(self._h, data, len(data)), self._h)
+        return self._output()
+
+    def bz2_decompress_device(self, d_ptr: int, n: int) -> int:
+        """Device-resident streams; returns the output size (output_device_ptr())."""
+        _check(self._L.starch_bz2_decompress_device(self._h, ctypes.c_void_p(d_ptr), n), self._h)
+        k = ctypes.c_uint64()
+        _check(self._L.starch_output_size(self._h, ctypes.byref(k)), self._h)
+        return k.value
+
+    def output_device_ptr(self) -> int:
+        p = ctypes.c_void_p()
+        _check(self._L.starch_output_device(self._h, ctypes.byref(p)), self._h)
+        return p.value or 0
+
+    def decoded_streams(self):
+        n = ctypes.c_uint64()
+        _check(self._L.starch_bz2_stream_count(self._h, ctypes.byref(n)), self._h)
+        arr = (DecStream * max(1, n.value))()
+        _check(self._L.starch_bz2_streams(self._h, arr, n.value), self._h)
+        return [{f: getattr(arr[i], f) for f, _ in DecStream._fields_} for i in range(n.value)]
+
+    def untransform(self, text: bytes, chromosome: bytes) -> bytes:
+        """One segment's transformed text -> its BED lines (inverse of hpp:428-504)."""
+        _check(self._L.starch_untransform_host(self._h, text, len(text), chromosome, len(chromosome)), self._h)
+        return self._output()
+
+    def unstarch(self, archive: bytes) -> bytes:
+        """An archive of this library back to BED (decode + inverse transform on the GPU)."""
+        _check(self._L.starch_unstarch_host(self._h, archive, len(archive)), self._h)
+        return self._output()
 
 
 def gen_bed(kind, total_lines, chroms=None, seed=20261015, into=None):

@@ -13,8 +13,10 @@
 
 #include "../../include/starch_amd.h"
 #include "bz2.hpp"
+#include "bz2_decode.hpp"
 #include "shard.hpp"
 #include "transform.hpp"
+#include "untransform.hpp"
 
 struct starch_ctx {
     int device = 0;
@@ -23,6 +25,14 @@ struct starch_ctx {
     TransformWorkspace tf;
     bz::Encoder enc;
     DevBuf input, archive, part, raw_in, raw_out, text_all;
+    // decompression / unstarch: the last result is out_dev[0, out_bytes)
+    bz::Decoder dec;
+    ut::Untransform untf;
+    DevBuf dec_in, dec_out, ut_out;
+    const uint8_t* out_dev = nullptr;
+    uint64_t out_bytes = 0;
+    bool have_out = false;
+    std::vector<bz::DecStream> dstreams;
     std::string err;
     // last result
     bool have = false;
@@ -765,6 +775,7 @@ const char* starch_strerror(int code)
         case STARCH_ERR_MEM: return "out of memory or buffer too small";
         case STARCH_ERR_STATE: return "no result available";
         case STARCH_ERR_DEVICE: return "HIP device error";
+        case STARCH_ERR_DATA: return "malformed or corrupt compressed data";
         default: return "internal error";
     }
 }
@@ -1340,6 +1351,203 @@ int starch_build_index_opt(const starch_segment* segs, const char* const* names,
     if (cap < s.size()) return STARCH_ERR_MEM;
     memcpy(dst, s.data(), s.size());
     return STARCH_OK;
+}
+
+}  // extern "C"
+
+namespace {
+
+// Reader of this library's archive index (build_index above): the footer's
+// index offset, then per stream its chromosome (JSON string, \u00XX escapes
+// byte-wise), offset and size.  Only what unstarch needs; anything else is
+// skipped.  Throws on a layout build_index does not write.
+struct IndexEntry { std::string chr; uint64_t offset, size; };
+
+std::vector<IndexEntry> read_index(const uint8_t* a, uint64_t n, uint64_t* index_off)
+{
+    auto bad = [](const char* m) { throw StarchError(STARCH_ERR_DATA, std::string("archive: ") + m); };
+    if (n < 4 + 32 || memcmp(a, kMagic, 4) != 0) bad("no magic / footer");
+    const char* f = reinterpret_cast<const char*>(a + n - 32);
+    uint64_t off = 0;
+    for (int i = 0; i < 20; ++i) {
+        if (f[i] < '0' || f[i] > '9') bad("footer");
+        off = off * 10 + (uint64_t)(f[i] - '0');
+    }
+    if (f[31] != '\n' || off < 4 || off > n - 32) bad("footer");
+    *index_off = off;
+    const std::string j(reinterpret_cast<const char*>(a + off), n - 32 - off);
+    std::vector<IndexEntry> out;
+    size_t p = j.find("\"streams\":[");
+    if (p == std::string::npos) bad("index without streams");
+    p += 11;
+    auto num = [&](const char* key, size_t from, size_t to) -> uint64_t {
+        const std::string k = std::string("\"") + key + "\":";
+        size_t q = j.find(k, from);
+        if (q == std::string::npos || q > to) bad("index field missing");
+        q += k.size();
+        uint64_t v = 0;
+        if (q >= j.size() || j[q] < '0' || j[q] > '9') bad("index number");
+        while (q < j.size() && j[q] >= '0' && j[q] <= '9') v = v * 10 + (uint64_t)(j[q++] - '0');
+        return v;
+    };
+    while (p < j.size() && j[p] == '{') {
+        const size_t e = j.find('}', p);   // entries hold no nested objects
+        if (e == std::string::npos) bad("index entry");
+        size_t q = j.find("\"chromosome\":\"", p);
+        if (q == std::string::npos || q > e) bad("index chromosome");
+        q += 14;
+        std::string chr;
+        for (;;) {
+            if (q >= e) bad("index string");
+            const char ch = j[q];
+            if (ch == '"') break;
+            if (ch != '\\') { chr += ch; ++q; continue; }
+            const char x = j[q + 1];
+            if (x == 'u') {
+                unsigned v = 0;
+                for (int k = 2; k < 6; ++k) {
+                    const char h = j[q + k];
+                    v = v * 16 + (unsigned)(h >= '0' && h <= '9' ? h - '0' : h >= 'a' && h <= 'f' ? h - 'a' + 10
+                                             : h >= 'A' && h <= 'F' ? h - 'A' + 10 : 0);
+                }
+                chr += (char)v;
+                q += 6;
+            } else {
+                chr += x == 'n' ? '\n' : x == 't' ? '\t' : x == 'r' ? '\r' : x == 'b' ? '\b' : x == 'f' ? '\f' : x;
+                q += 2;
+            }
+        }
+        out.push_back(IndexEntry{chr, num("offset", p, e), num("size", p, e)});
+        p = e + 1;
+        if (p < j.size() && j[p] == ',') ++p;
+    }
+    return out;
+}
+
+}  // namespace
+
+extern "C" {
+
+int starch_bz2_decompress_device(starch_ctx* c, const void* d_in, uint64_t n)
+{
+    GUARD(c)
+    if (n && !d_in) return STARCH_ERR_ARG;
+    c->have_out = false;
+    uint8_t* d = c->dec_in.as<uint8_t>(n + 256);   // aligned copy with read-ahead padding
+    if (n) HIP_CHECK(hipMemcpyAsync(d, d_in, n, hipMemcpyDeviceToDevice, c->st));
+    HIP_CHECK(hipMemsetAsync(d + n, 0, 256, c->st));
+    c->out_bytes = c->dec.decode(d, n, nullptr, c->st, c->dec_out, c->dstreams);
+    c->out_dev = static_cast<const uint8_t*>(c->dec_out.p);
+    c->have_out = true;
+    return STARCH_OK;
+    END_GUARD(c)
+}
+
+int starch_bz2_decompress_host(starch_ctx* c, const void* in, uint64_t n)
+{
+    GUARD(c)
+    if (n && !in) return STARCH_ERR_ARG;
+    c->have_out = false;
+    uint8_t* d = c->dec_in.as<uint8_t>(n + 256);
+    if (n) HIP_CHECK(hipMemcpyAsync(d, in, n, hipMemcpyHostToDevice, c->st));
+    HIP_CHECK(hipMemsetAsync(d + n, 0, 256, c->st));
+    c->out_bytes = c->dec.decode(d, n, static_cast<const uint8_t*>(in), c->st, c->dec_out, c->dstreams);
+    c->out_dev = static_cast<const uint8_t*>(c->dec_out.p);
+    c->have_out = true;
+    return STARCH_OK;
+    END_GUARD(c)
+}
+
+int starch_bz2_stream_count(starch_ctx* c, uint64_t* n)
+{
+    if (!c || !n) return STARCH_ERR_ARG;
+    if (!c->have_out) return STARCH_ERR_STATE;
+    *n = c->dstreams.size();
+    return STARCH_OK;
+}
+
+int starch_bz2_streams(starch_ctx* c, starch_dec_stream* out, uint64_t cap)
+{
+    if (!c || (cap && !out)) return STARCH_ERR_ARG;
+    if (!c->have_out) return STARCH_ERR_STATE;
+    if (cap < c->dstreams.size()) return STARCH_ERR_MEM;
+    for (size_t k = 0; k < c->dstreams.size(); ++k) {
+        const bz::DecStream& s = c->dstreams[k];
+        out[k] = starch_dec_stream{s.in_beg, s.in_end, s.out_off, s.out_len, s.level, s.n_blocks, s.stored_crc};
+    }
+    return STARCH_OK;
+}
+
+int starch_untransform_host(starch_ctx* c, const void* text, uint64_t n, const char* chr, uint64_t chr_len)
+{
+    GUARD(c)
+    if ((n && !text) || (chr_len && !chr)) return STARCH_ERR_ARG;
+    c->have_out = false;
+    uint8_t* d = c->dec_out.as<uint8_t>(n + 64);
+    if (n) HIP_CHECK(hipMemcpyAsync(d, text, n, hipMemcpyHostToDevice, c->st));
+    std::vector<ut::Untransform::Seg> segs;
+    if (n) segs.push_back(ut::Untransform::Seg{0, n, std::string(chr ? chr : "", chr_len)});
+    c->out_bytes = c->untf.run(c->tf, d, n, segs, c->st, c->ut_out);
+    c->out_dev = static_cast<const uint8_t*>(c->ut_out.p);
+    c->have_out = true;
+    return STARCH_OK;
+    END_GUARD(c)
+}
+
+int starch_unstarch_host(starch_ctx* c, const void* archive, uint64_t n)
+{
+    GUARD(c)
+    if (!archive) return STARCH_ERR_ARG;
+    c->have_out = false;
+    const uint8_t* a = static_cast<const uint8_t*>(archive);
+    uint64_t index_off = 0;
+    const std::vector<IndexEntry> idx = read_index(a, n, &index_off);
+    // the streams region [4, index_off) is the concatenated bzip2 streams, in index order
+    const uint64_t m = index_off - 4;
+    uint8_t* d = c->dec_in.as<uint8_t>(m + 256);
+    if (m) HIP_CHECK(hipMemcpyAsync(d, a + 4, m, hipMemcpyHostToDevice, c->st));
+    HIP_CHECK(hipMemsetAsync(d + m, 0, 256, c->st));
+    const uint64_t tbytes = c->dec.decode(d, m, a + 4, c->st, c->dec_out, c->dstreams);
+    if (c->dstreams.size() != idx.size()) throw StarchError(STARCH_ERR_DATA, "archive: index and streams disagree");
+    std::vector<ut::Untransform::Seg> segs;
+    for (size_t k = 0; k < idx.size(); ++k) {
+        const bz::DecStream& s = c->dstreams[k];
+        if (s.in_beg + 4 != idx[k].offset || s.in_end - s.in_beg != idx[k].size)
+            throw StarchError(STARCH_ERR_DATA, "archive: stream " + std::to_string(k) + " is not where the index says");
+        segs.push_back(ut::Untransform::Seg{s.out_off, s.out_len, idx[k].chr});
+    }
+    c->out_bytes = c->untf.run(c->tf, static_cast<const uint8_t*>(c->dec_out.p), tbytes, segs, c->st, c->ut_out);
+    c->out_dev = static_cast<const uint8_t*>(c->ut_out.p);
+    c->have_out = true;
+    return STARCH_OK;
+    END_GUARD(c)
+}
+
+int starch_output_size(starch_ctx* c, uint64_t* n)
+{
+    if (!c || !n) return STARCH_ERR_ARG;
+    if (!c->have_out) return STARCH_ERR_STATE;
+    *n = c->out_bytes;
+    return STARCH_OK;
+}
+
+int starch_output_device(starch_ctx* c, const void** d_ptr)
+{
+    if (!c || !d_ptr) return STARCH_ERR_ARG;
+    if (!c->have_out) return STARCH_ERR_STATE;
+    *d_ptr = c->out_dev;
+    return STARCH_OK;
+}
+
+int starch_output_copy(starch_ctx* c, void* dst, uint64_t cap)
+{
+    GUARD(c)
+    if (!c->have_out) return STARCH_ERR_STATE;
+    if (cap < c->out_bytes || (c->out_bytes && !dst)) return STARCH_ERR_MEM;
+    if (c->out_bytes) HIP_CHECK(hipMemcpyAsync(dst, c->out_dev, c->out_bytes, hipMemcpyDeviceToHost, c->st));
+    HIP_CHECK(hipStreamSynchronize(c->st));
+    return STARCH_OK;
+    END_GUARD(c)
 }
 
 }  // extern "C"

@@ -37,6 +37,7 @@ def lib():
         L.oracle_crc32_bzip2.restype = ctypes.c_uint32
         L.oracle_block_sort.restype = ctypes.c_int32
         L.oracle_base_counts.restype = ctypes.c_size_t
+        L.oracle_untransform.restype = ctypes.c_size_t
         _lib = L
     return _lib
 
@@ -128,3 +129,16 @@ def block_sort(block: bytes):
     fmap = (ctypes.c_uint32 * max(1, len(block)))()
     op = L.oracle_block_sort(block, ctypes.c_int32(len(block)), fmap)
     return op, list(fmap[:len(block)])
+
+
+def untransform(text: bytes, chromosome: bytes):
+    """One segment's text -> BED lines (oracle_untransform), or None when the
+    text is not invertible (negative p-value, malformed line)."""
+    L = lib()
+    cap = 4 * len(text) + (len(chromosome) + 48) * (text.count(b"\n") + 1) + 1024
+    out = ctypes.create_string_buffer(cap)
+    n = L.oracle_untransform(text, ctypes.c_size_t(len(text)), chromosome, ctypes.c_size_t(len(chromosome)), out,
+                             ctypes.c_size_t(cap))
+    if n == ctypes.c_size_t(-1).value:
+        return None
+    return out.raw[:n]

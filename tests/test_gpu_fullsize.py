@@ -37,3 +37,27 @@ def test_fullsize_streams_match_cpu_path(cfg):
         assert len(st) == want["stream_bytes"], want["chromosome"]
         assert hashlib.sha256(st).hexdigest() == want["sha256"], want["chromosome"]
     c.close()
+
+
+@pytest.mark.parametrize("cfg", ["cfg2", "cfg4"])
+def test_fullsize_unstarch_round_trip(cfg):
+    """unstarch(archive) == input at the full configs (decode ->
+    inverse transform on the GPU; a size-independent property)."""
+    import ctypes
+    import time
+    import torch
+    import starch_amd
+    g = json.load(open(os.path.join(GOLDEN, "fullsize_%s.json" % cfg)))
+    n = g["input_bytes"]
+    host = torch.empty(n, dtype=torch.uint8, pin_memory=True)
+    starch_amd.gen_bed(g["kind"], g["total_lines"], seed=g["seed"], into=ctypes.c_void_p(host.data_ptr()))
+    c = starch_amd.Starch(0)
+    c.compress_host_ptr(host.data_ptr(), n)
+    arch = c.archive()
+    t0 = time.perf_counter()
+    back = c.unstarch(arch)
+    dt = time.perf_counter() - t0
+    print("[unstarch %s] %.1f MB archive -> %.1f MB BED in %.3f s (host-to-host)" % (cfg, len(arch) / 1e6, n / 1e6, dt))
+    assert len(back) == n
+    assert torch.equal(torch.frombuffer(bytearray(back), dtype=torch.uint8), host)
+    c.close()
