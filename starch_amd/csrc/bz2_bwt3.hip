@@ -64,7 +64,14 @@ namespace {
 constexpr int PT = 256;                 // hist threads
 constexpr int PTILE = 32768;            // rotations per partition tile
 constexpr int PDIG = 12;
-constexpr int PNB = 1 << PDIG;          // 4096 top-level buckets per block
+constexpr int PNB = 1 << PDIG;          // 4096 top-level buckets per block (binary digit)
+// Blocks of 17..20 symbols (B = 5: narrowPeak / BED6+ text) take a mixed-radix
+// top-level digit instead: their first 3 symbols, s0*nin^2 + s1*nin + s2 <
+// 8000, so every bucket shares 15 key bits (the binary digit covers 2.4
+// symbols there and leaves buckets ~6x larger).  Batches holding such blocks
+// run the top-level kernels with 8192 bins.
+constexpr int PNB_WIDE = 8192;
+static_assert(PTILE <= 32768 && PNB_WIDE <= 8192, "k3_scatter_lds packs (digit << 15) | rotation-in-tile");
 constexpr int MAXT = (900064 + PTILE - 1) / PTILE;   // tiles per block (bs <= 9)
 // size classes: W rank-by-compare (one wave), S wave-private LDS sort,
 // M1..M3 workgroup LDS sort, L MSD partition
@@ -97,7 +104,22 @@ struct Geo {                   // per block key geometry
     uint32_t D;                // symbols per round-0 key (KB = D*B bits)
     uint32_t Dp;               // symbols per text-round key (52/B)
     uint32_t KB;
+    uint32_t nin;              // symbols in use
+    uint32_t D1;               // top-level digit: 3 = mixed radix over 3 symbols, 0 = top PDIG key bits
+    uint32_t SH;               // key bits every top-level bucket shares (3*B or PDIG)
+    uint32_t pad;
 };
+
+// top-level bucket of a rotation from its 64-bit key window (MSB first)
+__device__ __forceinline__ uint32_t top_digit(uint64_t v, const Geo& g)
+{
+    if (!g.D1) return (uint32_t)(v >> (64 - PDIG));
+    const uint32_t mask = (1u << g.B) - 1u;
+    const uint32_t s0 = (uint32_t)(v >> (64 - g.B)) & mask;
+    const uint32_t s1 = (uint32_t)(v >> (64 - 2 * g.B)) & mask;
+    const uint32_t s2 = (uint32_t)(v >> (64 - 3 * g.B)) & mask;
+    return (s0 * g.nin + s1) * g.nin + s2;
+}
 
 __host__ __device__ constexpr uint64_t pss_words(uint64_t stride) { return stride / 8 + 64; }
 
@@ -134,6 +156,7 @@ struct Ctx {
     uint32_t rtext;         // text round (0: round 0)
     uint32_t* qhead;        // 8 queue heads of the current persistent launch
     const uint32_t* qseg;   // 9 per-XCD segment offsets of the current binned list
+    uint32_t nbins;         // top-level bins of this batch (PNB or PNB_WIDE)
 };
 
 __device__ __forceinline__ int bits_for3(uint32_t x) { return x ? 32 - __clz(x) : 0; }
@@ -386,6 +409,10 @@ __global__ void __launch_bounds__(256) k3_pss(Ctx c)
         g.D = 64 / B;
         g.KB = g.D * B;
         g.Dp = (64 - PDIG) / B;
+        g.nin = nin;
+        g.D1 = (c.nbins == PNB_WIDE && B == 5 && nin <= 20) ? 3u : 0u;
+        g.SH = g.D1 ? 3 * B : PDIG;
+        g.pad = 0;
         c.L.geo[slot] = g;
         c.blocks[b].n_in_use = nin;
     }
@@ -419,21 +446,23 @@ __device__ __forceinline__ uint32_t* tile_hist(const Ctx& c, uint32_t slot)
 }
 
 // ---------------------------------------------------------------------------
-// k3_hist: per-tile bucket histogram -> thist[slot][tile][4096]
+// k3_hist: per-tile bucket histogram -> thist[slot][tile][NB]
 // ---------------------------------------------------------------------------
+template <int NB>
 __global__ void __launch_bounds__(PT) k3_hist(Ctx c)
 {
-    __shared__ uint32_t cnt[PNB];
+    __shared__ uint32_t cnt[NB];
     const uint32_t slot = blockIdx.y, b = c.b0 + slot, tile = blockIdx.x;
     const uint32_t n = c.blocks[b].n;
     const uint32_t t0 = tile * PTILE;
     if (t0 >= n) return;
-    const uint32_t B = c.L.geo[slot].B;
+    const Geo geo = c.L.geo[slot];
+    const uint32_t B = geo.B;
     const uint64_t* pss = c.scr.K + (uint64_t)slot * c.scr.stride;
-    for (int i = threadIdx.x; i < PNB; i += PT) cnt[i] = 0;
+    for (int i = threadIdx.x; i < NB; i += PT) cnt[i] = 0;
     __syncthreads();
     const uint32_t e = n - t0 < (uint32_t)PTILE ? n - t0 : (uint32_t)PTILE;
-    // 16 consecutive rotations per thread and step: their 12-bit digits all
+    // 16 consecutive rotations per thread and step: their top-level digits all
     // come from four PSS words (funnel shifts), not two loads per rotation
     for (uint32_t k0 = threadIdx.x * 16u; k0 < e; k0 += PT * 16u) {
         const uint64_t bit0 = (uint64_t)(t0 + k0) * B;
@@ -447,53 +476,76 @@ __global__ void __launch_bounds__(PT) k3_hist(Ctx c)
             const uint64_t a = ix == 0 ? w[0] : ix == 1 ? w[1] : w[2];
             const uint64_t nx = ix == 0 ? w[1] : ix == 1 ? w[2] : w[3];
             const uint64_t v = (a << p) | ((nx >> 1) >> (63u - p));
-            if (k0 + k < e) atomicAdd(&cnt[(uint32_t)(v >> (64 - PDIG))], 1u);
+            if (k0 + k < e) atomicAdd(&cnt[top_digit(v, geo)], 1u);
         }
     }
     __syncthreads();
-    uint32_t* th = tile_hist(c, slot) + (uint64_t)tile * PNB;
-    for (int i = threadIdx.x; i < PNB; i += PT) th[i] = cnt[i];
+    uint32_t* th = tile_hist(c, slot) + (uint64_t)tile * NB;
+    for (int i = threadIdx.x; i < NB; i += PT) th[i] = cnt[i];
 }
 
 // ---------------------------------------------------------------------------
 // k3_scan: per block -- totals, bucket starts, per-tile cursors, class lists
 // ---------------------------------------------------------------------------
-constexpr int ST = 1024;              // k3_scan threads: 4 buckets each
+constexpr int ST = 1024;              // k3_scan threads: NB/1024 consecutive buckets each
 
+template <int NB>
 __global__ void __launch_bounds__(ST) k3_scan(Ctx c)
 {
+    constexpr int Q = NB / (4 * ST);      // uint4 per thread
     __shared__ uint32_t scan_sh[ST / 64 + 1];
     __shared__ uint32_t cls_sh[16];
     const int tid = threadIdx.x;
     const uint32_t slot = blockIdx.x, b = c.b0 + slot;
     const uint32_t n = c.blocks[b].n;
     const uint32_t ntile = (n + PTILE - 1) / PTILE;
-    uint4* th = reinterpret_cast<uint4*>(tile_hist(c, slot));   // [tile][PNB/4]
-    uint4* tot = th + (uint64_t)MAXT * (PNB / 4);
-    uint4 a = make_uint4(0, 0, 0, 0);
+    uint4* th = reinterpret_cast<uint4*>(tile_hist(c, slot));   // [tile][NB/4]
+    uint4* tot = th + (uint64_t)MAXT * (NB / 4);
+    uint4 a[Q];
+#pragma unroll
+    for (int j = 0; j < Q; ++j) a[j] = make_uint4(0, 0, 0, 0);
 #pragma unroll 4
     for (uint32_t k = 0; k < ntile; ++k) {
-        const uint4 x = th[(uint64_t)k * (PNB / 4) + tid];
-        a.x += x.x; a.y += x.y; a.z += x.z; a.w += x.w;
+#pragma unroll
+        for (int j = 0; j < Q; ++j) {
+            const uint4 x = th[(uint64_t)k * (NB / 4) + tid * Q + j];
+            a[j].x += x.x; a[j].y += x.y; a[j].z += x.z; a[j].w += x.w;
+        }
     }
-    tot[tid] = a;
-    const uint32_t sum = a.x + a.y + a.z + a.w;
+    uint32_t sum = 0;
+#pragma unroll
+    for (int j = 0; j < Q; ++j) { tot[tid * Q + j] = a[j]; sum += a[j].x + a[j].y + a[j].z + a[j].w; }
     const uint32_t pre = block_excl_scan_add<uint32_t>(sum, scan_sh, (uint32_t*)nullptr);
-    uint4 run = make_uint4(pre, pre + a.x, pre + a.x + a.y, pre + a.x + a.y + a.z);
+    uint4 run[Q];
+    {
+        uint32_t r = pre;
+#pragma unroll
+        for (int j = 0; j < Q; ++j) {
+            run[j] = make_uint4(r, r + a[j].x, r + a[j].x + a[j].y, r + a[j].x + a[j].y + a[j].z);
+            r += a[j].x + a[j].y + a[j].z + a[j].w;
+        }
+    }
 #pragma unroll 4
     for (uint32_t k = 0; k < ntile; ++k) {
-        uint4& x = th[(uint64_t)k * (PNB / 4) + tid];
-        const uint4 v = x;
-        x = run;
-        run.x += v.x; run.y += v.y; run.z += v.z; run.w += v.w;
+#pragma unroll
+        for (int j = 0; j < Q; ++j) {
+            uint4& x = th[(uint64_t)k * (NB / 4) + tid * Q + j];
+            const uint4 v = x;
+            x = run[j];
+            run[j].x += v.x; run[j].y += v.y; run[j].z += v.z; run[j].w += v.w;
+        }
     }
-    const uint32_t shift = c.L.geo[slot].KB - PDIG;
-    const uint32_t cnt4[4] = {a.x, a.y, a.z, a.w};
+    const Geo geo = c.L.geo[slot];
+    const uint32_t shift = geo.KB - geo.SH;
     uint32_t st = pre;
 #pragma unroll
-    for (int q = 0; q < 4; ++q) {
-        wg_classify(c, cls_sh, cnt4[q] >= 2, slot, st, cnt4[q], shift, 0);
-        st += cnt4[q];
+    for (int j = 0; j < Q; ++j) {
+        const uint32_t cnt4[4] = {a[j].x, a[j].y, a[j].z, a[j].w};
+#pragma unroll
+        for (int q = 0; q < 4; ++q) {
+            wg_classify(c, cls_sh, cnt4[q] >= 2, slot, st, cnt4[q], shift, 0);
+            st += cnt4[q];
+        }
     }
 }
 
@@ -503,9 +555,10 @@ __global__ void __launch_bounds__(ST) k3_scan(Ctx c)
 // ---------------------------------------------------------------------------
 constexpr int SCT = 1024;
 
+template <int NB>
 __global__ void __launch_bounds__(SCT) k3_scatter(Ctx c)
 {
-    __shared__ uint32_t cur[PNB], tot[PNB];
+    __shared__ uint32_t cur[NB], tot[NB];
     __shared__ uint32_t qs[8];
     __shared__ uint32_t job_sh;
     const int tid = threadIdx.x;
@@ -523,9 +576,10 @@ __global__ void __launch_bounds__(SCT) k3_scatter(Ctx c)
         if (t0 >= n) continue;                       // uniform
         const uint64_t so = (uint64_t)slot * c.scr.stride;
         const uint32_t* th = tile_hist(c, slot);
-        for (int i = tid; i < PNB; i += SCT) { cur[i] = th[(uint64_t)tile * PNB + i]; tot[i] = th[(uint64_t)MAXT * PNB + i]; }
+        for (int i = tid; i < NB; i += SCT) { cur[i] = th[(uint64_t)tile * NB + i]; tot[i] = th[(uint64_t)MAXT * NB + i]; }
         __syncthreads();
-        const uint32_t B = c.L.geo[slot].B;
+        const Geo geo = c.L.geo[slot];
+        const uint32_t B = geo.B;
         const uint64_t* pss = c.scr.K + so;
         uint32_t* SA = c.scr.SA + so;
         const uint32_t e = n - t0 < (uint32_t)PTILE ? n - t0 : (uint32_t)PTILE;
@@ -546,7 +600,7 @@ __global__ void __launch_bounds__(SCT) k3_scatter(Ctx c)
                     const uint32_t ix = bit >> 6, pb = bit & 63u;
                     const uint64_t a = ix == 0 ? w[0] : ix == 1 ? w[1] : w[2];
                     const uint64_t nx = ix == 0 ? w[1] : ix == 1 ? w[2] : w[3];
-                    d[u] = (uint32_t)(((a << pb) | ((nx >> 1) >> (63u - pb))) >> (64 - PDIG));
+                    d[u] = top_digit((a << pb) | ((nx >> 1) >> (63u - pb)), geo);
                 }
             }
 #pragma unroll
@@ -574,16 +628,19 @@ __global__ void __launch_bounds__(SCT) k3_scatter(Ctx c)
 // ---------------------------------------------------------------------------
 // k3_scatter_lds: the same scatter with the writes staged in LDS.  Each 32 K
 // tile is handled in two 16 K halves: the half's rotations are counting-
-// sorted by bucket inside LDS (entry = digit << 20 | rotation), then written
+// sorted by bucket inside LDS (entry = digit << 15 | rotation in the tile), then written
 // out in local order, so consecutive threads store consecutive SA positions
 // of a bucket's run instead of one scattered 4-byte store per rotation (the
 // direct scatter's writes cost ~2.5-3.5x their bytes in HBM traffic).
 // ---------------------------------------------------------------------------
-constexpr uint32_t SH_HALF = PTILE / 2;       // rotations staged at a time
-
+template <int NB>
 __global__ void __launch_bounds__(SCT) k3_scatter_lds(Ctx c)
 {
-    __shared__ uint32_t cur[PNB], tot[PNB], lst[PNB + 1];
+    // rotations staged at a time: half a tile (4096 bins), a quarter (8192 bins: LDS)
+    constexpr uint32_t SH_HALF = NB == PNB ? PTILE / 2 : PTILE / 4;
+    constexpr int SU = (int)(SH_HALF / SCT);       // consecutive rotations per thread
+    constexpr int BPT = NB / SCT;                  // bins per thread in the local scan
+    __shared__ uint32_t cur[NB], tot[NB], lst[NB + 1];
     __shared__ uint32_t stage[SH_HALF];
     __shared__ uint32_t scan_sh[SCT / 64 + 1];
     __shared__ uint32_t qs[8];
@@ -603,17 +660,17 @@ __global__ void __launch_bounds__(SCT) k3_scatter_lds(Ctx c)
         if (t0 >= n) continue;                       // uniform
         const uint64_t so = (uint64_t)slot * c.scr.stride;
         const uint32_t* th = tile_hist(c, slot);
-        for (int i = tid; i < PNB; i += SCT) { cur[i] = th[(uint64_t)tile * PNB + i]; tot[i] = th[(uint64_t)MAXT * PNB + i]; }
-        const uint32_t B = c.L.geo[slot].B;
+        for (int i = tid; i < NB; i += SCT) { cur[i] = th[(uint64_t)tile * NB + i]; tot[i] = th[(uint64_t)MAXT * NB + i]; }
+        const Geo geo = c.L.geo[slot];
+        const uint32_t B = geo.B;
         const uint64_t* pss = c.scr.K + so;
         uint32_t* SA = c.scr.SA + so;
         const uint32_t e = n - t0 < (uint32_t)PTILE ? n - t0 : (uint32_t)PTILE;
         for (uint32_t h0 = 0; h0 < e; h0 += SH_HALF) {
             const uint32_t he = e - h0 < SH_HALF ? e - h0 : SH_HALF;
-            for (int i = tid; i < PNB; i += SCT) lst[i] = 0;
+            for (int i = tid; i < NB; i += SCT) lst[i] = 0;
             __syncthreads();
-            // digits of 16 consecutive rotations from four PSS words; local counts
-            constexpr int SU = 16;
+            // digits of SU consecutive rotations from four PSS words; local counts
             const uint32_t q0 = tid * SU;                // SCT * SU == SH_HALF
             uint32_t d[SU], p[SU];
             {
@@ -627,31 +684,31 @@ __global__ void __launch_bounds__(SCT) k3_scatter_lds(Ctx c)
                     const uint32_t ix = bit >> 6, pb = bit & 63u;
                     const uint64_t a = ix == 0 ? w[0] : ix == 1 ? w[1] : w[2];
                     const uint64_t nx = ix == 0 ? w[1] : ix == 1 ? w[2] : w[3];
-                    d[u] = (uint32_t)(((a << pb) | ((nx >> 1) >> (63u - pb))) >> (64 - PDIG));
+                    d[u] = top_digit((a << pb) | ((nx >> 1) >> (63u - pb)), geo);
                 }
             }
 #pragma unroll
             for (int u = 0; u < SU; ++u) p[u] = (q0 + u < he) ? atomicAdd(&lst[d[u]], 1u) : 0u;
             __syncthreads();
-            // local bucket starts (exclusive scan, 4 bins per thread)
+            // local bucket starts (exclusive scan, BPT bins per thread)
             {
-                uint32_t v[4], sum = 0;
+                uint32_t v[BPT], sum = 0;
 #pragma unroll
-                for (int q = 0; q < 4; ++q) { v[q] = lst[tid * 4 + q]; sum += v[q]; }
+                for (int q = 0; q < BPT; ++q) { v[q] = lst[tid * BPT + q]; sum += v[q]; }
                 uint32_t run = block_excl_scan_add<uint32_t>(sum, scan_sh, (uint32_t*)nullptr);
 #pragma unroll
-                for (int q = 0; q < 4; ++q) { lst[tid * 4 + q] = run; run += v[q]; }
-                if (tid == SCT - 1) lst[PNB] = run;
+                for (int q = 0; q < BPT; ++q) { lst[tid * BPT + q] = run; run += v[q]; }
+                if (tid == SCT - 1) lst[NB] = run;
             }
             __syncthreads();
 #pragma unroll
             for (int u = 0; u < SU; ++u)
-                if (q0 + u < he) stage[lst[d[u]] + p[u]] = (d[u] << 20) | (t0 + h0 + q0 + u);
+                if (q0 + u < he) stage[lst[d[u]] + p[u]] = (d[u] << 15) | (h0 + q0 + u);   // 13 + 15 bits
             __syncthreads();
             // write out in local (bucket) order: runs of a bucket land on consecutive SA slots
             for (uint32_t j = tid; j < he; j += SCT) {
                 const uint32_t v = stage[j];
-                const uint32_t dg = v >> 20, r = v & 0xFFFFFu;
+                const uint32_t dg = v >> 15, r = t0 + (v & 0x7FFFu);
                 const uint32_t pos = cur[dg] + (j - lst[dg]);
                 SA[pos] = r;
                 if (tot[dg] == 1u) {                   // singleton bucket: final
@@ -660,7 +717,7 @@ __global__ void __launch_bounds__(SCT) k3_scatter_lds(Ctx c)
                 }
             }
             __syncthreads();
-            for (int i = tid; i < PNB; i += SCT) cur[i] += lst[i + 1] - lst[i];
+            for (int i = tid; i < NB; i += SCT) cur[i] += lst[i + 1] - lst[i];
             __syncthreads();
         }
     }
@@ -898,63 +955,85 @@ __device__ __forceinline__ void emit_sorted(const Ctx& c, uint32_t slot, uint32_
 }
 
 // ---------------------------------------------------------------------------
-// k3_sort_w: groups of <= 64, one wave each (persistent, per wave)
+// k3_sort_w: groups of <= 64, packed several to a wave.  Each wave takes
+// chunks of 64 consecutive items of its XCD's segment (one item per lane,
+// one coalesced load); groups are laid out back to back over the 64 lanes as
+// far as they fit, so one round of loads (rotations, then keys) serves them
+// all -- text-round tie groups are mostly pairs, one group per wave left 60
+// lanes idle and paid a full load round trip per pair.  Every element ranks
+// itself among its group's members (keys by lane shuffle), then sorted order
+// goes through LDS; heads, ends and tie runs are per group.
 // ---------------------------------------------------------------------------
+__device__ __forceinline__ uint64_t shfl64(uint64_t v, uint32_t src)
+{
+    const uint32_t lo = (uint32_t)__shfl((int)(uint32_t)v, (int)src, 64);
+    const uint32_t hi = (uint32_t)__shfl((int)(uint32_t)(v >> 32), (int)src, 64);
+    return ((uint64_t)hi << 32) | lo;
+}
+
 template <bool DBL>
 __global__ void __launch_bounds__(256) k3_sort_w(Ctx c, const uint64_t* __restrict__ items)
 {
     __shared__ uint64_t skey[4][W_MAX + 1];
     __shared__ uint32_t sval[4][W_MAX];
-    const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
-    // dynamic assignment: every wave pops groups from its XCD's queue (list
-    // order per XCD: neighbouring groups share a block's PSS in its L2)
-#ifndef STARCH_W_DYN
-#define STARCH_W_DYN 0
-#endif
-    __shared__ uint32_t qs[8];
-    const uint32_t xs = xcc_id();
-    load_qsizes_binned(c, qs);
-    WaveQueue<4> wq;
-    const uint32_t xs8 = blockIdx.x & 7u, s_nwk = (gridDim.x >> 3) * 4u, s_end = c.qseg[xs8 + 1];
-    uint32_t it_s = c.qseg[xs8] + (blockIdx.x >> 3) * 4u + wid;
-    auto next_item = [&]() -> uint32_t {
-        if (!STARCH_W_DYN) {
-            const uint32_t r = it_s < s_end ? it_s : 0xFFFFFFFFu;
-            it_s += s_nwk;
-            return r;
+    const uint32_t lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
+    // static assignment: workgroup L works segment L mod 8 (the XCD it runs on);
+    // its waves take 64-item chunks of that segment in turn
+    const uint32_t xs8 = blockIdx.x & 7u, wseg = (gridDim.x >> 3) * 4u, w_in = (blockIdx.x >> 3) * 4u + wid;
+    const uint32_t seg0 = c.qseg[xs8], seg1 = c.qseg[xs8 + 1];
+    for (uint32_t cb = seg0 + w_in * 64u; cb < seg1; cb += wseg * 64u) {
+        const uint32_t cnt = seg1 - cb < 64u ? seg1 - cb : 64u;
+        const uint64_t myitem = lane < cnt ? items[cb + lane] : 0ull;
+        const uint32_t msz = lane < cnt ? it_size(myitem) : 0u;
+        for (uint32_t done = 0; done < cnt;) {
+            // the groups done.. whose sizes sum to <= 64 (the first always fits)
+            const uint32_t sz = (lane >= done && lane < cnt) ? msz : 0u;
+            const uint32_t incl = wave_incl_scan_add(sz);
+            const bool take = lane >= done && lane < cnt && incl <= 64u;
+            const uint32_t ng = (uint32_t)__popcll(__ballot(take));
+            const uint32_t off = incl - sz;
+            const uint32_t total = (uint32_t)__shfl((int)incl, (int)(done + ng - 1), 64);
+            const uint64_t smask = wave_reduce_or64(take ? (1ull << off) : 0ull);
+            const bool valid = lane < total;
+            const uint64_t upto = lane == 63 ? ~0ull : ((2ull << lane) - 1ull);
+            const uint32_t gi = valid ? done + (uint32_t)__popcll(smask & upto) - 1u : done;
+            const uint64_t item = shfl64(myitem, gi);
+            const uint32_t goff = (uint32_t)__shfl((int)off, (int)gi, 64);   // every lane: gi may be past `total`
+            const uint32_t gstart = valid ? goff : 0u;
+            const uint32_t slot = it_slot(item), s = it_start(item), m = it_size(item), par = it_par(item);
+            const uint32_t j = valid ? lane - gstart : 0u;
+            const uint32_t* sv = (par ? c.scr.V : c.scr.SA) + (uint64_t)slot * c.scr.stride + s;
+            const KeySrc ks = key_src(c, slot, par);
+            const uint32_t v = sv[j];
+            uint32_t ls;
+            uint64_t k = elem_key<DBL>(c, ks, slot, s + j, v, ls);
+            if (!valid) k = ~0ull;
+            // rank among the group's members (lanes gstart .. gstart + m - 1)
+            const uint32_t maxm = wave_reduce_max(valid ? m : 0u);
+            uint32_t r = 0;
+            for (uint32_t q = 0; q < maxm; ++q) {
+                const bool in = valid && q < m;
+                const uint64_t kq = shfl64(k, in ? gstart + q : lane);
+                r += (in && (kq < k || (kq == k && q < j))) ? 1u : 0u;
+            }
+            wave_sync_lds3();                            // the previous pass's reads are done
+            if (valid) { skey[wid][gstart + r] = k; sval[wid][gstart + r] = v | (ls << 24); }
+            wave_sync_lds3();
+            const uint64_t key = valid ? skey[wid][lane] : 0;
+            const uint32_t val = valid ? sval[wid][lane] : 0;
+            const bool head = valid && (j == 0 || skey[wid][lane - 1] != key);
+            const bool end = valid && (j + 1 == m || skey[wid][lane + 1] != key);
+            const uint32_t hp = wave_incl_scan_max<uint32_t>(head ? lane : 0u) - gstart;   // a group start is a head
+            asm volatile("s_waitcnt vmcnt(0)" ::: "memory");   // SA reads done before the writes
+            uint32_t runs = 0;
+            emit_sorted(c, slot, s, j, val & 0xFFFFFFu, valid, hp, end, runs, val >> 24);
+            if (c.mode) {                                // runs per group, by its first lane
+                const uint64_t em = __ballot(end);
+                const uint64_t gm = (m >= 64 ? ~0ull : ((1ull << m) - 1ull)) << gstart;
+                if (valid && j == 0) atomicAdd(&c.L.runs[slot], (uint32_t)__popcll(em & gm));
+            }
+            done += ng;
         }
-        return wq.next(c.qhead, qs, c.qseg, xs);
-    };
-    for (uint32_t it = next_item(); it != 0xFFFFFFFFu; it = next_item()) {
-        const uint64_t item = items[it];
-        const uint32_t slot = it_slot(item), s = it_start(item), m = it_size(item), par = it_par(item);
-        const uint64_t base = (uint64_t)slot * c.scr.stride + s;
-        const uint32_t* sv = (par ? c.scr.V : c.scr.SA) + base;
-        const KeySrc ks = key_src(c, slot, par);
-        const bool valid = (uint32_t)lane < m;
-        const uint32_t li = valid ? (uint32_t)lane : 0u;         // loads stay unconditional
-        const uint32_t v = sv[li];
-        uint32_t ls;
-        uint64_t k = elem_key<DBL>(c, ks, slot, s + li, v, ls);
-        if (!valid) k = ~0ull;
-        uint32_t r = 0;
-        for (uint32_t j = 0; j < m; ++j) {
-            const uint64_t kj = ((uint64_t)(uint32_t)__builtin_amdgcn_readlane((int)(k >> 32), (int)j) << 32) |
-                                (uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)k, (int)j);
-            r += (kj < k || (kj == k && (int)j < lane)) ? 1u : 0u;
-        }
-        wave_sync_lds3();                                // previous group's reads are done
-        if (valid) { skey[wid][r] = k; sval[wid][r] = v | (ls << 24); }
-        wave_sync_lds3();
-        const uint64_t key = valid ? skey[wid][lane] : 0;
-        const uint32_t val = valid ? sval[wid][lane] : 0;
-        const bool head = valid && (lane == 0 || skey[wid][lane - 1] != key);
-        const bool end = valid && ((uint32_t)lane + 1 == m || skey[wid][lane + 1] != key);
-        const uint32_t hp = wave_incl_scan_max<uint32_t>(head ? (uint32_t)lane : 0u);
-        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");   // SA reads of this group done before the writes
-        uint32_t runs = 0;
-        emit_sorted(c, slot, s, (uint32_t)lane, val & 0xFFFFFFu, valid, hp, end, runs, val >> 24);
-        if (c.mode && lane == 0) atomicAdd(&c.L.runs[slot], runs);
     }
 }
 
@@ -989,6 +1068,46 @@ __device__ __forceinline__ void gsync()
 {
     if constexpr (NW == 1) wave_sync_lds3();
     else __syncthreads();
+}
+
+template <int E>
+struct GrpIn {                 // one group's inputs, as loaded
+    uint64_t item;
+    KeySrc ks;
+    uint32_t v[E];
+    uint32_t v0;
+    uint64_t kx[E];
+    uint32_t ls[E];
+    uint64_t k0;
+};
+
+// loads of a group that does not exist (ok false) go to element 0 of slot 0's
+// SA, which always exists; their results are never used
+template <int NW, int E>
+__device__ __forceinline__ void grp_load_vals(const Ctx& c, GrpIn<E>& x, bool ok, int wid, int lane)
+{
+    if (!ok) x.item = mk_item(0, 0, 1, 0, 0);
+    const uint32_t slot = it_slot(x.item), s = it_start(x.item), m = it_size(x.item), par = it_par(x.item);
+    const uint32_t* sv = (par ? c.scr.V : c.scr.SA) + (uint64_t)slot * c.scr.stride + s;
+    x.ks = key_src(c, slot, par);
+#pragma unroll
+    for (int e = 0; e < E; ++e) {
+        const uint32_t i = (uint32_t)(wid * 64 * E + e * 64 + lane);
+        x.v[e] = sv[i < m ? i : 0u];
+    }
+    x.v0 = sv[0];
+}
+
+template <int NW, int E, bool DBL>
+__device__ __forceinline__ void grp_load_keys(const Ctx& c, GrpIn<E>& x, int wid, int lane)
+{
+    const uint32_t s = it_start(x.item), m = it_size(x.item), slot = it_slot(x.item);
+#pragma unroll
+    for (int e = 0; e < E; ++e) {
+        const uint32_t i = (uint32_t)(wid * 64 * E + e * 64 + lane);
+        x.kx[e] = elem_key<DBL>(c, x.ks, slot, s + (i < m ? i : 0u), x.v[e], x.ls[e]);
+    }
+    x.k0 = elem_key<DBL>(x.ks, s, x.v0);
 }
 
 // register budget (waves per SIMD) of the sort kernels: keeps a few groups
@@ -1073,43 +1192,35 @@ k3_sort_lds(Ctx c, const uint64_t* __restrict__ items,
             return j == NONE ? NONE : c.qseg[j >> 28] + (j & 0x0FFFFFFFu);
         }
     };
-    for (uint32_t it = next_item(); it != NONE; it = next_item()) {
-    const uint64_t item = items[it];
-    const uint32_t slot = it_slot(item), s = it_start(item), m = it_size(item), par = it_par(item);
-    const uint64_t base = (uint64_t)slot * c.scr.stride + s;
-    const uint32_t* sv = (par ? c.scr.V : c.scr.SA) + base;
-    const KeySrc ks = key_src(c, slot, par);
+    // software pipeline (as k3_sort_grp): while a group sorts, the next
+    // group's keys are in flight, and the rotations of the one after it
+    uint32_t it = next_item();
+    uint32_t it1 = it != NONE ? next_item() : NONE;
+    GrpIn<E> cur, nxt;
+    cur.item = it != NONE ? items[it] : 0ull;
+    grp_load_vals<NW, E>(c, cur, it != NONE, wid, lane);
+    grp_load_keys<NW, E, DBL>(c, cur, wid, lane);
+    nxt.item = it1 != NONE ? items[it1] : 0ull;
+    grp_load_vals<NW, E>(c, nxt, it1 != NONE, wid, lane);
+    while (it != NONE) {
+    const uint64_t item = cur.item;
+    const uint32_t slot = it_slot(item), s = it_start(item), m = it_size(item);
     gsync<NW>();                                   // the previous group's LDS reads are done
 
     uint64_t k[E];
     uint64_t diff = 0;
-    {
-        // every load unconditional (pads read element 0): all in flight at once
-        uint32_t vv[E], ls[E];
-        uint64_t kx[E];
 #pragma unroll
-        for (int e = 0; e < E; ++e) {
-            const uint32_t i = (uint32_t)(wid * 64 * E + e * 64 + lane);
-            vv[e] = sv[i < m ? i : 0u];
-        }
-        const uint64_t k0 = elem_key<DBL>(ks, s, sv[0]);
-#pragma unroll
-        for (int e = 0; e < E; ++e) {
-            const uint32_t i = (uint32_t)(wid * 64 * E + e * 64 + lane);
-            kx[e] = elem_key<DBL>(c, ks, slot, s + (i < m ? i : 0u), vv[e], ls[e]);
-        }
-#pragma unroll
-        for (int e = 0; e < E; ++e) {
-            const uint32_t i = (uint32_t)(wid * 64 * E + e * 64 + lane);
-            if (i < m) {
-                diff |= kx[e] ^ k0;
-                k[e] = ((kx[e] & KMASK) << IDXB) | i;
-                vb_all[g][i] = vv[e] | (ls[e] << 24);
-            } else {
-                k[e] = ~0ull;                          // pads: max key, last in stable order
-            }
+    for (int e = 0; e < E; ++e) {
+        const uint32_t i = (uint32_t)(wid * 64 * E + e * 64 + lane);
+        if (i < m) {
+            diff |= cur.kx[e] ^ cur.k0;
+            k[e] = ((cur.kx[e] & KMASK) << IDXB) | i;
+            vb_all[g][i] = cur.v[e] | (cur.ls[e] << 24);
+        } else {
+            k[e] = ~0ull;                              // pads: max key, last in stable order
         }
     }
+    grp_load_keys<NW, E, DBL>(c, nxt, wid, lane);     // next group's keys (its rotations: one group ago)
     diff = wave_reduce_or64(diff);
     if constexpr (NW > 1) {
         if (lane == 0) red_all[wave] = diff;
@@ -1418,9 +1529,9 @@ k3_sort_lds(Ctx c, const uint64_t* __restrict__ items,
             for (int e = 0; e < E; ++e) hp[e] = hp[e] > pre ? hp[e] : pre;
         }
     }
-    // values were loaded before the sort; every global read of the group's SA
-    // range happened before any write (vmcnt drain, and the barriers above)
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    // the group's rotations and keys were consumed into registers/LDS (their
+    // loads complete) before any write of its SA range; the loads in flight
+    // now belong to other groups' disjoint ranges
     uint32_t runs = 0;
 #pragma unroll
     for (int e = 0; e < E; ++e) {
@@ -1431,6 +1542,13 @@ k3_sort_lds(Ctx c, const uint64_t* __restrict__ items,
         emit_sorted(c, slot, s, j, vb & 0xFFFFFFu, valid, hp[e], end, runs, vb >> 24);
     }
     if (c.mode && lane == 0 && runs) atomicAdd(&c.L.runs[slot], runs);
+    // rotate the pipeline
+    const uint32_t it2 = it1 != NONE ? next_item() : NONE;
+    cur = nxt;
+    nxt.item = it2 != NONE ? items[it2] : 0ull;
+    grp_load_vals<NW, E>(c, nxt, it2 != NONE, wid, lane);
+    it = it1;
+    it1 = it2;
     }
 }
 
@@ -1449,46 +1567,6 @@ k3_sort_lds(Ctx c, const uint64_t* __restrict__ items,
 #define STARCH_HARD_Q 32
 #endif
 constexpr uint32_t HARD_Q = STARCH_HARD_Q;
-
-template <int E>
-struct GrpIn {                 // one group's inputs, as loaded
-    uint64_t item;
-    KeySrc ks;
-    uint32_t v[E];
-    uint32_t v0;
-    uint64_t kx[E];
-    uint32_t ls[E];
-    uint64_t k0;
-};
-
-// loads of a group that does not exist (ok false) go to element 0 of slot 0's
-// SA, which always exists; their results are never used
-template <int NW, int E>
-__device__ __forceinline__ void grp_load_vals(const Ctx& c, GrpIn<E>& x, bool ok, int wid, int lane)
-{
-    if (!ok) x.item = mk_item(0, 0, 1, 0, 0);
-    const uint32_t slot = it_slot(x.item), s = it_start(x.item), m = it_size(x.item), par = it_par(x.item);
-    const uint32_t* sv = (par ? c.scr.V : c.scr.SA) + (uint64_t)slot * c.scr.stride + s;
-    x.ks = key_src(c, slot, par);
-#pragma unroll
-    for (int e = 0; e < E; ++e) {
-        const uint32_t i = (uint32_t)(wid * 64 * E + e * 64 + lane);
-        x.v[e] = sv[i < m ? i : 0u];
-    }
-    x.v0 = sv[0];
-}
-
-template <int NW, int E, bool DBL>
-__device__ __forceinline__ void grp_load_keys(const Ctx& c, GrpIn<E>& x, int wid, int lane)
-{
-    const uint32_t s = it_start(x.item), m = it_size(x.item), slot = it_slot(x.item);
-#pragma unroll
-    for (int e = 0; e < E; ++e) {
-        const uint32_t i = (uint32_t)(wid * 64 * E + e * 64 + lane);
-        x.kx[e] = elem_key<DBL>(c, x.ks, slot, s + (i < m ? i : 0u), x.v[e], x.ls[e]);
-    }
-    x.k0 = elem_key<DBL>(x.ks, s, x.v0);
-}
 
 template <int NW, int E, bool DBL>
 __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(sort_wpe(NW, E))))
@@ -1712,17 +1790,61 @@ k3_sort_grp(Ctx c, const uint64_t* __restrict__ items,
 // ---------------------------------------------------------------------------
 // text rounds: classify the tie groups (keys come from the PSS at an offset)
 // ---------------------------------------------------------------------------
+constexpr uint32_t CT_IPT = 16;        // tie groups per thread in k3_classify_text
+
+__device__ __forceinline__ uint64_t* class_list(const Ctx& c, int cls)
+{
+    return cls == 0 ? c.L.w : cls == 1 ? c.L.s : cls == 2 ? c.L.s2 : cls == 3 ? c.L.m1 : cls == 4 ? c.L.m2
+         : cls == 5 ? c.L.m3 : c.L.l[c.lsel];
+}
+__device__ __forceinline__ uint32_t* class_ctr(const Ctx& c, int cls)
+{
+    return c.L.ctr + (cls == 0 ? C_W : cls == 1 ? C_S : cls == 2 ? C_S2 : cls == 3 ? C_M1 : cls == 4 ? C_M2
+                      : cls == 5 ? C_M3 : C_L0 + c.lsel);
+}
+
+// tie groups -> size-class lists for the next text round (as wg_classify, CT_IPT
+// groups per thread: one LDS atomic per thread and class, one global atomic
+// per workgroup and class, the groups held in registers between the passes)
 __global__ void __launch_bounds__(256) k3_classify_text(Ctx c, const uint64_t* __restrict__ items, uint32_t nitems)
 {
-    const int lane = threadIdx.x & 63;
-    const uint32_t i = blockIdx.x * 256 + threadIdx.x;
-    const bool active = i < nitems;
-    const uint64_t item = active ? items[i] : 0;
-    const uint32_t slot = it_slot(item), s = it_start(item), m = it_size(item);
-    const Geo g = c.L.geo[active ? slot : 0];
-    __shared__ uint32_t cls_sh[16];
-    wg_classify(c, cls_sh, active, slot, s, m, g.Dp * g.B, 0);
-    const uint32_t tied = wave_reduce_add<uint32_t>(active ? m : 0u);
+    __shared__ uint32_t cls_cnt[8], cls_base[8];
+    const uint32_t tid = threadIdx.x, lane = tid & 63;
+    if (tid < 8) cls_cnt[tid] = 0;
+    __syncthreads();
+    const uint64_t i0 = (uint64_t)blockIdx.x * 256u * CT_IPT + tid;
+    uint64_t it[CT_IPT];
+    uint32_t cnt[7] = {0, 0, 0, 0, 0, 0, 0}, tied = 0;
+#pragma unroll
+    for (uint32_t k = 0; k < CT_IPT; ++k) {
+        const uint64_t i = i0 + (uint64_t)k * 256u;
+        it[k] = i < nitems ? items[i] : 0ull;
+        if (i < nitems) {
+            const uint32_t m = it_size(it[k]);
+            ++cnt[size_class(m)];
+            tied += m;
+        }
+    }
+    uint32_t off[7];
+#pragma unroll
+    for (int q = 0; q < 7; ++q) off[q] = cnt[q] ? atomicAdd(&cls_cnt[q], cnt[q]) : 0u;
+    __syncthreads();
+    if (tid < 7 && cls_cnt[tid]) cls_base[tid] = atomicAdd(class_ctr(c, (int)tid), cls_cnt[tid]);
+    __syncthreads();
+#pragma unroll
+    for (uint32_t k = 0; k < CT_IPT; ++k) {
+        const uint64_t i = i0 + (uint64_t)k * 256u;
+        if (i < nitems) {
+            const uint32_t slot = it_slot(it[k]), m = it_size(it[k]);
+            const int cls = size_class(m);
+            uint32_t o = 0;
+#pragma unroll
+            for (int q = 0; q < 7; ++q) if (q == cls) o = off[q]++;
+            const Geo g = c.L.geo[slot];
+            class_list(c, cls)[cls_base[cls] + o] = mk_item(slot, it_start(it[k]), m, g.Dp * g.B, 0);
+        }
+    }
+    tied = wave_reduce_add<uint32_t>(tied);
     if (lane == 0 && tied) atomicAdd(&c.L.ctr[C_TIE_ELEMS], tied);
 }
 
@@ -1834,10 +1956,14 @@ __global__ void k3_finish(Ctx c, uint32_t nb, unsigned long long* stats)
 
 // Host orchestration.  A handful of host round trips per batch (list sizes).
 void launch_bwt3(BlockDesc* blocks, uint32_t b0, uint32_t nb, const uint8_t* blkbytes, uint64_t stride,
-                 const BwtScratch& scr, DevBuf& meta, uint32_t* hctr, unsigned long long* stats, hipStream_t st)
+                 const BwtScratch& scr, DevBuf& meta, uint32_t* hctr, unsigned long long* stats, hipStream_t st,
+                 bool wide)
 {
     if (nb == 0) return;
     if (nb > 4095) throw StarchError(-2, "bwt3: batch too large");
+    // the tile histograms live in K after the PSS: [MAXT + 1][bins] words (small
+    // blocks, -1 .. -2, have room for the 4096-bin binary digit only)
+    if (wide && pss_words(scr.stride) * 2 + (uint64_t)(MAXT + 1) * PNB_WIDE > 2 * scr.stride) wide = false;
     if (pss_words(scr.stride) * 2 + (uint64_t)(MAXT + 1) * PNB > 2 * scr.stride)
         throw StarchError(-2, "bwt3: block stride too small");
     const uint64_t N = (uint64_t)nb * scr.stride;
@@ -1846,7 +1972,7 @@ void launch_bwt3(BlockDesc* blocks, uint32_t b0, uint32_t nb, const uint8_t* blk
                    cap_m3 = N / (M2_MAX + 1) + 64, cap_l = N / ((L_MIN < M3_MAX ? L_MIN : M3_MAX) + 1) + 64;
     const uint64_t nwg_bin = BIN_MAXWG;
     constexpr uint32_t QSETS = 64, QSET = 8 * XQ_STRIDE + 32;   // queue heads (a line each) + segments per launch
-    const uint64_t words = 2 * C_N + 10ull * nb + QSETS * QSET + nwg_bin * nb +
+    const uint64_t words = 2 * C_N + 14ull * nb + QSETS * QSET + nwg_bin * nb +
                            2 * (cap_s + cap_s2 + cap_m1 + cap_m2 + cap_m3 + 2 * cap_l) + 64;
     uint32_t* mw = meta.as<uint32_t>(words);
     Ctx c;
@@ -1862,7 +1988,7 @@ void launch_bwt3(BlockDesc* blocks, uint32_t b0, uint32_t nb, const uint8_t* blk
     c.L.periodic = c.L.runs + nb;
     c.L.rounds = c.L.periodic + nb;
     c.L.tied = c.L.rounds + nb;
-    c.L.geo = reinterpret_cast<Geo*>(c.L.tied + nb);            // 4 words per slot
+    c.L.geo = reinterpret_cast<Geo*>(c.L.tied + nb);            // 8 words per slot
     uint32_t* qpool = reinterpret_cast<uint32_t*>(c.L.geo + nb);
     uint32_t* binh = qpool + QSETS * QSET;
     uintptr_t p = reinterpret_cast<uintptr_t>(binh + nwg_bin * nb);
@@ -1884,7 +2010,8 @@ void launch_bwt3(BlockDesc* blocks, uint32_t b0, uint32_t nb, const uint8_t* blk
     c.rtext = 0;
     c.qhead = nullptr;
     c.qseg = nullptr;
-    HIP_CHECK(hipMemsetAsync(mw, 0, (2 * C_N + 10ull * nb + QSETS * QSET) * sizeof(uint32_t), st));
+    c.nbins = wide ? PNB_WIDE : PNB;
+    HIP_CHECK(hipMemsetAsync(mw, 0, (2 * C_N + 14ull * nb + QSETS * QSET) * sizeof(uint32_t), st));
 
     uint32_t qnext = 0;
     auto next_q = [&](uint32_t*& head, uint32_t*& seg) {
@@ -2015,8 +2142,13 @@ void launch_bwt3(BlockDesc* blocks, uint32_t b0, uint32_t nb, const uint8_t* blk
     {
         const uint32_t maxw = (uint32_t)pss_words(scr.stride);
         hipLaunchKernelGGL(k3_pss, dim3((maxw + 255) / 256, nb), dim3(256), 0, st, c);
-        hipLaunchKernelGGL(k3_hist, dim3(MAXT, nb), dim3(PT), 0, st, c);
-        hipLaunchKernelGGL(k3_scan, dim3(nb), dim3(ST), 0, st, c);
+        if (wide) {
+            hipLaunchKernelGGL(k3_hist<PNB_WIDE>, dim3(MAXT, nb), dim3(PT), 0, st, c);
+            hipLaunchKernelGGL(k3_scan<PNB_WIDE>, dim3(nb), dim3(ST), 0, st, c);
+        } else {
+            hipLaunchKernelGGL(k3_hist<PNB>, dim3(MAXT, nb), dim3(PT), 0, st, c);
+            hipLaunchKernelGGL(k3_scan<PNB>, dim3(nb), dim3(ST), 0, st, c);
+        }
         uint32_t* head;
         uint32_t* seg;
         next_q(head, seg);
@@ -2025,8 +2157,11 @@ void launch_bwt3(BlockDesc* blocks, uint32_t b0, uint32_t nb, const uint8_t* blk
         // about one block in flight per XCD: one 1024-thread workgroup per CU,
         // a block's MAXT tiles spread over its XCD's CUs
         static const bool direct = [] { const char* e = getenv("STARCH_SCATTER"); return e && !strcmp(e, "direct"); }();
-        if (direct) hipLaunchKernelGGL(k3_scatter, dim3((ncu + 7) / 8 * 8), dim3(SCT), 0, st, c);
-        else hipLaunchKernelGGL(k3_scatter_lds, dim3((ncu + 7) / 8 * 8), dim3(SCT), 0, st, c);
+        const dim3 gsc((ncu + 7) / 8 * 8);
+        if (direct && wide) hipLaunchKernelGGL(k3_scatter<PNB_WIDE>, gsc, dim3(SCT), 0, st, c);
+        else if (direct) hipLaunchKernelGGL(k3_scatter<PNB>, gsc, dim3(SCT), 0, st, c);
+        else if (wide) hipLaunchKernelGGL(k3_scatter_lds<PNB_WIDE>, gsc, dim3(SCT), 0, st, c);
+        else hipLaunchKernelGGL(k3_scatter_lds<PNB>, gsc, dim3(SCT), 0, st, c);
         HIP_CHECK(hipGetLastError());
     }
     sort_groups();
@@ -2047,7 +2182,8 @@ void launch_bwt3(BlockDesc* blocks, uint32_t b0, uint32_t nb, const uint8_t* blk
         c.tsel ^= 1u;
         HIP_CHECK(hipMemsetAsync(c.L.ctr + C_T0 + c.tsel, 0, sizeof(uint32_t), st));
         HIP_CHECK(hipMemsetAsync(c.L.ctr + C_TS0 + c.tsel, 0, sizeof(uint32_t), st));
-        hipLaunchKernelGGL(k3_classify_text, dim3((nt + 255) / 256), dim3(256), 0, st, c, c.L.t[cur], nt);
+        hipLaunchKernelGGL(k3_classify_text, dim3((nt + 256 * CT_IPT - 1) / (256 * CT_IPT)), dim3(256), 0, st, c,
+                           c.L.t[cur], nt);
         HIP_CHECK(hipGetLastError());
         HIP_CHECK(hipMemsetAsync(c.L.ctr + C_T0 + cur, 0, sizeof(uint32_t), st));
         sort_groups();

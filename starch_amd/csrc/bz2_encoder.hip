@@ -273,8 +273,18 @@ void Encoder::plan(const uint8_t* d_text, const std::vector<StreamIn>& streams, 
             // STARCH_BWT=lsd selects the one-workgroup-per-block prefix-doubling sort of
             // bz2_bwt.hip (kept as an independent implementation for cross-checks)
             static const bool lsd = [] { const char* e = getenv("STARCH_BWT"); return e && !strcmp(e, "lsd"); }();
+            // blocks of 17..20 symbols take the 8192-bin mixed-radix top-level digit
+            // (STARCH_WIDE=0: binary 12-bit digit everywhere; tests compare the two)
+            static const bool wide_off = [] { const char* e = getenv("STARCH_WIDE"); return e && !strcmp(e, "0"); }();
+            bool wide = false;
+            for (uint32_t k = 0; k < cnt && !wide && !wide_off; ++k) {
+                const BlockDesc& bd = hb[reuse ? reps[b0 + k] : b0 + k];
+                uint32_t nin = 0;
+                for (int j = 0; j < 8; ++j) nin += (uint32_t)__builtin_popcount(bd.in_use[j]);
+                wide = nin >= 17 && nin <= 20;
+            }
             if (lsd) launch_bwt(d_bl, b0, cnt, d_bytes, blk_stride_, scr, d_stats, st);
-            else launch_bwt3(d_bl, b0, cnt, d_bytes, blk_stride_, scr, b_bwt3, h_ctr_.get(), d_stats, st);
+            else launch_bwt3(d_bl, b0, cnt, d_bytes, blk_stride_, scr, b_bwt3, h_ctr_.get(), d_stats, st, wide);
             HIP_CHECK(hipMemcpyAsync(hr.data() + b0, d_bl + b0, cnt * sizeof(BlockDesc), hipMemcpyDeviceToHost,
                                      st));
             HIP_CHECK(hipStreamSynchronize(st));

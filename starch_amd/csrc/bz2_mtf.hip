@@ -155,6 +155,10 @@ struct NibP {
     using List = uint64_t;
     static constexpr uint32_t LO = 1, HI = 16;        // nInUse range handled
     static constexpr uint32_t SW = 2, LW = 1;         // u64 words per State / List
+    static constexpr uint32_t IXB = 4;                // bits per stored MTF index (k_mtf_runs -> k_mtf_emit)
+    // nibble MTF is cheap: k_mtf_emit re-runs it from the last column (storing
+    // the indices measured slower: the stores queue behind the chunk's loads)
+    static constexpr bool SIX = false;
     __device__ static State empty() { State r; r.list = 0; r.set = 0; r.cnt = 0; return r; }
     __device__ static void add(State& st, uint32_t s)
     {
@@ -188,6 +192,8 @@ struct ByteP {
     // counts mtfFreq itself (k_tables reads the counts k_mtf_big leaves)
     static constexpr uint32_t LO = 17, HI = 30;
     static constexpr uint32_t SW = 5, LW = 4;
+    static constexpr uint32_t IXB = 8;
+    static constexpr bool SIX = true;                 // byte-list MTF: store the indices, emit reads them
     __device__ static void put(uint64_t* w, uint32_t i, uint32_t s)
     {
         const uint32_t j = i >> 3, sh = 8 * (i & 7);
@@ -273,6 +279,8 @@ struct MtfScr {
     __device__ typename P::List* l0() const { return reinterpret_cast<typename P::List*>(base + (uint64_t)P::SW * C); }
     __device__ RunSum* rs() const { return reinterpret_cast<RunSum*>(base + (uint64_t)(P::SW + P::LW) * C); }
     __device__ uint2* zo() const { return reinterpret_cast<uint2*>(base + (uint64_t)(P::SW + P::LW + 2) * C); }
+    // the MTF indices of the whole block (P::IXB bits each, chunk c at c * MCS symbols)
+    __device__ uint8_t* ix() const { return reinterpret_cast<uint8_t*>(base + (uint64_t)(P::SW + P::LW + 3) * C); }
 };
 
 template <class P>
@@ -389,7 +397,8 @@ __global__ void __launch_bounds__(MST) k_mtf_scan_lists(const BlockDesc* __restr
     }
 }
 
-// zero-run summary of each chunk's MTF indices (branch-free per symbol)
+// MTF of each chunk: its indices, stored for k_mtf_emit (P::IXB bits each,
+// one store per 16 symbols), and their zero-run summary (branch-free per symbol)
 template <class P>
 __global__ void __launch_bounds__(MCT) k_mtf_runs(const BlockDesc* __restrict__ blocks, uint32_t b0,
                                                   const uint8_t* __restrict__ LL, uint64_t ll_stride,
@@ -404,14 +413,43 @@ __global__ void __launch_bounds__(MCT) k_mtf_runs(const BlockDesc* __restrict__ 
     const MtfScr<P> ms = mtf_scr<P>(K, kstride, slot, C);
     typename P::List L = ms.l0()[ch];
     uint32_t z = 0, nz = 0, lz = 0, inner = 0;
+    uint8_t* ixp = ms.ix() + (uint64_t)a * P::IXB / 8;     // 16 symbols = 8 (IXB 4) or 16 (IXB 8) bytes
+    // indices enter at the top of a 64-bit (IXB 4) / 128-bit (IXB 8) shift
+    // register; after 16 symbols the first sits in the lowest bits
+    uint64_t lo = 0, hi = 0;
+    uint32_t k16 = 0, piece_no = 0;
     visit_chunk(LL + (uint64_t)slot * ll_stride, a, e, [&](uint32_t s) {
         const uint32_t x = P::mtf(L, s);
+        if constexpr (P::IXB == 4) {
+            lo = (lo >> 4) | ((uint64_t)x << 60);
+        } else {
+            lo = (lo >> 8) | (hi << 56);
+            hi = (hi >> 8) | ((uint64_t)x << 56);
+        }
+        if (P::SIX && ++k16 == 16) {
+            if constexpr (P::IXB == 4) reinterpret_cast<uint64_t*>(ixp)[piece_no] = lo;
+            else reinterpret_cast<uint4*>(ixp)[piece_no] = make_uint4((uint32_t)lo, (uint32_t)(lo >> 32),
+                                                                      (uint32_t)hi, (uint32_t)(hi >> 32));
+            k16 = 0;
+            ++piece_no;
+        }
         const uint32_t nzf = x != 0 ? 1u : 0u;
         inner += (nzf & nz) ? 1u + (31u - __clz(z + 1u)) : 0u;
         lz = (nzf & (nz ^ 1u)) ? z : lz;
         nz |= nzf;
         z = nzf ? 0u : z + 1u;
     });
+    if (P::SIX && k16) {                                 // partial last piece: align its first symbol to bit 0
+        const uint32_t sh = (16 - k16) * P::IXB;
+        if constexpr (P::IXB == 4) {
+            reinterpret_cast<uint64_t*>(ixp)[piece_no] = lo >> sh;
+        } else {
+            const uint64_t l2 = sh >= 64 ? hi >> (sh - 64) : ((lo >> sh) | (hi << (64 - sh)));
+            const uint64_t h2 = sh >= 64 ? 0 : hi >> sh;
+            reinterpret_cast<uint4*>(ixp)[piece_no] = make_uint4((uint32_t)l2, (uint32_t)(l2 >> 32), (uint32_t)h2,
+                                                                 (uint32_t)(h2 >> 32));
+        }
+    }
     RunSum r;
     r.nz = nz;
     r.lz = nz ? lz : z;
@@ -473,7 +511,8 @@ __global__ void __launch_bounds__(MST) k_mtf_scan_runs(BlockDesc* __restrict__ b
     }
 }
 
-// re-run each chunk's MTF and emit RUNA/RUNB + symbols at its offset
+// emit each chunk's RUNA/RUNB + symbols at its offset, from the MTF indices
+// k_mtf_runs stored
 template <class P>
 __global__ void __launch_bounds__(MCT) k_mtf_emit(const BlockDesc* __restrict__ blocks, uint32_t b0,
                                                   const uint8_t* __restrict__ LL, uint64_t ll_stride,
@@ -487,13 +526,11 @@ __global__ void __launch_bounds__(MCT) k_mtf_emit(const BlockDesc* __restrict__ 
     if (!mtf_mine<P>(nin) || a >= n) return;
     const uint32_t e = a + MCS < n ? a + MCS : n;
     const MtfScr<P> ms = mtf_scr<P>(const_cast<uint64_t*>(K), kstride, slot, C);
-    typename P::List L = ms.l0()[ch];
     const uint2 zo = ms.zo()[ch];
     Out16 out;
     out.init(mtfv_all + (uint64_t)b * mtf_stride, zo.y);
     uint32_t z = zo.x;
-    visit_chunk_lines(LL + (uint64_t)slot * ll_stride, a, e, [&](uint32_t s) {
-        const uint32_t x = P::mtf(L, s);
+    auto f = [&](uint32_t x) {
         if (x == 0) {
             ++z;
         } else {
@@ -501,7 +538,34 @@ __global__ void __launch_bounds__(MCT) k_mtf_emit(const BlockDesc* __restrict__ 
             out.put(x + 1);
             z = 0;
         }
-    });
+    };
+    if constexpr (!P::SIX) {                           // re-run the MTF from the chunk's start list
+        typename P::List L = ms.l0()[ch];
+        visit_chunk_lines(LL + (uint64_t)slot * ll_stride, a, e, [&](uint32_t s) { f(P::mtf(L, s)); });
+        out.flush();
+        return;
+    }
+    // one 16-B piece (32 or 16 indices) at a time, the next piece's load in flight
+    constexpr uint32_t SPP = 128 / P::IXB;             // symbols per 16-B piece
+    const uint4* q = reinterpret_cast<const uint4*>(ms.ix() + (uint64_t)a * P::IXB / 8);
+    const uint32_t cnt = e - a, np = (cnt + SPP - 1) / SPP;
+    uint4 cur = q[0];
+#pragma unroll 1
+    for (uint32_t i = 0; i < np; ++i) {
+        const uint4 nxt = q[i + 1 < np ? i + 1 : i];
+        const uint32_t wv[4] = {cur.x, cur.y, cur.z, cur.w};
+        const uint32_t lim = cnt - i * SPP;
+        if (lim >= SPP) {
+#pragma unroll
+            for (uint32_t k = 0; k < SPP; ++k)
+                f(P::IXB == 4 ? (wv[k >> 3] >> (4 * (k & 7))) & 15u : (wv[k >> 2] >> (8 * (k & 3))) & 255u);
+        } else {
+#pragma unroll
+            for (uint32_t k = 0; k < SPP; ++k)
+                if (k < lim) f(P::IXB == 4 ? (wv[k >> 3] >> (4 * (k & 7))) & 15u : (wv[k >> 2] >> (8 * (k & 3))) & 255u);
+        }
+        cur = nxt;
+    }
     out.flush();
 }
 

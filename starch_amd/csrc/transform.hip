@@ -885,10 +885,14 @@ __global__ void k_seg_info(const uint64_t* __restrict__ seg_first, uint64_t nseg
 // takes the two-pass path: a stale sscanf value (FX_FAIL: general path), a
 // line longer than the halo or a tile of > 2048 lines (FX_FALLBACK), or text /
 // segment capacity (FX_TEXT_CAP / FX_SEG_CAP: grow, rerun).
-constexpr uint32_t kFT = 8192;                 // tile bytes
+#ifndef STARCH_FT
+#define STARCH_FT 8192
+#endif
+constexpr uint32_t kFT = STARCH_FT;            // tile bytes
 constexpr uint32_t kFH = 1024;                 // halo bytes before the tile
-constexpr uint32_t kFMaxLines = 2048;
-constexpr uint32_t kFOut = 10240;              // LDS output bytes per tile
+constexpr uint32_t kFMaxLines = kFT / 4;
+constexpr uint32_t kFOut = kFT + kFT / 4;      // LDS output bytes per tile
+static_assert(kFT <= 16384, "tested tile sizes: 4, 8, 16 KiB (8 KiB measured fastest)");
 constexpr uint32_t kFSeg = 64;                 // segment records per tile in LDS
 enum : uint32_t { FX_FAIL = 1, FX_FALLBACK = 2, FX_TEXT_CAP = 4, FX_SEG_CAP = 8 };
 

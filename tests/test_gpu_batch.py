@@ -34,3 +34,36 @@ def test_small_bwt_batches_bit_identical(tmp_path, cap):
     out = subprocess.run([sys.executable, "-c", CHILD, str(f)], env=env, capture_output=True, timeout=300)
     assert out.returncode == 0, out.stderr.decode()[-2000:]
     assert out.stdout == arch
+
+
+@pytest.mark.gpu
+def test_wide_top_digit_bit_identical(tmp_path):
+    """Blocks of 17..20 symbols (narrowPeak text) sort with the 8192-bin
+    mixed-radix top-level digit (bz2_bwt3.hip top_digit); STARCH_WIDE=0 forces
+    the binary 12-bit digit.  Any exact sort gives bzip2's order, so both must
+    produce the same archive, also for a batch mixing 17..20-symbol blocks with
+    smaller and larger alphabets."""
+    import random
+
+    import starch_amd
+    from tests import oracle_lib
+    r = random.Random(5)
+    wide = starch_amd.gen_bed(1, 300_000, chroms=[20, 21])
+    odd = b"".join(b"chrZ\t%d\t%d\t%s\n" % (i * 10, i * 10 + 5, bytes(r.choice(b"ABCDEFGHIJKLMNOPQRSTUVWXYZ")
+                                                                     for _ in range(8)))
+                   for i in range(30_000))
+    data = bytes(wide) + starch_amd.gen_bed(0, 200_000, chroms=[22]) + odd
+    c = starch_amd.Starch(0)
+    arch = c.compress(data)
+    c.close()
+    idx, streams = starch_amd.parse_archive(arch)
+    _, osegs = oracle_lib.transform(data)
+    assert len(streams) == len(osegs)
+    for st, (_, _, text) in zip(streams, osegs):
+        assert st == oracle_lib.bz2(text, 9)
+    f = tmp_path / "in.bed"
+    f.write_bytes(data)
+    env = dict(os.environ, STARCH_WIDE="0")
+    out = subprocess.run([sys.executable, "-c", CHILD, str(f)], env=env, capture_output=True, timeout=300)
+    assert out.returncode == 0, out.stderr.decode()[-2000:]
+    assert out.stdout == arch
