@@ -56,7 +56,13 @@ typedef struct {
     int reference_compat;    /* 1: archive is exactly the reference's stdout (magic only) */
     const char* note;        /* --note text for the index (may be NULL) */
     int base_counts;         /* 1: per-segment base counts (hpp:61-62) in the segments and the index */
+    int compression_method;  /* STARCH_METHOD_BZIP2 (0, default) or STARCH_METHOD_GZIP (1): the reference's
+                              * compression_method_t (hpp:23-27); gzip there exits ENOSYS (hpp:777-779),
+                              * here every segment is one gzip member (fixed-Huffman deflate on the GPU) */
 } starch_options;
+
+#define STARCH_METHOD_BZIP2 0
+#define STARCH_METHOD_GZIP 1
 
 typedef struct {
     uint64_t line_count;     /* transform_state_t.line_count at flush (hpp:395) */

@@ -58,7 +58,8 @@ class Unit(ctypes.Structure):
 
 class Options(ctypes.Structure):
     _fields_ = [("block_size_100k", ctypes.c_int), ("emit_index", ctypes.c_int),
-                ("reference_compat", ctypes.c_int), ("note", ctypes.c_char_p), ("base_counts", ctypes.c_int)]
+                ("reference_compat", ctypes.c_int), ("note", ctypes.c_char_p), ("base_counts", ctypes.c_int),
+                ("compression_method", ctypes.c_int)]
 
 
 class Stats(ctypes.Structure):
@@ -225,7 +226,7 @@ class Starch:
 
     # -- the hot path ----------------------------------------------------------
     def _opts(self, emit_index=True, reference_compat=False):
-        if self._method == K_GZIP:
+        if self._method == K_GZIP and reference_compat:
             raise StarchError(-38, "This method is unsupported at this time")      # hpp:777-779
         if self._method == K_UNDEFINED:
             raise StarchError(-38, "This method is undefined")                      # hpp:780-782
@@ -235,6 +236,9 @@ class Starch:
         o.emit_index = 1 if emit_index else 0
         o.reference_compat = 1 if reference_compat else 0
         o.base_counts = 1 if self.base_counts else 0
+        # gzip (-g): one gzip member per segment (fixed-Huffman deflate on the GPU);
+        # the reference itself stops with ENOSYS (kept under reference_compat)
+        o.compression_method = 1 if self._method == K_GZIP else 0
         self._note_b = self._note.encode() if self._note else None
         o.note = self._note_b
         return o

@@ -14,6 +14,7 @@
 #include "../../include/starch_amd.h"
 #include "bz2.hpp"
 #include "bz2_decode.hpp"
+#include "gz.hpp"
 #include "shard.hpp"
 #include "transform.hpp"
 #include "untransform.hpp"
@@ -24,6 +25,7 @@ struct starch_ctx {
     hipStream_t st = nullptr;
     TransformWorkspace tf;
     bz::Encoder enc;
+    gz::Encoder genc;            // the gzip method (-g)
     DevBuf input, archive, part, raw_in, raw_out, text_all;
     // decompression / unstarch: the last result is out_dev[0, out_bytes)
     bz::Decoder dec;
@@ -143,12 +145,13 @@ void json_str(std::string& o, const char* p, size_t n, bool keep_utf8 = false)
 }
 
 std::string build_index(const starch_segment* segs, const char* const* names, const uint64_t* nlens, uint64_t nseg,
-                        uint64_t index_off, const char* note, int bs, bool base_counts = false)
+                        uint64_t index_off, const char* note, int bs, bool base_counts = false, int method = 0)
 {
     std::string j;
     j += "{\"archive\":{\"type\":\"starch\",\"format\":\"starch3-mi355x\",\"version\":{\"major\":3,\"minor\":0,"
-         "\"revision\":0},\"compressionFormat\":\"bzip2\",\"blockSize100k\":";
-    j += std::to_string(bs);
+         "\"revision\":0},\"compressionFormat\":";
+    j += method == STARCH_METHOD_GZIP ? "\"gzip\",\"blockSize100k\":" : "\"bzip2\",\"blockSize100k\":";
+    j += std::to_string(method == STARCH_METHOD_GZIP ? 0 : bs);
     j += ",\"note\":";
     json_str(j, note ? note : "", note ? strlen(note) : 0, true);
     j += "},\"streams\":[";
@@ -378,7 +381,9 @@ void encode_units(starch_ctx* c, const uint8_t* d_base, const std::vector<UnitIn
     }
     std::vector<bz::StreamOut> outs;
     bz::Stats bst;
-    c->enc.plan(text, sin, opt.block_size_100k, c->st, outs, &bst);
+    const bool gzip = opt.compression_method == STARCH_METHOD_GZIP;
+    if (gzip) c->genc.plan(text, sin, c->st, outs, &bst);
+    else c->enc.plan(text, sin, opt.block_size_100k, c->st, outs, &bst);
     uint64_t streams_bytes = 0;
     for (auto& o : outs) streams_bytes = std::max(streams_bytes, o.out_off + o.bytes);
     for (uint64_t s = 0; s < nseg; ++s) {
@@ -395,7 +400,8 @@ void encode_units(starch_ctx* c, const uint8_t* d_base, const std::vector<UnitIn
                                   256);
     uint8_t* out = (lay == L_ARCHIVE ? c->archive : c->part).as<uint8_t>(cap);
     if (lay == L_ARCHIVE) HIP_CHECK(hipMemcpyAsync(out, kMagic, 4, hipMemcpyHostToDevice, c->st));
-    c->enc.emit(out, cap, base, outs, c->st, &bst);
+    if (gzip) c->genc.emit(out, cap, base, outs, c->st, &bst);
+    else c->enc.emit(out, cap, base, outs, c->st, &bst);
     for (uint64_t s = 0; s < nseg; ++s) c->segs[s].combined_crc = outs[s].combined_crc;
     uint64_t total = index_off;
     std::string idx;
@@ -404,7 +410,7 @@ void encode_units(starch_ctx* c, const uint8_t* d_base, const std::vector<UnitIn
         std::vector<uint64_t> nl(nseg);
         for (uint64_t s = 0; s < nseg; ++s) { np[s] = c->names[s].data(); nl[s] = c->names[s].size(); }
         idx = build_index(c->segs.data(), np.data(), nl.data(), nseg, index_off, opt.note, opt.block_size_100k,
-                          opt.base_counts != 0);
+                          opt.base_counts != 0, opt.compression_method);
         if (index_off + idx.size() > cap) throw StarchError(STARCH_ERR_INTERNAL, "index capacity");
         HIP_CHECK(hipMemcpyAsync(out + index_off, idx.data(), idx.size(), hipMemcpyHostToDevice, c->st));
         total += idx.size();
@@ -518,7 +524,7 @@ void encode_multi(starch_ctx* const* ctxs, int nctx, const uint8_t* bed, uint64_
         std::vector<uint64_t> nl(nseg);
         for (uint64_t s = 0; s < nseg; ++s) { np[s] = names[s].data(); nl[s] = names[s].size(); }
         idx = build_index(segs.data(), np.data(), nl.data(), nseg, end, opt.note, opt.block_size_100k,
-                          opt.base_counts != 0);
+                          opt.base_counts != 0, opt.compression_method);
     }
     Ctx g(c0);
     const uint64_t total = opt.reference_compat ? 4 : end + idx.size();
@@ -830,6 +836,7 @@ void starch_options_init(starch_options* o)
     o->reference_compat = 0;
     o->note = nullptr;
     o->base_counts = 0;
+    o->compression_method = STARCH_METHOD_BZIP2;
 }
 
 int starch_encode_device(starch_ctx* c, const void* d_bed, uint64_t n, const starch_options* opt)
@@ -838,7 +845,8 @@ int starch_encode_device(starch_ctx* c, const void* d_bed, uint64_t n, const sta
     starch_options o;
     starch_options_init(&o);
     if (opt) o = *opt;
-    if (o.block_size_100k < 1 || o.block_size_100k > 9) return STARCH_ERR_ARG;
+    if (o.block_size_100k < 1 || o.block_size_100k > 9 ||
+        (o.compression_method != STARCH_METHOD_BZIP2 && o.compression_method != STARCH_METHOD_GZIP)) return STARCH_ERR_ARG;
     if (n && !d_bed) return STARCH_ERR_ARG;
     encode_device(c, static_cast<const uint8_t*>(d_bed), n, o);
     return STARCH_OK;
@@ -855,7 +863,8 @@ int starch_encode_host(starch_ctx* c, const void* bed, uint64_t n, const starch_
     starch_options o;
     starch_options_init(&o);
     if (opt) o = *opt;
-    if (o.block_size_100k < 1 || o.block_size_100k > 9) return STARCH_ERR_ARG;
+    if (o.block_size_100k < 1 || o.block_size_100k > 9 ||
+        (o.compression_method != STARCH_METHOD_BZIP2 && o.compression_method != STARCH_METHOD_GZIP)) return STARCH_ERR_ARG;
     encode_device(c, d, n, o);
     return STARCH_OK;
     END_GUARD(c)
@@ -879,7 +888,8 @@ int starch_encode_units_device(starch_ctx* c, const void* d_base, const starch_u
     starch_options o;
     starch_options_init(&o);
     if (opt) o = *opt;
-    if (o.block_size_100k < 1 || o.block_size_100k > 9 || (nunits && !d_base)) return STARCH_ERR_ARG;
+    if (o.block_size_100k < 1 || o.block_size_100k > 9 ||
+        (o.compression_method != STARCH_METHOD_BZIP2 && o.compression_method != STARCH_METHOD_GZIP) || (nunits && !d_base)) return STARCH_ERR_ARG;
     std::vector<UnitIn> u;
     int rc = units_in(units, unit_ids, nunits, u);
     if (rc) return rc;
@@ -921,7 +931,8 @@ int starch_encode_multi_host(starch_ctx* const* ctxs, int nctx, const void* bed,
     starch_options o;
     starch_options_init(&o);
     if (opt) o = *opt;
-    if (o.block_size_100k < 1 || o.block_size_100k > 9) return STARCH_ERR_ARG;
+    if (o.block_size_100k < 1 || o.block_size_100k > 9 ||
+        (o.compression_method != STARCH_METHOD_BZIP2 && o.compression_method != STARCH_METHOD_GZIP)) return STARCH_ERR_ARG;
     if (nctx == 1) {
         uint8_t* d = c->input.as<uint8_t>(n + 64);
         if (n) HIP_CHECK(hipMemcpyAsync(d, bed, n, hipMemcpyHostToDevice, c->st));
@@ -1181,7 +1192,8 @@ int starch_stream_begin(starch_ctx* c, const starch_options* opt, uint64_t batch
     starch_options o;
     starch_options_init(&o);
     if (opt) o = *opt;
-    if (o.block_size_100k < 1 || o.block_size_100k > 9) return STARCH_ERR_ARG;
+    if (o.block_size_100k < 1 || o.block_size_100k > 9 ||
+        (o.compression_method != STARCH_METHOD_BZIP2 && o.compression_method != STARCH_METHOD_GZIP)) return STARCH_ERR_ARG;
     c->stream_shutdown();                       // a session left open is abandoned
     auto& m = c->sm;
     m.active = true;
@@ -1282,7 +1294,8 @@ int starch_stream_end(starch_ctx* c)
         std::vector<uint64_t> nl(m.segs.size());
         for (size_t s = 0; s < m.segs.size(); ++s) { np[s] = m.names[s].data(); nl[s] = m.names[s].size(); }
         const std::string idx = build_index(m.segs.data(), np.data(), nl.data(), m.segs.size(), m.stream_end,
-                                            m.opt.note, m.opt.block_size_100k, m.opt.base_counts != 0);
+                                            m.opt.note, m.opt.block_size_100k, m.opt.base_counts != 0,
+                                            m.opt.compression_method);
         m.ready.insert(m.ready.end(), idx.begin(), idx.end());
         m.stats.archive_bytes = m.stream_end + idx.size();
     } else {
@@ -1345,7 +1358,7 @@ int starch_build_index_opt(const starch_segment* segs, const char* const* names,
 {
     if (!len || !opt || (nseg && (!segs || !names || !name_lens))) return STARCH_ERR_ARG;
     std::string s = build_index(segs, names, name_lens, nseg, index_offset, opt->note, opt->block_size_100k,
-                                opt->base_counts != 0);
+                                opt->base_counts != 0, opt->compression_method);
     *len = s.size();
     if (!dst) return STARCH_OK;
     if (cap < s.size()) return STARCH_ERR_MEM;

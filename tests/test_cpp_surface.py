@@ -86,8 +86,9 @@ def test_cli_two_methods_exits_1():
     assert r.returncode == 1 and b"Only one compression method" in r.stderr
 
 
-def test_cli_gzip_writes_magic_then_exits_38():
-    r = _cli(["-g"], input_bytes=b"chr1\t1\t2\n")
+def test_cli_gzip_reference_compat_writes_magic_then_exits_38():
+    """--reference-compat keeps the reference's gzip behaviour (hpp:765-769, 777-779)."""
+    r = _cli(["-g", "--reference-compat"], input_bytes=b"chr1\t1\t2\n")
     assert r.returncode == 38 and r.stdout == b"\xca\x5c\xad\x1a"
 
 

@@ -4,8 +4,9 @@
 // "n:bghv?", long options --note/--bzip2/--gzip/--help/--version, an optional
 // input filename (extra names warned and ignored, cpp:147-157), stdin checked
 // for a redirect (hpp:890-905), and the same exit codes: 61 (ENODATA) no input
-// / missing file, 38 (ENOSYS) gzip, 1 two methods, 22 (EINVAL) codec init.
-// The archive goes to stdout: magic ca5cad1a, one bzip2 stream per chromosome,
+// / missing file, 38 (ENOSYS) gzip under --reference-compat, 1 two methods, 22
+// (EINVAL) codec init.  The archive goes to stdout: magic ca5cad1a, one bzip2
+// stream (-g: one gzip member) per chromosome,
 // JSON index + footer.  Build-only flags: --level N, --no-index,
 // --reference-compat (stdout exactly as the reference: the 4 magic bytes),
 // --device N, --gpus N (shard chromosomes over devices 0..N-1 in one process),
@@ -45,7 +46,7 @@ static void usage(FILE* f)
             "     or:  %s [options] input > output\n\n"
             "  --note=\"text\"        note stored in the archive index\n"
             "  --bzip2 | -b          bzip2 streams (default)\n"
-            "  --gzip | -g           gzip streams (not supported)\n"
+            "  --gzip | -g           gzip members (one per chromosome; the reference: unsupported, exit 38)\n"
             "  --level N             bzip2 block size 1..9 (default 9)\n"
             "  --no-index            streams only, no JSON index/footer\n"
             "  --reference-compat    write exactly what the reference writes (magic bytes only)\n"
@@ -145,7 +146,7 @@ int main(int argc, char** argv)
         return ENODATA;
     }
     static const unsigned char magic[4] = {0xca, 0x5c, 0xad, 0x1a};
-    if (gzip) {   // the reference writes the magic, then fails (hpp:765-769, 777-779)
+    if (gzip && compat) {   // the reference writes the magic, then fails (hpp:765-769, 777-779)
         fwrite(magic, 1, 4, stdout);
         fprintf(stderr, "Error: This method is unsupported at this time\n");
         return ENOSYS;
@@ -170,6 +171,7 @@ int main(int argc, char** argv)
     opt.reference_compat = compat;
     opt.note = note.empty() ? nullptr : note.c_str();
     opt.base_counts = bases;
+    opt.compression_method = gzip ? STARCH_METHOD_GZIP : STARCH_METHOD_BZIP2;
     if (ctxs.size() == 1 && !slurp) {
         // streamed: read(2) straight into the session's pinned buffer while the
         // encoder thread works on the previous batch; drain finished streams
