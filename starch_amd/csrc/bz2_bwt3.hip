@@ -75,7 +75,7 @@ static_assert(PTILE <= 32768 && PNB_WIDE <= 8192, "k3_scatter_lds packs (digit <
 constexpr int MAXT = (900064 + PTILE - 1) / PTILE;   // tiles per block (bs <= 9)
 // size classes: W rank-by-compare (one wave), S wave-private LDS sort,
 // M1..M3 workgroup LDS sort, L MSD partition
-constexpr uint32_t W_MAX = 64, S1_MAX = 128, S_MAX = 256, M1_MAX = 1024, M2_MAX = 2048, M3_MAX = 4096;
+constexpr uint32_t W_MAX = 64, S1_MAX = 128, S_MAX = 256, M0_MAX = 512, M1_MAX = 1024, M2_MAX = 2048, M3_MAX = 4096;
 // groups above L_MIN are MSD-partitioned (k3_part_l) instead of sorted whole
 #ifndef STARCH_L_MIN
 #define STARCH_L_MIN 4096
@@ -86,7 +86,7 @@ constexpr uint32_t TEXT_ROUNDS = 4;     // max text-extension rounds before doub
 
 // counters (u32) in the meta buffer
 enum { C_W = 0, C_S, C_S2, C_M1, C_M2, C_M3, C_L0, C_L1, C_T0, C_T1, C_TIE_ELEMS, C_ERR, C_TS0, C_TS1, C_H, C_DBG2,
-       C_DBGL, C_N = 24 };
+       C_DBGL, C_M0, C_N = 24 };
 
 // item = slot[63:52] | start[51:32] | size[31:12] | parity[7] | shift[6:0]
 __device__ __forceinline__ uint64_t mk_item(uint32_t slot, uint32_t s, uint32_t m, uint32_t shift, uint32_t par)
@@ -128,6 +128,7 @@ struct Lists {
     uint64_t* w;            // m <= 64
     uint64_t* s;            // m <= 128
     uint64_t* s2;           // m <= 256
+    uint64_t* m0;           // m <= 512
     uint64_t* m1;           // m <= 1024
     uint64_t* m2;           // m <= 2048
     uint64_t* m3;           // m <= 4096
@@ -196,9 +197,21 @@ __device__ __forceinline__ void wave_push(uint32_t* ctr, uint64_t* list, bool pr
 // serialise).  Every thread of the workgroup must call it; sh: 16 u32 of LDS.
 __device__ __forceinline__ int size_class(uint32_t m)
 {
-    return m <= W_MAX ? 0 : m <= S1_MAX ? 1 : m <= S_MAX ? 2 : m > L_MIN ? 6 : m <= M1_MAX ? 3 : m <= M2_MAX ? 4
+    return m <= W_MAX ? 0 : m <= S1_MAX ? 1 : m <= S_MAX ? 2 : m > L_MIN ? 6 : m <= M0_MAX ? 7 : m <= M1_MAX ? 3 : m <= M2_MAX ? 4
          : m <= M3_MAX ? 5 : 6;
 }
+// class k's list and counter (0 W, 1 S, 2 S2, 3 M1, 4 M2, 5 M3, 6 L, 7 M0)
+__device__ __forceinline__ uint64_t* class_list(const Ctx& c, int cls)
+{
+    return cls == 0 ? c.L.w : cls == 1 ? c.L.s : cls == 2 ? c.L.s2 : cls == 3 ? c.L.m1 : cls == 4 ? c.L.m2
+         : cls == 5 ? c.L.m3 : cls == 7 ? c.L.m0 : c.L.l[c.lsel];
+}
+__device__ __forceinline__ uint32_t* class_ctr(const Ctx& c, int cls)
+{
+    return c.L.ctr + (cls == 0 ? C_W : cls == 1 ? C_S : cls == 2 ? C_S2 : cls == 3 ? C_M1 : cls == 4 ? C_M2
+                      : cls == 5 ? C_M3 : cls == 7 ? C_M0 : C_L0 + c.lsel);
+}
+
 __device__ __forceinline__ void wg_classify(const Ctx& c, uint32_t* sh, bool pred, uint32_t slot, uint32_t s,
                                             uint32_t m, uint32_t shift, uint32_t par)
 {
@@ -208,18 +221,9 @@ __device__ __forceinline__ void wg_classify(const Ctx& c, uint32_t* sh, bool pre
     uint32_t loff = 0;
     if (cls >= 0) loff = atomicAdd(&sh[cls], 1u);
     __syncthreads();
-    if (threadIdx.x < 7 && sh[threadIdx.x]) {
-        const uint32_t k = threadIdx.x;
-        uint32_t* ctr = c.L.ctr + (k == 0 ? C_W : k == 1 ? C_S : k == 2 ? C_S2 : k == 3 ? C_M1 : k == 4 ? C_M2
-                                   : k == 5 ? C_M3 : C_L0 + c.lsel);
-        sh[8 + k] = atomicAdd(ctr, sh[k]);
-    }
+    if (threadIdx.x < 8 && sh[threadIdx.x]) sh[8 + threadIdx.x] = atomicAdd(class_ctr(c, (int)threadIdx.x), sh[threadIdx.x]);
     __syncthreads();
-    if (cls >= 0) {
-        uint64_t* list = cls == 0 ? c.L.w : cls == 1 ? c.L.s : cls == 2 ? c.L.s2 : cls == 3 ? c.L.m1
-                       : cls == 4 ? c.L.m2 : cls == 5 ? c.L.m3 : c.L.l[c.lsel];
-        list[sh[8 + cls] + loff] = mk_item(slot, s, m, shift, par);
-    }
+    if (cls >= 0) class_list(c, cls)[sh[8 + cls] + loff] = mk_item(slot, s, m, shift, par);
     __syncthreads();
 }
 
@@ -1792,17 +1796,6 @@ k3_sort_grp(Ctx c, const uint64_t* __restrict__ items,
 // ---------------------------------------------------------------------------
 constexpr uint32_t CT_IPT = 16;        // tie groups per thread in k3_classify_text
 
-__device__ __forceinline__ uint64_t* class_list(const Ctx& c, int cls)
-{
-    return cls == 0 ? c.L.w : cls == 1 ? c.L.s : cls == 2 ? c.L.s2 : cls == 3 ? c.L.m1 : cls == 4 ? c.L.m2
-         : cls == 5 ? c.L.m3 : c.L.l[c.lsel];
-}
-__device__ __forceinline__ uint32_t* class_ctr(const Ctx& c, int cls)
-{
-    return c.L.ctr + (cls == 0 ? C_W : cls == 1 ? C_S : cls == 2 ? C_S2 : cls == 3 ? C_M1 : cls == 4 ? C_M2
-                      : cls == 5 ? C_M3 : C_L0 + c.lsel);
-}
-
 // tie groups -> size-class lists for the next text round (as wg_classify, CT_IPT
 // groups per thread: one LDS atomic per thread and class, one global atomic
 // per workgroup and class, the groups held in registers between the passes)
@@ -1814,7 +1807,7 @@ __global__ void __launch_bounds__(256) k3_classify_text(Ctx c, const uint64_t* _
     __syncthreads();
     const uint64_t i0 = (uint64_t)blockIdx.x * 256u * CT_IPT + tid;
     uint64_t it[CT_IPT];
-    uint32_t cnt[7] = {0, 0, 0, 0, 0, 0, 0}, tied = 0;
+    uint32_t cnt[8] = {0, 0, 0, 0, 0, 0, 0, 0}, tied = 0;
 #pragma unroll
     for (uint32_t k = 0; k < CT_IPT; ++k) {
         const uint64_t i = i0 + (uint64_t)k * 256u;
@@ -1825,11 +1818,11 @@ __global__ void __launch_bounds__(256) k3_classify_text(Ctx c, const uint64_t* _
             tied += m;
         }
     }
-    uint32_t off[7];
+    uint32_t off[8];
 #pragma unroll
-    for (int q = 0; q < 7; ++q) off[q] = cnt[q] ? atomicAdd(&cls_cnt[q], cnt[q]) : 0u;
+    for (int q = 0; q < 8; ++q) off[q] = cnt[q] ? atomicAdd(&cls_cnt[q], cnt[q]) : 0u;
     __syncthreads();
-    if (tid < 7 && cls_cnt[tid]) cls_base[tid] = atomicAdd(class_ctr(c, (int)tid), cls_cnt[tid]);
+    if (tid < 8 && cls_cnt[tid]) cls_base[tid] = atomicAdd(class_ctr(c, (int)tid), cls_cnt[tid]);
     __syncthreads();
 #pragma unroll
     for (uint32_t k = 0; k < CT_IPT; ++k) {
@@ -1839,7 +1832,7 @@ __global__ void __launch_bounds__(256) k3_classify_text(Ctx c, const uint64_t* _
             const int cls = size_class(m);
             uint32_t o = 0;
 #pragma unroll
-            for (int q = 0; q < 7; ++q) if (q == cls) o = off[q]++;
+            for (int q = 0; q < 8; ++q) if (q == cls) o = off[q]++;
             const Geo g = c.L.geo[slot];
             class_list(c, cls)[cls_base[cls] + o] = mk_item(slot, it_start(it[k]), m, g.Dp * g.B, 0);
         }
@@ -1967,13 +1960,14 @@ void launch_bwt3(BlockDesc* blocks, uint32_t b0, uint32_t nb, const uint8_t* blk
     if (pss_words(scr.stride) * 2 + (uint64_t)(MAXT + 1) * PNB > 2 * scr.stride)
         throw StarchError(-2, "bwt3: block stride too small");
     const uint64_t N = (uint64_t)nb * scr.stride;
-    const uint64_t cap_s = N / (W_MAX + 1) + 64, cap_s2 = N / (S1_MAX + 1) + 64, cap_m1 = N / (S_MAX + 1) + 64,
+    const uint64_t cap_s = N / (W_MAX + 1) + 64, cap_s2 = N / (S1_MAX + 1) + 64, cap_m0 = N / (S_MAX + 1) + 64,
+                   cap_m1 = N / (M0_MAX + 1) + 64,
                    cap_m2 = N / (M1_MAX + 1) + 64,
                    cap_m3 = N / (M2_MAX + 1) + 64, cap_l = N / ((L_MIN < M3_MAX ? L_MIN : M3_MAX) + 1) + 64;
     const uint64_t nwg_bin = BIN_MAXWG;
     constexpr uint32_t QSETS = 64, QSET = 8 * XQ_STRIDE + 32;   // queue heads (a line each) + segments per launch
     const uint64_t words = 2 * C_N + 14ull * nb + QSETS * QSET + nwg_bin * nb +
-                           2 * (cap_s + cap_s2 + cap_m1 + cap_m2 + cap_m3 + 2 * cap_l) + 64;
+                           2 * (cap_s + cap_s2 + cap_m0 + cap_m1 + cap_m2 + cap_m3 + 2 * cap_l) + 64;
     uint32_t* mw = meta.as<uint32_t>(words);
     Ctx c;
     c.blocks = blocks;
@@ -1995,7 +1989,8 @@ void launch_bwt3(BlockDesc* blocks, uint32_t b0, uint32_t nb, const uint8_t* blk
     p = (p + 7) & ~(uintptr_t)7;
     c.L.s = reinterpret_cast<uint64_t*>(p);
     c.L.s2 = c.L.s + cap_s;
-    c.L.m1 = c.L.s2 + cap_s2;
+    c.L.m0 = c.L.s2 + cap_s2;
+    c.L.m1 = c.L.m0 + cap_m0;
     c.L.m2 = c.L.m1 + cap_m1;
     c.L.m3 = c.L.m2 + cap_m2;
     c.L.l[0] = c.L.m3 + cap_m3;
@@ -2074,12 +2069,13 @@ void launch_bwt3(BlockDesc* blocks, uint32_t b0, uint32_t nb, const uint8_t* blk
             lsel ^= 1u;
         }
         c.lsel = 0;
+        const uint32_t n0 = hctr[C_M0];
         const uint32_t nw = hctr[C_W], ns = hctr[C_S], ns2 = hctr[C_S2], n1 = hctr[C_M1], n2 = hctr[C_M2],
                        n3 = hctr[C_M3];
         static const bool dbg = getenv("STARCH_BWT_DEBUG") != nullptr;
         if (dbg)
-            fprintf(stderr, "[bwt3] rtext %u mode %u: W %u S %u S2 %u M1 %u M2 %u M3 %u | level-2 %u lsd %u (so far)\n",
-                    c.rtext, c.mode, nw, ns, ns2, n1, n2, n3, hctr[C_DBG2], hctr[C_DBGL]);
+            fprintf(stderr, "[bwt3] rtext %u mode %u: W %u S %u S2 %u M0 %u M1 %u M2 %u M3 %u | level-2 %u lsd %u (so far)\n",
+                    c.rtext, c.mode, nw, ns, ns2, n0, n1, n2, n3, hctr[C_DBG2], hctr[C_DBGL]);
         // every launch reads its own binned copy; stream order lets them share one buffer
         // grids: a multiple of 8 (static per-XCD segments), about one resident wave of workgroups
         auto g8 = [](uint32_t x) { return dim3((x + 7) / 8 * 8); };
@@ -2100,6 +2096,7 @@ void launch_bwt3(BlockDesc* blocks, uint32_t b0, uint32_t nb, const uint8_t* blk
             static const dim3 gm3 = resident(reinterpret_cast<const void*>(&k3_sort_lds<4, 16, D>));
             static const dim3 gm2 = resident(reinterpret_cast<const void*>(&k3_sort_lds<4, 8, D>));
             static const dim3 gm1 = resident(reinterpret_cast<const void*>(&k3_sort_lds<4, 4, D>));
+            static const dim3 gm0 = resident(reinterpret_cast<const void*>(&k3_sort_lds<4, 2, D>));
             static const dim3 gs = resident(reinterpret_cast<const void*>(&k3_sort_grp<1, 2, D>));
             static const dim3 gs2 = resident(reinterpret_cast<const void*>(&k3_sort_grp<1, 4, D>));
             static const dim3 gw = resident(reinterpret_cast<const void*>(&k3_sort_w<D>));
@@ -2110,6 +2107,10 @@ void launch_bwt3(BlockDesc* blocks, uint32_t b0, uint32_t nb, const uint8_t* blk
             if (n2) {
                 bin(c.L.m2, n2, bout);
                 hipLaunchKernelGGL((k3_sort_lds<4, 8, D>), gm2, dim3(256), 0, st, c, bout, nullptr);
+            }
+            if (n0) {
+                bin(c.L.m0, n0, bout);
+                hipLaunchKernelGGL((k3_sort_lds<4, 2, D>), gm0, dim3(256), 0, st, c, bout, nullptr);
             }
             if (n1) {
                 bin(c.L.m1, n1, bout);
@@ -2136,6 +2137,7 @@ void launch_bwt3(BlockDesc* blocks, uint32_t b0, uint32_t nb, const uint8_t* blk
         else leaf(std::false_type{});
         HIP_CHECK(hipGetLastError());
         HIP_CHECK(hipMemsetAsync(c.L.ctr + C_W, 0, 6 * sizeof(uint32_t), st));
+        HIP_CHECK(hipMemsetAsync(c.L.ctr + C_M0, 0, sizeof(uint32_t), st));
     };
 
     // ---- round 0: packed prefix keys ----
