@@ -67,3 +67,23 @@ def test_wide_top_digit_bit_identical(tmp_path):
     out = subprocess.run([sys.executable, "-c", CHILD, str(f)], env=env, capture_output=True, timeout=300)
     assert out.returncode == 0, out.stderr.decode()[-2000:]
     assert out.stdout == arch
+
+
+@pytest.mark.gpu
+def test_alternate_lsd_block_sort_bit_identical(tmp_path):
+    """STARCH_BWT=lsd selects the independent one-workgroup-per-block
+    prefix-doubling sort (bz2_bwt.hip k_bwt): it must give
+    the default sort's archive byte for byte -- BED3 and narrowPeak blocks, a
+    periodic block (fallbackSort tie order) and long repeats."""
+    import starch_amd
+    data = (bytes(starch_amd.gen_bed(0, 200_000, chroms=[3, 20])) + bytes(starch_amd.gen_bed(1, 60_000, chroms=[21]))
+            + b"".join(b"chrP\t%d\t%d\n" % (i, i + 1) for i in range(200_000)))
+    c = starch_amd.Starch(0)
+    arch = c.compress(data)
+    c.close()
+    f = tmp_path / "in.bed"
+    f.write_bytes(data)
+    env = dict(os.environ, STARCH_BWT="lsd")
+    out = subprocess.run([sys.executable, "-c", CHILD, str(f)], env=env, capture_output=True, timeout=300)
+    assert out.returncode == 0, out.stderr.decode()[-2000:]
+    assert out.stdout == arch

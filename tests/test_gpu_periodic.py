@@ -69,3 +69,4 @@ def test_periodic_full_block(ctx, name, make):
     _times[name] = {"bytes": len(data), "seconds": round(dt, 4)}
     print("%s: %d bytes, %.1f ms" % (name, len(data), dt * 1e3))
     assert got == oracle_lib.bz2(data, 9), name
+    assert dt < 5.0, (name, dt)          # measured 0.09-0.6 s per block; catches a serial blow-up
