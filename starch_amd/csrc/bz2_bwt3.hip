@@ -811,6 +811,10 @@ __global__ void __launch_bounds__(256) k3_bin_scatter(const uint64_t* __restrict
 // ---------------------------------------------------------------------------
 constexpr int LT = 512;
 constexpr int LW = LT / 64;
+// round 0 / text rounds: the first pass keeps every element's digit in LDS,
+// so the scatter pass re-reads only the (coalesced) rotations, not their
+// PSS keys (random 8-byte loads); groups above PL_CAP recompute the keys
+constexpr uint32_t PL_CAP = 40960;
 
 template <bool DBL>
 __global__ void __launch_bounds__(LT) k3_part_l(Ctx c, const uint64_t* __restrict__ items)
@@ -822,6 +826,7 @@ __global__ void __launch_bounds__(LT) k3_part_l(Ctx c, const uint64_t* __restric
     __shared__ uint32_t qs[8];
     __shared__ uint32_t job_sh;
     __shared__ uint32_t cls_sh[16];
+    __shared__ uint8_t dcache[DBL ? 4 : PL_CAP];
     const int tid = threadIdx.x, wid = tid >> 6;
     const uint32_t x = xcc_id();
     load_qsizes_binned(c, qs);
@@ -857,6 +862,7 @@ __global__ void __launch_bounds__(LT) k3_part_l(Ctx c, const uint64_t* __restric
                 const uint32_t i = i0 + u * LT + tid;
                 const uint32_t ic = i < m ? i : 0u;
                 d[u] = (uint32_t)((elem_key<DBL>(ks, s + ic, sv[ic]) >> sh2) & dmask);
+                if (!DBL && m <= PL_CAP && i < m) dcache[i] = (uint8_t)d[u];
             }
 #pragma unroll
             for (int u = 0; u < PU; ++u)
@@ -876,7 +882,8 @@ __global__ void __launch_bounds__(LT) k3_part_l(Ctx c, const uint64_t* __restric
                 const uint32_t i = i0 + u * LT + tid;
                 const uint32_t ic = i < m ? i : 0u;
                 v[u] = sv[ic];
-                k[u] = elem_key<DBL>(ks, s + ic, v[u]);
+                if (!DBL && m <= PL_CAP) k[u] = (uint64_t)dcache[ic] << sh2;   // only the digit is used below
+                else k[u] = elem_key<DBL>(ks, s + ic, v[u]);
             }
 #pragma unroll
             for (int u = 0; u < PU; ++u) {

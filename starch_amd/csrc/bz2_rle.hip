@@ -392,17 +392,39 @@ __global__ void __launch_bounds__(64) k_cut(const StreamIn* __restrict__ streams
                 if (tend > end) tend = end;
                 const uint64_t y0 = tstart < bs ? bs : tstart;
                 const uint64_t W0 = tstart < bs ? wbs : tile_wpre[lo] - w0;
-                const uint64_t a = y0 + (uint64_t)lane * 64;
-                const uint64_t e = (a + 64 < tend) ? a + 64 : tend;
+                // each lane: one 64-byte aligned stretch of the tile's tpos, in
+                // registers (four 16-B loads); bytes outside [y0, tend) weigh 0
+                const uint64_t a = beg + ((y0 - beg) & ~63ull) + (uint64_t)lane * 64;
+                uint32_t tw[16];
+                {
+                    const uint4* p4 = reinterpret_cast<const uint4*>(tpos + a);
+                    const bool in = a < tend;
+#pragma unroll
+                    for (int k = 0; k < 4; ++k) {
+                        const uint4 v = in ? p4[k] : make_uint4(0, 0, 0, 0);
+                        tw[4 * k] = v.x; tw[4 * k + 1] = v.y; tw[4 * k + 2] = v.z; tw[4 * k + 3] = v.w;
+                    }
+                }
                 uint32_t ssum = 0;
-                for (uint64_t y = a; y < e; ++y) ssum += rle_w(tpos[y]);
+#pragma unroll
+                for (int k = 0; k < 64; ++k) {
+                    const uint64_t y = a + (uint64_t)k;
+                    if (y >= y0 && y < tend) ssum += rle_w((tw[k >> 2] >> (8 * (k & 3))) & 0xffu);
+                }
                 const uint32_t incl = wave_incl_scan_add(ssum);
                 const uint64_t ball = __ballot(a < tend && W0 + incl >= target);
                 if (ball) {
                     const int L = __ffsll((unsigned long long)ball) - 1;
-                    uint64_t x = a, Wx = W0 + incl - ssum;
-                    if (lane == L) {
-                        while (Wx < target) { Wx += rle_w(tpos[x]); ++x; }
+                    uint64_t x = a < y0 ? y0 : a, Wx = W0 + incl - ssum;
+                    if (lane == L) {               // the crossing byte, from the registers
+#pragma unroll
+                        for (int k = 0; k < 64; ++k) {
+                            const uint64_t y = a + (uint64_t)k;
+                            if (Wx < target) {
+                                if (y >= y0 && y < tend) Wx += rle_w((tw[k >> 2] >> (8 * (k & 3))) & 0xffu);
+                                x = y + 1;
+                            }
+                        }
                     }
                     q = __shfl(x, L, 64);
                     Wq = __shfl(Wx, L, 64);
