@@ -1019,13 +1019,22 @@ __global__ void __launch_bounds__(256) k3_sort_w(Ctx c, const uint64_t* __restri
             uint32_t ls;
             uint64_t k = elem_key<DBL>(c, ks, slot, s + j, v, ls);
             if (!valid) k = ~0ull;
-            // rank among the group's members (lanes gstart .. gstart + m - 1)
-            const uint32_t maxm = wave_reduce_max(valid ? m : 0u);
+            // rank among the group's members (lanes gstart .. gstart + m - 1):
+            // scalar broadcasts when the pass holds one group, lane shuffles otherwise
             uint32_t r = 0;
-            for (uint32_t q = 0; q < maxm; ++q) {
-                const bool in = valid && q < m;
-                const uint64_t kq = shfl64(k, in ? gstart + q : lane);
-                r += (in && (kq < k || (kq == k && q < j))) ? 1u : 0u;
+            if (ng == 1) {
+                for (uint32_t q = 0; q < total; ++q) {
+                    const uint64_t kq = ((uint64_t)(uint32_t)__builtin_amdgcn_readlane((int)(k >> 32), (int)q) << 32) |
+                                        (uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)k, (int)q);
+                    r += (kq < k || (kq == k && q < j)) ? 1u : 0u;
+                }
+            } else {
+                const uint32_t maxm = wave_reduce_max(valid ? m : 0u);
+                for (uint32_t q = 0; q < maxm; ++q) {
+                    const bool in = valid && q < m;
+                    const uint64_t kq = shfl64(k, in ? gstart + q : lane);
+                    r += (in && (kq < k || (kq == k && q < j))) ? 1u : 0u;
+                }
             }
             wave_sync_lds3();                            // the previous pass's reads are done
             if (valid) { skey[wid][gstart + r] = k; sval[wid][gstart + r] = v | (ls << 24); }
