@@ -961,11 +961,21 @@ __device__ __forceinline__ LineKey shfl_up_key(const LineKey& k)
 // output length, one block scan, output and segment records into LDS at
 // tile-relative offsets.  A line's predecessor comes by shuffle (wave
 // boundaries and chunk starts through LDS).  Returns (bytes, segments).
+// prev_ls < first_ls: the line before the tile's first one, [prev_ls, first_ls),
+// still to be parsed -- by the last thread, whose two line slots of the first
+// chunk are empty (nl <= 2 * kThreads - 2), while the others parse theirs.
 __device__ __forceinline__ void fused_lines(FusedShared& S, const uint8_t* tb, uint64_t a0, uint32_t nl,
                                             uint32_t first_ls, bool input_start, uint32_t* __restrict__ xflags,
-                                            uint64_t& bytes_out, uint32_t& segs_out)
+                                            uint64_t& bytes_out, uint32_t& segs_out, uint32_t prev_ls = 0,
+                                            bool parse_prev = false)
 {
     const uint32_t tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+    if (parse_prev && tid == kThreads - 1) {      // its slots 2*tid, 2*tid+1 are past nl
+        LineVals pr;
+        if (!parse_fast(tb, prev_ls, first_ls - prev_ls, a0 + prev_ls, pr))
+            pr = parse_line_at(LSrc{tb, a0}, a0 + prev_ls, a0 + first_ls);
+        S.wlast[0] = LineKey{pr.a, pr.b, prev_ls, pr.chr_len};   // read after the chunk's first barrier
+    }
     const LSrc lsrc{tb, a0};
     uint8_t* ob = reinterpret_cast<uint8_t*>(S.ob4);
     uint64_t run = 0;
@@ -1161,9 +1171,13 @@ k_tf_fused(const uint8_t* __restrict__ bed, uint64_t n, uint32_t* __restrict__ t
     } else {
         fallback = fallback || nl_tile > 0;        // first line longer than the halo
     }
+    // the previous line: parsed inside fused_lines by an idle thread when the
+    // tile's lines leave one free, else here by thread 0
+    const bool need_prev = !fallback && !input_start && nl_tile > 0;
+    const bool prev_in_lines = need_prev && nl_tile <= 2 * kThreads - 2;
     if (tid == 0) {
         LineKey pk{0, 0, 0, 0};
-        if (!fallback && !input_start && nl_tile > 0) {
+        if (need_prev && !prev_in_lines) {
             LineVals pr;
             const uint32_t ple = first_ls;         // one past the previous line's '\n'
             if (!parse_fast(tb, prev_ls, ple - prev_ls, a0 + prev_ls, pr))
@@ -1175,7 +1189,8 @@ k_tf_fused(const uint8_t* __restrict__ bed, uint64_t n, uint32_t* __restrict__ t
     __syncthreads();
     uint64_t bytes = 0;
     uint32_t segs = 0;
-    if (!fallback && nl_tile > 0) fused_lines(S, tb, a0, nl_tile, first_ls, input_start, xflags, bytes, segs);
+    if (!fallback && nl_tile > 0)
+        fused_lines(S, tb, a0, nl_tile, first_ls, input_start, xflags, bytes, segs, prev_ls, prev_in_lines);
     fallback = fallback || S.over;
     if (fallback && tid == 0) atomicOr(xflags, FX_FALLBACK);
     const TileAgg local{bytes, fallback ? 0ull : nl_tile, segs, ffpos != 0xFFFFFFFFu ? 1ull : 0ull};
