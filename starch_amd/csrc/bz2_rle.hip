@@ -247,36 +247,44 @@ __device__ __forceinline__ RunSum64 rs64_combine(const RunSum64& A, const RunSum
     return R;
 }
 
-__global__ void __launch_bounds__(256) k_rle_carry(const uint64_t* __restrict__ seg_tile0, uint32_t nstreams,
-                                                    const TileSum* __restrict__ sums, uint32_t* __restrict__ carry)
+// one 1024-thread workgroup per stream: each thread folds a run of tiles,
+// one workgroup scan of the run summaries, then each thread re-walks its run
+// (the run-summary combine is associative) -- two passes over the tile
+// summaries instead of a barrier-bound scan per 256 tiles
+constexpr int CT = 1024;
+__global__ void __launch_bounds__(CT) k_rle_carry(const uint64_t* __restrict__ seg_tile0, uint32_t nstreams,
+                                                   const TileSum* __restrict__ sums, uint32_t* __restrict__ carry)
 {
-    __shared__ RunSum64 sh[256];
+    __shared__ RunSum64 sh[CT];
     const uint32_t s = blockIdx.x;
     const int tid = threadIdx.x;
     const uint64_t t0 = seg_tile0[s], t1 = seg_tile0[s + 1];
-    RunSum64 acc;
-    acc.len = 0; acc.trail = 0; acc.first = acc.last = -1; acc.uni = 1; acc.pad = 0;
-    for (uint64_t c0 = t0; c0 < t1; c0 += 256) {
-        const uint64_t t = c0 + tid;
+    const uint64_t per = (t1 - t0 + CT - 1) / CT;
+    const uint64_t a = t0 + (uint64_t)tid * per, e = a + per < t1 ? a + per : t1;
+    auto load = [&](uint64_t t) {
+        const TileSum x = sums[t];
         RunSum64 S;
-        S.len = 0; S.trail = 0; S.first = S.last = -1; S.uni = 1; S.pad = 0;
-        if (t < t1) {
-            TileSum x = sums[t];
-            S.len = x.len; S.trail = x.trail; S.first = x.first; S.last = x.last; S.uni = x.uni;
-        }
-        sh[tid] = S;
+        S.len = x.len; S.trail = x.trail; S.first = x.first; S.last = x.last; S.uni = x.uni; S.pad = 0;
+        return S;
+    };
+    RunSum64 agg;
+    agg.len = 0; agg.trail = 0; agg.first = agg.last = -1; agg.uni = 1; agg.pad = 0;
+    for (uint64_t t = a; t < e; ++t) agg = rs64_combine(agg, load(t));
+    sh[tid] = agg;
+    __syncthreads();
+    for (int d = 1; d < CT; d <<= 1) {                  // inclusive scan of the run folds
+        const RunSum64 v = (tid >= d) ? rs64_combine(sh[tid - d], sh[tid]) : sh[tid];
         __syncthreads();
-        for (int d = 1; d < 256; d <<= 1) {
-            RunSum64 v = (tid >= d) ? rs64_combine(sh[tid - d], sh[tid]) : sh[tid];
-            __syncthreads();
-            sh[tid] = v;
-            __syncthreads();
-        }
-        RunSum64 P = tid ? rs64_combine(acc, sh[tid - 1]) : acc;
-        if (t < t1)
-            carry[t] = (t > t0 && P.len > 0 && P.last == S.first) ? (uint32_t)(P.trail % 255u) : 0u;
-        acc = rs64_combine(acc, sh[255]);
+        sh[tid] = v;
         __syncthreads();
+    }
+    RunSum64 P;
+    if (tid) P = sh[tid - 1];
+    else { P.len = 0; P.trail = 0; P.first = P.last = -1; P.uni = 1; P.pad = 0; }
+    for (uint64_t t = a; t < e; ++t) {
+        const RunSum64 S = load(t);
+        carry[t] = (t > t0 && P.len > 0 && P.last == S.first) ? (uint32_t)(P.trail % 255u) : 0u;
+        P = rs64_combine(P, S);
     }
 }
 
@@ -699,7 +707,7 @@ void rle_sum(const uint8_t* text, const TileDesc* tiles, uint64_t ntiles, TileSu
 }
 void rle_carry(const uint64_t* tile0, uint32_t ns, const TileSum* sums, uint32_t* carry, hipStream_t st)
 {
-    hipLaunchKernelGGL(k_rle_carry, dim3(ns), dim3(256), 0, st, tile0, ns, sums, carry);
+    hipLaunchKernelGGL(k_rle_carry, dim3(ns), dim3(CT), 0, st, tile0, ns, sums, carry);
 }
 void rle_pos(const uint8_t* text, const TileDesc* tiles, uint64_t ntiles, const uint32_t* carry, uint8_t* tpos,
              uint32_t* tile_w, hipStream_t st)
