@@ -86,7 +86,7 @@ constexpr uint32_t TEXT_ROUNDS = 4;     // max text-extension rounds before doub
 
 // counters (u32) in the meta buffer
 enum { C_W = 0, C_S, C_S2, C_M1, C_M2, C_M3, C_L0, C_L1, C_T0, C_T1, C_TIE_ELEMS, C_ERR, C_TS0, C_TS1, C_H, C_DBG2,
-       C_DBGL, C_M0, C_N = 24 };
+       C_DBGL, C_M0, C_STG, C_STA, C_STW, C_STE, C_STLP, C_STH, C_N = 24 };
 
 // item = slot[63:52] | start[51:32] | size[31:12] | parity[7] | shift[6:0]
 __device__ __forceinline__ uint64_t mk_item(uint32_t slot, uint32_t s, uint32_t m, uint32_t shift, uint32_t par)
@@ -965,6 +965,50 @@ __device__ __forceinline__ void emit_sorted(const Ctx& c, uint32_t slot, uint32_
     runs_acc += (uint32_t)__popcll(__ballot(valid && end));
 }
 
+// The values half of emit_sorted, for the kernels that reserve their tie-list
+// slots once per group (tie_reserve) instead of once per wave and row
+__device__ __forceinline__ void emit_vals(const Ctx& c, uint32_t slot, uint32_t s, uint32_t j, uint32_t v, bool valid,
+                                          uint32_t hp, uint32_t lsym)
+{
+    if (valid) {
+        const uint64_t so = (uint64_t)slot * c.scr.stride;
+        c.scr.SA[so + s + j] = v;
+        c.scr.LL[so + s + j] = (uint8_t)lsym;
+        if (c.mode) c.scr.RK[so + v] = s + hp;
+        if (v == 0) c.blocks[c.b0 + slot].orig_ptr = s + j;
+    }
+}
+
+// First tie-list slot for a group's tcnt tie runs (tcnt: this wave's count,
+// uniform per wave): one global atomic per group.  The tie-list counter is
+// one address shared by every wave of the launch; a returning atomic per wave
+// and row serialised there (text with many short repeats -- narrowPeak --
+// pushes millions of tie runs per batch).  NW > 1: every wave of the
+// workgroup (one group) calls it; tc/tb: NW + 1 words of LDS.
+template <int NW>
+__device__ __forceinline__ uint32_t tie_reserve(const Ctx& c, uint32_t tcnt, uint32_t* tc, int wid, int lane)
+{
+    uint32_t* ctr = c.L.ctr + C_T0 + c.tsel;
+    if constexpr (NW == 1) {
+        uint32_t base = 0;
+        if (lane == 0 && tcnt) base = atomicAdd(ctr, tcnt);
+        return (uint32_t)__shfl((int)base, 0, 64);
+    } else {
+        if (lane == 0) tc[wid] = tcnt;
+        __syncthreads();
+        if (wid == 0 && lane == 0) {
+            uint32_t t = 0;
+#pragma unroll
+            for (int w = 0; w < NW; ++w) t += tc[w];
+            tc[NW] = t ? atomicAdd(ctr, t) : 0u;
+        }
+        __syncthreads();
+        uint32_t base = tc[NW];
+        for (int w = 0; w < wid; ++w) base += tc[w];
+        return base;
+    }
+}
+
 // ---------------------------------------------------------------------------
 // k3_sort_w: groups of <= 64, packed several to a wave.  Each wave takes
 // chunks of 64 consecutive items of its XCD's segment (one item per lane,
@@ -1096,9 +1140,12 @@ struct GrpIn {                 // one group's inputs, as loaded
     KeySrc ks;
     uint32_t v[E];
     uint32_t v0;
-    uint64_t kx[E];
-    uint32_t ls[E];
+    uint64_t kx[E];            // keys (PSS rounds: the first raw key word until grp_finish_keys)
+    uint32_t ls[E];            // last-column symbols (PSS rounds: the first raw 32-bit window word)
     uint64_t k0;
+    uint64_t kb[E];            // PSS rounds: the second raw key word
+    uint32_t lb[E];            // ... and the second raw window word of the last-column symbol
+    uint64_t k0b;
 };
 
 // loads of a group that does not exist (ok false) go to element 0 of slot 0's
@@ -1118,16 +1165,67 @@ __device__ __forceinline__ void grp_load_vals(const Ctx& c, GrpIn<E>& x, bool ok
     x.v0 = sv[0];
 }
 
+// PSS rounds: the key of rotation r is stream bits [(r + off) * B, + kbits) and its
+// last-column symbol bits [(r - 1) * B, + B) (mod n).  grp_load_keys only issues
+// the loads (two u64 words for the key, two 32-bit words for the symbol, in the
+// stream's MSB-first order: the 32-bit word j of the stream sits at u32 index
+// j ^ 1 of the little-endian u64 words); grp_finish_keys combines them one group
+// later, so the random PSS reads overlap the current group's sort instead of
+// being waited on where they are issued.
+__device__ __forceinline__ uint32_t pss_rr(const KeySrc& ks, uint32_t r)
+{
+    const uint32_t rr = r + ks.off;
+    return rr >= ks.n ? rr - ks.n : rr;
+}
+__device__ __forceinline__ uint32_t pss_pr(const KeySrc& ks, uint32_t r) { return r ? r - 1u : ks.n - 1u; }
+
 template <int NW, int E, bool DBL>
 __device__ __forceinline__ void grp_load_keys(const Ctx& c, GrpIn<E>& x, int wid, int lane)
 {
     const uint32_t s = it_start(x.item), m = it_size(x.item), slot = it_slot(x.item);
+    if constexpr (DBL) {
 #pragma unroll
-    for (int e = 0; e < E; ++e) {
-        const uint32_t i = (uint32_t)(wid * 64 * E + e * 64 + lane);
-        x.kx[e] = elem_key<DBL>(c, x.ks, slot, s + (i < m ? i : 0u), x.v[e], x.ls[e]);
+        for (int e = 0; e < E; ++e) {
+            const uint32_t i = (uint32_t)(wid * 64 * E + e * 64 + lane);
+            x.kx[e] = elem_key<DBL>(c, x.ks, slot, s + (i < m ? i : 0u), x.v[e], x.ls[e]);
+        }
+        x.k0 = elem_key<DBL>(x.ks, s, x.v0);
+    } else {
+        const uint64_t* __restrict__ w = x.ks.pss;
+        const uint32_t* __restrict__ w32 = reinterpret_cast<const uint32_t*>(w);
+#pragma unroll
+        for (int e = 0; e < E; ++e) {
+            const uint64_t q = ((uint64_t)pss_rr(x.ks, x.v[e]) * x.ks.B) >> 6;
+            x.kx[e] = w[q];
+            x.kb[e] = w[q + 1];
+            const uint64_t j = ((uint64_t)pss_pr(x.ks, x.v[e]) * x.ks.B) >> 5;
+            x.ls[e] = w32[j ^ 1u];
+            x.lb[e] = w32[(j + 1u) ^ 1u];
+        }
+        const uint64_t q0 = ((uint64_t)pss_rr(x.ks, x.v0) * x.ks.B) >> 6;
+        x.k0 = w[q0];
+        x.k0b = w[q0 + 1];
     }
-    x.k0 = elem_key<DBL>(x.ks, s, x.v0);
+}
+
+template <int E, bool DBL>
+__device__ __forceinline__ void grp_finish_keys(GrpIn<E>& x)
+{
+    if constexpr (!DBL) {
+        const KeySrc& ks = x.ks;
+#pragma unroll
+        for (int e = 0; e < E; ++e) {
+            const uint32_t p = (uint32_t)(((uint64_t)pss_rr(ks, x.v[e]) * ks.B) & 63u);
+            const uint64_t v = (x.kx[e] << p) | ((x.kb[e] >> 1) >> (63u - p));
+            x.kx[e] = v >> (64u - ks.kbits);
+            const uint32_t pl = (uint32_t)(((uint64_t)pss_pr(ks, x.v[e]) * ks.B) & 31u);
+            const uint64_t lw = ((uint64_t)x.ls[e] << 32) | x.lb[e];
+            x.ls[e] = (uint32_t)((lw << pl) >> (64u - ks.B));
+        }
+        const uint32_t p0 = (uint32_t)(((uint64_t)pss_rr(ks, x.v0) * ks.B) & 63u);
+        const uint64_t v0 = (x.k0 << p0) | ((x.k0b >> 1) >> (63u - p0));
+        x.k0 = v0 >> (64u - ks.kbits);
+    }
 }
 
 // register budget (waves per SIMD) of the sort kernels: keeps a few groups
@@ -1173,6 +1271,8 @@ k3_sort_lds(Ctx c, const uint64_t* __restrict__ items,
     __shared__ uint64_t red_all[4];
     __shared__ uint32_t wmax_all[4];
     __shared__ uint32_t flag_all[4];
+    __shared__ uint32_t tc_all[5];
+    uint32_t tacc = 0;                             // tied elements pushed (flushed at exit)
     const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
     const int g = wave / NW, wid = wave % NW, w0 = g * NW;
     uint64_t* xk = xk_all[g];
@@ -1225,6 +1325,7 @@ k3_sort_lds(Ctx c, const uint64_t* __restrict__ items,
     while (it != NONE) {
     const uint64_t item = cur.item;
     const uint32_t slot = it_slot(item), s = it_start(item), m = it_size(item);
+    grp_finish_keys<E, DBL>(cur);
     gsync<NW>();                                   // the previous group's LDS reads are done
 
     uint64_t k[E];
@@ -1326,7 +1427,13 @@ k3_sort_lds(Ctx c, const uint64_t* __restrict__ items,
                 const uint32_t d = (uint32_t)((kj >> (lo + IDXB)) & (uint64_t)(NBIN - 1));
                 rs = bst[d];
                 re = bst[d + 1];
+#ifdef STARCH_SORT_STATS
+                atomicAdd(&c.L.ctr[C_STW], re - rs);
+#endif
             });
+#ifdef STARCH_SORT_STATS
+            if (tid % (64 * NW) == 0) atomicAdd(&c.L.ctr[C_STA], 1u);
+#endif
             moved = true;
         } else if (lo > 0) {
             // Second MSD digit for the sub-buckets larger than LIMIT: the w2 bits
@@ -1348,7 +1455,10 @@ k3_sort_lds(Ctx c, const uint64_t* __restrict__ items,
                 nbig = (uint32_t)__builtin_amdgcn_readlane((int)binc, 63);
             }
             uint32_t w2 = 0;
-            while (w2 < 6 && (nbig << (w2 + 1)) <= (uint32_t)NB2) ++w2;
+#ifndef STARCH_W2_MAX
+#define STARCH_W2_MAX 6
+#endif
+            while (w2 < STARCH_W2_MAX && (nbig << (w2 + 1)) <= (uint32_t)NB2) ++w2;
             if (w2 > (uint32_t)lo) w2 = (uint32_t)lo;
             const int lo2 = lo - (int)w2;
             const uint32_t nb2 = nbig << w2;
@@ -1442,6 +1552,9 @@ k3_sort_lds(Ctx c, const uint64_t* __restrict__ items,
         }
     }
     if (!moved && kdiff && tid % (64 * NW) == 0) atomicAdd(&c.L.ctr[C_DBGL], 1u);
+#ifdef STARCH_SORT_STATS
+    if (tid % (64 * NW) == 0) { atomicAdd(&c.L.ctr[C_STG], 1u); atomicAdd(&c.L.ctr[C_STE], m); }
+#endif
     bool lsd_moved = false;
     for (int dbit = 0; dbit < KEYB && !moved; dbit += 8) {
         if ((kdiff >> dbit & 0xffull) == 0) continue;    // uniform per group
@@ -1504,6 +1617,9 @@ k3_sort_lds(Ctx c, const uint64_t* __restrict__ items,
 #pragma unroll
         for (int e = 0; e < E; ++e) k[e] = xk[wid * 64 * E + e * 64 + lane];
         lsd_moved = true;
+#ifdef STARCH_SORT_STATS
+        if (tid % (64 * NW) == 0) atomicAdd(&c.L.ctr[C_STLP], 1u);
+#endif
     }
     moved |= lsd_moved;
     if (!moved) {
@@ -1552,16 +1668,32 @@ k3_sort_lds(Ctx c, const uint64_t* __restrict__ items,
     // the group's rotations and keys were consumed into registers/LDS (their
     // loads complete) before any write of its SA range; the loads in flight
     // now belong to other groups' disjoint ranges
-    uint32_t runs = 0;
+    uint32_t runs = 0, tcnt = 0;
+    uint64_t tm[E];
 #pragma unroll
     for (int e = 0; e < E; ++e) {
         const uint32_t j = (uint32_t)(wid * 64 * E + e * 64 + lane);
         const bool valid = j < m;
         const uint32_t vb = valid ? vb_all[g][(uint32_t)(k[e] & ((1u << IDXB) - 1u))] : 0u;
         const bool end = valid && (!ties || j + 1 == m || ((xk[j + 1] ^ k[e]) >> IDXB) != 0);
-        emit_sorted(c, slot, s, j, vb & 0xFFFFFFu, valid, hp[e], end, runs, vb >> 24);
+        emit_vals(c, slot, s, j, vb & 0xFFFFFFu, valid, hp[e], vb >> 24);
+        const bool tie = end && j > hp[e];
+        tm[e] = __ballot(tie);
+        tcnt += (uint32_t)__popcll(tm[e]);
+        tacc += tie ? j - hp[e] + 1u : 0u;
+        runs += (uint32_t)__popcll(__ballot(end));
     }
     if (c.mode && lane == 0 && runs) atomicAdd(&c.L.runs[slot], runs);
+    if (ties) {                                    // uniform per group
+        uint32_t tb = tie_reserve<NW>(c, tcnt, tc_all, wid, lane);
+        uint64_t* tl = c.L.t[c.tsel];
+#pragma unroll
+        for (int e = 0; e < E; ++e) {
+            const uint32_t j = (uint32_t)(wid * 64 * E + e * 64 + lane);
+            if ((tm[e] >> lane) & 1ull) tl[tb + (uint32_t)__popcll(tm[e] & lt)] = mk_item(slot, s + hp[e], j - hp[e] + 1u, 0, 0);
+            tb += (uint32_t)__popcll(tm[e]);
+        }
+    }
     // rotate the pipeline
     const uint32_t it2 = it1 != NONE ? next_item() : NONE;
     cur = nxt;
@@ -1570,6 +1702,8 @@ k3_sort_lds(Ctx c, const uint64_t* __restrict__ items,
     it = it1;
     it1 = it2;
     }
+    tacc = wave_reduce_add<uint32_t>(tacc);
+    if (lane == 0 && tacc) atomicAdd(c.L.ctr + C_TS0 + c.tsel, tacc);
 }
 
 // ---------------------------------------------------------------------------
@@ -1612,6 +1746,9 @@ k3_sort_grp(Ctx c, const uint64_t* __restrict__ items,
     __shared__ uint32_t wsq_all[4];
     __shared__ uint32_t wmax_all[4];
     __shared__ uint32_t flag_all[4];
+    __shared__ uint32_t tc_all[5];
+    uint32_t tacc = 0;                             // tied elements pushed (flushed at exit)
+    const uint64_t lt = lanemask_lt();
     const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
     const int g = wave / NW, wid = wave % NW, w0 = g * NW;
     uint64_t* xk = xk_all[g];
@@ -1645,6 +1782,7 @@ k3_sort_grp(Ctx c, const uint64_t* __restrict__ items,
     while (it != NONE) {
     const uint64_t item = cur.item;
     const uint32_t slot = it_slot(item), s = it_start(item), m = it_size(item);
+    grp_finish_keys<E, DBL>(cur);
     gsync<NW>();                                   // the previous group's LDS reads are done
 
     uint64_t k[E];
@@ -1703,6 +1841,9 @@ k3_sort_grp(Ctx c, const uint64_t* __restrict__ items,
             for (int w = 0; w < NW; ++w) sq += wsq_all[w0 + w];
         }
         is_hard = sq > HARD_Q * m;                 // uniform per group
+#ifdef STARCH_SORT_STATS
+        if (tg == 0) { atomicAdd(&c.L.ctr[C_STG], 1u); atomicAdd(&c.L.ctr[C_STE], m); if (is_hard) atomicAdd(&c.L.ctr[C_STH], 1u); }
+#endif
         if (!is_hard) {
 #pragma unroll
             for (int q = 0; q < BPT; ++q) { bst[tg * BPT + q] = run; bcur[tg * BPT + q] = run; run += loc[q]; }
@@ -1724,6 +1865,9 @@ k3_sort_grp(Ctx c, const uint64_t* __restrict__ items,
                     const uint32_t d = (uint32_t)((kj >> (lo + IDXB)) & (uint64_t)(NBIN - 1));
                     const uint32_t bs = bst[d], be = bst[d + 1];
                     pos[e] = bs + rank_in(xk, bs, be, kj);
+#ifdef STARCH_SORT_STATS
+                    atomicAdd(&c.L.ctr[C_STW], be - bs);
+#endif
                     k[e] = kj;
                 }
             }
@@ -1785,16 +1929,32 @@ k3_sort_grp(Ctx c, const uint64_t* __restrict__ items,
         }
     }
     // the group's SA range was read (values consumed above) before any write
-    uint32_t runs = 0;
+    uint32_t runs = 0, tcnt = 0;
+    uint64_t tm[E];
 #pragma unroll
     for (int e = 0; e < E; ++e) {
         const uint32_t j = (uint32_t)(wid * 64 * E + e * 64 + lane);
         const bool valid = j < m;
         const uint32_t vb = valid ? vb_all[g][(uint32_t)(k[e] & ((1u << IDXB) - 1u))] : 0u;
         const bool end = valid && (!ties || j + 1 == m || ((xk[j + 1] ^ k[e]) >> IDXB) != 0);
-        emit_sorted(c, slot, s, j, vb & 0xFFFFFFu, valid, hp[e], end, runs, vb >> 24);
+        emit_vals(c, slot, s, j, vb & 0xFFFFFFu, valid, hp[e], vb >> 24);
+        const bool tie = end && j > hp[e];
+        tm[e] = __ballot(tie);
+        tcnt += (uint32_t)__popcll(tm[e]);
+        tacc += tie ? j - hp[e] + 1u : 0u;
+        runs += (uint32_t)__popcll(__ballot(end));
     }
     if (c.mode && lane == 0 && runs) atomicAdd(&c.L.runs[slot], runs);
+    if (ties) {                                    // uniform per group
+        uint32_t tb = tie_reserve<NW>(c, tcnt, tc_all, wid, lane);
+        uint64_t* tl = c.L.t[c.tsel];
+#pragma unroll
+        for (int e = 0; e < E; ++e) {
+            const uint32_t j = (uint32_t)(wid * 64 * E + e * 64 + lane);
+            if ((tm[e] >> lane) & 1ull) tl[tb + (uint32_t)__popcll(tm[e] & lt)] = mk_item(slot, s + hp[e], j - hp[e] + 1u, 0, 0);
+            tb += (uint32_t)__popcll(tm[e]);
+        }
+    }
     }
     // rotate the pipeline: next group's rotations, the one after it
     cur = nxt;
@@ -1805,6 +1965,8 @@ k3_sort_grp(Ctx c, const uint64_t* __restrict__ items,
     it1 = it2;
     it2 = it3;
     }
+    tacc = wave_reduce_add<uint32_t>(tacc);
+    if (lane == 0 && tacc) atomicAdd(c.L.ctr + C_TS0 + c.tsel, tacc);
 }
 
 // ---------------------------------------------------------------------------
@@ -2107,6 +2269,19 @@ void launch_bwt3(BlockDesc* blocks, uint32_t b0, uint32_t nb, const uint8_t* blk
         // Doubling rounds (keys in K/K2) run their own instantiations.
         const uint32_t* hard_n = c.L.ctr + C_H;
         auto clear_h = [&]() { HIP_CHECK(hipMemsetAsync(c.L.ctr + C_H, 0, sizeof(uint32_t), st)); };
+        auto sstat = [&](const char* name) {
+#ifdef STARCH_SORT_STATS
+            HIP_CHECK(hipMemcpyAsync(hctr, c.L.ctr, C_N * sizeof(uint32_t), hipMemcpyDeviceToHost, st));
+            HIP_CHECK(hipStreamSynchronize(st));
+            fprintf(stderr, "[sort] r%u m%u %-8s groups %u elems %u pathA %u rankwork %u lsdpasses %u hard %u lvl2 %u lsdg %u\n",
+                    c.rtext, c.mode, name, hctr[C_STG], hctr[C_STE], hctr[C_STA], hctr[C_STW], hctr[C_STLP], hctr[C_STH],
+                    hctr[C_DBG2], hctr[C_DBGL]);
+            HIP_CHECK(hipMemsetAsync(c.L.ctr + C_DBG2, 0, 2 * sizeof(uint32_t), st));
+            HIP_CHECK(hipMemsetAsync(c.L.ctr + C_STG, 0, 6 * sizeof(uint32_t), st));
+#else
+            (void)name;
+#endif
+        };
         auto leaf = [&](auto dbl) {
             constexpr bool D = decltype(dbl)::value;
             static const dim3 gm3 = resident(reinterpret_cast<const void*>(&k3_sort_lds<4, 16, D>));
@@ -2119,34 +2294,50 @@ void launch_bwt3(BlockDesc* blocks, uint32_t b0, uint32_t nb, const uint8_t* blk
             if (n3) {
                 bin(c.L.m3, n3, bout);
                 hipLaunchKernelGGL((k3_sort_lds<4, 16, D>), gm3, dim3(256), 0, st, c, bout, nullptr);
+                sstat("M3");
             }
             if (n2) {
                 bin(c.L.m2, n2, bout);
                 hipLaunchKernelGGL((k3_sort_lds<4, 8, D>), gm2, dim3(256), 0, st, c, bout, nullptr);
+                sstat("M2");
             }
             if (n0) {
                 bin(c.L.m0, n0, bout);
+#ifdef STARCH_M0_1W
+                static const dim3 gm0w = resident(reinterpret_cast<const void*>(&k3_sort_grp<1, 8, D>));
+                clear_h();
+                hipLaunchKernelGGL((k3_sort_grp<1, 8, D>), gm0w, dim3(256), 0, st, c, bout, c.L.m0);
+                hipLaunchKernelGGL((k3_sort_lds<1, 8, D>), dim3(ncu / 2), dim3(256), 0, st, c, c.L.m0, hard_n);
+#else
                 hipLaunchKernelGGL((k3_sort_lds<4, 2, D>), gm0, dim3(256), 0, st, c, bout, nullptr);
+#endif
+                sstat("M0");
             }
             if (n1) {
                 bin(c.L.m1, n1, bout);
                 hipLaunchKernelGGL((k3_sort_lds<4, 4, D>), gm1, dim3(256), 0, st, c, bout, nullptr);
+                sstat("M1");
             }
             if (ns) {
                 bin(c.L.s, ns, bout);
                 clear_h();
                 hipLaunchKernelGGL((k3_sort_grp<1, 2, D>), gs, dim3(256), 0, st, c, bout, c.L.s);
+                sstat("S");
                 hipLaunchKernelGGL((k3_sort_lds<1, 2, D>), dim3(ncu / 2), dim3(256), 0, st, c, c.L.s, hard_n);
+                sstat("S-hard");
             }
             if (ns2) {
                 bin(c.L.s2, ns2, bout);
                 clear_h();
                 hipLaunchKernelGGL((k3_sort_grp<1, 4, D>), gs2, dim3(256), 0, st, c, bout, c.L.s2);
+                sstat("S2");
                 hipLaunchKernelGGL((k3_sort_lds<1, 4, D>), dim3(ncu / 2), dim3(256), 0, st, c, c.L.s2, hard_n);
+                sstat("S2-hard");
             }
             if (nw) {
                 bin(c.L.w, nw, bout);
                 hipLaunchKernelGGL(k3_sort_w<D>, gw, dim3(256), 0, st, c, bout);
+                sstat("W");
             }
         };
         if (c.keysrc) leaf(std::true_type{});

@@ -239,7 +239,10 @@ void Encoder::plan(const uint8_t* d_text, const std::vector<StreamIn>& streams, 
     HIP_CHECK(hipMemGetInfo(&free_b, &total_b));
     const uint64_t per_slot = blk_stride_ * 41ull;       // 40 B of sort scratch + 1 B last column
     uint64_t max_batch = std::max<uint64_t>(1, (uint64_t)(free_b * 0.45) / per_slot);
-    uint32_t batch = (uint32_t)std::min<uint64_t>({(uint64_t)nr, max_batch, 2048ull});
+#ifndef STARCH_BATCH_MAX
+#define STARCH_BATCH_MAX 2048
+#endif
+    uint32_t batch = (uint32_t)std::min<uint64_t>({(uint64_t)nr, max_batch, (uint64_t)STARCH_BATCH_MAX});
     // STARCH_BWT_BATCH=k caps the batch (tests: exercises batches after the first)
     static const uint64_t batch_cap = [] { const char* e = getenv("STARCH_BWT_BATCH"); return e ? (uint64_t)atoll(e) : 0ull; }();
     if (batch_cap) batch = (uint32_t)std::min<uint64_t>(batch, batch_cap);
