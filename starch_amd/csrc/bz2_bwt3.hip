@@ -1179,11 +1179,17 @@ __device__ __forceinline__ uint32_t pss_rr(const KeySrc& ks, uint32_t r)
 }
 __device__ __forceinline__ uint32_t pss_pr(const KeySrc& ks, uint32_t r) { return r ? r - 1u : ks.n - 1u; }
 
+#ifndef STARCH_DEFER
+#define STARCH_DEFER 1     // deferred key combination: 0 never, 1 one-wave sorts only (measured best), 2 all
+#endif
+template <int NW, bool DBL>
+constexpr bool defer_keys() { return !DBL && (STARCH_DEFER == 2 || (STARCH_DEFER == 1 && NW == 1)); }
+
 template <int NW, int E, bool DBL>
 __device__ __forceinline__ void grp_load_keys(const Ctx& c, GrpIn<E>& x, int wid, int lane)
 {
     const uint32_t s = it_start(x.item), m = it_size(x.item), slot = it_slot(x.item);
-    if constexpr (DBL) {
+    if constexpr (!defer_keys<NW, DBL>()) {
 #pragma unroll
         for (int e = 0; e < E; ++e) {
             const uint32_t i = (uint32_t)(wid * 64 * E + e * 64 + lane);
@@ -1208,10 +1214,10 @@ __device__ __forceinline__ void grp_load_keys(const Ctx& c, GrpIn<E>& x, int wid
     }
 }
 
-template <int E, bool DBL>
+template <int NW, int E, bool DBL>
 __device__ __forceinline__ void grp_finish_keys(GrpIn<E>& x)
 {
-    if constexpr (!DBL) {
+    if constexpr (defer_keys<NW, DBL>()) {
         const KeySrc& ks = x.ks;
 #pragma unroll
         for (int e = 0; e < E; ++e) {
@@ -1325,7 +1331,7 @@ k3_sort_lds(Ctx c, const uint64_t* __restrict__ items,
     while (it != NONE) {
     const uint64_t item = cur.item;
     const uint32_t slot = it_slot(item), s = it_start(item), m = it_size(item);
-    grp_finish_keys<E, DBL>(cur);
+    grp_finish_keys<NW, E, DBL>(cur);
     gsync<NW>();                                   // the previous group's LDS reads are done
 
     uint64_t k[E];
@@ -1782,7 +1788,7 @@ k3_sort_grp(Ctx c, const uint64_t* __restrict__ items,
     while (it != NONE) {
     const uint64_t item = cur.item;
     const uint32_t slot = it_slot(item), s = it_start(item), m = it_size(item);
-    grp_finish_keys<E, DBL>(cur);
+    grp_finish_keys<NW, E, DBL>(cur);
     gsync<NW>();                                   // the previous group's LDS reads are done
 
     uint64_t k[E];
