@@ -17,16 +17,31 @@
  * consume_tf_buffer, hpp:158-391) are replaced by compress_in_stream(): the
  * whole input goes to the GPU(s) at once -- transform, per-chromosome bzip2
  * -9 streams, archive -- and everything after the magic is written to the out
- * stream.  The per-chromosome hand-off process_tf_buffer (hpp:393-407) keeps
- * its role as a hook: given one chromosome's transformed text it compresses
- * it on the GPU into that chromosome's stream; finish_tf_buffers() then writes
- * the collected streams and the index.
+ * stream.
+ *
+ * The per-chromosome hand-off keeps the reference's shape: the types bed_t,
+ * transform_state_t and shared_buffer_t (hpp:37-88), the bz_stream lifecycle
+ * initialize_bz_stream_ptr / setup_bz_stream_callbacks / delete_bz_stream_ptr
+ * and the block-close callbacks (hpp:126-129, 819-888), and
+ *   static void process_tf_buffer(shared_buffer_t* sb)      (hpp:393-407)
+ * which here FEEDS the patched-libbz2 ABI (include/starch_bzlib.h, on the
+ * GPU): sb->tf_buffer[0, tf_buffer_size) goes through BZ2_bzCompress(BZ_FINISH)
+ * of starch3::self's bz_stream, the stream is written to the out stream, and
+ * the stream's block_close_functor (bz:bzlib.c:470) records the chromosome
+ * (tf_state->current_chr, ->line_count) for the index; then, as in the
+ * reference, the transformation state and tf_buffer are reset.  One bzip2
+ * stream per chromosome: the bz_stream is re-initialised after each.
+ * transform_and_flush_in_stream() drives it like consume_tf_buffer would
+ * (GPU transform, one process_tf_buffer per chromosome); finish_tf_buffers()
+ * writes the index.  As in the reference (cpp:10, hpp:921) the program defines
+ * `starch3::Starch* starch3::self` and points it at its Starch.
  *
  * Link with -lstarch_amd.  Compiles as C++11.
  */
 #ifndef STARCH3_AMD_HPP_
 #define STARCH3_AMD_HPP_
 
+#include <pthread.h>
 #include <sys/stat.h>
 #include <unistd.h>
 
@@ -39,6 +54,7 @@
 #include <vector>
 
 #include "starch_amd.h"
+#include "starch_bzlib.h"
 
 namespace starch3
 {
@@ -51,16 +67,147 @@ public:
         k_compression_method_undefined
     } compression_method_t;
 
+    // ---- the reference's pipeline types (hpp:37-88), same fields ---------------
+    typedef struct bed {
+        char* chr;
+        size_t chr_capacity;
+        char* start_str;
+        size_t start_str_capacity;
+        int64_t start;
+        char* stop_str;
+        size_t stop_str_capacity;
+        int64_t stop;
+        char* rem;
+        size_t rem_capacity;
+        int token;
+    } bed_t;
+
+    typedef struct transform_state {
+        int64_t line_count;
+        char* last_chr;
+        int64_t last_start;
+        int64_t last_stop;
+        int64_t last_coord_diff;
+        char* current_chr;
+        int64_t current_start;
+        int64_t current_stop;
+        int64_t current_coord_diff;
+        int64_t base_count_unique;
+        int64_t base_count_nonunique;
+    } transform_state_t;
+
+    typedef struct shared_buffer {
+        pthread_mutex_t lock;
+        pthread_cond_t new_line_is_available;
+        pthread_cond_t new_line_is_empty;
+        pthread_cond_t new_chromosome_is_available;
+        pthread_cond_t new_tf_buffer_is_available;
+        char* in_line;
+        size_t in_line_capacity;
+        int next_in;
+        int next_out;
+        bool is_new_line_available;
+        bool is_new_chromosome_available;
+        bool is_new_tf_buffer_available;
+        bool is_eof;
+        FILE* in_stream;
+        bed_t* bed;
+        transform_state_t* tf_state;
+        char* tf_line;
+        size_t tf_line_capacity;
+        char* tf_buffer;
+        size_t tf_buffer_capacity;
+        size_t tf_buffer_size;
+    } shared_buffer_t;
+
+    static const int tf_buffer_initial_length = 1024;   // hpp:152
+
+    shared_buffer_t buffer;
+
     Starch()
-        : _in_stream(NULL), _out_stream(NULL), _block_size(9), _reference_compat(false), _emit_index(true),
-          _base_counts(false)
+        : _bz_stream_ptr(NULL), _bz_stream_used(false), _in_stream(NULL), _out_stream(NULL), _block_size(9),
+          _reference_compat(false), _emit_index(true), _base_counts(false), _stream_end(4)
     {
         set_note(std::string());
         set_compression_method(k_compression_method_undefined);   // hpp:912-916
         initialize_header_magic_bytes();
         _devices.push_back(0);
+        std::memset(&buffer, 0, sizeof(buffer));
+        std::memset(&_tf_state, 0, sizeof(_tf_state));
+        buffer.tf_state = &_tf_state;
     }
-    ~Starch() { delete_out_compression_stream(); }
+    ~Starch()
+    {
+        delete_bz_stream_ptr();
+        delete_out_compression_stream();
+        std::free(buffer.tf_buffer);
+        std::free(_tf_state.current_chr);
+        std::free(_tf_state.last_chr);
+    }
+
+    // ---- the bz_stream lifecycle (hpp:819-888) over the GPU-backed ABI ---------
+    void initialize_bz_stream_ptr(void)
+    {
+        _bz_stream_ptr = new bz_stream;
+        std::memset(_bz_stream_ptr, 0, sizeof(*_bz_stream_ptr));
+        _bz_stream_ptr->bzalloc = NULL;
+        _bz_stream_ptr->bzfree = NULL;
+        _bz_stream_ptr->opaque = NULL;
+        switch (BZ2_bzCompressInit(_bz_stream_ptr, _block_size, 0, 30)) {   // hpp:835-837
+        case BZ_CONFIG_ERROR:
+            std::fprintf(stderr, "Error: bzip2 initialization failed - library was miscompiled\n");
+            std::exit(EINVAL);
+        case BZ_PARAM_ERROR:
+            std::fprintf(stderr, "Error: bzip2 initialization failed - incorrect parameters\n");
+            std::exit(EINVAL);
+        case BZ_MEM_ERROR:
+            std::fprintf(stderr, "Error: bzip2 initialization failed - insufficient memory\n");
+            std::exit(EINVAL);
+        default:
+            break;
+        }
+        _bz_stream_used = false;
+    }
+    // the reference installs &h, the address of its by-value parameter
+    // (hpp:860, dangling); the handler here is the instance itself
+    void setup_bz_stream_callbacks(starch3::Starch* h)
+    {
+        if (!_bz_stream_ptr) return;
+        _bz_stream_ptr->handler = h;
+        _bz_stream_ptr->block_close_functor = bzip2_block_close_static_callback;
+    }
+    void delete_bz_stream_ptr(void)
+    {
+        if (!_bz_stream_ptr) return;
+        if (BZ2_bzCompressEnd(_bz_stream_ptr) == BZ_PARAM_ERROR) {   // hpp:868-872
+            std::fprintf(stderr, "Error: Could not release internals of bz_stream pointer\n");
+            std::exit(EINVAL);
+        }
+        delete _bz_stream_ptr;
+        _bz_stream_ptr = NULL;
+    }
+    static void bzip2_block_close_static_callback(void* s)   // hpp:882-884
+    {
+        reinterpret_cast<starch3::Starch*>(s)->bzip2_block_close_callback();
+    }
+    // BZ_STREAM_END of a chromosome's stream: its index entry
+    void bzip2_block_close_callback(void)
+    {
+        starch_segment sg;
+        std::memset(&sg, 0, sizeof(sg));
+        unsigned nb = 0, crc = 0;
+        starch_bzstream_info(_bz_stream_ptr, &nb, &crc);
+        sg.line_count = (uint64_t)_closing_lines;
+        sg.text_bytes = _closing_text;
+        sg.stream_offset = _stream_end;
+        sg.stream_bytes = (uint64_t)_bz_stream_ptr->total_out_hi32 << 32 | _bz_stream_ptr->total_out_lo32;
+        sg.name_len = _closing_chr.size();
+        sg.n_blocks = nb;
+        sg.combined_crc = crc;
+        sg.unit = _closed.size();
+        _stream_end += sg.stream_bytes;
+        _closed.push_back(Closed(_closing_chr, sg));
+    }
 
     // ---- I/O (hpp:724-769) ------------------------------------------------
     FILE* get_in_stream(void) { return _in_stream; }
@@ -181,76 +328,103 @@ public:
         return STARCH_OK;
     }
 
-    // The per-chromosome hand-off (hpp:393-407): one chromosome's transformed
-    // text -> its bzip2 -N stream, compressed on the GPU and kept for
-    // finish_tf_buffers().
-    int process_tf_buffer(const std::string& chr, int64_t line_count, const char* tf_buffer, size_t tf_buffer_size)
+    // The per-chromosome hand-off (hpp:393-407), static as in the reference:
+    // the chromosome's transformed text goes through starch3::self's bz_stream
+    // (BZ2_bzCompress with BZ_FINISH, on the GPU), its stream to the out stream;
+    // the block-close callback records the index entry.  Then the
+    // transformation state and tf_buffer are reset as in the reference.
+    static void process_tf_buffer(shared_buffer_t* sb);
+
+    // consume_tf_buffer's loop (hpp:371-391) over the GPU transform: the in
+    // stream is transformed on the GPU and every chromosome segment handed to
+    // process_tf_buffer in input order.
+    int transform_and_flush_in_stream(void)
     {
+        std::vector<unsigned char> in, buf(1 << 24);
+        size_t k;
+        while ((k = std::fread(&buf[0], 1, buf.size(), _in_stream)) > 0) in.insert(in.end(), buf.begin(), buf.begin() + k);
         int rc = open_devices();
         if (rc) return rc;
-        std::vector<unsigned char> st(tf_buffer_size + tf_buffer_size / 50 + 4096);
-        uint64_t len = 0;
-        rc = starch_bz2_compress_host(_ctx[0], tf_buffer, tf_buffer_size, _block_size, &st[0], st.size(), &len);
-        if (rc) return rc;
-        st.resize(len);
-        starch_segment s;
-        std::memset(&s, 0, sizeof(s));
-        s.line_count = (uint64_t)line_count;
-        s.text_bytes = tf_buffer_size;
-        s.stream_bytes = len;
-        s.name_len = chr.size();
-        s.unit = _pending.size();
-        uint32_t nb = 0, crc = 0;
-        if ((rc = starch_bz2_stream_info(_ctx[0], &nb, &crc))) return rc;
-        s.n_blocks = nb;
-        s.combined_crc = crc;
-        _pending.push_back(Pending(chr, s, st));
+        starch_ctx* c = _ctx[0];
+        if ((rc = starch_transform_host(c, in.empty() ? NULL : &in[0], in.size()))) return rc;
+        uint64_t nseg = 0, tb = 0;
+        if ((rc = starch_segment_count(c, &nseg)) || (rc = starch_text_size(c, &tb))) return rc;
+        std::vector<char> text(tb + 1);
+        std::vector<starch_segment> segs(nseg + 1);
+        if ((rc = starch_text_copy(c, &text[0], tb)) || (rc = starch_segments(c, &segs[0], nseg))) return rc;
+        for (uint64_t s = 0; s < nseg; ++s) {
+            std::string name(segs[s].name_len, '\0');
+            uint64_t len = 0;
+            if ((rc = starch_segment_name(c, s, name.empty() ? NULL : &name[0], name.size(), &len))) return rc;
+            // the state consume_line leaves for the flush: current_chr, line_count, tf_buffer
+            std::free(_tf_state.current_chr);
+            _tf_state.current_chr = static_cast<char*>(std::malloc(name.size() + 1));
+            std::memcpy(_tf_state.current_chr, name.data(), name.size());
+            _tf_state.current_chr[name.size()] = '\0';
+            _tf_state.line_count = (int64_t)segs[s].line_count;
+            std::free(buffer.tf_buffer);
+            buffer.tf_buffer_capacity = segs[s].text_bytes + 1;
+            buffer.tf_buffer = static_cast<char*>(std::malloc(buffer.tf_buffer_capacity));
+            // transform-only results carry the text offset in stream_offset
+            std::memcpy(buffer.tf_buffer, &text[segs[s].stream_offset], segs[s].text_bytes);
+            buffer.tf_buffer_size = segs[s].text_bytes;
+            _closing_name_len = name.size();
+            process_tf_buffer(&buffer);
+            if (_hook_error) return STARCH_ERR_INTERNAL;
+        }
         return STARCH_OK;
     }
 
-    // Write the streams collected by process_tf_buffer, then the index, to the
-    // out stream (after the magic initialize_out_stream wrote).
+    // Write the index of the streams process_tf_buffer wrote (after the magic
+    // initialize_out_stream wrote and the streams themselves).
     int finish_tf_buffers(void)
     {
-        uint64_t off = 4;
-        std::vector<starch_segment> segs;
-        std::vector<const char*> names;
-        std::vector<uint64_t> lens;
-        for (size_t i = 0; i < _pending.size(); ++i) {
-            _pending[i].seg.stream_offset = off;
-            off += _pending[i].stream.size();
-            if (!_pending[i].stream.empty())
-                std::fwrite(&_pending[i].stream[0], 1, _pending[i].stream.size(), _out_stream);
-            segs.push_back(_pending[i].seg);
-            names.push_back(_pending[i].chr.data());
-            lens.push_back(_pending[i].chr.size());
-        }
         if (_emit_index) {
+            std::vector<starch_segment> segs;
+            std::vector<const char*> names;
+            std::vector<uint64_t> lens;
+            for (size_t i = 0; i < _closed.size(); ++i) {
+                segs.push_back(_closed[i].seg);
+                names.push_back(_closed[i].chr.data());
+                lens.push_back(_closed[i].chr.size());
+            }
             uint64_t n = 0;
-            int rc = starch_build_index(segs.empty() ? NULL : &segs[0], names.empty() ? NULL : &names[0],
-                                        lens.empty() ? NULL : &lens[0], segs.size(), off, _note.c_str(),
-                                        _block_size, NULL, 0, &n);
+            starch_options o = options();
+            int rc = starch_build_index_opt(segs.empty() ? NULL : &segs[0], names.empty() ? NULL : &names[0],
+                                            lens.empty() ? NULL : &lens[0], segs.size(), _stream_end, &o, NULL, 0, &n);
             if (rc) return rc;
             std::vector<char> idx(n);
-            rc = starch_build_index(segs.empty() ? NULL : &segs[0], names.empty() ? NULL : &names[0],
-                                    lens.empty() ? NULL : &lens[0], segs.size(), off, _note.c_str(), _block_size,
-                                    &idx[0], n, &n);
+            rc = starch_build_index_opt(segs.empty() ? NULL : &segs[0], names.empty() ? NULL : &names[0],
+                                        lens.empty() ? NULL : &lens[0], segs.size(), _stream_end, &o, &idx[0], n, &n);
             if (rc) return rc;
             std::fwrite(&idx[0], 1, n, _out_stream);
         }
-        _pending.clear();
+        _closed.clear();
+        _stream_end = 4;
         std::fflush(_out_stream);
         return STARCH_OK;
     }
 
 private:
-    struct Pending {
+    struct Closed {
         std::string chr;
         starch_segment seg;
-        std::vector<unsigned char> stream;
-        Pending(const std::string& c, const starch_segment& s, const std::vector<unsigned char>& st)
-            : chr(c), seg(s), stream(st) {}
+        Closed(const std::string& c, const starch_segment& s) : chr(c), seg(s) {}
     };
+
+    // hpp:523-536
+    static void reset_transformation_state(transform_state_t** tfs)
+    {
+        (*tfs)->line_count = 0;
+        (*tfs)->last_start = 0;
+        (*tfs)->last_stop = 0;
+        (*tfs)->last_coord_diff = 0;
+        (*tfs)->current_start = 0;
+        (*tfs)->current_stop = 0;
+        (*tfs)->current_coord_diff = 0;
+        (*tfs)->base_count_unique = 0;
+        (*tfs)->base_count_nonunique = 0;
+    }
 
     int open_devices(void)
     {
@@ -280,6 +454,8 @@ private:
 
     std::string _input_fn;
     std::string _note;
+    bz_stream* _bz_stream_ptr;
+    bool _bz_stream_used;
     FILE* _in_stream;
     FILE* _out_stream;
     compression_method_t _compression_method;
@@ -290,8 +466,61 @@ private:
     bool _reference_compat;
     bool _emit_index;
     bool _base_counts;
-    std::vector<Pending> _pending;
+    transform_state_t _tf_state;
+    std::vector<Closed> _closed;
+    uint64_t _stream_end;
+    std::string _closing_chr;
+    int64_t _closing_lines = 0;
+    uint64_t _closing_text = 0;
+    size_t _closing_name_len = 0;
+    bool _hook_error = false;
 };
+
+extern Starch* self;   // hpp:921; the program defines it (cpp:10)
+
+inline void Starch::process_tf_buffer(shared_buffer_t* sb)
+{
+    if (!sb->tf_buffer) return;
+    Starch* s = self;
+    if (s) {
+        if (!s->_bz_stream_ptr || s->_bz_stream_used) {   // one bzip2 stream per chromosome
+            s->delete_bz_stream_ptr();
+            s->initialize_bz_stream_ptr();
+            s->setup_bz_stream_callbacks(s);
+        }
+        bz_stream* z = s->_bz_stream_ptr;
+        const char* chr = sb->tf_state && sb->tf_state->current_chr ? sb->tf_state->current_chr : "";
+        s->_closing_chr.assign(chr, s->_closing_name_len ? s->_closing_name_len : std::strlen(chr));
+        s->_closing_name_len = 0;
+        s->_closing_lines = sb->tf_state ? sb->tf_state->line_count : 0;
+        s->_closing_text = sb->tf_buffer_size;
+        z->next_in = sb->tf_buffer;
+        z->avail_in = (unsigned int)sb->tf_buffer_size;
+        std::vector<char> out(1 << 20);
+        int rc;
+        do {
+            z->next_out = &out[0];
+            z->avail_out = (unsigned int)out.size();
+            rc = BZ2_bzCompress(z, BZ_FINISH);
+            const size_t k = out.size() - z->avail_out;
+            if (k && s->_out_stream) std::fwrite(&out[0], 1, k, s->_out_stream);
+        } while (rc == BZ_FINISH_OK);
+        s->_bz_stream_used = true;
+        if (rc != BZ_STREAM_END) {
+            std::fprintf(stderr, "Error: bzip2 compression failed (%d)\n", rc);
+            s->_hook_error = true;
+        }
+    }
+    reset_transformation_state(&sb->tf_state);   // hpp:396-405
+    std::free(sb->tf_buffer);
+    sb->tf_buffer = static_cast<char*>(std::calloc(tf_buffer_initial_length, sizeof(*sb->tf_buffer)));
+    if (!sb->tf_buffer) {
+        std::fprintf(stderr, "Error: Not enough memory for shared_buffer_t transformation buffer\n");
+        std::exit(ENOMEM);
+    }
+    sb->tf_buffer_capacity = tf_buffer_initial_length;
+    sb->tf_buffer_size = 0;
+}
 }  // namespace starch3
 
 #endif  // STARCH3_AMD_HPP_

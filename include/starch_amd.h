@@ -148,6 +148,54 @@ int starch_archive_layout(const uint64_t* unit_of, const uint64_t* bytes, uint64
 int starch_encode_multi_host(starch_ctx* const* ctxs, int nctx, const void* bed, uint64_t n,
                              const starch_options* opt);
 
+/* Same as starch_encode_units_device with the units in host memory (offsets
+ * relative to bed): only the listed units are copied to HBM, packed. */
+int starch_encode_units_host(starch_ctx* ctx, const void* bed, const starch_unit* units, const uint64_t* unit_ids,
+                             uint64_t nunits, const starch_options* opt);
+
+/* ---- the multi-rank gather (one process per GPU) ----------
+ * Every rank encodes its units (starch_encode_units_*); starch_gather_archive
+ * then collects all ranks' streams into rank 0's archive -- magic + streams in
+ * unit order + index, byte-identical to the one-GPU archive -- with RCCL over
+ * xGMI: an all-gather of segment counts, an all-gather of the segment records
+ * and names, and grouped ncclSend/ncclRecv of the stream bytes straight into
+ * their archive offsets.  Rank 0 reads the result through starch_archive_*,
+ * starch_segments, starch_segment_name; other ranks see archive size 0.
+ * Collective: every rank of the communicator calls it.  librccl is loaded on
+ * first use (STARCH_ERR_DEVICE if absent). */
+typedef struct starch_comm starch_comm;
+#define STARCH_COMM_ID_BYTES 128
+/* rank 0: a fresh RCCL unique id (ncclGetUniqueId) to hand to every rank */
+int starch_comm_id(void* id);
+/* one communicator per process, on the context's device */
+int starch_comm_create(int device, int rank, int world, const void* id, starch_comm** out);
+/* same, with the id handed out by rank 0 over TCP (rank 0 listens on port;
+ * the others connect to host:port, retrying for up to 10 minutes) */
+int starch_comm_create_tcp(int device, int rank, int world, const char* host, int port, starch_comm** out);
+void starch_comm_destroy(starch_comm* comm);
+const char* starch_comm_last_error(void);   /* detail of the last failed starch_comm_* / starch_gather_host */
+int starch_gather_archive(starch_ctx* ctx, starch_comm* comm, const starch_options* opt);
+
+/* The same gather over caller-supplied primitives on host memory (a test or
+ * non-RCCL transport, e.g. torch.distributed gloo): all_gather(send, recv,
+ * bytes) fills recv with world x bytes in rank order; send/recv post point-
+ * to-point transfers whose order per peer pair matches on both sides and
+ * which complete by the next group_end.  segs/names: this rank's segments
+ * (stream_offset into streams; unit = global unit index).  Rank 0 receives
+ * the archive in *archive (free with starch_free); elsewhere *archive = NULL. */
+typedef struct {
+    int rank, world;
+    void* user;
+    int (*all_gather)(void* user, const void* send, void* recv, uint64_t bytes);
+    int (*send)(void* user, const void* buf, uint64_t n, int peer);
+    int (*recv)(void* user, void* buf, uint64_t n, int peer);
+    int (*group_end)(void* user);
+} starch_host_comm;
+int starch_gather_host(const starch_host_comm* comm, const starch_segment* segs, const char* const* names,
+                       const uint64_t* name_lens, uint64_t nseg, const void* streams, const starch_options* opt,
+                       void** archive, uint64_t* len);
+void starch_free(void* p);
+
 /* Streaming ingestion (replaces the reference's line-at-a-time
  * produce_line / consume_line hand-off, include/starch3api.hpp:158-345, and
  * the per-chromosome flush, hpp:393-407).  Feed host BED bytes in pieces of

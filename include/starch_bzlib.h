@@ -12,10 +12,13 @@
  * Differences from the patched library (documented in INTEGRATION.md):
  *  - a NULL block_close_functor is allowed (the patched library calls it
  *    unconditionally at BZ_STREAM_END, bz:bzlib.c:470, and crashes);
- *  - the compressed bytes are produced on the GPU when the stream is
- *    finished; BZ_RUN and BZ_FLUSH consume input and return at once.  The
- *    final bytes are identical to the patched library for the same call
- *    sequence (including BZ_FLUSH block boundaries).
+ *  - the compressed bytes are produced on the GPU, one flush-delimited piece
+ *    at a time: BZ_FLUSH encodes the input since the previous FLUSH and makes
+ *    every whole byte so far readable (BZ_FLUSH_OK while it does not fit
+ *    avail_out, then BZ_RUN_OK, bz:bzlib.c:437-459), exactly as the library
+ *    does; BZ_RUN only consumes input (the library also emits a block once
+ *    900 k are buffered).  The bytes, and total_out after every FLUSH and
+ *    FINISH, are identical to the patched library for the same call sequence.
  */
 #ifndef STARCH_BZLIB_H_
 #define STARCH_BZLIB_H_
@@ -68,6 +71,11 @@ int BZ2_bzCompressInit(bz_stream* strm, int blockSize100k, int verbosity, int wo
 int BZ2_bzCompress(bz_stream* strm, int action);
 int BZ2_bzCompressEnd(bz_stream* strm);
 const char* BZ2_bzlibVersion(void);
+
+/* Not in libbz2: blocks written so far and their combined CRC (the value the
+ * stream trailer carries; bz:compress.c:606-608) -- what a block-close
+ * callback needs for the archive index. */
+int starch_bzstream_info(bz_stream* strm, unsigned int* n_blocks, unsigned int* combined_crc);
 
 #ifdef __cplusplus
 }

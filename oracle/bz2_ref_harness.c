@@ -45,8 +45,21 @@ int ref_bz2_compress(const uint8_t* in, size_t n, int bs100k, int wf,
  * FINISH_OK/FLUSH_OK draining loops are exercised.  rcs[k] gets the last
  * return code of op k.
  */
+int ref_bz2_script_trace(const uint8_t* in, const int32_t* ops, int nops, int bs100k, int wf,
+                         size_t out_chunk, uint8_t* out, size_t cap, size_t* out_len, int32_t* rcs,
+                         uint64_t* produced_after);
+
 int ref_bz2_script(const uint8_t* in, const int32_t* ops, int nops, int bs100k, int wf,
                    size_t out_chunk, uint8_t* out, size_t cap, size_t* out_len, int32_t* rcs)
+{
+    return ref_bz2_script_trace(in, ops, nops, bs100k, wf, out_chunk, out, cap, out_len, rcs, NULL);
+}
+
+/* Same, and produced_after[k] = total output bytes once op k completed (the
+ * library's total_out after each call: what BZ_FLUSH makes readable). */
+int ref_bz2_script_trace(const uint8_t* in, const int32_t* ops, int nops, int bs100k, int wf,
+                         size_t out_chunk, uint8_t* out, size_t cap, size_t* out_len, int32_t* rcs,
+                         uint64_t* produced_after)
 {
     bz_stream s;
     memset(&s, 0, sizeof(s));
@@ -73,6 +86,7 @@ int ref_bz2_script(const uint8_t* in, const int32_t* ops, int nops, int bs100k, 
             if (act == BZ_FINISH && rc == BZ_STREAM_END) break;
             if (produced >= cap) { *out_len = produced; BZ2_bzCompressEnd(&s); return -101; }
         }
+        if (produced_after) produced_after[k] = produced;
     }
     *out_len = produced;
     BZ2_bzCompressEnd(&s);

@@ -16,7 +16,7 @@ import json
 import os
 
 __all__ = ["Starch", "StarchError", "load", "gen_bed", "build_index", "parse_archive", "plan_units", "assign_shards",
-           "archive_layout", "compress_multi", "Unit", "Segment", "MAGIC", "HG38", "HG38_LEN"]
+           "archive_layout", "compress_multi", "Unit", "Segment", "Comm", "gather_host", "MAGIC", "HG38", "HG38_LEN"]
 
 _HERE = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.environ.get("STARCH_AMD_LIB") or os.path.join(_HERE, "_build", "libstarch_amd.so")
@@ -71,6 +71,17 @@ class Stats(ctypes.Structure):
 
 
 _lib = None
+
+# starch_host_comm (include/starch_amd.h): the gather's four primitives
+_AG_FN = ctypes.CFUNCTYPE(ctypes.c_int, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_uint64)
+_SEND_FN = ctypes.CFUNCTYPE(ctypes.c_int, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_uint64, ctypes.c_int)
+_RECV_FN = ctypes.CFUNCTYPE(ctypes.c_int, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_uint64, ctypes.c_int)
+_END_FN = ctypes.CFUNCTYPE(ctypes.c_int, ctypes.c_void_p)
+
+
+class HostComm(ctypes.Structure):
+    _fields_ = [("rank", ctypes.c_int), ("world", ctypes.c_int), ("user", ctypes.c_void_p),
+                ("all_gather", _AG_FN), ("send", _SEND_FN), ("recv", _RECV_FN), ("group_end", _END_FN)]
 
 
 class DecStream(ctypes.Structure):
@@ -157,6 +168,18 @@ def load():
         "starch_output_size": ([vp, pu64], ctypes.c_int),
         "starch_output_copy": ([vp, vp, u64], ctypes.c_int),
         "starch_output_device": ([vp, ctypes.POINTER(vp)], ctypes.c_int),
+        "starch_encode_units_host": ([vp, vp, ctypes.POINTER(Unit), pu64, u64, ctypes.POINTER(Options)],
+                                     ctypes.c_int),
+        "starch_comm_id": ([vp], ctypes.c_int),
+        "starch_comm_create": ([ctypes.c_int, ctypes.c_int, ctypes.c_int, vp, ctypes.POINTER(vp)], ctypes.c_int),
+        "starch_comm_create_tcp": ([ctypes.c_int, ctypes.c_int, ctypes.c_int, ctypes.c_char_p, ctypes.c_int,
+                                    ctypes.POINTER(vp)], ctypes.c_int),
+        "starch_comm_destroy": ([vp], None),
+        "starch_comm_last_error": ([], ctypes.c_char_p),
+        "starch_gather_archive": ([vp, vp, ctypes.POINTER(Options)], ctypes.c_int),
+        "starch_gather_host": ([ctypes.POINTER(HostComm), ctypes.POINTER(Segment), ctypes.POINTER(ctypes.c_char_p),
+                                pu64, u64, vp, ctypes.POINTER(Options), ctypes.POINTER(vp), pu64], ctypes.c_int),
+        "starch_free": ([vp], None),
     }
     for name, (args, res) in sig.items():
         f = getattr(L, name)
@@ -316,6 +339,22 @@ class Starch:
         ids = (ctypes.c_uint64 * max(1, k))(*(unit_ids if unit_ids is not None else range(k)))
         _check(self._L.starch_encode_units_device(self._h, ctypes.c_void_p(d_base), U, ids, k, ctypes.byref(o)),
                self._h)
+
+    def encode_units_host(self, bed, units, unit_ids=None, emit_index=False):
+        """One shard from host bytes: only the listed units (offsets into bed)
+        are copied to HBM, packed; then as encode_units_device."""
+        o = self._opts(emit_index)
+        k = len(units)
+        U = (Unit * max(1, k))(*units)
+        ids = (ctypes.c_uint64 * max(1, k))(*(unit_ids if unit_ids is not None else range(k)))
+        ptr = bed if isinstance(bed, int) else ctypes.cast(ctypes.c_char_p(bed), ctypes.c_void_p).value
+        _check(self._L.starch_encode_units_host(self._h, ctypes.c_void_p(ptr), U, ids, k, ctypes.byref(o)), self._h)
+
+    def gather_archive(self, comm, emit_index=True):
+        """Collective over comm (one rank per GPU): every rank's streams from
+        its last encode_units_* into rank 0's archive (RCCL, starch_gather_archive)."""
+        o = self._opts(emit_index)
+        _check(self._L.starch_gather_archive(self._h, comm._h, ctypes.byref(o)), self._h)
 
     def streams_device(self):
         """(device pointer, bytes) of the last starch_encode_units_device result."""
@@ -531,6 +570,116 @@ def compress_multi(ctxs, bed: bytes, emit_index=True, reference_compat=False) ->
     H = (ctypes.c_void_p * len(ctxs))(*[c._h.value for c in ctxs])
     _check(L.starch_encode_multi_host(H, len(ctxs), bed, len(bed), ctypes.byref(o)), ctxs[0]._h)
     return ctxs[0].archive()
+
+
+class Comm:
+    """One RCCL communicator per process (starch_comm_*): rank 0 makes the id
+    (``Comm.new_id()``) and every rank passes it, or use ``Comm.tcp``."""
+
+    def __init__(self, device, rank, world, comm_id):
+        L = load()
+        h = ctypes.c_void_p()
+        rc = L.starch_comm_create(device, rank, world, ctypes.c_char_p(bytes(comm_id)), ctypes.byref(h))
+        if rc:
+            raise StarchError(rc, L.starch_comm_last_error().decode(errors="replace"))
+        self._h, self._L, self.rank, self.world = h, L, rank, world
+
+    @staticmethod
+    def new_id() -> bytes:
+        L = load()
+        buf = ctypes.create_string_buffer(128)
+        rc = L.starch_comm_id(buf)
+        if rc:
+            raise StarchError(rc, L.starch_comm_last_error().decode(errors="replace"))
+        return buf.raw
+
+    @classmethod
+    def tcp(cls, device, rank, world, host, port):
+        self = cls.__new__(cls)
+        L = load()
+        h = ctypes.c_void_p()
+        rc = L.starch_comm_create_tcp(device, rank, world, host.encode(), port, ctypes.byref(h))
+        if rc:
+            raise StarchError(rc, L.starch_comm_last_error().decode(errors="replace"))
+        self._h, self._L, self.rank, self.world = h, L, rank, world
+        return self
+
+    def close(self):
+        if getattr(self, "_h", None):
+            self._L.starch_comm_destroy(self._h)
+            self._h = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+
+def gather_host(rank, world, all_gather, send, recv, group_end, segs, names, streams: bytes, note=None, level=9,
+                emit_index=True, base_counts=False, reference_compat=False):
+    """The library's gather (starch_gather_host) over caller primitives on host
+    bytes: all_gather(bytes) -> [bytes per rank]; send(bytes, peer);
+    recv(n, peer) -> a handle; group_end() -> {handle: bytes} for the recvs
+    posted since the last group_end.  Returns the archive on rank 0, else None."""
+    L = load()
+    pending = {}
+
+    def _ag(_u, sp, rp, n):
+        try:
+            parts = all_gather(ctypes.string_at(sp, n))
+            for r, p in enumerate(parts):
+                ctypes.memmove(rp + r * n, p, n)
+            return 0
+        except Exception:
+            return 1
+
+    def _send(_u, p, n, peer):
+        try:
+            send(ctypes.string_at(p, n), peer)
+            return 0
+        except Exception:
+            return 1
+
+    def _recv(_u, p, n, peer):
+        try:
+            pending[recv(n, peer)] = (p, n)
+            return 0
+        except Exception:
+            return 1
+
+    def _end(_u):
+        try:
+            got = group_end()
+            for h, data in got.items():
+                p, n = pending.pop(h)
+                ctypes.memmove(p, data, n)
+            return 0
+        except Exception:
+            return 1
+
+    hc = HostComm(rank, world, None, _AG_FN(_ag), _SEND_FN(_send), _RECV_FN(_recv), _END_FN(_end))
+    k = len(segs)
+    arr = (Segment * max(1, k))(*segs)
+    nm = (ctypes.c_char_p * max(1, k))(*names)
+    nl = (ctypes.c_uint64 * max(1, k))(*[len(x) for x in names])
+    o = Options()
+    L.starch_options_init(ctypes.byref(o))
+    note_b = note.encode() if note else None
+    o.block_size_100k, o.note, o.base_counts = level, note_b, 1 if base_counts else 0
+    o.emit_index, o.reference_compat = 1 if emit_index else 0, 1 if reference_compat else 0
+    sbuf = ctypes.create_string_buffer(streams, max(1, len(streams)))
+    out, n = ctypes.c_void_p(), ctypes.c_uint64()
+    rc = L.starch_gather_host(ctypes.byref(hc), arr, nm, nl, k, sbuf, ctypes.byref(o), ctypes.byref(out),
+                              ctypes.byref(n))
+    if rc:
+        raise StarchError(rc, L.starch_comm_last_error().decode(errors="replace"))
+    if not out.value:
+        return None
+    try:
+        return ctypes.string_at(out.value, n.value)
+    finally:
+        L.starch_free(out)
 
 
 def parse_archive(blob: bytes):

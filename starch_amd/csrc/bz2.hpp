@@ -43,6 +43,7 @@ struct StreamOut {
     uint32_t first_block, n_blocks;
     uint32_t combined_crc;
     uint32_t pad;
+    uint64_t block_bits;       // bits of the blocks alone (no header, trailer or padding)
 };
 
 struct Stats {                 // per-stage device timings (ms) from HIP events

@@ -343,8 +343,10 @@ void Encoder::plan(const uint8_t* d_text, const std::vector<StreamIn>& streams, 
     // stream sizes: 32 header bits + blocks + 80 trailer bits, padded to a byte
     uint64_t off = 0;
     for (uint32_t s = 0; s < ngroups_; ++s) {
-        uint64_t bits = 32 + 80;
+        uint64_t bits = 0;
         for (uint32_t k = 0; k < outs[s].n_blocks; ++k) bits += hb[outs[s].first_block + k].bits;
+        outs[s].block_bits = bits;
+        bits += 32 + 80;
         outs[s].bytes = (bits + 7) / 8;
         outs[s].out_off = off;
         off += outs[s].bytes;

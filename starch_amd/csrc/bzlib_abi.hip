@@ -3,13 +3,18 @@
 //
 // Mirrors the state machine of bz:bzlib.c:148-500 (modes RUNNING / FLUSHING /
 // FINISHING / IDLE, avail_in_expect, return codes, total_in/out counters,
-// block_close_functor at BZ_STREAM_END), but instead of compressing a block
-// at a time on the CPU it records the input and the BZ_FLUSH boundaries and
-// encodes the whole stream on the GPU when BZ_FINISH arrives.  The bytes are
-// those of the patched library for the same call sequence: each flush-
-// delimited piece is RLE1-coded and block-cut on its own (flush_RL resets the
-// run state, bz:bzlib.c:393-397), and a piece's final single-byte run joins a
-// full block only when the terminating FLUSH/FINISH call supplied input.
+// block_close_functor at BZ_STREAM_END).  Input is recorded until the caller
+// ends a piece with BZ_FLUSH or BZ_FINISH; the piece is then RLE1-coded,
+// block-cut, sorted and coded on the GPU on its own (flush_RL resets the run
+// state, bz:bzlib.c:393-397; its final single-byte run joins a full block
+// only when the terminating call supplied input), and its blocks' bits are
+// appended to the stream's bit string: at BZ_FLUSH every whole byte so far is
+// output, the last 0..7 bits stay pending (the library's bsBuff/bsLive carry
+// across BZ2_compressBlock, bz:compress.c:609); BZ_FINISH appends the trailer
+// with the combined CRC and pads to a byte (bz:compress.c:657-666).  The
+// bytes and the total_out after every call are those of the patched library
+// for the same call sequence; only BZ_RUN differs in timing (the library emits
+// a block as soon as 900 k are buffered, here at the next FLUSH/FINISH).
 #include <string.h>
 
 #include <condition_variable>
@@ -30,12 +35,14 @@ struct GpuStreamState {
     bz_stream* strm;
     int bs100k;
     int mode;
-    std::vector<uint8_t> input;
-    std::vector<bz::StreamIn> pieces;   // closed pieces
-    uint64_t piece_start = 0;
-    std::vector<uint8_t> output;
+    std::vector<uint8_t> input;         // bytes of the open piece
+    std::vector<uint8_t> output;        // whole bytes not yet drained
     uint64_t out_pos = 0;
-    bool encoded = false;
+    uint32_t tail = 0, tail_bits = 0;   // bits not yet a whole byte (right-aligned, < 8)
+    bool header = false;                // "BZh<level>" written (first BZ2_compressBlock)
+    bool pending_piece = false;         // a FINISH failed: the closed piece is still to encode
+    bool pending_supplied = false, pending_finish = false;
+    uint32_t n_blocks = 0, combined = 0;
 };
 
 // Encoder slots: each stream borrows one for its BZ_FINISH encode, so
@@ -131,47 +138,109 @@ void consume(GpuStreamState* g)
     }
 }
 
-void close_piece(GpuStreamState* g, bool supplied)
+void put_bits(GpuStreamState* g, uint32_t v, uint32_t n)   // n <= 24, MSB first
 {
-    bz::StreamIn p;
-    p.text_off = g->piece_start;
-    p.text_len = g->input.size() - g->piece_start;
-    p.final_run_joins = supplied ? 1u : 0u;
-    p.group = 0;
-    g->pieces.push_back(p);
-    g->piece_start = g->input.size();
+    g->tail = (g->tail << n) | (v & ((1u << n) - 1u));
+    g->tail_bits += n;
+    while (g->tail_bits >= 8) {
+        g->tail_bits -= 8;
+        g->output.push_back((uint8_t)(g->tail >> g->tail_bits));
+    }
+    g->tail &= (1u << g->tail_bits) - 1u;
 }
 
-int encode_on_gpu(GpuStreamState* g)
+// append bits [bit0, bit0 + nbits) of src (MSB-first bit string)
+void put_stream_bits(GpuStreamState* g, const uint8_t* src, uint64_t bit0, uint64_t nbits)
 {
-    Slot* sl = nullptr;
-    try {
-        const int dev = target_device();
-        DeviceGuard guard(dev);
-        sl = acquire(dev);
-        if (!sl->st) HIP_CHECK(hipStreamCreateWithFlags(&sl->st, hipStreamNonBlocking));
-        uint64_t n = g->input.size();
-        uint8_t* d_in = sl->in.as<uint8_t>(n + 64);
-        if (n) HIP_CHECK(hipMemcpyAsync(d_in, g->input.data(), n, hipMemcpyHostToDevice, sl->st));
-        std::vector<bz::StreamOut> outs;
-        sl->enc.plan(d_in, g->pieces, g->bs100k, sl->st, outs, nullptr);
-        uint64_t bytes = outs.empty() ? 0 : outs[0].bytes;
-        uint64_t cap = (bytes + 64 + 255) / 256 * 256;
-        uint8_t* d_out = sl->out.as<uint8_t>(cap);
-        sl->enc.emit(d_out, cap, 0, outs, sl->st, nullptr);
-        g->output.resize(bytes);
-        if (bytes) HIP_CHECK(hipMemcpyAsync(g->output.data(), d_out, bytes, hipMemcpyDeviceToHost, sl->st));
-        HIP_CHECK(hipStreamSynchronize(sl->st));
-        release(sl);
-    } catch (const std::exception&) {
-        if (sl) release(sl);
-        g->output.clear();
-        return BZ_CONFIG_ERROR;
+    uint64_t b = bit0;
+    const uint64_t e = bit0 + nbits;
+    while (b < e && (b & 7)) {   // to a source byte boundary
+        put_bits(g, (src[b >> 3] >> (7 - (b & 7))) & 1u, 1);
+        ++b;
+    }
+    const uint64_t whole = (e - b) / 8;
+    const uint8_t* p = src + (b >> 3);
+    if (g->tail_bits == 0) {
+        g->output.insert(g->output.end(), p, p + whole);
+    } else {
+        const uint32_t t = g->tail_bits;
+        uint32_t acc = g->tail;
+        const size_t o = g->output.size();
+        g->output.resize(o + whole);
+        for (uint64_t i = 0; i < whole; ++i) {
+            acc = (acc << 8) | p[i];
+            g->output[o + i] = (uint8_t)(acc >> t);
+            acc &= (1u << t) - 1u;
+        }
+        g->tail = acc;
+    }
+    b += whole * 8;
+    for (; b < e; ++b) put_bits(g, (src[b >> 3] >> (7 - (b & 7))) & 1u, 1);
+}
+
+// BZ2_compressBlock for the open piece (bz:compress.c:602-667): encode it on
+// the GPU as a stream of its own and append its blocks' bits
+int encode_piece(GpuStreamState* g, bool supplied)
+{
+    std::vector<uint8_t> tmp;
+    bz::StreamOut so{};
+    if (!g->input.empty()) {
+        Slot* sl = nullptr;
+        try {
+            const int dev = target_device();
+            DeviceGuard guard(dev);
+            sl = acquire(dev);
+            if (!sl->st) HIP_CHECK(hipStreamCreateWithFlags(&sl->st, hipStreamNonBlocking));
+            const uint64_t n = g->input.size();
+            uint8_t* d_in = sl->in.as<uint8_t>(n + 64);
+            HIP_CHECK(hipMemcpyAsync(d_in, g->input.data(), n, hipMemcpyHostToDevice, sl->st));
+            std::vector<bz::StreamIn> pieces(1);
+            pieces[0].text_off = 0;
+            pieces[0].text_len = n;
+            pieces[0].final_run_joins = supplied ? 1u : 0u;
+            pieces[0].group = 0;
+            std::vector<bz::StreamOut> outs;
+            sl->enc.plan(d_in, pieces, g->bs100k, sl->st, outs, nullptr);
+            const uint64_t cap = (outs[0].bytes + 64 + 255) / 256 * 256;
+            uint8_t* d_out = sl->out.as<uint8_t>(cap);
+            sl->enc.emit(d_out, cap, 0, outs, sl->st, nullptr);
+            so = outs[0];
+            tmp.resize(so.bytes);
+            HIP_CHECK(hipMemcpyAsync(tmp.data(), d_out, so.bytes, hipMemcpyDeviceToHost, sl->st));
+            HIP_CHECK(hipStreamSynchronize(sl->st));
+            release(sl);
+        } catch (const std::exception&) {
+            if (sl) release(sl);
+            return BZ_CONFIG_ERROR;
+        }
+    }
+    if (!g->header) {   // the first compressBlock writes the stream header, data or not
+        put_bits(g, 'B', 8);
+        put_bits(g, 'Z', 8);
+        put_bits(g, 'h', 8);
+        put_bits(g, (uint32_t)('0' + g->bs100k), 8);
+        g->header = true;
+    }
+    if (so.n_blocks) {
+        put_stream_bits(g, tmp.data(), 32, so.block_bits);   // after the piece stream's own header
+        // combined CRC over all blocks: c = rotl1(c) ^ blockCRC per block, so a
+        // piece of k blocks folds in as rotl_k(c) ^ (its own combined CRC)
+        const uint32_t k = so.n_blocks & 31u;
+        g->combined = (k ? (g->combined << k) | (g->combined >> (32 - k)) : g->combined) ^ so.combined_crc;
+        g->n_blocks += so.n_blocks;
     }
     g->input.clear();
-    g->input.shrink_to_fit();
-    g->encoded = true;
     return BZ_OK;
+}
+
+void finish_stream(GpuStreamState* g)   // trailer + combined CRC + byte pad
+{
+    put_bits(g, 0x177245u, 24);
+    put_bits(g, 0x385090u, 24);
+    put_bits(g, g->combined >> 16, 16);
+    put_bits(g, g->combined & 0xFFFFu, 16);
+    if (g->tail_bits) put_bits(g, 0, 8 - g->tail_bits);
+    g->input.shrink_to_fit();
 }
 
 bool drain(GpuStreamState* g)
@@ -185,6 +254,10 @@ bool drain(GpuStreamState* g)
         s->avail_out -= (unsigned)k;
         g->out_pos += k;
         add_out(s, k);
+    }
+    if (g->out_pos == g->output.size()) {
+        g->output.clear();
+        g->out_pos = 0;
     }
     return k > 0;
 }
@@ -234,32 +307,48 @@ int BZ2_bzCompress(bz_stream* strm, int action)
                 consume(g);
                 return progress ? BZ_RUN_OK : BZ_PARAM_ERROR;           // bz:bzlib.c:432-434
             }
-            if (action == BZ_FLUSH) {
-                bool supplied = strm->avail_in > 0;
+            if (action == BZ_FLUSH || action == BZ_FINISH) {
+                const bool supplied = strm->avail_in > 0;
                 consume(g);
-                close_piece(g, supplied);
-                return BZ_RUN_OK;
-            }
-            if (action == BZ_FINISH) {
-                bool supplied = strm->avail_in > 0;
-                consume(g);
-                close_piece(g, supplied);
-                int rc = encode_on_gpu(g);
-                if (rc != BZ_OK) {   // never report BZ_STREAM_END for a stream that was not encoded
+                if (int rc = encode_piece(g, supplied)) {   // input kept: the same call may be retried
                     g->mode = M_FAILED;
+                    g->pending_piece = true;
+                    g->pending_supplied = supplied;
+                    g->pending_finish = action == BZ_FINISH;
                     return rc;
                 }
+                if (action == BZ_FLUSH) {
+                    drain(g);
+                    if (!g->output.empty()) { g->mode = M_FLUSHING; return BZ_FLUSH_OK; }   // bz:bzlib.c:451-459
+                    return BZ_RUN_OK;
+                }
+                finish_stream(g);
                 g->mode = M_FINISHING;
                 break;
             }
             return BZ_PARAM_ERROR;
+        case M_FLUSHING:   // avail_in_expect is 0: everything was consumed by the first FLUSH call
+            if (action != BZ_FLUSH || strm->avail_in != 0) return BZ_SEQUENCE_ERROR;
+            drain(g);
+            if (!g->output.empty()) return BZ_FLUSH_OK;
+            g->mode = M_RUNNING;
+            return BZ_RUN_OK;
         case M_FINISHING:
             if (action != BZ_FINISH) return BZ_SEQUENCE_ERROR;
             if (strm->avail_in != 0) return BZ_SEQUENCE_ERROR;          // avail_in_expect mismatch
             break;
-        case M_FAILED:   // the input is still held: a BZ_FINISH retries the encode
-            if (action != BZ_FINISH || strm->avail_in != 0) return BZ_SEQUENCE_ERROR;
-            if (int rc = encode_on_gpu(g)) return rc;
+        case M_FAILED:   // the piece is still held: the same action retries its encode
+            if ((action == BZ_FINISH) != g->pending_finish || action == BZ_RUN || strm->avail_in != 0)
+                return BZ_SEQUENCE_ERROR;
+            if (int rc = encode_piece(g, g->pending_supplied)) return rc;
+            g->pending_piece = false;
+            if (!g->pending_finish) {
+                g->mode = M_RUNNING;
+                drain(g);
+                if (!g->output.empty()) { g->mode = M_FLUSHING; return BZ_FLUSH_OK; }
+                return BZ_RUN_OK;
+            }
+            finish_stream(g);
             g->mode = M_FINISHING;
             break;
         default:
@@ -267,7 +356,7 @@ int BZ2_bzCompress(bz_stream* strm, int action)
     }
     // FINISHING: drain the encoded stream
     bool progress = drain(g);
-    if (g->out_pos < g->output.size()) return progress ? BZ_FINISH_OK : BZ_SEQUENCE_ERROR;
+    if (!g->output.empty()) return progress ? BZ_FINISH_OK : BZ_SEQUENCE_ERROR;
     g->mode = M_IDLE;
     if (strm->block_close_functor) strm->block_close_functor(strm->handler);   // bz:bzlib.c:470
     return BZ_STREAM_END;
@@ -284,5 +373,14 @@ int BZ2_bzCompressEnd(bz_stream* strm)
 }
 
 const char* BZ2_bzlibVersion(void) { return "1.0.6-starch-mi355x"; }
+
+int starch_bzstream_info(bz_stream* strm, unsigned int* n_blocks, unsigned int* combined_crc)
+{
+    GpuStreamState* g = state_of(strm);
+    if (!g || !n_blocks || !combined_crc) return BZ_PARAM_ERROR;
+    *n_blocks = g->n_blocks;
+    *combined_crc = g->combined;
+    return BZ_OK;
+}
 
 }  // extern "C"

@@ -5,47 +5,16 @@ and gather the finished bzip2 streams to rank 0, which writes the archive.
 The reference has no distributed layer: its unit of independence
 is the per-chromosome hand-off process_tf_buffer (include/starch3api.hpp:
 393-407), so chromosome streams shard with no data-path exchange and the only
-collective is the gather of compressed streams.  The transport is
-pluggable: ``TorchTransport`` wraps a torch.distributed process group
-(backend "nccl" = RCCL over xGMI on MI355X; "gloo" on CPU for tests).
+collective is the gather of compressed streams.
 
+The gather itself is the library's C++ (starch_amd/csrc/gather.hip): on GPUs
+``Starch.gather_archive(Comm)`` runs it over RCCL (xGMI) with no Python in the
+data path; ``gather_archive`` below drives the SAME C++ gather through host
+primitives backed by a torch.distributed group (gloo on the CPU tests).
 Planning, LPT assignment, archive layout and the index writer are the
-library's host code (starch_plan_units / starch_assign_shards /
-starch_archive_layout / starch_build_index); this module only moves bytes.
+library's host code too; this module only adapts transports.
 """
 import starch_amd
-
-# metadata columns exchanged per segment
-_COLS = ("unit", "stream_offset", "stream_bytes", "line_count", "text_bytes", "n_blocks", "combined_crc", "name_len",
-         "base_count_unique", "base_count_nonunique")
-
-
-class TorchTransport:
-    """torch.distributed process group as the gather transport."""
-
-    def __init__(self, device, group=None):
-        import torch.distributed as dist
-        self.dist = dist
-        self.group = group
-        self.device = device
-        self.rank = dist.get_rank(group)
-        self.world = dist.get_world_size(group)
-
-    def all_gather(self, t):
-        """Same-shape tensors from every rank -> list indexed by rank."""
-        import torch
-        out = [torch.empty_like(t) for _ in range(self.world)]
-        self.dist.all_gather(out, t, group=self.group)
-        return out
-
-    def exchange(self, sends, recvs):
-        """sends: [(tensor, dst)], recvs: [(tensor, src)]; per peer pair the
-        ops match in issue order."""
-        ops = [self.dist.P2POp(self.dist.isend, t, p, group=self.group) for t, p in sends]
-        ops += [self.dist.P2POp(self.dist.irecv, t, p, group=self.group) for t, p in recvs]
-        if ops:
-            for w in self.dist.batch_isend_irecv(ops):
-                w.wait()
 
 
 def shard_units(bed: bytes, world: int, max_units_per_rank: int = 64):
@@ -55,103 +24,80 @@ def shard_units(bed: bytes, world: int, max_units_per_rank: int = 64):
     return units, starch_amd.assign_shards(units, world)
 
 
-def local_segments(ctx):
-    """This rank's segments after Starch.encode_units_device: (records, names)."""
-    segs = ctx.segments()
-    rec = [[getattr(s, c) for c in _COLS] for _, s in segs]
-    return rec, [n for n, _ in segs]
-
-
-def gather_archive(tr, records, names, streams, note=None, level=9, emit_index=True, base_counts=False):
-    """Gather every rank's streams to rank 0 in archive (unit) order.
-
-    records / names: this rank's segments (``local_segments``); streams: a
-    uint8 tensor holding this rank's stream bytes (offsets in records are
-    relative to it), on the transport's device.  Returns the archive as a
-    uint8 tensor on rank 0 (magic + streams + index + footer, byte-identical
-    to a one-GPU run) and None on the other ranks.
-    """
+def comm_from_torch(device, group=None):
+    """An RCCL communicator (starch_amd.Comm) for the ranks of a torch
+    process group: rank 0's unique id is broadcast over the group."""
     import torch
-    dev = tr.device
-    n = torch.tensor([len(records), sum(len(x) for x in names)], dtype=torch.int64, device=dev)
-    counts = [tuple(int(v) for v in x.tolist()) for x in tr.all_gather(n)]
-    maxn = max(1, max(c[0] for c in counts))
-    maxb = max(1, max(c[1] for c in counts))
-    rec = torch.zeros((maxn, len(_COLS)), dtype=torch.int64, device=dev)
-    if records:
-        rec[:len(records)] = torch.tensor(records, dtype=torch.int64)
-    nm = torch.zeros(maxb, dtype=torch.uint8, device=dev)
-    blob = b"".join(names)
-    if blob:
-        nm[:len(blob)] = torch.frombuffer(bytearray(blob), dtype=torch.uint8)
-    all_rec = [x.cpu().tolist() for x in tr.all_gather(rec)]
-    all_nm = [bytes(x.cpu().numpy().tobytes()) for x in tr.all_gather(nm)]
+    import torch.distributed as dist
+    rank, world = dist.get_rank(group), dist.get_world_size(group)
+    dev = torch.device("cuda", device) if dist.get_backend(group) == "nccl" else torch.device("cpu")
+    t = torch.zeros(128, dtype=torch.uint8, device=dev)
+    if rank == 0:
+        t.copy_(torch.frombuffer(bytearray(starch_amd.Comm.new_id()), dtype=torch.uint8))
+    dist.broadcast(t, 0, group=group)
+    return starch_amd.Comm(device, rank, world, t.cpu().numpy().tobytes())
 
-    # global segment list in (rank, local order); layout is computed on every
-    # rank so senders and the receiver agree on the coalesced runs
-    segs = []          # (rank, record, name)
-    for r in range(tr.world):
-        pos = 0
-        for row in all_rec[r][:counts[r][0]]:
-            ln = row[_COLS.index("name_len")]
-            segs.append((r, row, all_nm[r][pos:pos + ln]))
-            pos += ln
-    unit_of = [row[0] for _, row, _ in segs]
-    nbytes = [row[2] for _, row, _ in segs]
-    order, offset, end = starch_amd.archive_layout(unit_of, nbytes, base=4)
-    runs = []          # (rank, src offset, dst offset, length): adjacent in part and archive
-    for g in order:
-        r, row, _ = segs[g]
-        if runs and runs[-1][0] == r and runs[-1][1] + runs[-1][3] == row[1] and runs[-1][2] + runs[-1][3] == offset[g]:
-            runs[-1][3] += row[2]
-        else:
-            runs.append([r, row[1], offset[g], row[2]])
-    runs = [x for x in runs if x[3] > 0]
 
-    if tr.rank != 0:
-        tr.exchange([(streams[s:s + ln], 0) for r, s, _, ln in runs if r == tr.rank], [])
-        return None
-    out_segs, out_names = [], []
-    for g in order:
-        r, row, name = segs[g]
-        d = dict(zip(_COLS, row))
-        out_segs.append(starch_amd.Segment(line_count=d["line_count"], text_bytes=d["text_bytes"],
-                                           stream_offset=offset[g], stream_bytes=d["stream_bytes"],
-                                           name_len=len(name), n_blocks=d["n_blocks"],
-                                           combined_crc=d["combined_crc"] & 0xFFFFFFFF, unit=d["unit"],
-                                           base_count_unique=d["base_count_unique"],
-                                           base_count_nonunique=d["base_count_nonunique"]))
-        out_names.append(name)
-    idx = (starch_amd.build_index(out_segs, out_names, end, note=note, level=level, base_counts=base_counts)
-           if emit_index else b"")
-    arch = torch.empty(end + len(idx), dtype=torch.uint8, device=dev)
-    arch[0:4] = torch.frombuffer(bytearray(starch_amd.MAGIC), dtype=torch.uint8)
-    for r, s, d, ln in runs:
-        if r == 0:
-            arch[d:d + ln].copy_(streams[s:s + ln])
-    tr.exchange([], [(arch[d:d + ln], r) for r, s, d, ln in runs if r != 0])
-    if idx:
-        arch[end:] = torch.frombuffer(bytearray(idx), dtype=torch.uint8)
-    return arch
+class TorchHostPrimitives:
+    """The four primitives of starch_gather_host over a torch.distributed group
+    (host bytes; gloo on CPU)."""
+
+    def __init__(self, group=None):
+        import torch.distributed as dist
+        self.dist = dist
+        self.group = group
+        self.rank = dist.get_rank(group)
+        self.world = dist.get_world_size(group)
+        self._ops = []
+
+    def all_gather(self, data: bytes):
+        import torch
+        t = torch.frombuffer(bytearray(data), dtype=torch.uint8) if data else torch.empty(0, dtype=torch.uint8)
+        out = [torch.empty_like(t) for _ in range(self.world)]
+        self.dist.all_gather(out, t, group=self.group)
+        return [x.numpy().tobytes() for x in out]
+
+    def send(self, data: bytes, peer):
+        import torch
+        self._ops.append(("s", torch.frombuffer(bytearray(data), dtype=torch.uint8), peer))
+
+    def recv(self, n, peer):
+        import torch
+        t = torch.empty(n, dtype=torch.uint8)
+        self._ops.append(("r", t, peer))
+        return len(self._ops) - 1
+
+    def group_end(self):
+        d = self.dist
+        ops = [d.P2POp(d.isend if k == "s" else d.irecv, t, p, group=self.group) for k, t, p in self._ops]
+        if ops:
+            for w in d.batch_isend_irecv(ops):
+                w.wait()
+        got = {i: t.numpy().tobytes() for i, (k, t, _) in enumerate(self._ops) if k == "r"}
+        self._ops = []
+        return got
+
+
+def gather_archive(prims, segments, names, streams: bytes, note=None, level=9, emit_index=True, base_counts=False):
+    """The library's gather over host primitives (TorchHostPrimitives):
+    segments = this rank's starch_amd.Segment list (stream_offset into
+    `streams`, unit = global unit index), names = their chromosome bytes.
+    Returns the archive bytes on rank 0 (byte-identical to a one-GPU run),
+    None elsewhere."""
+    return starch_amd.gather_host(prims.rank, prims.world, prims.all_gather, prims.send, prims.recv,
+                                  prims.group_end, segments, names, streams, note=note, level=level,
+                                  emit_index=emit_index, base_counts=base_counts)
 
 
 def encode_rank(ctx, d_base, units, unit_ids, note=None, level=9):
-    """Encode this rank's units (resident in HBM at d_base) -> (records, names,
-    streams tensor view on the GPU)."""
+    """Encode this rank's units (resident in HBM at d_base) -> ctx holds the
+    streams for ctx.gather_archive / local_segments."""
     ctx.block_size_100k = level
     ctx.set_note(note or "")
     ctx.encode_units_device(d_base, units, unit_ids)
-    p, nbytes = ctx.streams_device()
-    return local_segments(ctx) + (device_bytes(p, nbytes),)
 
 
-def device_bytes(ptr, nbytes):
-    """A uint8 CUDA tensor view of library-owned HBM (no copy)."""
-    import torch
-
-    class _A:
-        __cuda_array_interface__ = {"shape": (nbytes,), "typestr": "|u1", "data": (ptr or 1, False), "version": 3}
-    if nbytes == 0:
-        return torch.empty(0, dtype=torch.uint8, device="cuda")
-    return torch.as_tensor(_A(), device="cuda")
-
+def local_segments(ctx):
+    """This rank's segments after encode_units_*: ([Segment], [name bytes])."""
+    segs = ctx.segments()
+    return [s for _, s in segs], [n for n, _ in segs]

@@ -49,6 +49,7 @@ def ref():
         R = ctypes.CDLL(REF_SO)
         R.ref_bz2_compress.restype = ctypes.c_int
         R.ref_bz2_script.restype = ctypes.c_int
+        R.ref_bz2_script_trace.restype = ctypes.c_int
         R.ref_bz2_version.restype = ctypes.c_char_p
         _ref = R
     return _ref
@@ -122,6 +123,21 @@ def ref_bz2_script(data: bytes, ops, bs=9, wf=30, out_chunk=0):
                           ctypes.c_size_t(cap), ctypes.byref(n), rcs)
     assert rc == 0, rc
     return out.raw[:n.value], list(rcs)
+
+
+def ref_bz2_script_trace(data: bytes, ops, bs=9, wf=30, out_chunk=0):
+    """ops: [(action, nbytes)] -> (stream bytes, [rc per op], [total output after each op])"""
+    R = ref()
+    arr = (ctypes.c_int32 * (2 * len(ops)))(*[v for op in ops for v in op])
+    rcs = (ctypes.c_int32 * len(ops))()
+    after = (ctypes.c_uint64 * len(ops))()
+    cap = len(data) + len(data) // 50 + 4096 + 64 * len(ops)
+    out = ctypes.create_string_buffer(cap)
+    n = ctypes.c_size_t(0)
+    rc = R.ref_bz2_script_trace(data, arr, len(ops), bs, wf, ctypes.c_size_t(out_chunk), out,
+                                ctypes.c_size_t(cap), ctypes.byref(n), rcs, after)
+    assert rc == 0, rc
+    return out.raw[:n.value], list(rcs), list(after)
 
 
 def block_sort(block: bytes):

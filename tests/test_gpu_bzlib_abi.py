@@ -30,8 +30,9 @@ def _lib():
     return L
 
 
-def run_script(data, ops, bs=9, out_chunk=0):
-    """Drive the GPU bzlib ABI like ref_bz2_script does."""
+def run_script(data, ops, bs=9, out_chunk=0, trace=None):
+    """Drive the GPU bzlib ABI like ref_bz2_script does (trace: list that gets
+    the total output after each op)."""
     L = _lib()
     s = BzStream()
     assert L.BZ2_bzCompressInit(ctypes.byref(s), bs, 0, 30) == 0
@@ -65,6 +66,8 @@ def run_script(data, ops, bs=9, out_chunk=0):
             if act == BZ_FINISH and rc == BZ_STREAM_END:
                 break
         rcs.append(rc)
+        if trace is not None:
+            trace.append(produced)
     assert (s.total_in_hi32 << 32 | s.total_in_lo32) == used
     assert (s.total_out_hi32 << 32 | s.total_out_lo32) == produced
     assert L.BZ2_bzCompressEnd(ctypes.byref(s)) == 0
@@ -117,6 +120,37 @@ def test_full_block_then_empty_finish_final_run_rule():
             want, _ = oracle_lib.ref_bz2_script(data, ops, bs=1)
             got, _ = run_script(data, ops, bs=1)
             assert got == want, ops
+
+
+@pytest.mark.skipif(oracle_lib.ref() is None, reason="oracle/_ref not built")
+def test_flush_emits_the_flushed_blocks():
+    """BZ_FLUSH makes every whole byte so far readable, as the patched library
+    does (bz:bzlib.c:437-459, the bit buffer carried across blocks by
+    bz:compress.c:609): after every FLUSH the GPU ABI has produced exactly the
+    bytes the reference libbz2 has (prefix of the final stream), also when the
+    output arrives in 997-byte pieces (BZ_FLUSH_OK draining)."""
+    r = random.Random(23)
+    for trial in range(10):
+        n = r.randint(2000, 600000)
+        data = bytes(r.choice(b"0123456789\np-") for _ in range(n))
+        ops, left = [], n
+        while left > 1 and len(ops) < 7:
+            act = r.choice([BZ_RUN, BZ_FLUSH, BZ_FLUSH])
+            k = r.randint(1 if act == BZ_RUN else 0, left // 2 + 1)
+            ops.append((act, k))
+            left -= k
+        ops.append((BZ_FLUSH, 0))                    # an empty flush: nothing new
+        ops.append((BZ_FINISH, left))
+        bs = r.choice([1, 9])
+        chunk = r.choice([0, 997])
+        want, wrcs, wafter = oracle_lib.ref_bz2_script_trace(data, ops, bs=bs, out_chunk=chunk)
+        trace = []
+        got, rcs = run_script(data, ops, bs=bs, out_chunk=chunk, trace=trace)
+        assert got == want, (trial, ops)
+        assert rcs == wrcs, (trial, ops)
+        for (act, _), a, b in zip(ops, trace, wafter):
+            if act != BZ_RUN:                        # the library also emits full blocks during RUN
+                assert a == b, (trial, ops, trace, wafter)
 
 
 def test_param_and_sequence_errors():

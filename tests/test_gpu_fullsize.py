@@ -61,3 +61,42 @@ def test_fullsize_unstarch_round_trip(cfg):
     assert len(back) == n
     assert torch.equal(torch.frombuffer(bytearray(back), dtype=torch.uint8), host)
     c.close()
+
+
+def test_cfg5_chr1_chr21_chrY_fullsize():
+    """cfg5 (per-position BED, every base of hg38) at full size for chr1
+    (248,956,422 lines, 6.0 GB -- the largest stream), chr21 and chrY:
+    each stream's SHA-256 equals the CPU path's (tests/golden/
+    fullsize_cfg5.json), and the byte-identical "0\\n" blocks are sorted once
+    (exact block reuse: at most a handful of distinct blocks per stream, the
+    rest dedup'd -- the BWT of bz:blocksort.c:1031-1089 is a pure function of
+    the block bytes)."""
+    import ctypes
+    import torch
+    import starch_amd
+    g = json.load(open(os.path.join(GOLDEN, "fullsize_cfg5.json")))
+    want = {s["chromosome"]: s for s in g["streams"]}
+    chroms = [starch_amd.HG38.index(c) for c in ("chr1", "chr21", "chrY")]
+    sizes = starch_amd.gen_bed_sizes(2, 0, chroms, seed=g["seed"])
+    for c, sz in zip(("chr1", "chr21", "chrY"), sizes):
+        assert sz == want[c]["input_bytes"], c
+    n = sum(sizes)
+    host = torch.empty(n, dtype=torch.uint8, pin_memory=True)
+    starch_amd.gen_bed(2, 0, chroms, seed=g["seed"], into=ctypes.c_void_p(host.data_ptr()))
+    dev = host.to("cuda")
+    del host
+    c = starch_amd.Starch(0)
+    c.compress_device(dev.data_ptr(), n)
+    st = c.stats()
+    idx, streams = starch_amd.parse_archive(c.archive())
+    assert [m["chromosome"] for m in idx["streams"]] == ["chr1", "chr21", "chrY"]
+    for s, meta in zip(streams, idx["streams"]):
+        w = want[meta["chromosome"]]
+        assert meta["uncompressedLineCount"] == w["lines"]
+        assert meta["transformedBytes"] == w["text_bytes"]
+        assert len(s) == w["stream_bytes"], meta["chromosome"]
+        assert hashlib.sha256(s).hexdigest() == w["sha256"], meta["chromosome"]
+    nblk = sum(m["blocks"] for m in idx["streams"])
+    assert st["n_blocks"] == nblk and nblk > 800
+    assert 0 < st["dedup_blocks"] and st["dedup_blocks"] >= nblk - 4 * 3, (st["dedup_blocks"], nblk)
+    c.close()

@@ -11,7 +11,15 @@
 // --reference-compat (stdout exactly as the reference: the 4 magic bytes),
 // --device N, --gpus N (shard chromosomes over devices 0..N-1 in one process),
 // --devices LIST (explicit device list, e.g. 0,1 or 0,0 for virtual shards),
-// --stats, --batch-mb N, --slurp.
+// --stats, --batch-mb N, --slurp, --distributed.
+//
+// --distributed: one process per GPU (e.g. `torchrun --no-python
+// --nproc-per-node 8 starch3 --distributed in.bed > out`): RANK / WORLD_SIZE /
+// LOCAL_RANK / MASTER_ADDR from the environment, the RCCL id handed out by
+// rank 0 over TCP on STARCH_COMM_PORT (default MASTER_PORT + 1).  Every rank
+// maps the input file, plans the chromosome units, encodes its LPT share on
+// its GPU, and the library's RCCL gather (starch_gather_archive) assembles the
+// archive on rank 0, which writes it to stdout.
 //
 // One device (the default): streaming ingestion -- the input
 // is read(2) in 64 MiB pieces straight into the session's pinned buffer
@@ -25,6 +33,8 @@
 #include <stdio.h>
 #include <stdlib.h>
 #include <string.h>
+#include <fcntl.h>
+#include <sys/mman.h>
 #include <sys/stat.h>
 #include <unistd.h>
 
@@ -57,15 +67,116 @@ static void usage(FILE* f)
             "  --batch-mb N          streamed encode: encode once N MiB are held (default 256)\n"
             "  --slurp               read the whole input, then encode it in one call\n"
             "  --base-counts         per-chromosome unique / non-unique base counts in the index\n"
+            "  --distributed         one process per GPU (RANK/WORLD_SIZE/LOCAL_RANK/MASTER_ADDR from the env;\n"
+            "                        input must be a file); rank 0 writes the archive\n"
             "  --help | -h           this message\n"
             "  --version | -v        version\n",
             kName, kVersion, kName, kName);
+}
+
+static int env_int(const char* k, int dflt)
+{
+    const char* v = getenv(k);
+    return v && *v ? atoi(v) : dflt;
+}
+
+static void print_stats(starch_ctx* ctx, std::chrono::steady_clock::time_point t0, uint64_t input_bytes)
+{
+    const double wall = std::chrono::duration<double>(std::chrono::steady_clock::now() - t0).count();
+    starch_stats s;
+    starch_get_stats(ctx, &s);
+    fprintf(stderr,
+            "{\"input_bytes\": %llu, \"lines\": %llu, \"segments\": %llu, \"text_bytes\": %llu, "
+            "\"archive_bytes\": %llu, \"blocks\": %llu, \"ms_total\": %.3f, \"ms_transform\": %.3f, "
+            "\"ms_rle\": %.3f, \"ms_bwt\": %.3f, \"ms_mtf\": %.3f, \"ms_tables\": %.3f, \"ms_emit\": %.3f, "
+            "\"wall_s\": %.3f, \"e2e_mb_s\": %.1f}\n",
+            (unsigned long long)input_bytes, (unsigned long long)s.n_lines, (unsigned long long)s.n_segments,
+            (unsigned long long)s.text_bytes, (unsigned long long)s.archive_bytes, (unsigned long long)s.n_blocks,
+            s.ms_total, s.ms_transform, s.ms_rle, s.ms_bwt, s.ms_mtf, s.ms_tables, s.ms_emit, wall,
+            wall > 0 ? input_bytes / wall / 1e6 : 0.0);
+}
+
+// One rank of a multi-process run: map the file, plan units, LPT
+// them over the ranks, encode this rank's share on LOCAL_RANK's GPU, gather
+// over RCCL; rank 0 writes the archive.
+static int run_distributed(const std::string& input, FILE* in, const starch_options& opt, int stats,
+                           std::chrono::steady_clock::time_point t0)
+{
+    const int rank = env_int("RANK", 0), world = env_int("WORLD_SIZE", 1), local = env_int("LOCAL_RANK", rank);
+    const char* host = getenv("MASTER_ADDR") ? getenv("MASTER_ADDR") : "127.0.0.1";
+    const int port = env_int("STARCH_COMM_PORT", env_int("MASTER_PORT", 29500) + 1);
+    if (input.empty()) {
+        fprintf(stderr, "Error: --distributed needs an input file (every rank maps it)\n");
+        return ENODATA;
+    }
+    if (in != stdin) fclose(in);
+    // stdout is the archive: anything the communication library prints (RCCL
+    // writes its version banner to stdout) goes to stderr instead
+    fflush(stdout);
+    const int out_fd = dup(STDOUT_FILENO);
+    dup2(STDERR_FILENO, STDOUT_FILENO);
+    const int fd = open(input.c_str(), O_RDONLY);
+    struct stat sb;
+    if (fd < 0 || fstat(fd, &sb) != 0) {
+        fprintf(stderr, "Error: Input file handle could not be created\n");
+        return ENODATA;
+    }
+    const uint64_t n = (uint64_t)sb.st_size;
+    const uint8_t* bed = nullptr;
+    if (n) {
+        void* m = mmap(nullptr, n, PROT_READ, MAP_PRIVATE, fd, 0);
+        if (m == MAP_FAILED) {
+            fprintf(stderr, "Error: cannot map %s\n", input.c_str());
+            close(fd);
+            return ENODATA;
+        }
+        bed = static_cast<const uint8_t*>(m);
+    }
+    std::vector<starch_unit> units(64ull * (uint64_t)world);
+    uint64_t nu = 0;
+    int rc = starch_plan_units(bed, n, units.size(), units.data(), &nu);
+    units.resize(nu);
+    std::vector<int32_t> shard_of(nu);
+    if (rc == STARCH_OK) rc = starch_assign_shards(units.data(), nu, world, shard_of.data());
+    std::vector<starch_unit> mine;
+    std::vector<uint64_t> ids;
+    for (uint64_t k = 0; k < nu; ++k)
+        if (shard_of[k] == rank) { mine.push_back(units[k]); ids.push_back(k); }
+    starch_ctx* ctx = nullptr;
+    starch_comm* comm = nullptr;
+    if (rc == STARCH_OK && (rc = starch_create(local, &ctx)) != STARCH_OK)
+        fprintf(stderr, "Error: could not open MI355X device %d (%s)\n", local, starch_strerror(rc));
+    if (rc == STARCH_OK && (rc = starch_comm_create_tcp(local, rank, world, host, port, &comm)) != STARCH_OK)
+        fprintf(stderr, "Error: rank %d: communicator (%s)\n", rank, starch_comm_last_error());
+    if (rc == STARCH_OK) rc = starch_encode_units_host(ctx, bed, mine.data(), ids.data(), mine.size(), &opt);
+    if (rc == STARCH_OK) rc = starch_gather_archive(ctx, comm, &opt);
+    if (rc == STARCH_OK && rank == 0) {
+        uint64_t an = 0;
+        starch_archive_size(ctx, &an);
+        std::vector<char> out(an);
+        rc = starch_archive_copy(ctx, out.data(), an);
+        for (uint64_t w = 0; rc == STARCH_OK && w < an;) {
+            const ssize_t k = write(out_fd, out.data() + w, an - w);
+            if (k < 0 && errno == EINTR) continue;
+            if (k <= 0) { rc = STARCH_ERR_INTERNAL; break; }
+            w += (uint64_t)k;
+        }
+    }
+    if (rc != STARCH_OK && ctx) fprintf(stderr, "Error: rank %d: %s (%s)\n", rank, starch_strerror(rc), starch_last_error(ctx));
+    if (rc == STARCH_OK && stats) print_stats(ctx, t0, n);
+    if (comm) starch_comm_destroy(comm);
+    if (ctx) starch_destroy(ctx);
+    if (bed) munmap(const_cast<uint8_t*>(bed), n);
+    close(fd);
+    close(out_fd);
+    return rc == STARCH_OK ? 0 : (rc == STARCH_ERR_MEM ? ENOMEM : EINVAL);
 }
 
 int main(int argc, char** argv)
 {
     std::string note, input;
     int methods = 0, gzip = 0, level = 9, emit_index = 1, compat = 0, device = 0, stats = 0, slurp = 0, bases = 0;
+    int distributed = 0;
     uint64_t batch_mb = 256;
     std::vector<int> devices;
     static struct option longs[] = {
@@ -76,7 +187,7 @@ int main(int argc, char** argv)
         {"device", required_argument, nullptr, 'D'}, {"stats", no_argument, nullptr, 'S'},
         {"gpus", required_argument, nullptr, 'G'},   {"devices", required_argument, nullptr, 'E'},
         {"batch-mb", required_argument, nullptr, 'M'}, {"slurp", no_argument, nullptr, 'U'},
-        {"base-counts", no_argument, nullptr, 'B'},
+        {"base-counts", no_argument, nullptr, 'B'}, {"distributed", no_argument, nullptr, 'P'},
         {nullptr, 0, nullptr, 0}};
     opterr = 0;
     int c, li;
@@ -96,6 +207,7 @@ int main(int argc, char** argv)
             case 'M': batch_mb = strtoull(optarg, nullptr, 10); break;
             case 'U': slurp = 1; break;
             case 'B': bases = 1; break;
+            case 'P': distributed = 1; break;
             case 'G': {
                 devices.clear();
                 for (int i = 0, k = atoi(optarg); i < k; ++i) devices.push_back(i);
@@ -152,6 +264,15 @@ int main(int argc, char** argv)
         return ENOSYS;
     }
     const auto t0 = std::chrono::steady_clock::now();
+    starch_options opt;
+    starch_options_init(&opt);
+    opt.block_size_100k = level;
+    opt.emit_index = emit_index;
+    opt.reference_compat = compat;
+    opt.note = note.empty() ? nullptr : note.c_str();
+    opt.base_counts = bases;
+    opt.compression_method = gzip ? STARCH_METHOD_GZIP : STARCH_METHOD_BZIP2;
+    if (distributed) return run_distributed(input, in, opt, stats, t0);
     if (devices.empty()) devices.push_back(device);
     std::vector<starch_ctx*> ctxs(devices.size(), nullptr);
     int rc = STARCH_OK;
@@ -164,14 +285,6 @@ int main(int argc, char** argv)
         }
     }
     starch_ctx* ctx = ctxs[0];
-    starch_options opt;
-    starch_options_init(&opt);
-    opt.block_size_100k = level;
-    opt.emit_index = emit_index;
-    opt.reference_compat = compat;
-    opt.note = note.empty() ? nullptr : note.c_str();
-    opt.base_counts = bases;
-    opt.compression_method = gzip ? STARCH_METHOD_GZIP : STARCH_METHOD_BZIP2;
     if (ctxs.size() == 1 && !slurp) {
         // streamed: read(2) straight into the session's pinned buffer while the
         // encoder thread works on the previous batch; drain finished streams
@@ -226,18 +339,9 @@ int main(int argc, char** argv)
     }
     fflush(stdout);
     if (stats) {
-        const double wall = std::chrono::duration<double>(std::chrono::steady_clock::now() - t0).count();
         starch_stats s;
         starch_get_stats(ctx, &s);
-        fprintf(stderr,
-                "{\"input_bytes\": %llu, \"lines\": %llu, \"segments\": %llu, \"text_bytes\": %llu, "
-                "\"archive_bytes\": %llu, \"blocks\": %llu, \"ms_total\": %.3f, \"ms_transform\": %.3f, "
-                "\"ms_rle\": %.3f, \"ms_bwt\": %.3f, \"ms_mtf\": %.3f, \"ms_tables\": %.3f, \"ms_emit\": %.3f, "
-                "\"wall_s\": %.3f, \"e2e_mb_s\": %.1f}\n",
-                (unsigned long long)s.input_bytes, (unsigned long long)s.n_lines, (unsigned long long)s.n_segments,
-                (unsigned long long)s.text_bytes, (unsigned long long)s.archive_bytes, (unsigned long long)s.n_blocks,
-                s.ms_total, s.ms_transform, s.ms_rle, s.ms_bwt, s.ms_mtf, s.ms_tables, s.ms_emit, wall,
-                wall > 0 ? s.input_bytes / wall / 1e6 : 0.0);
+        print_stats(ctx, t0, s.input_bytes);
     }
     for (auto* c : ctxs) starch_destroy(c);
     return 0;

@@ -1,17 +1,23 @@
 // tools/starch3_hpp_example.cpp -- the reference's main() (src/starch3.cpp:14-70)
 // written against include/starch3_amd.hpp: same call order on starch3::Starch,
 // with the four pthreads replaced by compress_in_stream().  With --hook the
-// archive is produced through the per-chromosome hand-off instead: the GPU
-// transform gives each chromosome's text, process_tf_buffer (hpp:393-407)
-// compresses it, finish_tf_buffers writes streams + index.  Both must give the
-// same bytes as the starch3 CLI.
+// archive is produced through the reference's per-chromosome hand-off
+// instead: the GPU transform gives each chromosome's text in `buffer`, and
+// the static process_tf_buffer (hpp:393-407) feeds it to the bz_stream set up
+// by initialize_bz_stream_ptr / setup_bz_stream_callbacks (hpp:819-862, the
+// GPU-backed patched-libbz2 ABI), whose block_close_functor records the index
+// entry; finish_tf_buffers writes the index.  Both must give the same bytes as
+// the starch3 CLI.
 #include <cstring>
 
 #include "../include/starch3_amd.hpp"
 
+starch3::Starch* starch3::self = NULL;   // cpp:10
+
 int main(int argc, char** argv)
 {
     starch3::Starch starch;
+    starch3::self = &starch;
     bool hook = argc > 1 && std::strcmp(argv[1], "--hook") == 0;
     if (argc > 1 + (hook ? 1 : 0)) starch.set_input_fn(argv[1 + (hook ? 1 : 0)]);
     starch.set_compression_method(starch3::Starch::k_bzip2);
@@ -23,28 +29,11 @@ int main(int argc, char** argv)
     if (!hook) {
         rc = starch.compress_in_stream();
     } else {
-        std::vector<unsigned char> in, buf(1 << 20);
-        size_t k;
-        while ((k = std::fread(&buf[0], 1, buf.size(), starch.get_in_stream())) > 0)
-            in.insert(in.end(), buf.begin(), buf.begin() + k);
-        starch_ctx* c = starch.context();
-        rc = starch_transform_host(c, in.empty() ? NULL : &in[0], in.size());
-        uint64_t nseg = 0, tb = 0;
-        if (!rc) rc = starch_segment_count(c, &nseg);
-        if (!rc) rc = starch_text_size(c, &tb);
-        std::vector<char> text(tb + 1);
-        std::vector<starch_segment> segs(nseg + 1);
-        if (!rc) rc = starch_text_copy(c, &text[0], tb);
-        if (!rc) rc = starch_segments(c, &segs[0], nseg);
-        for (uint64_t s = 0; s < nseg && !rc; ++s) {
-            std::string name(segs[s].name_len, '\0');
-            uint64_t len = 0;
-            rc = starch_segment_name(c, s, name.empty() ? NULL : &name[0], name.size(), &len);
-            if (!rc)   // transform-only results carry the text offset in stream_offset
-                rc = starch.process_tf_buffer(name, (int64_t)segs[s].line_count, &text[segs[s].stream_offset],
-                                              segs[s].text_bytes);
-        }
+        starch.initialize_bz_stream_ptr();          // hpp:773-776
+        starch.setup_bz_stream_callbacks(&starch);
+        rc = starch.transform_and_flush_in_stream();
         if (!rc) rc = starch.finish_tf_buffers();
+        starch.delete_bz_stream_ptr();
     }
     if (rc) {
         std::fprintf(stderr, "Error: %s\n", starch_strerror(rc));
