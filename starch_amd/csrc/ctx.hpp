@@ -4,6 +4,7 @@
 #pragma once
 #include <stdint.h>
 
+#include <atomic>
 #include <condition_variable>
 #include <mutex>
 #include <string>
@@ -17,10 +18,77 @@
 #include "transform.hpp"
 #include "untransform.hpp"
 
+// A few persistent host threads for large memcpys (streamed input lands in
+// pinned memory at several times one core's copy bandwidth).
+struct CopyPool {
+    std::vector<std::thread> th;
+    std::mutex mu;
+    std::condition_variable cv, done;
+    uint8_t* dst = nullptr;
+    const uint8_t* src = nullptr;
+    uint64_t n = 0, chunk = 0, gen = 0;
+    std::atomic<uint64_t> next{0};
+    int pending = 0;
+    bool stop = false;
+    void run(int id, uint64_t seen)
+    {
+        (void)id;
+        for (;;) {
+            {
+                std::unique_lock<std::mutex> lk(mu);
+                cv.wait(lk, [&] { return stop || gen != seen; });
+                if (stop) return;
+                seen = gen;
+            }
+            for (;;) {
+                const uint64_t k = next.fetch_add(1);
+                const uint64_t o = k * chunk;
+                if (o >= n) break;
+                memcpy(dst + o, src + o, std::min(chunk, n - o));
+            }
+            std::lock_guard<std::mutex> lk(mu);
+            if (--pending == 0) done.notify_all();
+        }
+    }
+    void copy(uint8_t* d, const uint8_t* s, uint64_t len)
+    {
+        if (len < (8ull << 20)) { memcpy(d, s, len); return; }
+        if (th.empty()) {
+            unsigned hw = std::thread::hardware_concurrency();
+            const int k = (int)std::max(1u, std::min(8u, hw / 2));
+            for (int i = 0; i < k; ++i) th.emplace_back(&CopyPool::run, this, i, (uint64_t)0);
+        }
+        {
+            std::lock_guard<std::mutex> lk(mu);
+            dst = d;
+            src = s;
+            n = len;
+            chunk = 4ull << 20;
+            next = 0;
+            pending = (int)th.size();
+            ++gen;
+        }
+        cv.notify_all();
+        std::unique_lock<std::mutex> lk(mu);
+        done.wait(lk, [&] { return pending == 0; });
+    }
+    ~CopyPool()
+    {
+        {
+            std::lock_guard<std::mutex> lk(mu);
+            stop = true;
+        }
+        cv.notify_all();
+        for (auto& t : th) t.join();
+    }
+};
+
 struct starch_ctx {
     int device = 0;
     hipStream_t own = nullptr;
     hipStream_t st = nullptr;
+    hipStream_t cst = nullptr;       // copy stream: H2D of the next batch while one encodes (pipelined host input)
+    DevBuf pin_in[2];                // the pipelined path's two device input slots
     TransformWorkspace tf;
     bz::Encoder enc;
     gz::Encoder genc;            // the gzip method (-g)
@@ -54,6 +122,12 @@ struct starch_ctx {
         // thread while the tail moves to the other buffer (double buffering)
         uint8_t* buf[2] = {nullptr, nullptr};
         uint64_t cap[2] = {0, 0};
+        // device mirrors: every committed piece is copied to dbuf[cur] at once
+        // (copy stream), so a batch is in HBM when it is handed over and the
+        // encoder thread only encodes
+        DevBuf dbuf[2];
+        hipEvent_t job_ev = nullptr;  // the handed-over batch's bytes are in HBM
+        CopyPool pool;
         int cur = 0;
         uint64_t held_n = 0, try_at = 0, batch = 0, batches = 0;
         int64_t init_start = 0, init_stop = 0;   // sscanf values current before buf[cur][0]
@@ -62,7 +136,7 @@ struct starch_ctx {
         std::mutex mu;                // guards the job slot, ready, segs/names/stats, err
         std::condition_variable cv;
         bool job = false, busy = false, stop = false;
-        const uint8_t* job_buf = nullptr;
+        const uint8_t* job_buf = nullptr;   // device (dbuf)
         uint64_t job_n = 0;
         int64_t job_is = 0, job_ip = 0;
         int err = 0;
@@ -91,6 +165,7 @@ struct starch_ctx {
         stream_shutdown();
         for (int i = 0; i < 2; ++i)
             if (sm.buf[i]) (void)hipHostFree(sm.buf[i]);
+        if (sm.job_ev) (void)hipEventDestroy(sm.job_ev);
     }
 };
 

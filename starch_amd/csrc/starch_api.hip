@@ -158,7 +158,7 @@ bool junction_differs(starch_ctx* c, const uint8_t* d_base, uint64_t lo, uint64_
 // and the unit of every segment.
 const uint8_t* transform_units(starch_ctx* c, const uint8_t* d_base, const std::vector<UnitIn>& u,
                                std::vector<SegInfo>& si, std::vector<uint64_t>& unit_of, uint64_t& text_bytes,
-                               uint64_t& n_lines)
+                               uint64_t& n_lines, bool planned = false)
 {
     si.clear();
     unit_of.clear();
@@ -166,7 +166,8 @@ const uint8_t* transform_units(starch_ctx* c, const uint8_t* d_base, const std::
     if (u.empty()) return nullptr;
     bool joint = true;
     for (size_t k = 1; k < u.size() && joint; ++k) joint = u[k].off == u[k - 1].off + u[k - 1].len;
-    for (size_t k = 1; k < u.size() && joint; ++k)
+    // units from shard::plan_units start a new chromosome by construction
+    for (size_t k = 1; k < u.size() && joint && !planned; ++k)
         if (u[k].len && u[k - 1].len) joint = junction_differs(c, d_base, u[k - 1].off, u[k].off, u[k].off + u[k].len);
     if (joint) {
         const uint64_t beg = u[0].off, end = u.back().off + u.back().len;
@@ -237,7 +238,7 @@ enum Layout { L_ARCHIVE, L_STREAMS };
 // c->archive (the whole-input result); L_STREAMS: the streams alone, back to
 // back from offset 0 of c->part (one shard of a multi-GPU run).
 void encode_units(starch_ctx* c, const uint8_t* d_base, const std::vector<UnitIn>& units, const starch_options& opt,
-                  Layout lay)
+                  Layout lay, bool planned = false)
 {
     hipEvent_t e0, e1, e2;
     HIP_CHECK(hipEventCreate(&e0));
@@ -251,7 +252,7 @@ void encode_units(starch_ctx* c, const uint8_t* d_base, const std::vector<UnitIn
     std::vector<SegInfo> si;
     std::vector<uint64_t> unit_of;
     uint64_t tbytes = 0, nlines = 0;
-    const uint8_t* text = transform_units(c, d_base, units, si, unit_of, tbytes, nlines);
+    const uint8_t* text = transform_units(c, d_base, units, si, unit_of, tbytes, nlines, planned);
     std::vector<uint64_t> bc_u, bc_n;
     if (opt.base_counts) {   // per unit (units start segments), in segment order
         std::vector<uint64_t> uu, nn;
@@ -375,6 +376,150 @@ void encode_device(starch_ctx* c, const uint8_t* d_bed, uint64_t n, const starch
 {
     std::vector<UnitIn> u(1, UnitIn{0, n, 0, 0, 0});
     encode_units(c, d_bed, u, opt, L_ARCHIVE);
+}
+
+// Pipelined encode of pinned host bytes (the one-call host path): the input
+// is cut at chromosome boundaries (shard::plan_units) into batches; batch k+1
+// crosses PCIe on the copy stream (one of two device slots) while batch k is
+// encoded, and every batch's streams are appended to the archive in HBM.  The
+// bytes equal encode_device's: units are independent (shard.cpp), the index is
+// built over all segments at the end.  Batches: about a sixth of the input
+// (at least 64 MiB), the last ones smaller, so the encode after the final
+// copy is short.
+bool host_is_pinned(const void* p)
+{
+    hipPointerAttribute_t a;
+    if (hipPointerGetAttributes(&a, p) != hipSuccess) {
+        (void)hipGetLastError();
+        return false;
+    }
+    return a.type == hipMemoryTypeHost;
+}
+
+void encode_host_pipelined(starch_ctx* c, const uint8_t* bed, uint64_t n, const starch_options& opt)
+{
+    using clk = std::chrono::steady_clock;
+    const auto t0 = clk::now();
+    std::vector<shard::Unit> plan;
+    shard::plan_units(bed, n, 4096, plan);
+    const uint64_t lim = shard::input_limit(bed, n);
+    // batches of consecutive units: a sixth of the input, shrinking toward the end
+    std::vector<std::pair<size_t, size_t>> batches;   // [u0, u1)
+    {
+        const uint64_t target = std::max<uint64_t>(64ull << 20, lim / 6);
+        uint64_t left = lim;
+        for (size_t k = 0; k < plan.size();) {
+            const uint64_t want = std::max<uint64_t>(32ull << 20, std::min<uint64_t>(target, left / 2));
+            size_t e = k;
+            uint64_t b = 0;
+            while (e < plan.size() && (b == 0 || b + plan[e].length <= want)) b += plan[e++].length;
+            batches.emplace_back(k, e);
+            left -= b;
+            k = e;
+        }
+    }
+    uint64_t maxb = 0;
+    for (auto& bt : batches) {
+        uint64_t b = 0;
+        for (size_t k = bt.first; k < bt.second; ++k) b += plan[k].length;
+        maxb = std::max(maxb, b);
+    }
+    if (!c->cst) HIP_CHECK(hipStreamCreateWithFlags(&c->cst, hipStreamNonBlocking));
+    uint8_t* slot[2] = {c->pin_in[0].as<uint8_t>(maxb + 64), c->pin_in[1].as<uint8_t>(maxb + 64)};
+    std::vector<hipEvent_t> ev(batches.size());
+    for (auto& e : ev) HIP_CHECK(hipEventCreateWithFlags(&e, hipEventDisableTiming));
+    auto h2d = [&](size_t k) {
+        const uint64_t o = plan[batches[k].first].offset;
+        uint64_t b = 0;
+        for (size_t u = batches[k].first; u < batches[k].second; ++u) b += plan[u].length;
+        if (b) HIP_CHECK(hipMemcpyAsync(slot[k & 1], bed + o, b, hipMemcpyHostToDevice, c->cst));
+        HIP_CHECK(hipEventRecord(ev[k], c->cst));
+    };
+    std::vector<starch_segment> segs;
+    std::vector<std::string> names;
+    starch_stats st{};
+    uint64_t arch_cap = 0, end = 4;
+    uint8_t* arch = nullptr;
+    auto grow = [&](uint64_t need) {
+        if (need <= arch_cap) return;
+        const uint64_t ncap = align_up(std::max<uint64_t>(need, arch_cap + arch_cap / 2) + 4096, 1 << 20);
+        DevBuf nb;
+        uint8_t* np = nb.as<uint8_t>(ncap);
+        if (arch && end) HIP_CHECK(hipMemcpyAsync(np, arch, end, hipMemcpyDeviceToDevice, c->st));
+        HIP_CHECK(hipStreamSynchronize(c->st));
+        std::swap(c->archive.p, nb.p);
+        std::swap(c->archive.cap, nb.cap);
+        arch = np;
+        arch_cap = ncap;
+    };
+    grow(lim / 3 + (1 << 20));
+    HIP_CHECK(hipMemcpyAsync(arch, kMagic, 4, hipMemcpyHostToDevice, c->st));
+    try {
+        if (!batches.empty()) h2d(0);
+        for (size_t k = 0; k < batches.size(); ++k) {
+            // slot (k+1)&1 held batch k-1, whose encode has finished (encode_units syncs)
+            if (k + 1 < batches.size()) h2d(k + 1);
+            HIP_CHECK(hipStreamWaitEvent(c->st, ev[k], 0));
+            const uint64_t base = plan[batches[k].first].offset;
+            std::vector<UnitIn> u;
+            for (size_t q = batches[k].first; q < batches[k].second; ++q)
+                u.push_back(UnitIn{plan[q].offset - base, plan[q].length, plan[q].init_start, plan[q].init_stop, q});
+            encode_units(c, slot[k & 1], u, opt, L_STREAMS, true);
+            grow(end + c->part_bytes + 64);
+            if (c->part_bytes)
+                HIP_CHECK(hipMemcpyAsync(arch + end, c->part.p, c->part_bytes, hipMemcpyDeviceToDevice, c->st));
+            for (size_t s = 0; s < c->segs.size(); ++s) {
+                starch_segment g = c->segs[s];
+                g.stream_offset += end;
+                segs.push_back(g);
+                names.push_back(c->names[s]);
+            }
+            end += c->part_bytes;
+            const starch_stats& x = c->stats;
+            st.n_lines += x.n_lines;
+            st.text_bytes += x.text_bytes;
+            st.n_blocks += x.n_blocks;
+            st.rle_bytes += x.rle_bytes;
+            st.bwt_rounds += x.bwt_rounds;
+            st.periodic_blocks += x.periodic_blocks;
+            st.bwt_tied += x.bwt_tied;
+            st.dedup_blocks += x.dedup_blocks;
+            st.ms_transform += x.ms_transform;
+            st.ms_rle += x.ms_rle;
+            st.ms_bwt += x.ms_bwt;
+            st.ms_mtf += x.ms_mtf;
+            st.ms_tables += x.ms_tables;
+            st.ms_emit += x.ms_emit;
+        }
+    } catch (...) {
+        (void)hipStreamSynchronize(c->cst);
+        for (auto& e : ev) (void)hipEventDestroy(e);
+        throw;
+    }
+    for (auto& e : ev) (void)hipEventDestroy(e);
+    std::string idx;
+    if (opt.emit_index) {
+        std::vector<const char*> np(segs.size());
+        std::vector<uint64_t> nl(segs.size());
+        for (size_t s = 0; s < segs.size(); ++s) { np[s] = names[s].data(); nl[s] = names[s].size(); }
+        idx = build_index(segs.data(), np.data(), nl.data(), segs.size(), end, opt.note, opt.block_size_100k,
+                          opt.base_counts != 0, opt.compression_method);
+        grow(end + idx.size() + 64);
+        HIP_CHECK(hipMemcpyAsync(arch + end, idx.data(), idx.size(), hipMemcpyHostToDevice, c->st));
+    }
+    HIP_CHECK(hipStreamSynchronize(c->st));
+    st.input_bytes = n;
+    st.n_segments = segs.size();
+    st.archive_bytes = end + idx.size();
+    st.ms_total = std::chrono::duration<float, std::milli>(clk::now() - t0).count();
+    c->segs.swap(segs);
+    c->names.swap(names);
+    c->stats = st;
+    c->text_bytes = 0;
+    c->text_dev = nullptr;
+    c->archive_bytes = st.archive_bytes;
+    c->have = true;
+    c->streamed = false;
 }
 
 // Multi-device encode of host bytes: plan units, LPT them over the contexts,
@@ -543,20 +688,27 @@ void stream_reserve(starch_ctx* c, int i, uint64_t need)
     const uint64_t cap = align_up(std::max<uint64_t>(need, 2 * m.cap[i]), 1ull << 20);
     void* p = nullptr;
     HIP_CHECK(hipHostMalloc(&p, cap, hipHostMallocDefault));
-    if (i == m.cur && m.held_n) memcpy(p, m.buf[i], m.held_n);
+    const bool keep = i == m.cur && m.held_n;
+    if (keep) memcpy(p, m.buf[i], m.held_n);
     if (m.buf[i]) (void)hipHostFree(m.buf[i]);
     m.buf[i] = static_cast<uint8_t*>(p);
     m.cap[i] = cap;
+    // the device mirror keeps the held bytes too (their H2D is ordered before on cst)
+    DevBuf nb;
+    uint8_t* d = nb.as<uint8_t>(cap + 64);
+    if (keep) HIP_CHECK(hipMemcpyAsync(d, m.dbuf[i].p, m.held_n, hipMemcpyDeviceToDevice, c->cst));
+    HIP_CHECK(hipStreamSynchronize(c->cst));
+    std::swap(m.dbuf[i].p, nb.p);
+    std::swap(m.dbuf[i].cap, nb.cap);
 }
 
 // encoder thread: encode b[0, n) (segment boundary to segment boundary, or to
 // the end) with the given initial values and append its streams
-void stream_encode(starch_ctx* c, const uint8_t* b, uint64_t n, int64_t is, int64_t ip)
+void stream_encode(starch_ctx* c, const uint8_t* d, uint64_t n, int64_t is, int64_t ip)
 {
     auto& m = c->sm;
     if (m.opt.reference_compat) return;   // the reference writes only the magic (hpp:765-769)
-    uint8_t* d = c->input.as<uint8_t>(n + 64);
-    HIP_CHECK(hipMemcpyAsync(d, b, n, hipMemcpyHostToDevice, c->st));
+    HIP_CHECK(hipStreamWaitEvent(c->st, m.job_ev, 0));   // the batch's H2D (copy stream) is done
     std::vector<UnitIn> u(1, UnitIn{0, n, is, ip, 0});
     encode_units(c, d, u, m.opt, L_STREAMS);
     std::vector<uint8_t> part(c->part_bytes);
@@ -646,10 +798,11 @@ void stream_submit(starch_ctx* c, uint64_t n)
 {
     auto& m = c->sm;
     m.stats.input_bytes += n;
+    HIP_CHECK(hipEventRecord(m.job_ev, c->cst));
     {
         std::lock_guard<std::mutex> lk(m.mu);
         m.job = true;
-        m.job_buf = m.buf[m.cur];
+        m.job_buf = static_cast<const uint8_t*>(m.dbuf[m.cur].p);
         m.job_n = n;
         m.job_is = m.init_start;
         m.job_ip = m.init_stop;
@@ -678,6 +831,9 @@ void stream_cut(starch_ctx* c)
     const int o = 1 - m.cur;
     stream_reserve(c, o, std::max<uint64_t>(tail + m.batch + (m.batch >> 2), 1ull << 20));
     memcpy(m.buf[o], h + cut, tail);
+    if (tail)   // the tail's device bytes move with it (ordered after their H2D on cst)
+        HIP_CHECK(hipMemcpyAsync(m.dbuf[o].p, static_cast<uint8_t*>(m.dbuf[m.cur].p) + cut, tail,
+                                 hipMemcpyDeviceToDevice, c->cst));
     stream_submit(c, cut);
     m.cur = o;
     m.held_n = tail;
@@ -745,6 +901,7 @@ void starch_destroy(starch_ctx* c)
     c->stream_shutdown();
     (void)hipSetDevice(c->device);
     (void)hipStreamSynchronize(c->st);
+    if (c->cst) (void)hipStreamDestroy(c->cst);
     if (c->own) (void)hipStreamDestroy(c->own);
     delete c;
 }
@@ -785,14 +942,21 @@ int starch_encode_host(starch_ctx* c, const void* bed, uint64_t n, const starch_
 {
     GUARD(c)
     if (n && !bed) return STARCH_ERR_ARG;
-    uint8_t* d = c->input.as<uint8_t>(n + 64);
-    if (n) HIP_CHECK(hipMemcpyAsync(d, bed, n, hipMemcpyHostToDevice, c->st));
-    HIP_CHECK(hipStreamSynchronize(c->st));
     starch_options o;
     starch_options_init(&o);
     if (opt) o = *opt;
     if (o.block_size_100k < 1 || o.block_size_100k > 9 ||
         (o.compression_method != STARCH_METHOD_BZIP2 && o.compression_method != STARCH_METHOD_GZIP)) return STARCH_ERR_ARG;
+    // large pinned inputs: PCIe copy of the next batch overlaps the encode
+    // (STARCH_PIPELINE=0 turns it off; pageable memory has no async copy)
+    static const bool pipe_off = [] { const char* e = getenv("STARCH_PIPELINE"); return e && !strcmp(e, "0"); }();
+    if (!pipe_off && !o.reference_compat && n >= (256ull << 20) && host_is_pinned(bed)) {
+        encode_host_pipelined(c, static_cast<const uint8_t*>(bed), n, o);
+        return STARCH_OK;
+    }
+    uint8_t* d = c->input.as<uint8_t>(n + 64);
+    if (n) HIP_CHECK(hipMemcpyAsync(d, bed, n, hipMemcpyHostToDevice, c->st));
+    HIP_CHECK(hipStreamSynchronize(c->st));
     encode_device(c, d, n, o);
     return STARCH_OK;
     END_GUARD(c)
@@ -1153,6 +1317,9 @@ int starch_stream_begin(starch_ctx* c, const starch_options* opt, uint64_t batch
         (o.compression_method != STARCH_METHOD_BZIP2 && o.compression_method != STARCH_METHOD_GZIP)) return STARCH_ERR_ARG;
     c->stream_shutdown();                       // a session left open is abandoned
     auto& m = c->sm;
+    if (!c->cst) HIP_CHECK(hipStreamCreateWithFlags(&c->cst, hipStreamNonBlocking));
+    if (!m.job_ev) HIP_CHECK(hipEventCreateWithFlags(&m.job_ev, hipEventDisableTiming));
+    HIP_CHECK(hipStreamSynchronize(c->cst));
     m.active = true;
     m.eof = false;
     m.note = o.note ? o.note : "";
@@ -1210,6 +1377,9 @@ int starch_stream_commit(starch_ctx* c, uint64_t n)
     if (m.eof || n == 0) return STARCH_OK;
     const uint64_t k = shard::input_limit(m.buf[m.cur] + m.held_n, n);   // 0xFF reads as EOF (hpp:181)
     if (k < n) m.eof = true;
+    if (k && !m.opt.reference_compat)
+        HIP_CHECK(hipMemcpyAsync(static_cast<uint8_t*>(m.dbuf[m.cur].p) + m.held_n, m.buf[m.cur] + m.held_n, k,
+                                 hipMemcpyHostToDevice, c->cst));
     m.held_n += k;
     if (m.held_n >= m.try_at) stream_cut(c);
     return STARCH_OK;
@@ -1225,7 +1395,7 @@ int starch_stream_feed(starch_ctx* c, const void* bed, uint64_t n)
     uint64_t cap = 0;
     int rc = starch_stream_window(c, n, &w, &cap);
     if (rc) return rc;
-    memcpy(w, bed, n);
+    c->sm.pool.copy(static_cast<uint8_t*>(w), static_cast<const uint8_t*>(bed), n);
     return starch_stream_commit(c, n);
 }
 

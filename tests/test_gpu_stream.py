@@ -134,3 +134,27 @@ def test_cli_streams_stdin(tmp_path):
     b = subprocess.run([exe, "--slurp", str(f)], capture_output=True, timeout=120)
     assert a.returncode == 0 and b.returncode == 0, (a.stderr, b.stderr)
     assert a.stdout == b.stdout == _one_call(data)
+
+
+def test_pipelined_host_encode_equals_device_encode():
+    """starch_encode_host on pinned input >= 256 MiB takes the pipelined path
+    (batches of chromosome units, H2D of the next batch on a copy stream while
+    one encodes): the archive equals the device-resident encode byte for byte."""
+    import ctypes
+    import torch
+    import starch_amd
+    n = sum(starch_amd.gen_bed_sizes(0, 12_000_000))
+    host = torch.empty(n, dtype=torch.uint8, pin_memory=True)
+    starch_amd.gen_bed(0, 12_000_000, into=ctypes.c_void_p(host.data_ptr()))
+    assert n >= (256 << 20)
+    c = starch_amd.Starch(0)
+    dev = host.to("cuda")
+    c.compress_device(dev.data_ptr(), n)
+    want = c.archive()
+    c.compress_host_ptr(host.data_ptr(), n)
+    got = c.archive()
+    assert got == want
+    segs = c.segments()
+    assert [nm.decode() for nm, _ in segs] == starch_amd.HG38
+    assert c.stats()["n_lines"] == 12_000_000
+    c.close()
