@@ -67,6 +67,11 @@ public:
               std::vector<StreamOut>& outs, Stats* stats = nullptr);
     void emit(uint8_t* d_out, uint64_t out_cap, uint64_t out_base, std::vector<StreamOut>& outs, hipStream_t st,
               Stats* stats = nullptr);
+    // Bit length of the last code written for output stream g (its last
+    // block's EOB symbol, bz:compress.c:580-593): libbz2 keeps the bits of its
+    // last bsW call in its bit buffer when a block ends (bz:compress.c:37-52),
+    // which decides how many bytes a BZ_FLUSH makes readable.  0: no blocks.
+    uint32_t last_write_bits(uint32_t g, const StreamOut& so, hipStream_t st);
 
 private:
     DevBuf b_streams, b_tiles, b_tile_sum, b_tile_carry, b_tile_w, b_tile_wpre, b_tpos, b_seg_tile0, b_seg_nblk,
@@ -83,6 +88,7 @@ private:
     uint64_t blk_stride_ = 0;
     uint64_t gpre_off_ = 0;                 // words: the per-block prefix rows in b_gbits
     const uint32_t* src_of_dev_ = nullptr;  // block -> data index (null: identity)
+    std::vector<uint32_t> src_of_host_;     // the same on the host (empty: identity)
     std::vector<StreamIn> streams_;
     std::vector<BlockDesc> host_blocks_;
 };

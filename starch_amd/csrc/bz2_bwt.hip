@@ -346,125 +346,272 @@ __device__ void fb_qsort3(uint32_t* fmap, const uint32_t* ecls, int32_t lo0, int
     }
 }
 
-// One workgroup per periodic block.  fmap <- V, eclass <- RK (as scratch),
-// head flags <- U (u32 0/1), mixed flags <- U2.
-__global__ void __launch_bounds__(BT) k_fallback_exact(BlockDesc* __restrict__ blocks, uint32_t b0,
-                                                        const uint32_t* __restrict__ which, uint32_t nwhich,
-                                                        const uint8_t* __restrict__ blkbytes, uint64_t stride,
-                                                        BwtScratch scr)
+// ---------------------------------------------------------------------------
+// fallbackSort for periodic blocks, round by round on the whole GPU.
+//
+// The reference's tie order is the output here, so every step is the exact
+// bz:blocksort.c:211-329 procedure; only the work placement is new:
+//   * per doubling round H, grid-wide kernels: eclass from the bucket heads
+//     (a max-scan of head positions), then key[i] = eclass[fmap[i]] next to
+//     fmap (eclass does not change while a round's buckets are sorted, so the
+//     sort moves (key, fmap) pairs and never gathers), mixed-bucket detection
+//     and the count of not-done elements (nNotDone), then new heads;
+//   * fallbackQSort3 (bz:blocksort.c:93-180) on each MIXED bucket -- an
+//     all-equal bucket is left exactly as it is by it -- one wave per bucket,
+//     buckets in parallel (r restarts at 0 per call, bz:blocksort.c:104): a
+//     bucket of <= FB_CAP elements is staged in the wave's LDS and sorted
+//     there by lane 0 (the whole call, stack and LCG included); a larger one
+//     is partitioned by lane 0 in HBM until the range it pops fits, then that
+//     range's whole subtree is sorted in LDS, so the order of partition steps
+//     -- and with it the LCG sequence -- is the serial one.
+// fmap lives in SA, eclass in RK, key in V, head flags in U, mixed stamps in
+// U2, the head-position scan in K, the mixed-bucket list in K2, counters in V2.
+// ---------------------------------------------------------------------------
+constexpr int FB_WAVES = 4;
+constexpr uint32_t FB_CAP = 4096;          // pairs per wave in LDS (32 KB)
+
+// fallbackSimpleSort (bz:blocksort.c:30-59) on (key, fmap) pairs
+__device__ __forceinline__ void fbp_simple(uint32_t* key, uint32_t* fm, int32_t lo, int32_t hi)
+{
+    if (lo == hi) return;
+    if (hi - lo > 3) {
+        for (int32_t a = hi - 4; a >= lo; --a) {
+            const uint32_t x = fm[a], kx = key[a];
+            int32_t q = a + 4;
+            while (q <= hi && kx > key[q]) { fm[q - 4] = fm[q]; key[q - 4] = key[q]; q += 4; }
+            fm[q - 4] = x;
+            key[q - 4] = kx;
+        }
+    }
+    for (int32_t a = hi - 1; a >= lo; --a) {
+        const uint32_t x = fm[a], kx = key[a];
+        int32_t q = a + 1;
+        while (q <= hi && kx > key[q]) { fm[q - 1] = fm[q]; key[q - 1] = key[q]; ++q; }
+        fm[q - 1] = x;
+        key[q - 1] = kx;
+    }
+}
+
+__device__ __forceinline__ void fbp_swap(uint32_t* key, uint32_t* fm, int32_t a, int32_t b)
+{
+    const uint32_t t = fm[a], k = key[a];
+    fm[a] = fm[b];
+    key[a] = key[b];
+    fm[b] = t;
+    key[b] = k;
+}
+
+// one partition step of fallbackQSort3 on [lo, hi] (hi - lo >= 10): the LCG
+// advance, the pivot, the 3-way partition and the two vswaps; returns the
+// two sub-ranges [lo, *n] and [*m, hi] (n < lo / m > hi: empty) in the order
+// they are pushed (a first), or false when every key equals the pivot
+__device__ __forceinline__ bool fbp_partition(uint32_t* key, uint32_t* fm, int32_t lo, int32_t hi, uint32_t& r, int32_t& alo,
+                              int32_t& ahi, int32_t& blo, int32_t& bhi)
+{
+    r = (r * 7621u + 1u) % 32768u;                              // bz:blocksort.c:126-130
+    const uint32_t r3 = r % 3u;
+    const uint32_t med = r3 == 0 ? key[lo] : r3 == 1 ? key[(lo + hi) >> 1] : key[hi];
+    int32_t unLo = lo, ltLo = lo, unHi = hi, gtHi = hi;
+    for (;;) {
+        while (unLo <= unHi) {
+            const uint32_t k = key[unLo];
+            if (k == med) { fbp_swap(key, fm, unLo, ltLo); ++ltLo; ++unLo; continue; }
+            if (k > med) break;
+            ++unLo;
+        }
+        while (unLo <= unHi) {
+            const uint32_t k = key[unHi];
+            if (k == med) { fbp_swap(key, fm, unHi, gtHi); --gtHi; --unHi; continue; }
+            if (k < med) break;
+            --unHi;
+        }
+        if (unLo > unHi) break;
+        fbp_swap(key, fm, unLo, unHi);
+        ++unLo;
+        --unHi;
+    }
+    if (gtHi < ltLo) return false;
+    int32_t n = ltLo - lo < unLo - ltLo ? ltLo - lo : unLo - ltLo;
+    for (int32_t a = lo, b = unLo - n; n > 0; --n, ++a, ++b) fbp_swap(key, fm, a, b);
+    int32_t m = hi - gtHi < gtHi - unHi ? hi - gtHi : gtHi - unHi;
+    for (int32_t a = unLo, b = hi - m + 1; m > 0; --m, ++a, ++b) fbp_swap(key, fm, a, b);
+    const int32_t nn = lo + unLo - ltLo - 1, mm = hi - (gtHi - unHi) + 1;
+    if (nn - lo > hi - mm) { alo = lo; ahi = nn; blo = mm; bhi = hi; }   // larger pushed first
+    else { alo = mm; ahi = hi; blo = lo; bhi = nn; }
+    return true;
+}
+
+// the whole fallbackQSort3 call on [lo0, hi0] (any memory), continuing LCG r
+__device__ __forceinline__ void fbp_qsort3(uint32_t* key, uint32_t* fm, int32_t lo0, int32_t hi0, uint32_t& r)
+{
+    int32_t slo[100], shi[100];                                  // FALLBACK_QSORT_STACK_SIZE
+    int32_t sp = 0;
+    slo[sp] = lo0; shi[sp] = hi0; ++sp;
+    while (sp > 0) {
+        --sp;
+        const int32_t lo = slo[sp], hi = shi[sp];
+        if (hi - lo < 10) { fbp_simple(key, fm, lo, hi); continue; }   // FALLBACK_QSORT_SMALL_THRESH
+        int32_t alo, ahi, blo, bhi;
+        if (!fbp_partition(key, fm, lo, hi, r, alo, ahi, blo, bhi)) continue;
+        slo[sp] = alo; shi[sp] = ahi; ++sp;
+        slo[sp] = blo; shi[sp] = bhi; ++sp;
+    }
+}
+
+// 1-byte bucket sort of the block (bz:blocksort.c:240-249: indices descending
+// inside a bucket) and the first heads; one workgroup
+__global__ void __launch_bounds__(BT) k_fb_init(const uint8_t* __restrict__ blk, uint32_t n, BwtScratch scr,
+                                                 uint64_t so)
 {
     __shared__ RadixSmem sm;
-    __shared__ uint32_t carry[4];
     const int tid = threadIdx.x;
-    if (blockIdx.x >= nwhich) return;
-    const uint32_t slot = which[blockIdx.x];        // batch-relative block index
-    const uint32_t b = b0 + slot;
-    const uint32_t n = blocks[b].n;
-    const uint8_t* blk = blkbytes + (uint64_t)b * stride;
-    const uint64_t so = (uint64_t)slot * scr.stride;
     uint64_t* K = scr.K + so;
     uint64_t* K2 = scr.K2 + so;
-    uint32_t* fmap = scr.V + so;
+    uint32_t* V = scr.V + so;
     uint32_t* V2 = scr.V2 + so;
-    uint32_t* SA = scr.SA + so;
-    uint32_t* ecls = scr.RK + so;
+    uint32_t* fmap = scr.SA + so;
     uint32_t* head = scr.U + so;
-    uint32_t* mixed = scr.U2 + so;
-
-    // initial 1-byte bucket sort: within a bucket, indices DESCENDING (bz:blocksort.c:245-249)
-    for (uint32_t i = tid; i < n; i += BT) { K[i] = blk[i]; fmap[i] = i; }
+    for (uint32_t i = tid; i < n; i += BT) { K[i] = blk[i]; V[i] = i; }
     __syncthreads();
-    uint64_t* Kp = K; uint64_t* K2p = K2; uint32_t* Vp = fmap; uint32_t* V2p = V2;
-    radix_sort<uint32_t>(Kp, Vp, K2p, V2p, n, 8, sm);
-    // bucket bounds: reuse hist via a fresh count
-    for (int i = tid; i < 256; i += BT) { sm.hist[i] = 0; }
+    uint64_t* Kp = K; uint64_t* K2p = K2; uint32_t* Vp = V; uint32_t* V2p = V2;
+    radix_sort<uint32_t>(Kp, Vp, K2p, V2p, n, 8, sm);          // stable ascending
+    for (int i = tid; i < 256; i += BT) sm.hist[i] = 0;
     __syncthreads();
     for (uint32_t i = tid; i < n; i += BT) atomicAdd(&sm.hist[blk[i]], 1u);
     __syncthreads();
     if (tid == 0) { uint32_t a = 0; for (int c = 0; c < 256; ++c) { sm.base[c] = a; a += sm.hist[c]; } }
     __syncthreads();
     for (uint32_t j = tid; j < n; j += BT) {
-        uint32_t c = (uint32_t)Kp[j];
-        uint32_t bs = sm.base[c], be = bs + sm.hist[c];
-        SA[bs + be - 1 - j] = Vp[j];
+        const uint32_t c = (uint32_t)Kp[j];
+        const uint32_t bs = sm.base[c], be = bs + sm.hist[c];
+        fmap[bs + be - 1 - j] = Vp[j];
         head[j] = 0;
     }
     __syncthreads();
     for (int c = tid; c < 256; c += BT) if (sm.hist[c]) head[sm.base[c]] = 1;
-    __syncthreads();
-    fmap = SA;   // fmap now lives in SA
-    for (uint64_t H = 1;; H *= 2) {
-        // eclass[fmap[i]-H] = last head at or before i
-        if (tid == 0) carry[0] = 0;
-        __syncthreads();
-        for (uint32_t t0 = 0; t0 < n; t0 += BT) {
-            uint32_t i = t0 + tid;
-            bool valid = i < n;
-            uint32_t hv = (valid && head[i]) ? i : 0u;
-            uint32_t j = block_incl_scan_max<uint32_t>(hv, sm.scan);
-            uint32_t cm = carry[0];
-            j = j > cm ? j : cm;
-            if (valid) {
-                int64_t k = (int64_t)fmap[i] - (int64_t)H;
-                k %= (int64_t)n;
-                if (k < 0) k += n;
-                ecls[k] = j;
-                mixed[i] = 0;
-            }
-            if (tid == BT - 1) carry[0] = j;
-            __syncthreads();
-        }
-        // mark buckets whose keys are not all equal (group head l = max-scan of heads)
-        if (tid == 0) { carry[0] = 0; carry[1] = 0; }
-        __syncthreads();
-        for (uint32_t t0 = 0; t0 < n; t0 += BT) {
-            uint32_t i = t0 + tid;
-            bool valid = i < n;
-            uint32_t hv = (valid && head[i]) ? i : 0u;
-            uint32_t l = block_incl_scan_max<uint32_t>(hv, sm.scan);
-            uint32_t cm = carry[0];
-            l = l > cm ? l : cm;
-            bool nd = valid && !(head[i] && (i + 1 >= n || head[i + 1]));
-            if (valid && !head[i] && ecls[fmap[i]] != ecls[fmap[l]]) mixed[l] = 1;
-            uint32_t c = 0;
-            c = nd ? 1u : 0u;
-            uint32_t tot;
-            (void)block_excl_scan_add<uint32_t>(c, sm.scan, &tot);
-            if (tid == BT - 1) { carry[0] = l; carry[1] += tot; }
-            __syncthreads();
-        }
-        uint32_t not_done = carry[1];
-        __syncthreads();
-        // mixed buckets: exact fallbackQSort3, one thread per bucket, in any order
-        // (buckets are disjoint and r restarts per call, bz:blocksort.c:104)
-        for (uint32_t l = tid; l < n; l += BT) {
-            if (head[l] && mixed[l]) {
-                uint32_t r = l + 1;
-                while (r < n && !head[r]) ++r;
-                fb_qsort3(fmap, ecls, (int32_t)l, (int32_t)(r - 1));
-            }
-        }
-        __syncthreads();
-        // new heads where eclass changes inside mixed buckets
-        for (uint32_t t0 = 0; t0 < n; t0 += BT) {
-            uint32_t i = t0 + tid;
-            bool valid = i < n;
-            uint32_t hv = (valid && head[i]) ? i : 0u;
-            uint32_t l = block_incl_scan_max<uint32_t>(hv, sm.scan);
-            if (tid == 0 && t0 == 0) carry[0] = 0;
-            uint32_t cm = (t0 == 0) ? 0u : carry[0];
-            l = l > cm ? l : cm;
-            bool set = valid && !head[i] && mixed[l] && ecls[fmap[i]] != ecls[fmap[i - 1]];
-            __syncthreads();
-            if (set) head[i] = 1;
-            if (tid == BT - 1) carry[0] = l;
-            __syncthreads();
-        }
-        if (2 * H > n || not_done == 0) break;
+}
+
+__global__ void k_fb_hp(const uint32_t* __restrict__ head, uint64_t* __restrict__ hp, uint32_t n)
+{
+    const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
+    if (i < n) hp[i] = head[i] ? i : 0u;
+}
+
+// eclass[fmap[i] - H mod n] = bucket start of i (bz:blocksort.c:258-263)
+__global__ void k_fb_eclass(const uint32_t* __restrict__ fmap, const uint64_t* __restrict__ hp,
+                            uint32_t* __restrict__ ecls, uint32_t n, uint32_t hmod)
+{
+    const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= n) return;
+    uint32_t k = fmap[i] + (n - hmod);
+    if (k >= n) k -= n;
+    ecls[k] = (uint32_t)hp[i];
+}
+
+// key[i] = eclass[fmap[i]]; mixed buckets stamped; not-done elements counted
+__global__ void __launch_bounds__(256) k_fb_key(const uint32_t* __restrict__ fmap, const uint32_t* __restrict__ ecls,
+                                                const uint32_t* __restrict__ head, const uint64_t* __restrict__ hp,
+                                                uint32_t* __restrict__ key, uint32_t* __restrict__ mixed,
+                                                uint32_t* __restrict__ ctr, uint32_t n, uint32_t stamp)
+{
+    const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
+    uint32_t nd = 0;
+    if (i < n) {
+        const uint32_t k = ecls[fmap[i]];
+        key[i] = k;
+        const uint32_t l = (uint32_t)hp[i];
+        if (!head[i] && k != ecls[fmap[l]]) mixed[l] = stamp;
+        nd = (head[i] && (i + 1 == n || head[i + 1])) ? 0u : 1u;   // in a bucket of >= 2
     }
-    __syncthreads();
-    for (uint32_t j = tid; j < n; j += BT)
-        if (SA[j] == 0) blocks[b].orig_ptr = j;
+    nd = wave_reduce_add<uint32_t>(nd);
+    if ((threadIdx.x & 63) == 0 && nd) atomicAdd(ctr, nd);
+}
+
+// list the mixed buckets [l, r] (packed l << 32 | r)
+__global__ void k_fb_list(const uint32_t* __restrict__ head, const uint64_t* __restrict__ hp,
+                          const uint32_t* __restrict__ mixed, uint64_t* __restrict__ list, uint32_t* __restrict__ ctr,
+                          uint32_t n, uint32_t stamp)
+{
+    const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x + 1;   // bucket ending at i - 1
+    if (i > n) return;
+    if (i < n && !head[i]) return;
+    const uint32_t l = (uint32_t)hp[i - 1];
+    if (mixed[l] != stamp) return;
+    list[atomicAdd(ctr, 1u)] = ((uint64_t)l << 32) | (i - 1);
+}
+
+// fallbackQSort3 on every listed bucket: one wave per bucket (persistent)
+__global__ void __launch_bounds__(64 * FB_WAVES) k_fb_sort(uint32_t* __restrict__ fmap, uint32_t* __restrict__ key,
+                                                           const uint64_t* __restrict__ list,
+                                                           const uint32_t* __restrict__ nlist, uint32_t* __restrict__ next)
+{
+    __shared__ uint32_t sk_all[FB_WAVES][FB_CAP], sf_all[FB_WAVES][FB_CAP];
+    __shared__ int32_t cmd_all[FB_WAVES][4];
+    const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+    uint32_t* sk = sk_all[w];
+    uint32_t* sf = sf_all[w];
+    int32_t* cmd = cmd_all[w];
+    const uint32_t total = *nlist;
+    for (;;) {
+        uint32_t idx = 0;
+        if (lane == 0) idx = atomicAdd(next, 1u);
+        idx = (uint32_t)__shfl((int)idx, 0, 64);
+        if (idx >= total) break;
+        const uint64_t e = list[idx];
+        const int32_t l = (int32_t)(e >> 32), rr = (int32_t)(uint32_t)e;
+        // lane 0 drives the call's stack; the wave stages ranges that fit the LDS
+        int32_t slo[100], shi[100];
+        int32_t sp = 0;
+        uint32_t lcg = 0;
+        if (lane == 0) { slo[0] = l; shi[0] = rr; sp = 1; }
+        for (;;) {
+            if (lane == 0) {
+                cmd[0] = 0;
+                while (sp > 0) {
+                    --sp;
+                    const int32_t lo = slo[sp], hi = shi[sp];
+                    if (hi - lo < 10) { fbp_simple(key, fmap, lo, hi); continue; }
+                    if ((uint32_t)(hi - lo + 1) <= FB_CAP) { cmd[0] = 1; cmd[1] = lo; cmd[2] = hi; break; }
+                    int32_t alo, ahi, blo, bhi;
+                    if (!fbp_partition(key, fmap, lo, hi, lcg, alo, ahi, blo, bhi)) continue;
+                    slo[sp] = alo; shi[sp] = ahi; ++sp;
+                    slo[sp] = blo; shi[sp] = bhi; ++sp;
+                }
+            }
+            __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+            __builtin_amdgcn_wave_barrier();
+            __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+            if (cmd[0] == 0) break;                                // the call is done
+            const int32_t lo = cmd[1], hi = cmd[2], m = hi - lo + 1;
+            for (int32_t q = lane; q < m; q += 64) { sk[q] = key[lo + q]; sf[q] = fmap[lo + q]; }
+            __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+            __builtin_amdgcn_wave_barrier();
+            __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+            if (lane == 0) fbp_qsort3(sk, sf, 0, m - 1, lcg);      // the range's whole subtree, in order
+            __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+            __builtin_amdgcn_wave_barrier();
+            __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+            for (int32_t q = lane; q < m; q += 64) { key[lo + q] = sk[q]; fmap[lo + q] = sf[q]; }
+            __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+            __builtin_amdgcn_wave_barrier();
+            __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+        }
+    }
+}
+
+// new heads where the key changes inside a sorted mixed bucket (bz:blocksort.c:299-306)
+__global__ void k_fb_heads(const uint32_t* __restrict__ key, const uint64_t* __restrict__ hp,
+                           const uint32_t* __restrict__ mixed, uint32_t* __restrict__ head, uint32_t n, uint32_t stamp)
+{
+    const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
+    if (i == 0 || i >= n || head[i]) return;
+    if (mixed[(uint32_t)hp[i]] == stamp && key[i] != key[i - 1]) head[i] = 1;
+}
+
+__global__ void k_fb_origptr(const uint32_t* __restrict__ fmap, BlockDesc* __restrict__ blocks, uint32_t b, uint32_t n)
+{
+    const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
+    if (i < n && fmap[i] == 0) blocks[b].orig_ptr = i;
 }
 
 void launch_bwt(BlockDesc* blocks, uint32_t b0, uint32_t nb, const uint8_t* blkbytes, uint64_t stride,
@@ -474,13 +621,53 @@ void launch_bwt(BlockDesc* blocks, uint32_t b0, uint32_t nb, const uint8_t* blkb
     HIP_CHECK(hipGetLastError());
 }
 
-void launch_fallback(BlockDesc* blocks, uint32_t b0, const uint32_t* which, uint32_t nwhich,
-                     const uint8_t* blkbytes, uint64_t stride, const BwtScratch& scr, hipStream_t st)
+void launch_fallback(BlockDesc* blocks, uint32_t b0, const uint32_t* which_host, const uint32_t* n_host,
+                     uint32_t nwhich, const uint8_t* blkbytes, uint64_t stride, const BwtScratch& scr, DevBuf& tmp,
+                     uint32_t* hctr, hipStream_t st)
 {
-    if (!nwhich) return;
-    hipLaunchKernelGGL(k_fallback_exact, dim3(nwhich), dim3(BT), 0, st, blocks, b0, which, nwhich, blkbytes, stride,
-                       scr);
-    HIP_CHECK(hipGetLastError());
+    int dev = 0, ncu = 256;
+    HIP_CHECK(hipGetDevice(&dev));
+    hipDeviceProp_t prop;
+    if (hipGetDeviceProperties(&prop, dev) == hipSuccess && prop.multiProcessorCount > 0) ncu = prop.multiProcessorCount;
+    for (uint32_t q = 0; q < nwhich; ++q) {
+        const uint32_t slot = which_host[q], b = b0 + slot, n = n_host[q];
+        if (n == 0) continue;
+        const uint64_t so = (uint64_t)slot * scr.stride;
+        uint32_t* fmap = scr.SA + so;
+        uint32_t* ecls = scr.RK + so;
+        uint32_t* key = scr.V + so;
+        uint32_t* head = scr.U + so;
+        uint32_t* mixed = scr.U2 + so;
+        uint64_t* hp = scr.K + so;
+        uint64_t* list = scr.K2 + so;
+        uint32_t* ctr = scr.V2 + so;                      // [0] not done, [1] mixed buckets, [2] next bucket
+        hipLaunchKernelGGL(k_fb_init, dim3(1), dim3(BT), 0, st, blkbytes + (uint64_t)b * stride, n, scr, so);
+        HIP_CHECK(hipMemsetAsync(mixed, 0, (uint64_t)n * sizeof(uint32_t), st));
+        const dim3 g((n + 255) / 256), g1((n + 256) / 256);
+        uint32_t stamp = 0;
+        for (uint64_t H = 1;; H *= 2) {
+            ++stamp;
+            HIP_CHECK(hipMemsetAsync(ctr, 0, 4 * sizeof(uint32_t), st));
+            hipLaunchKernelGGL(k_fb_hp, g, dim3(256), 0, st, head, hp, n);
+            scan::incl_max_u64(hp, n, tmp, st);
+            hipLaunchKernelGGL(k_fb_eclass, g, dim3(256), 0, st, fmap, hp, ecls, n, (uint32_t)(H % n));
+            hipLaunchKernelGGL(k_fb_key, g, dim3(256), 0, st, fmap, ecls, head, hp, key, mixed, ctr, n, stamp);
+            hipLaunchKernelGGL(k_fb_list, g1, dim3(256), 0, st, head, hp, mixed, list, ctr + 1, n, stamp);
+            HIP_CHECK(hipGetLastError());
+            HIP_CHECK(hipMemcpyAsync(hctr, ctr, 2 * sizeof(uint32_t), hipMemcpyDeviceToHost, st));
+            HIP_CHECK(hipStreamSynchronize(st));
+            const uint32_t not_done = hctr[0], nmixed = hctr[1];
+            if (nmixed) {
+                const uint32_t wg = std::min<uint32_t>((nmixed + FB_WAVES - 1) / FB_WAVES, (uint32_t)ncu);
+                hipLaunchKernelGGL(k_fb_sort, dim3(wg), dim3(64 * FB_WAVES), 0, st, fmap, key, list, ctr + 1, ctr + 2);
+                hipLaunchKernelGGL(k_fb_heads, g, dim3(256), 0, st, key, hp, mixed, head, n, stamp);
+                HIP_CHECK(hipGetLastError());
+            }
+            if (2 * H > n || not_done == 0) break;         // H *= 2; if (H > nblock || nNotDone == 0) break
+        }
+        hipLaunchKernelGGL(k_fb_origptr, g, dim3(256), 0, st, fmap, blocks, b, n);
+        HIP_CHECK(hipGetLastError());
+    }
 }
 
 }  // namespace bz

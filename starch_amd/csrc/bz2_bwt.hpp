@@ -24,8 +24,12 @@ void launch_bwt(BlockDesc* blocks, uint32_t b0, uint32_t nb, const uint8_t* blkb
 void launch_bwt3(BlockDesc* blocks, uint32_t b0, uint32_t nb, const uint8_t* blkbytes, uint64_t stride,
                  const BwtScratch& scr, DevBuf& meta, uint32_t* hctr, unsigned long long* stats, hipStream_t st,
                  bool wide = false);   // wide: some block has 17..20 symbols (8192-bin mixed-radix top digit)
-void launch_fallback(BlockDesc* blocks, uint32_t b0, const uint32_t* which, uint32_t nwhich,
-                     const uint8_t* blkbytes, uint64_t stride, const BwtScratch& scr, hipStream_t st);
+// periodic blocks: bzip2's exact fallbackSort tie order (bz:blocksort.c:211-329),
+// round by round on the GPU; which_host / n_host: batch slots and block sizes;
+// hctr: pinned host memory (>= 2 u32)
+void launch_fallback(BlockDesc* blocks, uint32_t b0, const uint32_t* which_host, const uint32_t* n_host,
+                     uint32_t nwhich, const uint8_t* blkbytes, uint64_t stride, const BwtScratch& scr, DevBuf& tmp,
+                     uint32_t* hctr, hipStream_t st);
 // last column for blocks whose SA was produced elsewhere (fallback / LSD path)
 void launch_last_col(const BlockDesc* blocks, uint32_t b0, const uint32_t* which, uint32_t nwhich,
                      const uint8_t* blkbytes, uint64_t stride, const BwtScratch& scr, hipStream_t st);

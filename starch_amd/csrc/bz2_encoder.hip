@@ -211,7 +211,9 @@ void Encoder::plan(const uint8_t* d_text, const std::vector<StreamIn>& streams, 
     BlockDesc* d_bl = d_blocks;              // blocks the sort / MTF / tables run over
     const uint8_t* d_bytes = d_blkbytes;
     src_of_dev_ = nullptr;
+    src_of_host_.clear();
     if (reuse) {
+        src_of_host_ = src_of;
         uint32_t* d_idx = b_dedupe.as<uint32_t>(2ull * nb + 16);
         HIP_CHECK(hipMemcpyAsync(d_idx, reps.data(), nr * sizeof(uint32_t), hipMemcpyHostToDevice, st));
         HIP_CHECK(hipMemcpyAsync(d_idx + nb, src_of.data(), nb * sizeof(uint32_t), hipMemcpyHostToDevice, st));
@@ -291,13 +293,14 @@ void Encoder::plan(const uint8_t* d_text, const std::vector<StreamIn>& streams, 
             HIP_CHECK(hipMemcpyAsync(hr.data() + b0, d_bl + b0, cnt * sizeof(BlockDesc), hipMemcpyDeviceToHost,
                                      st));
             HIP_CHECK(hipStreamSynchronize(st));
-            std::vector<uint32_t> which;
+            std::vector<uint32_t> which, wn;
             for (uint32_t k = 0; k < cnt; ++k)
-                if (hr[b0 + k].flags & 1u) which.push_back(k);
+                if (hr[b0 + k].flags & 1u) { which.push_back(k); wn.push_back(hr[b0 + k].n); }
             if (!which.empty()) {
                 HIP_CHECK(hipMemcpyAsync(d_which, which.data(), which.size() * sizeof(uint32_t),
                                          hipMemcpyHostToDevice, st));
-                launch_fallback(d_bl, b0, d_which, (uint32_t)which.size(), d_bytes, blk_stride_, scr, st);
+                launch_fallback(d_bl, b0, which.data(), wn.data(), (uint32_t)which.size(), d_bytes, blk_stride_, scr,
+                                b_tmp, h_ctr_.get(), st);
                 if (stats) stats->periodic_blocks += which.size();
             }
             // the v3 sort writes the last column next to SA; the v1 sort and the
@@ -396,6 +399,23 @@ void Encoder::emit(uint8_t* d_out, uint64_t out_cap, uint64_t out_base, std::vec
         outs[s].combined_crc = comb;
     }
     te.stop();
+}
+
+uint32_t Encoder::last_write_bits(uint32_t g, const StreamOut& so, hipStream_t st)
+{
+    (void)g;
+    if (so.n_blocks == 0) return 0;
+    const uint32_t b = so.first_block + so.n_blocks - 1;
+    const BlockDesc& bd = host_blocks_[b];
+    const uint32_t src = src_of_host_.empty() ? b : src_of_host_[b];
+    const uint8_t* d_sel = static_cast<const uint8_t*>(b_sel.p) + (uint64_t)src * 2 * kMaxSelectors + (bd.n_sel - 1);
+    uint8_t t = 0, len = 0;
+    HIP_CHECK(hipMemcpyAsync(&t, d_sel, 1, hipMemcpyDeviceToHost, st));
+    HIP_CHECK(hipStreamSynchronize(st));
+    const Tables* tab = static_cast<const Tables*>(b_tabs.p) + src;
+    HIP_CHECK(hipMemcpyAsync(&len, &tab->len[t][bd.n_in_use + 1], 1, hipMemcpyDeviceToHost, st));   // EOB = nInUse + 1
+    HIP_CHECK(hipStreamSynchronize(st));
+    return len;
 }
 
 uint64_t Encoder::plan_and_encode(const uint8_t* d_text, const std::vector<StreamIn>& streams, int bs100k,

@@ -38,6 +38,9 @@ struct GpuStreamState {
     std::vector<uint8_t> input;         // bytes of the open piece
     std::vector<uint8_t> output;        // whole bytes not yet drained
     uint64_t out_pos = 0;
+    uint64_t released = 0;              // output[0, released) may be drained (the library's numZ)
+    uint64_t total_bits = 0;            // bits of the stream so far
+    uint32_t last_n = 0;                // bits of the last write (bsW) so far
     uint32_t tail = 0, tail_bits = 0;   // bits not yet a whole byte (right-aligned, < 8)
     bool header = false;                // "BZh<level>" written (first BZ2_compressBlock)
     bool pending_piece = false;         // a FINISH failed: the closed piece is still to encode
@@ -140,6 +143,7 @@ void consume(GpuStreamState* g)
 
 void put_bits(GpuStreamState* g, uint32_t v, uint32_t n)   // n <= 24, MSB first
 {
+    g->total_bits += n;
     g->tail = (g->tail << n) | (v & ((1u << n) - 1u));
     g->tail_bits += n;
     while (g->tail_bits >= 8) {
@@ -152,6 +156,7 @@ void put_bits(GpuStreamState* g, uint32_t v, uint32_t n)   // n <= 24, MSB first
 // append bits [bit0, bit0 + nbits) of src (MSB-first bit string)
 void put_stream_bits(GpuStreamState* g, const uint8_t* src, uint64_t bit0, uint64_t nbits)
 {
+    const uint64_t tb = g->total_bits;
     uint64_t b = bit0;
     const uint64_t e = bit0 + nbits;
     while (b < e && (b & 7)) {   // to a source byte boundary
@@ -176,6 +181,16 @@ void put_stream_bits(GpuStreamState* g, const uint8_t* src, uint64_t bit0, uint6
     }
     b += whole * 8;
     for (; b < e; ++b) put_bits(g, (src[b >> 3] >> (7 - (b & 7))) & 1u, 1);
+    g->total_bits = tb + nbits;
+}
+
+// bytes libbz2 has emitted at the end of a block: bsW flushes whole bytes only
+// BEFORE adding bits (bsNEEDW, bz:compress.c:37-52), so after the last write of
+// n bits, ((T - n) mod 8) + n bits stay in its buffer
+void release(GpuStreamState* g)
+{
+    const uint64_t keep = ((g->total_bits - g->last_n) & 7u) + g->last_n;
+    g->released = (g->total_bits - keep) / 8;
 }
 
 // BZ2_compressBlock for the open piece (bz:compress.c:602-667): encode it on
@@ -184,6 +199,7 @@ int encode_piece(GpuStreamState* g, bool supplied)
 {
     std::vector<uint8_t> tmp;
     bz::StreamOut so{};
+    uint32_t last = 0;
     if (!g->input.empty()) {
         Slot* sl = nullptr;
         try {
@@ -205,6 +221,7 @@ int encode_piece(GpuStreamState* g, bool supplied)
             uint8_t* d_out = sl->out.as<uint8_t>(cap);
             sl->enc.emit(d_out, cap, 0, outs, sl->st, nullptr);
             so = outs[0];
+            last = sl->enc.last_write_bits(0, so, sl->st);
             tmp.resize(so.bytes);
             HIP_CHECK(hipMemcpyAsync(tmp.data(), d_out, so.bytes, hipMemcpyDeviceToHost, sl->st));
             HIP_CHECK(hipStreamSynchronize(sl->st));
@@ -220,6 +237,7 @@ int encode_piece(GpuStreamState* g, bool supplied)
         put_bits(g, 'h', 8);
         put_bits(g, (uint32_t)('0' + g->bs100k), 8);
         g->header = true;
+        g->last_n = 8;
     }
     if (so.n_blocks) {
         put_stream_bits(g, tmp.data(), 32, so.block_bits);   // after the piece stream's own header
@@ -228,7 +246,9 @@ int encode_piece(GpuStreamState* g, bool supplied)
         const uint32_t k = so.n_blocks & 31u;
         g->combined = (k ? (g->combined << k) | (g->combined >> (32 - k)) : g->combined) ^ so.combined_crc;
         g->n_blocks += so.n_blocks;
+        g->last_n = last;
     }
+    release(g);
     g->input.clear();
     return BZ_OK;
 }
@@ -240,13 +260,14 @@ void finish_stream(GpuStreamState* g)   // trailer + combined CRC + byte pad
     put_bits(g, g->combined >> 16, 16);
     put_bits(g, g->combined & 0xFFFFu, 16);
     if (g->tail_bits) put_bits(g, 0, 8 - g->tail_bits);
+    g->released = g->output.size();   // bsFinishWrite
     g->input.shrink_to_fit();
 }
 
 bool drain(GpuStreamState* g)
 {
     bz_stream* s = g->strm;
-    uint64_t left = g->output.size() - g->out_pos;
+    uint64_t left = g->released - g->out_pos;
     uint64_t k = left < s->avail_out ? left : s->avail_out;
     if (k) {
         memcpy(s->next_out, g->output.data() + g->out_pos, k);
@@ -255,8 +276,9 @@ bool drain(GpuStreamState* g)
         g->out_pos += k;
         add_out(s, k);
     }
-    if (g->out_pos == g->output.size()) {
-        g->output.clear();
+    if (g->out_pos == g->released && g->out_pos > (1u << 20)) {   // compact the drained prefix
+        g->output.erase(g->output.begin(), g->output.begin() + (std::ptrdiff_t)g->out_pos);
+        g->released -= g->out_pos;
         g->out_pos = 0;
     }
     return k > 0;
@@ -319,7 +341,7 @@ int BZ2_bzCompress(bz_stream* strm, int action)
                 }
                 if (action == BZ_FLUSH) {
                     drain(g);
-                    if (!g->output.empty()) { g->mode = M_FLUSHING; return BZ_FLUSH_OK; }   // bz:bzlib.c:451-459
+                    if (g->out_pos < g->released) { g->mode = M_FLUSHING; return BZ_FLUSH_OK; }   // bz:bzlib.c:451-459
                     return BZ_RUN_OK;
                 }
                 finish_stream(g);
@@ -330,7 +352,7 @@ int BZ2_bzCompress(bz_stream* strm, int action)
         case M_FLUSHING:   // avail_in_expect is 0: everything was consumed by the first FLUSH call
             if (action != BZ_FLUSH || strm->avail_in != 0) return BZ_SEQUENCE_ERROR;
             drain(g);
-            if (!g->output.empty()) return BZ_FLUSH_OK;
+            if (g->out_pos < g->released) return BZ_FLUSH_OK;
             g->mode = M_RUNNING;
             return BZ_RUN_OK;
         case M_FINISHING:
@@ -345,7 +367,7 @@ int BZ2_bzCompress(bz_stream* strm, int action)
             if (!g->pending_finish) {
                 g->mode = M_RUNNING;
                 drain(g);
-                if (!g->output.empty()) { g->mode = M_FLUSHING; return BZ_FLUSH_OK; }
+                if (g->out_pos < g->released) { g->mode = M_FLUSHING; return BZ_FLUSH_OK; }
                 return BZ_RUN_OK;
             }
             finish_stream(g);
@@ -356,7 +378,7 @@ int BZ2_bzCompress(bz_stream* strm, int action)
     }
     // FINISHING: drain the encoded stream
     bool progress = drain(g);
-    if (!g->output.empty()) return progress ? BZ_FINISH_OK : BZ_SEQUENCE_ERROR;
+    if (g->out_pos < g->released) return progress ? BZ_FINISH_OK : BZ_SEQUENCE_ERROR;
     g->mode = M_IDLE;
     if (strm->block_close_functor) strm->block_close_functor(strm->handler);   // bz:bzlib.c:470
     return BZ_STREAM_END;

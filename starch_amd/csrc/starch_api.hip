@@ -20,6 +20,26 @@ const uint8_t kMagic[4] = {0xca, 0x5c, 0xad, 0x1a};   // hpp:907-910
 
 namespace {
 
+// STARCH_TRACE=1: host-side timeline of the batched paths on stderr
+double trace_t0()
+{
+    static const auto t0 = std::chrono::steady_clock::now();
+    return std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count();
+}
+bool tracing()
+{
+    static const bool on = getenv("STARCH_TRACE") != nullptr;
+    return on;
+}
+#define STRACE(...)                                                              \
+    do {                                                                         \
+        if (tracing()) {                                                         \
+            fprintf(stderr, "[starch %9.3f ms] ", trace_t0());                   \
+            fprintf(stderr, __VA_ARGS__);                                        \
+            fputc('\n', stderr);                                                \
+        }                                                                        \
+    } while (0)
+
 int fail(starch_ctx* c, const StarchError& e)
 {
     if (c) c->err = e.what();
@@ -438,8 +458,8 @@ void encode_host_pipelined(starch_ctx* c, const uint8_t* bed, uint64_t n, const 
     std::vector<starch_segment> segs;
     std::vector<std::string> names;
     starch_stats st{};
-    uint64_t arch_cap = 0, end = 4;
-    uint8_t* arch = nullptr;
+    uint64_t arch_cap = c->archive.cap, end = 4;   // the context's archive buffer is reused across calls
+    uint8_t* arch = static_cast<uint8_t*>(c->archive.p);
     auto grow = [&](uint64_t need) {
         if (need <= arch_cap) return;
         const uint64_t ncap = align_up(std::max<uint64_t>(need, arch_cap + arch_cap / 2) + 4096, 1 << 20);
@@ -464,7 +484,10 @@ void encode_host_pipelined(starch_ctx* c, const uint8_t* bed, uint64_t n, const 
             std::vector<UnitIn> u;
             for (size_t q = batches[k].first; q < batches[k].second; ++q)
                 u.push_back(UnitIn{plan[q].offset - base, plan[q].length, plan[q].init_start, plan[q].init_stop, q});
+            STRACE("pipelined batch %zu: %zu units, encode", k, u.size());
             encode_units(c, slot[k & 1], u, opt, L_STREAMS, true);
+            STRACE("pipelined batch %zu: encoded, %llu stream bytes, device %.3f ms", k,
+                   (unsigned long long)c->part_bytes, c->stats.ms_total);
             grow(end + c->part_bytes + 64);
             if (c->part_bytes)
                 HIP_CHECK(hipMemcpyAsync(arch + end, c->part.p, c->part_bytes, hipMemcpyDeviceToDevice, c->st));
@@ -708,13 +731,16 @@ void stream_encode(starch_ctx* c, const uint8_t* d, uint64_t n, int64_t is, int6
 {
     auto& m = c->sm;
     if (m.opt.reference_compat) return;   // the reference writes only the magic (hpp:765-769)
+    STRACE("stream batch %llu: %llu bytes, encode", (unsigned long long)m.batches, (unsigned long long)n);
     HIP_CHECK(hipStreamWaitEvent(c->st, m.job_ev, 0));   // the batch's H2D (copy stream) is done
     std::vector<UnitIn> u(1, UnitIn{0, n, is, ip, 0});
     encode_units(c, d, u, m.opt, L_STREAMS);
+    STRACE("stream batch %llu: encoded, device %.3f ms", (unsigned long long)m.batches, c->stats.ms_total);
     std::vector<uint8_t> part(c->part_bytes);
     if (c->part_bytes)
         HIP_CHECK(hipMemcpyAsync(part.data(), c->part.p, c->part_bytes, hipMemcpyDeviceToHost, c->st));
     HIP_CHECK(hipStreamSynchronize(c->st));
+    STRACE("stream batch %llu: streams read back", (unsigned long long)m.batches);
     std::lock_guard<std::mutex> lk(m.mu);
     m.ready.insert(m.ready.end(), part.begin(), part.end());
     for (size_t s = 0; s < c->segs.size(); ++s) {
@@ -827,7 +853,9 @@ void stream_cut(starch_ctx* c)
         return;
     }
     const uint64_t cut = u.back().offset, tail = m.held_n - cut;
+    STRACE("stream cut at %llu of %llu held: wait for the encoder", (unsigned long long)cut, (unsigned long long)m.held_n);
     stream_wait(c);                                   // the other buffer is free again
+    STRACE("stream cut: encoder idle");
     const int o = 1 - m.cur;
     stream_reserve(c, o, std::max<uint64_t>(tail + m.batch + (m.batch >> 2), 1ull << 20));
     memcpy(m.buf[o], h + cut, tail);

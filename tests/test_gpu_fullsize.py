@@ -97,6 +97,6 @@ def test_cfg5_chr1_chr21_chrY_fullsize():
         assert len(s) == w["stream_bytes"], meta["chromosome"]
         assert hashlib.sha256(s).hexdigest() == w["sha256"], meta["chromosome"]
     nblk = sum(m["blocks"] for m in idx["streams"])
-    assert st["n_blocks"] == nblk and nblk > 800
+    assert st["n_blocks"] == nblk and nblk > 700   # 553 + 104 + 127 full blocks + tails
     assert 0 < st["dedup_blocks"] and st["dedup_blocks"] >= nblk - 4 * 3, (st["dedup_blocks"], nblk)
     c.close()
