@@ -4,9 +4,13 @@
 
 namespace bz {
 
-struct BwtScratch {            // 40 bytes per rotation per batch slot
+struct BwtScratch {            // 58 bytes per rotation per batch slot
     uint64_t* K;
     uint64_t* K2;
+    uint64_t* KM0;             // round 0 (bwt3): every rotation's key window next to SA, and the
+    uint64_t* KM1;             //   partition ping-pong copy (no key gathers in the round-0 sorts)
+    uint8_t* LS0;              // round 0: the rotation's last-column symbol next to SA, ping-pong
+    uint8_t* LS1;
     uint32_t* V;
     uint32_t* V2;
     uint32_t* SA;              // sorted rotation order (ptr[] of bz:blocksort.c)

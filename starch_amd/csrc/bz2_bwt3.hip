@@ -153,7 +153,11 @@ struct Ctx {
     uint32_t lsel;          // L list that part/classify pushes into
     uint32_t tsel;          // tie list the sorts push into
     uint32_t mode;          // 0: SA only (round 0, text rounds); 1: doubling (RK, runs)
-    uint32_t keysrc;        // 0: PSS at the text-round offset; 1: K2/K (doubling)
+    uint32_t keysrc;        // 0: PSS at the text-round offset; 1: keys by group position (kA/kB)
+    uint64_t* kA;           // keysrc 1: keys of parity-0 items (round 0: KM0, doubling: K2) ...
+    uint64_t* kB;           // ... and of parity-1 items (round 0: KM1, doubling: K)
+    uint8_t* lA;            // round 0: last-column symbols by position, parity 0 / 1 (LS0 / LS1);
+    uint8_t* lB;            //   null while doubling (then read from the block bytes)
     uint32_t rtext;         // text round (0: round 0)
     uint32_t* qhead;        // 8 queue heads of the current persistent launch
     const uint32_t* qseg;   // 9 per-XCD segment offsets of the current binned list
@@ -240,7 +244,8 @@ __device__ __forceinline__ uint64_t pss_bits(const uint64_t* __restrict__ w, uin
 // Key of a group element: rotation r (PSS modes) or group position q (K2/K).
 struct KeySrc {
     const uint64_t* pss;
-    const uint64_t* k;      // doubling keys of this group's buffer (K2 or K by parity), slot base
+    const uint64_t* k;      // keys by position of this group's buffer (kA or kB by parity), slot base
+    const uint8_t* l;       // last-column symbols by position (lA / lB by parity), slot base; or null
     uint32_t B, kbits, n, off, usek;
     __device__ __forceinline__ uint64_t operator()(uint64_t q, uint32_t r) const
     {
@@ -305,7 +310,8 @@ __device__ __forceinline__ KeySrc key_src(const Ctx& c, uint32_t slot, uint32_t 
     k.B = g.B;
     k.usek = c.keysrc;
     k.pss = c.scr.K + so;
-    k.k = (par ? c.scr.K : c.scr.K2) + so;
+    k.k = (par ? c.kB : c.kA) + so;
+    k.l = c.lA ? (par ? c.lB : c.lA) + so : nullptr;
     if (c.rtext == 0) {
         k.kbits = g.KB;
         k.off = 0;
@@ -343,7 +349,7 @@ __device__ __forceinline__ uint64_t elem_key(const Ctx& c, const KeySrc& ks, uin
                                              uint32_t& ls)
 {
     if constexpr (DBL) {
-        ls = last_sym(c, slot, v);
+        ls = ks.l ? ks.l[q] : last_sym(c, slot, v);
         return ks.k[q];
     } else {
         return ks.key_pss(v, ls);
@@ -649,6 +655,11 @@ __global__ void __launch_bounds__(SCT) k3_scatter_lds(Ctx c)
     __shared__ uint32_t scan_sh[SCT / 64 + 1];
     __shared__ uint32_t qs[8];
     __shared__ uint32_t job_sh;
+    // round 0 writes every rotation's key window and last-column symbol next to
+    // its SA entry (KM0 / LS0), from the stage's PSS words held in LDS
+    constexpr uint32_t PWN = (SH_HALF + 1) * 8 / 64 + 4;   // words for B <= 8
+    __shared__ uint64_t pw[PWN];
+    const bool mat = c.lA != nullptr;
     const int tid = threadIdx.x;
     const uint32_t x = xcc_id();
     if (tid < 8) qs[tid] = ((uint32_t)tid < c.nb ? (c.nb - tid + 7) / 8 : 0u) * MAXT;
@@ -669,10 +680,20 @@ __global__ void __launch_bounds__(SCT) k3_scatter_lds(Ctx c)
         const uint32_t B = geo.B;
         const uint64_t* pss = c.scr.K + so;
         uint32_t* SA = c.scr.SA + so;
+        uint64_t* KM = c.kA + so;
+        uint8_t* LS = c.lA ? c.lA + so : nullptr;
         const uint32_t e = n - t0 < (uint32_t)PTILE ? n - t0 : (uint32_t)PTILE;
         for (uint32_t h0 = 0; h0 < e; h0 += SH_HALF) {
             const uint32_t he = e - h0 < SH_HALF ? e - h0 : SH_HALF;
             for (int i = tid; i < NB; i += SCT) lst[i] = 0;
+            // PSS words of this stage's keys and last symbols: rotations
+            // [t0 + h0 - 1, t0 + h0 + he) plus one key window
+            const uint32_t rs = t0 + h0;
+            const uint64_t wbase = rs ? ((uint64_t)(rs - 1) * B) >> 6 : 0;
+            if (mat) {
+                const uint64_t wend = (((uint64_t)(rs + he) * B + 64) >> 6) + 2;
+                for (uint64_t w = wbase + tid; w < wend; w += SCT) pw[w - wbase] = pss[w];
+            }
             __syncthreads();
             // digits of SU consecutive rotations from four PSS words; local counts
             const uint32_t q0 = tid * SU;                // SCT * SU == SH_HALF
@@ -715,8 +736,22 @@ __global__ void __launch_bounds__(SCT) k3_scatter_lds(Ctx c)
                 const uint32_t dg = v >> 15, r = t0 + (v & 0x7FFFu);
                 const uint32_t pos = cur[dg] + (j - lst[dg]);
                 SA[pos] = r;
+                uint32_t ls = 0;
+                if (mat && r) {
+                    const uint64_t bit = (uint64_t)(r - 1) * B - (wbase << 6);
+                    const uint32_t q = (uint32_t)(bit >> 6), p = (uint32_t)(bit & 63u);
+                    ls = (uint32_t)(((pw[q] << p) | ((pw[q + 1] >> 1) >> (63u - p))) >> (64u - B));
+                } else if (mat || tot[dg] == 1u) {
+                    ls = (uint32_t)pss_bits(pss, (uint64_t)(r ? r - 1u : n - 1u) * B, B);
+                }
+                if (mat) {
+                    const uint64_t bit = (uint64_t)r * B - (wbase << 6);
+                    const uint32_t q = (uint32_t)(bit >> 6), p = (uint32_t)(bit & 63u);
+                    KM[pos] = ((pw[q] << p) | ((pw[q + 1] >> 1) >> (63u - p))) >> (64u - geo.KB);
+                    LS[pos] = (uint8_t)ls;
+                }
                 if (tot[dg] == 1u) {                   // singleton bucket: final
-                    c.scr.LL[so + pos] = (uint8_t)pss_bits(pss, (uint64_t)(r ? r - 1u : n - 1u) * B, B);
+                    c.scr.LL[so + pos] = (uint8_t)ls;
                     if (r == 0) c.blocks[b].orig_ptr = pos;
                 }
             }
@@ -842,7 +877,8 @@ __global__ void __launch_bounds__(LT) k3_part_l(Ctx c, const uint64_t* __restric
         const KeySrc ks = key_src(c, slot, par);
         const uint32_t* sv = (par ? c.scr.V : c.scr.SA) + base;
         uint32_t* dv = (par ? c.scr.SA : c.scr.V) + base;
-        uint64_t* dk = (par ? c.scr.K2 : c.scr.K) + base;      // doubling keys only
+        uint64_t* dk = (par ? c.kA : c.kB) + base;              // keys by position (keysrc 1) only
+        uint8_t* dl = DBL && ks.l ? (par ? c.lA : c.lB) + base : nullptr;   // round 0: last symbols move too
         uint32_t* SA = c.scr.SA + base;
         uint32_t* RK = c.scr.RK + so;
         const uint32_t db = shift < 8 ? shift : 8;
@@ -877,6 +913,7 @@ __global__ void __launch_bounds__(LT) k3_part_l(Ctx c, const uint64_t* __restric
         for (uint32_t i0 = 0; i0 < m; i0 += PU * LT) {
             uint32_t v[PU];
             uint64_t k[PU];
+            uint8_t lsy[PU];
 #pragma unroll
             for (int u = 0; u < PU; ++u) {
                 const uint32_t i = i0 + u * LT + tid;
@@ -884,6 +921,7 @@ __global__ void __launch_bounds__(LT) k3_part_l(Ctx c, const uint64_t* __restric
                 v[u] = sv[ic];
                 if (!DBL && m <= PL_CAP) k[u] = (uint64_t)dcache[ic] << sh2;   // only the digit is used below
                 else k[u] = elem_key<DBL>(ks, s + ic, v[u]);
+                lsy[u] = dl ? ks.l[s + ic] : (uint8_t)0;
             }
 #pragma unroll
             for (int u = 0; u < PU; ++u) {
@@ -891,6 +929,7 @@ __global__ void __launch_bounds__(LT) k3_part_l(Ctx c, const uint64_t* __restric
                     const uint32_t p = atomicAdd(&cur[(uint32_t)((k[u] >> sh2) & dmask)], 1u);
                     dv[p] = v[u];
                     if constexpr (DBL) dk[p] = k[u];
+                    if (dl) dl[p] = lsy[u];
                 }
             }
         }
@@ -901,7 +940,7 @@ __global__ void __launch_bounds__(LT) k3_part_l(Ctx c, const uint64_t* __restric
             if (cc == 1) {
                 const uint32_t v = dv[ss];
                 if (!par) SA[ss] = v;
-                c.scr.LL[base + ss] = last_sym(c, slot, v);
+                c.scr.LL[base + ss] = dl ? dl[ss] : last_sym(c, slot, v);
                 if (c.mode) RK[v] = s + ss;
                 if (v == 0) c.blocks[b].orig_ptr = s + ss;
                 nruns = 1;
@@ -927,7 +966,7 @@ __global__ void __launch_bounds__(LT) k3_part_l(Ctx c, const uint64_t* __restric
             for (uint32_t i = tid; i < cc; i += LT) {
                 const uint32_t v = dv[ss + i];
                 if (!par) SA[ss + i] = v;
-                c.scr.LL[base + ss + i] = last_sym(c, slot, v);
+                c.scr.LL[base + ss + i] = dl ? dl[ss + i] : last_sym(c, slot, v);
                 if (c.mode) RK[v] = s + ss;
                 if (v == 0) c.blocks[b].orig_ptr = s + ss + i;
             }
@@ -2186,6 +2225,9 @@ void launch_bwt3(BlockDesc* blocks, uint32_t b0, uint32_t nb, const uint8_t* blk
     c.tsel = 0;
     c.mode = 0;
     c.keysrc = 0;
+    c.kA = scr.K2;
+    c.kB = scr.K;
+    c.lA = c.lB = nullptr;
     c.rtext = 0;
     c.qhead = nullptr;
     c.qseg = nullptr;
@@ -2353,7 +2395,17 @@ void launch_bwt3(BlockDesc* blocks, uint32_t b0, uint32_t nb, const uint8_t* blk
         HIP_CHECK(hipMemsetAsync(c.L.ctr + C_M0, 0, sizeof(uint32_t), st));
     };
 
-    // ---- round 0: packed prefix keys ----
+    // ---- round 0: packed prefix keys, materialised next to SA by the scatter
+    // (STARCH_KMAT=0: gathered from the PSS by every sort, as the text rounds do) ----
+    static const bool direct = [] { const char* e = getenv("STARCH_SCATTER"); return e && !strcmp(e, "direct"); }();
+    static const bool kmat = [] { const char* e = getenv("STARCH_KMAT"); return !(e && !strcmp(e, "0")); }();
+    if (kmat && !direct) {   // (the direct scatter writes SA only)
+        c.keysrc = 1;
+        c.kA = scr.KM0;
+        c.kB = scr.KM1;
+        c.lA = scr.LS0;
+        c.lB = scr.LS1;
+    }
     {
         const uint32_t maxw = (uint32_t)pss_words(scr.stride);
         hipLaunchKernelGGL(k3_pss, dim3((maxw + 255) / 256, nb), dim3(256), 0, st, c);
@@ -2371,7 +2423,6 @@ void launch_bwt3(BlockDesc* blocks, uint32_t b0, uint32_t nb, const uint8_t* blk
         c.qseg = nullptr;
         // about one block in flight per XCD: one 1024-thread workgroup per CU,
         // a block's MAXT tiles spread over its XCD's CUs
-        static const bool direct = [] { const char* e = getenv("STARCH_SCATTER"); return e && !strcmp(e, "direct"); }();
         const dim3 gsc((ncu + 7) / 8 * 8);
         if (direct && wide) hipLaunchKernelGGL(k3_scatter<PNB_WIDE>, gsc, dim3(SCT), 0, st, c);
         else if (direct) hipLaunchKernelGGL(k3_scatter<PNB>, gsc, dim3(SCT), 0, st, c);
@@ -2380,6 +2431,10 @@ void launch_bwt3(BlockDesc* blocks, uint32_t b0, uint32_t nb, const uint8_t* blk
         HIP_CHECK(hipGetLastError());
     }
     sort_groups();
+    c.keysrc = 0;                    // text rounds read the PSS at an offset
+    c.kA = scr.K2;
+    c.kB = scr.K;
+    c.lA = c.lB = nullptr;
     // ---- text rounds: extend the tied rotations' keys from the PSS ----
     uint32_t rtext = 0;
     uint64_t prev_tied = ~0ull;
