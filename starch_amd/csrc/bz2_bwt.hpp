@@ -4,10 +4,10 @@
 
 namespace bz {
 
-struct BwtScratch {            // 58 bytes per rotation per batch slot
+struct BwtScratch {            // 40 (+18 with bwt_kmat) bytes per rotation per batch slot
     uint64_t* K;
     uint64_t* K2;
-    uint64_t* KM0;             // round 0 (bwt3): every rotation's key window next to SA, and the
+    uint64_t* KM0;             // round 0 (bwt3, bwt_kmat() only, else null): every rotation's key window next to SA, and the
     uint64_t* KM1;             //   partition ping-pong copy (no key gathers in the round-0 sorts)
     uint8_t* LS0;              // round 0: the rotation's last-column symbol next to SA, ping-pong
     uint8_t* LS1;
@@ -21,6 +21,10 @@ struct BwtScratch {            // 58 bytes per rotation per batch slot
     uint64_t stride;           // elements per slot
 };
 
+// STARCH_KMAT=1: round 0 materialises keys + last symbols next to SA (measured
+// slower on cfg2: 25.9 vs 23.7 ms, the extra 18 B/rotation of writes cost more
+// than the gathers they save); the encoder allocates KM0..LS1 only when set
+bool bwt_kmat();
 void launch_bwt(BlockDesc* blocks, uint32_t b0, uint32_t nb, const uint8_t* blkbytes, uint64_t stride,
                 const BwtScratch& scr, unsigned long long* stats, hipStream_t st);
 // v3 (default): batch-wide segmented sort + doubling on ties (bz2_bwt3.hip).

@@ -2171,6 +2171,12 @@ __global__ void k3_finish(Ctx c, uint32_t nb, unsigned long long* stats)
 }  // namespace
 
 // Host orchestration.  A handful of host round trips per batch (list sizes).
+bool bwt_kmat()
+{
+    static const bool on = [] { const char* e = getenv("STARCH_KMAT"); return e && !strcmp(e, "1"); }();
+    return on;
+}
+
 void launch_bwt3(BlockDesc* blocks, uint32_t b0, uint32_t nb, const uint8_t* blkbytes, uint64_t stride,
                  const BwtScratch& scr, DevBuf& meta, uint32_t* hctr, unsigned long long* stats, hipStream_t st,
                  bool wide)
@@ -2395,11 +2401,10 @@ void launch_bwt3(BlockDesc* blocks, uint32_t b0, uint32_t nb, const uint8_t* blk
         HIP_CHECK(hipMemsetAsync(c.L.ctr + C_M0, 0, sizeof(uint32_t), st));
     };
 
-    // ---- round 0: packed prefix keys, materialised next to SA by the scatter
-    // (STARCH_KMAT=0: gathered from the PSS by every sort, as the text rounds do) ----
+    // ---- round 0: packed prefix keys gathered from the PSS by every sort, as
+    // the text rounds do (bwt_kmat(): materialised next to SA by the scatter) ----
     static const bool direct = [] { const char* e = getenv("STARCH_SCATTER"); return e && !strcmp(e, "direct"); }();
-    static const bool kmat = [] { const char* e = getenv("STARCH_KMAT"); return !(e && !strcmp(e, "0")); }();
-    if (kmat && !direct) {   // (the direct scatter writes SA only)
+    if (bwt_kmat() && scr.KM0 && !direct) {   // (the direct scatter writes SA only)
         c.keysrc = 1;
         c.kA = scr.KM0;
         c.kB = scr.KM1;

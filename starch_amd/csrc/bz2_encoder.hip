@@ -239,7 +239,8 @@ void Encoder::plan(const uint8_t* d_text, const std::vector<StreamIn>& streams, 
     uint32_t* d_gbits = b_gbits.as<uint32_t>((uint64_t)(nr + nb) * kMaxSelectors);
     gpre_off_ = (uint64_t)nr * kMaxSelectors;
     HIP_CHECK(hipMemGetInfo(&free_b, &total_b));
-    const uint64_t per_slot = blk_stride_ * 59ull;       // 58 B of sort scratch + 1 B last column
+    const bool kmat = bwt_kmat();
+    const uint64_t per_slot = blk_stride_ * (kmat ? 59ull : 41ull);   // sort scratch + 1 B last column
     uint64_t max_batch = std::max<uint64_t>(1, (uint64_t)(free_b * 0.45) / per_slot);
 #ifndef STARCH_BATCH_MAX
 #define STARCH_BATCH_MAX 2048
@@ -265,11 +266,17 @@ void Encoder::plan(const uint8_t* d_text, const std::vector<StreamIn>& streams, 
         scr.RK = scr.SA + S * batch;
         scr.U = scr.RK + S * batch;
         scr.U2 = scr.U + S * batch;
-        scr.KM0 = reinterpret_cast<uint64_t*>(scr.U2 + S * batch);
-        scr.KM1 = scr.KM0 + S * batch;
-        scr.LS0 = reinterpret_cast<uint8_t*>(scr.KM1 + S * batch);
-        scr.LS1 = scr.LS0 + S * batch;
-        scr.LL = scr.LS1 + S * batch;
+        if (kmat) {
+            scr.KM0 = reinterpret_cast<uint64_t*>(scr.U2 + S * batch);
+            scr.KM1 = scr.KM0 + S * batch;
+            scr.LS0 = reinterpret_cast<uint8_t*>(scr.KM1 + S * batch);
+            scr.LS1 = scr.LS0 + S * batch;
+            scr.LL = scr.LS1 + S * batch;
+        } else {
+            scr.KM0 = scr.KM1 = nullptr;
+            scr.LS0 = scr.LS1 = nullptr;
+            scr.LL = reinterpret_cast<uint8_t*>(scr.U2 + S * batch);
+        }
     }
     unsigned long long* d_stats = reinterpret_cast<unsigned long long*>(d_scal);
     HIP_CHECK(hipMemsetAsync(d_stats, 0, 4 * sizeof(uint64_t), st));

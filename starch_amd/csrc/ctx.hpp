@@ -4,8 +4,12 @@
 #pragma once
 #include <stdint.h>
 
+#include <string.h>
+
+#include <algorithm>
 #include <atomic>
 #include <condition_variable>
+#include <memory>
 #include <mutex>
 #include <string>
 #include <thread>
@@ -28,6 +32,8 @@ struct CopyPool {
     const uint8_t* src = nullptr;
     uint64_t n = 0, chunk = 0, gen = 0;
     std::atomic<uint64_t> next{0};
+    std::atomic<uint64_t> ff{0};
+    bool find_ff = false;
     int pending = 0;
     bool stop = false;
     void run(int id, uint64_t seen)
@@ -44,11 +50,34 @@ struct CopyPool {
                 const uint64_t k = next.fetch_add(1);
                 const uint64_t o = k * chunk;
                 if (o >= n) break;
-                memcpy(dst + o, src + o, std::min(chunk, n - o));
+                const uint64_t len = std::min(chunk, n - o);
+                memcpy(dst + o, src + o, len);
+                if (find_ff) {   // while the chunk is in cache: its first 0xFF
+                    const void* f = memchr(dst + o, 0xFF, len);
+                    if (f) {
+                        const uint64_t at = o + (uint64_t)(static_cast<const uint8_t*>(f) - (dst + o));
+                        uint64_t cur = ff.load();
+                        while (at < cur && !ff.compare_exchange_weak(cur, at)) {}
+                    }
+                }
             }
             std::lock_guard<std::mutex> lk(mu);
             if (--pending == 0) done.notify_all();
         }
+    }
+    // copy and return the offset of the first 0xFF in the bytes (len if none)
+    uint64_t copy_find_ff(uint8_t* d, const uint8_t* s, uint64_t len)
+    {
+        if (len < (8ull << 20)) {
+            memcpy(d, s, len);
+            const void* f = memchr(d, 0xFF, len);
+            return f ? (uint64_t)(static_cast<const uint8_t*>(f) - d) : len;
+        }
+        find_ff = true;
+        ff = len;
+        copy(d, s, len);
+        find_ff = false;
+        return ff.load();
     }
     void copy(uint8_t* d, const uint8_t* s, uint64_t len)
     {
@@ -89,6 +118,8 @@ struct starch_ctx {
     hipStream_t st = nullptr;
     hipStream_t cst = nullptr;       // copy stream: H2D of the next batch while one encodes (pipelined host input)
     DevBuf pin_in[2];                // the pipelined path's two device input slots
+    DevBuf collect;                  // the pipelined path: this lane's finished streams, batch after batch
+    std::vector<std::unique_ptr<starch_ctx>> lanes;   // the pipelined path's extra lanes (same device)
     TransformWorkspace tf;
     bz::Encoder enc;
     gz::Encoder genc;            // the gzip method (-g)
@@ -130,6 +161,8 @@ struct starch_ctx {
         CopyPool pool;
         int cur = 0;
         uint64_t held_n = 0, try_at = 0, batch = 0, batches = 0;
+        double t_copy = 0, t_commit = 0;   // STARCH_TRACE: feed-side time
+        uint64_t fed = 0;
         int64_t init_start = 0, init_stop = 0;   // sscanf values current before buf[cur][0]
         // encoder thread and its one job slot
         std::thread worker;
@@ -160,9 +193,17 @@ struct starch_ctx {
         sm.stop = false;
         sm.active = false;
     }
+    bool is_lane = false;             // an extra lane: owns its streams (starch_destroy does the others')
     ~starch_ctx()
     {
         stream_shutdown();
+        lanes.clear();
+        if (is_lane) {
+            (void)hipSetDevice(device);
+            if (own) (void)hipStreamSynchronize(own);
+            if (cst) (void)hipStreamDestroy(cst);
+            if (own) (void)hipStreamDestroy(own);
+        }
         for (int i = 0; i < 2; ++i)
             if (sm.buf[i]) (void)hipHostFree(sm.buf[i]);
         if (sm.job_ev) (void)hipEventDestroy(sm.job_ev);

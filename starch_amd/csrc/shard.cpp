@@ -124,8 +124,13 @@ uint64_t input_limit(const uint8_t* b, uint64_t n)
 void plan_units(const uint8_t* b, uint64_t n, uint64_t max_units, std::vector<Unit>& out, int64_t init_start0,
                 int64_t init_stop0)
 {
+    plan_units_upto(b, input_limit(b, n), max_units, out, init_start0, init_stop0);
+}
+
+void plan_units_upto(const uint8_t* b, uint64_t lim, uint64_t max_units, std::vector<Unit>& out, int64_t init_start0,
+                     int64_t init_stop0)
+{
     out.clear();
-    const uint64_t lim = input_limit(b, n);
     if (lim == 0) return;
     if (max_units < 1) max_units = 1;
     uint64_t s = 0;

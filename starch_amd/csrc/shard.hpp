@@ -17,6 +17,9 @@ uint64_t input_limit(const uint8_t* b, uint64_t n);
 // (init_start0, init_stop0) = the sscanf values current before byte 0 (0, 0 at the input start)
 void plan_units(const uint8_t* b, uint64_t n, uint64_t max_units, std::vector<Unit>& out, int64_t init_start0 = 0,
                 int64_t init_stop0 = 0);
+// the same over [0, lim) when the caller knows there is no 0xFF before lim (no scan)
+void plan_units_upto(const uint8_t* b, uint64_t lim, uint64_t max_units, std::vector<Unit>& out,
+                     int64_t init_start0 = 0, int64_t init_stop0 = 0);
 // longest-processing-time assignment of units to shards by byte length
 void assign_lpt(const std::vector<Unit>& units, int nshards, std::vector<int32_t>& shard_of);
 // archive order of gathered segments (stable by unit) and their byte offsets from `base`

@@ -170,6 +170,8 @@ bool junction_differs(starch_ctx* c, const uint8_t* d_base, uint64_t lo, uint64_
     return la != lb || memcmp(a + ls, b, la) != 0;
 }
 
+struct FFInBatch {};   // transform_units(planned): the batch holds a 0xFF (hpp:181: EOF)
+
 // Transform stage over units.  One launch sequence over the whole range when
 // the units are back to back, every junction changes chromosome (so it is a
 // segment start in the concatenation too) and no sscanf value goes stale;
@@ -193,6 +195,7 @@ const uint8_t* transform_units(starch_ctx* c, const uint8_t* d_base, const std::
         const uint64_t beg = u[0].off, end = u.back().off + u.back().len;
         TransformResult tr;
         c->tf.run(d_base + beg, end - beg, c->st, tr, u[0].init_start, u[0].init_stop);
+        if (planned && tr.ff_pos != ~0ull) throw FFInBatch{};
         if (u.size() > 1 && tr.ff_pos != ~0ull)
             throw StarchError(STARCH_ERR_ARG, "a unit contains byte 0xFF (plan units with starch_plan_units)");
         if (u.size() == 1 || !tr.general) {
@@ -219,6 +222,7 @@ const uint8_t* transform_units(starch_ctx* c, const uint8_t* d_base, const std::
     for (size_t k = 0; k < u.size(); ++k) {
         TransformResult tr;
         c->tf.run(d_base + u[k].off, u[k].len, c->st, tr, u[k].init_start, u[k].init_stop);
+        if (planned && tr.ff_pos != ~0ull) throw FFInBatch{};
         if (tr.ff_pos != ~0ull)
             throw StarchError(STARCH_ERR_ARG, "a unit contains byte 0xFF (plan units with starch_plan_units)");
         std::vector<SegInfo> part(tr.n_segments);
@@ -398,14 +402,20 @@ void encode_device(starch_ctx* c, const uint8_t* d_bed, uint64_t n, const starch
     encode_units(c, d_bed, u, opt, L_ARCHIVE);
 }
 
-// Pipelined encode of pinned host bytes (the one-call host path): the input
-// is cut at chromosome boundaries (shard::plan_units) into batches; batch k+1
-// crosses PCIe on the copy stream (one of two device slots) while batch k is
-// encoded, and every batch's streams are appended to the archive in HBM.  The
-// bytes equal encode_device's: units are independent (shard.cpp), the index is
-// built over all segments at the end.  Batches: about a sixth of the input
-// (at least 64 MiB), the last ones smaller, so the encode after the final
-// copy is short.
+// Pipelined encode of pinned host bytes (the one-call host path).  The input
+// is cut at chromosome boundaries (shard::plan_units) into batches; every
+// batch crosses PCIe in input order on one copy stream into one device buffer,
+// and the batches go round robin to "lanes": the context itself and extra
+// contexts on the same device (ctx->lanes), each with its own stream, encoder
+// scratch and host thread.  A lane encodes a batch as soon as its bytes are in
+// HBM, and the lanes' encodes run concurrently, so one lane's host syncs and
+// small end-of-round launches are filled by the other's kernels.  Every
+// batch's streams are appended to its lane's collect buffer; the archive is
+// then laid out in batch (= input) order, and its bytes equal encode_device's:
+// units are independent (shard.cpp), the index is built over all segments at
+// the end.  The planner runs to the end of the bytes without a host 0xFF scan;
+// a batch whose transform meets a 0xFF (which reads as EOF, hpp:181) abandons
+// the pipeline and the caller takes the one-copy path.
 bool host_is_pinned(const void* p)
 {
     hipPointerAttribute_t a;
@@ -416,20 +426,98 @@ bool host_is_pinned(const void* p)
     return a.type == hipMemoryTypeHost;
 }
 
-void encode_host_pipelined(starch_ctx* c, const uint8_t* bed, uint64_t n, const starch_options& opt)
+struct LaneBatch {
+    int lane = 0;
+    uint64_t coll_off = 0, bytes = 0;
+    std::vector<starch_segment> segs;
+    std::vector<std::string> names;
+    starch_stats stats{};
+};
+
+starch_ctx* lane_ctx(starch_ctx* c, int i)
+{
+    if (i == 0) return c;
+    while ((int)c->lanes.size() < i) {
+        std::unique_ptr<starch_ctx> L(new starch_ctx());
+        L->device = c->device;
+        L->is_lane = true;
+        HIP_CHECK(hipStreamCreateWithFlags(&L->own, hipStreamNonBlocking));
+        L->st = L->own;
+        c->lanes.push_back(std::move(L));
+    }
+    return c->lanes[i - 1].get();
+}
+
+// append n device bytes to a lane's collect buffer (grown keeping its bytes)
+void collect_append(starch_ctx* L, uint64_t& end, const void* src, uint64_t n)
+{
+    if (end + n > L->collect.cap) {
+        const uint64_t ncap = align_up(std::max<uint64_t>(end + n, L->collect.cap + L->collect.cap / 2) + 4096, 1 << 20);
+        DevBuf nb;
+        uint8_t* np = nb.as<uint8_t>(ncap);
+        if (end) HIP_CHECK(hipMemcpyAsync(np, L->collect.p, end, hipMemcpyDeviceToDevice, L->st));
+        HIP_CHECK(hipStreamSynchronize(L->st));
+        std::swap(L->collect.p, nb.p);
+        std::swap(L->collect.cap, nb.cap);
+    }
+    if (n) HIP_CHECK(hipMemcpyAsync(static_cast<uint8_t*>(L->collect.p) + end, src, n, hipMemcpyDeviceToDevice, L->st));
+    end += n;
+}
+
+// one lane: batches `mine` (indices into `batches`) in order, each once its
+// bytes are in HBM (ev[k], recorded on the shared copy stream after its H2D)
+void run_lane(starch_ctx* L, const uint8_t* d_in, const std::vector<shard::Unit>& plan,
+              const std::vector<std::pair<size_t, size_t>>& batches, const std::vector<hipEvent_t>& ev,
+              const std::vector<size_t>& mine, const starch_options& opt, std::vector<LaneBatch>& out, int lane,
+              const std::atomic<bool>& stop)
+{
+    uint64_t total = 0;
+    for (size_t k : mine)
+        for (size_t u = batches[k].first; u < batches[k].second; ++u) total += plan[u].length;
+    uint64_t cend = 0;
+    if (L->collect.cap < total / 3 + (1 << 20)) L->collect.as<uint8_t>(total / 3 + (1 << 20));
+    for (size_t j = 0; j < mine.size() && !stop.load(); ++j) {
+        const size_t k = mine[j];
+        HIP_CHECK(hipStreamWaitEvent(L->st, ev[k], 0));
+        const uint64_t base = plan[batches[k].first].offset;
+        std::vector<UnitIn> u;
+        for (size_t q = batches[k].first; q < batches[k].second; ++q)
+            u.push_back(UnitIn{plan[q].offset - base, plan[q].length, plan[q].init_start, plan[q].init_stop, q});
+        STRACE("lane %d batch %zu: %zu units, encode", lane, k, u.size());
+        encode_units(L, d_in + base, u, opt, L_STREAMS, true);
+        STRACE("lane %d batch %zu: encoded, %llu stream bytes, device %.3f ms", lane, k,
+               (unsigned long long)L->part_bytes, L->stats.ms_total);
+        LaneBatch& r = out[k];
+        r.lane = lane;
+        r.coll_off = cend;
+        r.bytes = L->part_bytes;
+        r.segs = L->segs;
+        r.names = L->names;
+        r.stats = L->stats;
+        collect_append(L, cend, L->part.p, L->part_bytes);
+    }
+    HIP_CHECK(hipStreamSynchronize(L->st));
+}
+
+bool encode_host_pipelined(starch_ctx* c, const uint8_t* bed, uint64_t n, const starch_options& opt)
 {
     using clk = std::chrono::steady_clock;
     const auto t0 = clk::now();
     std::vector<shard::Unit> plan;
-    shard::plan_units(bed, n, 4096, plan);
-    const uint64_t lim = shard::input_limit(bed, n);
-    // batches of consecutive units: a sixth of the input, shrinking toward the end
+    shard::plan_units_upto(bed, n, 4096, plan);
+    // batches of consecutive units: a small first one (the GPU starts early),
+    // then an eighth of the input, halving toward the end (the encode after the
+    // last copy is short)
+    static const int nbatch = [] { const char* e = getenv("STARCH_PIPE_BATCHES"); return e ? std::max(1, atoi(e)) : 8; }();
+    static const int nlanes = [] { const char* e = getenv("STARCH_LANES"); return e ? std::min(4, std::max(1, atoi(e))) : 2; }();
+    static const int first_div = [] { const char* e = getenv("STARCH_PIPE_FIRST"); return e ? std::max(1, atoi(e)) : 24; }();
     std::vector<std::pair<size_t, size_t>> batches;   // [u0, u1)
     {
-        const uint64_t target = std::max<uint64_t>(64ull << 20, lim / 6);
-        uint64_t left = lim;
+        const uint64_t target = std::max<uint64_t>(64ull << 20, n / (uint64_t)nbatch);
+        uint64_t left = n;
         for (size_t k = 0; k < plan.size();) {
-            const uint64_t want = std::max<uint64_t>(32ull << 20, std::min<uint64_t>(target, left / 2));
+            uint64_t want = std::max<uint64_t>(32ull << 20, std::min<uint64_t>(target, left / 2));
+            if (k == 0) want = std::max<uint64_t>(32ull << 20, std::min<uint64_t>(want, n / (uint64_t)first_div));
             size_t e = k;
             uint64_t b = 0;
             while (e < plan.size() && (b == 0 || b + plan[e].length <= want)) b += plan[e++].length;
@@ -438,98 +526,113 @@ void encode_host_pipelined(starch_ctx* c, const uint8_t* bed, uint64_t n, const 
             k = e;
         }
     }
-    uint64_t maxb = 0;
-    for (auto& bt : batches) {
-        uint64_t b = 0;
-        for (size_t k = bt.first; k < bt.second; ++k) b += plan[k].length;
-        maxb = std::max(maxb, b);
-    }
+    const int nl = (int)std::min<size_t>((size_t)nlanes, std::max<size_t>(1, batches.size()));
+    std::vector<std::vector<size_t>> mine(nl);
+    for (size_t k = 0; k < batches.size(); ++k) mine[k % nl].push_back(k);
+    std::vector<starch_ctx*> lane(nl);
+    for (int i = 0; i < nl; ++i) lane[i] = lane_ctx(c, i);
+    std::vector<LaneBatch> res(batches.size());
+    std::atomic<bool> stop{false}, saw_ff{false};
+    std::vector<int> codes(nl, 0);
+    std::vector<std::string> errs(nl);
+    // every batch crosses PCIe in input order on one copy stream, into one
+    // device buffer, so the first batch arrives at full link rate
     if (!c->cst) HIP_CHECK(hipStreamCreateWithFlags(&c->cst, hipStreamNonBlocking));
-    uint8_t* slot[2] = {c->pin_in[0].as<uint8_t>(maxb + 64), c->pin_in[1].as<uint8_t>(maxb + 64)};
-    std::vector<hipEvent_t> ev(batches.size());
+    uint8_t* d_in = c->input.as<uint8_t>(n + 64);
+    std::vector<hipEvent_t> ev(batches.size(), nullptr);
     for (auto& e : ev) HIP_CHECK(hipEventCreateWithFlags(&e, hipEventDisableTiming));
-    auto h2d = [&](size_t k) {
-        const uint64_t o = plan[batches[k].first].offset;
-        uint64_t b = 0;
-        for (size_t u = batches[k].first; u < batches[k].second; ++u) b += plan[u].length;
-        if (b) HIP_CHECK(hipMemcpyAsync(slot[k & 1], bed + o, b, hipMemcpyHostToDevice, c->cst));
-        HIP_CHECK(hipEventRecord(ev[k], c->cst));
-    };
-    std::vector<starch_segment> segs;
-    std::vector<std::string> names;
-    starch_stats st{};
-    uint64_t arch_cap = c->archive.cap, end = 4;   // the context's archive buffer is reused across calls
-    uint8_t* arch = static_cast<uint8_t*>(c->archive.p);
-    auto grow = [&](uint64_t need) {
-        if (need <= arch_cap) return;
-        const uint64_t ncap = align_up(std::max<uint64_t>(need, arch_cap + arch_cap / 2) + 4096, 1 << 20);
-        DevBuf nb;
-        uint8_t* np = nb.as<uint8_t>(ncap);
-        if (arch && end) HIP_CHECK(hipMemcpyAsync(np, arch, end, hipMemcpyDeviceToDevice, c->st));
-        HIP_CHECK(hipStreamSynchronize(c->st));
-        std::swap(c->archive.p, nb.p);
-        std::swap(c->archive.cap, nb.cap);
-        arch = np;
-        arch_cap = ncap;
-    };
-    grow(lim / 3 + (1 << 20));
-    HIP_CHECK(hipMemcpyAsync(arch, kMagic, 4, hipMemcpyHostToDevice, c->st));
     try {
-        if (!batches.empty()) h2d(0);
         for (size_t k = 0; k < batches.size(); ++k) {
-            // slot (k+1)&1 held batch k-1, whose encode has finished (encode_units syncs)
-            if (k + 1 < batches.size()) h2d(k + 1);
-            HIP_CHECK(hipStreamWaitEvent(c->st, ev[k], 0));
-            const uint64_t base = plan[batches[k].first].offset;
-            std::vector<UnitIn> u;
-            for (size_t q = batches[k].first; q < batches[k].second; ++q)
-                u.push_back(UnitIn{plan[q].offset - base, plan[q].length, plan[q].init_start, plan[q].init_stop, q});
-            STRACE("pipelined batch %zu: %zu units, encode", k, u.size());
-            encode_units(c, slot[k & 1], u, opt, L_STREAMS, true);
-            STRACE("pipelined batch %zu: encoded, %llu stream bytes, device %.3f ms", k,
-                   (unsigned long long)c->part_bytes, c->stats.ms_total);
-            grow(end + c->part_bytes + 64);
-            if (c->part_bytes)
-                HIP_CHECK(hipMemcpyAsync(arch + end, c->part.p, c->part_bytes, hipMemcpyDeviceToDevice, c->st));
-            for (size_t s = 0; s < c->segs.size(); ++s) {
-                starch_segment g = c->segs[s];
-                g.stream_offset += end;
-                segs.push_back(g);
-                names.push_back(c->names[s]);
-            }
-            end += c->part_bytes;
-            const starch_stats& x = c->stats;
-            st.n_lines += x.n_lines;
-            st.text_bytes += x.text_bytes;
-            st.n_blocks += x.n_blocks;
-            st.rle_bytes += x.rle_bytes;
-            st.bwt_rounds += x.bwt_rounds;
-            st.periodic_blocks += x.periodic_blocks;
-            st.bwt_tied += x.bwt_tied;
-            st.dedup_blocks += x.dedup_blocks;
-            st.ms_transform += x.ms_transform;
-            st.ms_rle += x.ms_rle;
-            st.ms_bwt += x.ms_bwt;
-            st.ms_mtf += x.ms_mtf;
-            st.ms_tables += x.ms_tables;
-            st.ms_emit += x.ms_emit;
+            const uint64_t o = plan[batches[k].first].offset;
+            const uint64_t e = batches[k].second < plan.size() ? plan[batches[k].second].offset : n;
+            if (e > o) HIP_CHECK(hipMemcpyAsync(d_in + o, bed + o, e - o, hipMemcpyHostToDevice, c->cst));
+            HIP_CHECK(hipEventRecord(ev[k], c->cst));
         }
     } catch (...) {
         (void)hipStreamSynchronize(c->cst);
         for (auto& e : ev) (void)hipEventDestroy(e);
         throw;
     }
+    auto work = [&](int i) {
+        try {
+            Ctx g(lane[i]);
+            run_lane(lane[i], d_in, plan, batches, ev, mine[i], opt, res, i, stop);
+        } catch (const FFInBatch&) {
+            saw_ff = true;
+            stop = true;
+        } catch (const StarchError& e) {
+            codes[i] = e.code;
+            errs[i] = e.what();
+            stop = true;
+        } catch (const std::exception& e) {
+            codes[i] = STARCH_ERR_INTERNAL;
+            errs[i] = e.what();
+            stop = true;
+        }
+    };
+    {
+        std::vector<std::thread> th;
+        for (int i = 1; i < nl; ++i) th.emplace_back(work, i);
+        work(0);
+        for (auto& t : th) t.join();
+    }
+    (void)hipStreamSynchronize(c->cst);
     for (auto& e : ev) (void)hipEventDestroy(e);
+    for (int i = 0; i < nl; ++i)
+        if (codes[i]) throw StarchError(codes[i], errs[i]);
+    if (saw_ff) return false;
+    // archive: magic, the batches' streams in input order, index
+    uint64_t end = 4;
+    std::vector<starch_segment> segs;
+    std::vector<std::string> names;
+    starch_stats st{};
+    for (auto& r : res) {
+        for (size_t s = 0; s < r.segs.size(); ++s) {
+            starch_segment g = r.segs[s];
+            g.stream_offset += end;
+            segs.push_back(g);
+            names.push_back(r.names[s]);
+        }
+        end += r.bytes;
+        const starch_stats& x = r.stats;
+        st.n_lines += x.n_lines;
+        st.text_bytes += x.text_bytes;
+        st.n_blocks += x.n_blocks;
+        st.rle_bytes += x.rle_bytes;
+        st.bwt_rounds += x.bwt_rounds;
+        st.periodic_blocks += x.periodic_blocks;
+        st.bwt_tied += x.bwt_tied;
+        st.dedup_blocks += x.dedup_blocks;
+        st.ms_transform += x.ms_transform;
+        st.ms_rle += x.ms_rle;
+        st.ms_bwt += x.ms_bwt;
+        st.ms_mtf += x.ms_mtf;
+        st.ms_tables += x.ms_tables;
+        st.ms_emit += x.ms_emit;
+    }
     std::string idx;
     if (opt.emit_index) {
         std::vector<const char*> np(segs.size());
-        std::vector<uint64_t> nl(segs.size());
-        for (size_t s = 0; s < segs.size(); ++s) { np[s] = names[s].data(); nl[s] = names[s].size(); }
-        idx = build_index(segs.data(), np.data(), nl.data(), segs.size(), end, opt.note, opt.block_size_100k,
+        std::vector<uint64_t> nlen(segs.size());
+        for (size_t s = 0; s < segs.size(); ++s) { np[s] = names[s].data(); nlen[s] = names[s].size(); }
+        idx = build_index(segs.data(), np.data(), nlen.data(), segs.size(), end, opt.note, opt.block_size_100k,
                           opt.base_counts != 0, opt.compression_method);
-        grow(end + idx.size() + 64);
-        HIP_CHECK(hipMemcpyAsync(arch + end, idx.data(), idx.size(), hipMemcpyHostToDevice, c->st));
     }
+    uint8_t* arch = c->archive.as<uint8_t>(align_up(end + idx.size() + 64, 256));
+    HIP_CHECK(hipMemcpyAsync(arch, kMagic, 4, hipMemcpyHostToDevice, c->st));
+    uint64_t o = 4;
+    for (size_t k = 0; k < res.size();) {   // one copy per run of batches adjacent in a lane's collect buffer
+        const int ln = res[k].lane;
+        uint64_t len = res[k].bytes;
+        size_t k2 = k + 1;
+        while (k2 < res.size() && res[k2].lane == ln && res[k2].coll_off == res[k].coll_off + len) len += res[k2++].bytes;
+        if (len)
+            HIP_CHECK(hipMemcpyAsync(arch + o, static_cast<uint8_t*>(lane[ln]->collect.p) + res[k].coll_off, len,
+                                     hipMemcpyDeviceToDevice, c->st));
+        o += len;
+        k = k2;
+    }
+    if (!idx.empty()) HIP_CHECK(hipMemcpyAsync(arch + end, idx.data(), idx.size(), hipMemcpyHostToDevice, c->st));
     HIP_CHECK(hipStreamSynchronize(c->st));
     st.input_bytes = n;
     st.n_segments = segs.size();
@@ -543,6 +646,7 @@ void encode_host_pipelined(starch_ctx* c, const uint8_t* bed, uint64_t n, const 
     c->archive_bytes = st.archive_bytes;
     c->have = true;
     c->streamed = false;
+    return true;
 }
 
 // Multi-device encode of host bytes: plan units, LPT them over the contexts,
@@ -846,7 +950,7 @@ void stream_cut(starch_ctx* c)
     std::vector<shard::Unit> u;
     if (nl) {
         const uint64_t lim = (uint64_t)(static_cast<const uint8_t*>(nl) - h) + 1;
-        shard::plan_units(h, lim, 4096, u, m.init_start, m.init_stop);
+        shard::plan_units_upto(h, lim, 4096, u, m.init_start, m.init_stop);   // commit cut the bytes at any 0xFF
     }
     if (u.size() < 2) {   // no boundary yet: the held run continues
         m.try_at = m.held_n + m.batch / 2;
@@ -858,7 +962,7 @@ void stream_cut(starch_ctx* c)
     STRACE("stream cut: encoder idle");
     const int o = 1 - m.cur;
     stream_reserve(c, o, std::max<uint64_t>(tail + m.batch + (m.batch >> 2), 1ull << 20));
-    memcpy(m.buf[o], h + cut, tail);
+    m.pool.copy(m.buf[o], h + cut, tail);
     if (tail)   // the tail's device bytes move with it (ordered after their H2D on cst)
         HIP_CHECK(hipMemcpyAsync(m.dbuf[o].p, static_cast<uint8_t*>(m.dbuf[m.cur].p) + cut, tail,
                                  hipMemcpyDeviceToDevice, c->cst));
@@ -978,10 +1082,9 @@ int starch_encode_host(starch_ctx* c, const void* bed, uint64_t n, const starch_
     // large pinned inputs: PCIe copy of the next batch overlaps the encode
     // (STARCH_PIPELINE=0 turns it off; pageable memory has no async copy)
     static const bool pipe_off = [] { const char* e = getenv("STARCH_PIPELINE"); return e && !strcmp(e, "0"); }();
-    if (!pipe_off && !o.reference_compat && n >= (256ull << 20) && host_is_pinned(bed)) {
-        encode_host_pipelined(c, static_cast<const uint8_t*>(bed), n, o);
+    if (!pipe_off && !o.reference_compat && n >= (256ull << 20) && host_is_pinned(bed) &&
+        encode_host_pipelined(c, static_cast<const uint8_t*>(bed), n, o))
         return STARCH_OK;
-    }
     uint8_t* d = c->input.as<uint8_t>(n + 64);
     if (n) HIP_CHECK(hipMemcpyAsync(d, bed, n, hipMemcpyHostToDevice, c->st));
     HIP_CHECK(hipStreamSynchronize(c->st));
@@ -1396,14 +1499,16 @@ int starch_stream_window(starch_ctx* c, uint64_t min_bytes, void** ptr, uint64_t
     END_GUARD(c)
 }
 
-int starch_stream_commit(starch_ctx* c, uint64_t n)
+// commit n window bytes of which the first k precede any 0xFF (0xFF reads as
+// EOF, hpp:181); ff_known: k was found while copying (starch_stream_feed)
+static int stream_commit_k(starch_ctx* c, uint64_t n, uint64_t k, bool ff_known)
 {
     GUARD(c)
     auto& m = c->sm;
     if (!m.active) return STARCH_ERR_STATE;
     if (m.held_n + n > m.cap[m.cur]) return STARCH_ERR_ARG;
     if (m.eof || n == 0) return STARCH_OK;
-    const uint64_t k = shard::input_limit(m.buf[m.cur] + m.held_n, n);   // 0xFF reads as EOF (hpp:181)
+    if (!ff_known) k = shard::input_limit(m.buf[m.cur] + m.held_n, n);
     if (k < n) m.eof = true;
     if (k && !m.opt.reference_compat)
         HIP_CHECK(hipMemcpyAsync(static_cast<uint8_t*>(m.dbuf[m.cur].p) + m.held_n, m.buf[m.cur] + m.held_n, k,
@@ -1414,6 +1519,8 @@ int starch_stream_commit(starch_ctx* c, uint64_t n)
     END_GUARD(c)
 }
 
+int starch_stream_commit(starch_ctx* c, uint64_t n) { return stream_commit_k(c, n, 0, false); }
+
 int starch_stream_feed(starch_ctx* c, const void* bed, uint64_t n)
 {
     if (!c) return STARCH_ERR_ARG;
@@ -1423,8 +1530,16 @@ int starch_stream_feed(starch_ctx* c, const void* bed, uint64_t n)
     uint64_t cap = 0;
     int rc = starch_stream_window(c, n, &w, &cap);
     if (rc) return rc;
-    c->sm.pool.copy(static_cast<uint8_t*>(w), static_cast<const uint8_t*>(bed), n);
-    return starch_stream_commit(c, n);
+    const double t0 = tracing() ? trace_t0() : 0.0;
+    const uint64_t k = c->sm.pool.copy_find_ff(static_cast<uint8_t*>(w), static_cast<const uint8_t*>(bed), n);
+    const double t1 = tracing() ? trace_t0() : 0.0;
+    rc = stream_commit_k(c, n, k, true);
+    if (tracing()) {
+        c->sm.t_copy += t1 - t0;
+        c->sm.t_commit += trace_t0() - t1;
+        c->sm.fed += n;
+    }
+    return rc;
 }
 
 int starch_stream_end(starch_ctx* c)
@@ -1443,6 +1558,10 @@ int starch_stream_end(starch_ctx* c)
         throw;
     }
     c->stream_shutdown();
+    STRACE("stream end: fed %.1f MB, copy %.1f ms (%.1f GB/s), commit+cut %.1f ms", m.fed / 1e6, m.t_copy,
+           m.t_copy > 0 ? m.fed / m.t_copy / 1e6 : 0.0, m.t_commit);
+    m.t_copy = m.t_commit = 0;
+    m.fed = 0;
     m.held_n = 0;
     if (m.opt.emit_index && !m.opt.reference_compat) {
         std::vector<const char*> np(m.segs.size());

@@ -8,6 +8,7 @@ tails, stale sscanf values across a cut, revisited chromosomes, NUL bytes and
 a 0xFF that ends the input mid-piece."""
 import os
 import subprocess
+import sys
 
 import pytest
 
@@ -77,6 +78,18 @@ def test_stream_ff_ends_input():
     data = head + b"chrZ\t1\t2\n\xffchrZ\t3\t4\n" + head
     ref = _one_call(data)
     got, st = _streamed(data, 4096, 1)
+    assert got == ref
+    assert st["input_bytes"] == data.index(b"\xff")
+
+
+def test_stream_ff_in_large_piece():
+    """Pieces >= 8 MiB are copied by the session's thread pool, which finds the
+    first 0xFF while copying: the input still ends there."""
+    import starch_amd
+    head = starch_amd.gen_bed(0, 1_500_000)
+    data = head + b"chrZ\t1\t2\n\xffchrZ\t3\t4\n" + head
+    ref = _one_call(data)
+    got, st = _streamed(data, 24 << 20, 1 << 20)
     assert got == ref
     assert st["input_bytes"] == data.index(b"\xff")
 
@@ -158,3 +171,53 @@ def test_pipelined_host_encode_equals_device_encode():
     assert [nm.decode() for nm, _ in segs] == starch_amd.HG38
     assert c.stats()["n_lines"] == 12_000_000
     c.close()
+
+
+@pytest.mark.parametrize("lanes", ["1", "3"])
+def test_pipelined_lanes_and_batches(lanes):
+    """The lane count and batch count of the pipelined path change only the
+    schedule: 1 and 3 lanes (subprocess, STARCH_LANES / STARCH_PIPE_BATCHES read
+    at first use) give the device-resident archive."""
+    env = dict(os.environ, STARCH_LANES=lanes, STARCH_PIPE_BATCHES="5")
+    r = subprocess.run([sys.executable, "-c", _PIPE_SRC], cwd=ROOT, env=env, capture_output=True, timeout=600)
+    assert r.returncode == 0, r.stderr[-3000:]
+    assert r.stdout.decode().strip().endswith("same")
+
+
+def test_pipelined_input_with_0xff_falls_back():
+    """A 0xFF (EOF for the reference, hpp:181) inside a pipelined input: the
+    batch that meets it abandons the pipeline and the one-copy path encodes
+    the input -- archive == device encode (which stops at the 0xFF)."""
+    import ctypes
+    import torch
+    import starch_amd
+    n = sum(starch_amd.gen_bed_sizes(0, 12_000_000))
+    host = torch.empty(n, dtype=torch.uint8, pin_memory=True)
+    starch_amd.gen_bed(0, 12_000_000, into=ctypes.c_void_p(host.data_ptr()))
+    host[n // 2 + 12345] = 0xFF
+    c = starch_amd.Starch(0)
+    dev = host.to("cuda")
+    c.compress_device(dev.data_ptr(), n)
+    want = c.archive()
+    c.compress_host_ptr(host.data_ptr(), n)
+    assert c.archive() == want
+    assert c.stats()["n_lines"] < 12_000_000
+    c.close()
+
+
+_PIPE_SRC = r'''
+import ctypes, torch, starch_amd
+n = sum(starch_amd.gen_bed_sizes(0, 12_000_000, seed=7))
+host = torch.empty(n, dtype=torch.uint8, pin_memory=True)
+starch_amd.gen_bed(0, 12_000_000, seed=7, into=ctypes.c_void_p(host.data_ptr()))
+c = starch_amd.Starch(0)
+dev = host.to("cuda")
+c.compress_device(dev.data_ptr(), n)
+want = c.archive()
+c.compress_host_ptr(host.data_ptr(), n)
+got = c.archive()
+c.compress_host_ptr(host.data_ptr(), n)
+again = c.archive()
+c.close()
+print("same" if got == want and again == want else "differ")
+'''
