@@ -77,6 +77,7 @@ private:
     DevBuf b_streams, b_tiles, b_tile_sum, b_tile_carry, b_tile_w, b_tile_wpre, b_tpos, b_seg_tile0, b_seg_nblk,
         b_blk_tmp, b_blk, b_blkbytes, b_scal, b_tmp, b_bwt, b_mtfv, b_freq, b_sel, b_tabs, b_gbits, b_souts,
         b_fallback, b_bwt3, b_crc, b_dedupe, b_rep_bytes, b_rep_blk;
+    PinnedBuf h_wtot_, h_nblk_, h_blocks_, h_hr_;   // read-back targets (pinned)
     struct PinnedCtr {
         uint32_t* p = nullptr;
         uint32_t* get();

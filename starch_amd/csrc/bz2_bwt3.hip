@@ -643,7 +643,7 @@ __global__ void __launch_bounds__(SCT) k3_scatter(Ctx c)
 // of a bucket's run instead of one scattered 4-byte store per rotation (the
 // direct scatter's writes cost ~2.5-3.5x their bytes in HBM traffic).
 // ---------------------------------------------------------------------------
-template <int NB>
+template <int NB, bool MAT>
 __global__ void __launch_bounds__(SCT) k3_scatter_lds(Ctx c)
 {
     // rotations staged at a time: half a tile (4096 bins), a quarter (8192 bins: LDS)
@@ -657,9 +657,10 @@ __global__ void __launch_bounds__(SCT) k3_scatter_lds(Ctx c)
     __shared__ uint32_t job_sh;
     // round 0 writes every rotation's key window and last-column symbol next to
     // its SA entry (KM0 / LS0), from the stage's PSS words held in LDS
-    constexpr uint32_t PWN = (SH_HALF + 1) * 8 / 64 + 4;   // words for B <= 8
+    // (MAT: bwt_kmat() only; the plain instantiation keeps no PSS window in LDS)
+    constexpr uint32_t PWN = MAT ? (SH_HALF + 1) * 8 / 64 + 4 : 1;   // words for B <= 8
     __shared__ uint64_t pw[PWN];
-    const bool mat = c.lA != nullptr;
+    constexpr bool mat = MAT;
     const int tid = threadIdx.x;
     const uint32_t x = xcc_id();
     if (tid < 8) qs[tid] = ((uint32_t)tid < c.nb ? (c.nb - tid + 7) / 8 : 0u) * MAXT;
@@ -690,7 +691,7 @@ __global__ void __launch_bounds__(SCT) k3_scatter_lds(Ctx c)
             // [t0 + h0 - 1, t0 + h0 + he) plus one key window
             const uint32_t rs = t0 + h0;
             const uint64_t wbase = rs ? ((uint64_t)(rs - 1) * B) >> 6 : 0;
-            if (mat) {
+            if constexpr (mat) {
                 const uint64_t wend = (((uint64_t)(rs + he) * B + 64) >> 6) + 2;
                 for (uint64_t w = wbase + tid; w < wend; w += SCT) pw[w - wbase] = pss[w];
             }
@@ -737,7 +738,7 @@ __global__ void __launch_bounds__(SCT) k3_scatter_lds(Ctx c)
                 const uint32_t pos = cur[dg] + (j - lst[dg]);
                 SA[pos] = r;
                 uint32_t ls = 0;
-                if (mat && r) {
+                if (mat && r) {   // (MAT: compile-time)
                     const uint64_t bit = (uint64_t)(r - 1) * B - (wbase << 6);
                     const uint32_t q = (uint32_t)(bit >> 6), p = (uint32_t)(bit & 63u);
                     ls = (uint32_t)(((pw[q] << p) | ((pw[q + 1] >> 1) >> (63u - p))) >> (64u - B));
@@ -1278,7 +1279,10 @@ __device__ __forceinline__ void grp_finish_keys(GrpIn<E>& x)
 #ifndef STARCH_WPE_GRP
 #define STARCH_WPE_GRP 1
 #endif
-constexpr int sort_wpe(int NW, int E) { return NW == 4 && E == 8 ? 3 : (NW == 1 ? STARCH_WPE_GRP : 1); }
+#ifndef STARCH_WPE_M2
+#define STARCH_WPE_M2 3
+#endif
+constexpr int sort_wpe(int NW, int E) { return NW == 4 && E == 8 ? STARCH_WPE_M2 : (NW == 1 ? STARCH_WPE_GRP : 1); }
 
 template <int NW, int E, bool DBL>
 __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(sort_wpe(NW, E))))
@@ -2431,8 +2435,10 @@ void launch_bwt3(BlockDesc* blocks, uint32_t b0, uint32_t nb, const uint8_t* blk
         const dim3 gsc((ncu + 7) / 8 * 8);
         if (direct && wide) hipLaunchKernelGGL(k3_scatter<PNB_WIDE>, gsc, dim3(SCT), 0, st, c);
         else if (direct) hipLaunchKernelGGL(k3_scatter<PNB>, gsc, dim3(SCT), 0, st, c);
-        else if (wide) hipLaunchKernelGGL(k3_scatter_lds<PNB_WIDE>, gsc, dim3(SCT), 0, st, c);
-        else hipLaunchKernelGGL(k3_scatter_lds<PNB>, gsc, dim3(SCT), 0, st, c);
+        else if (wide && c.lA) hipLaunchKernelGGL((k3_scatter_lds<PNB_WIDE, true>), gsc, dim3(SCT), 0, st, c);
+        else if (wide) hipLaunchKernelGGL((k3_scatter_lds<PNB_WIDE, false>), gsc, dim3(SCT), 0, st, c);
+        else if (c.lA) hipLaunchKernelGGL((k3_scatter_lds<PNB, true>), gsc, dim3(SCT), 0, st, c);
+        else hipLaunchKernelGGL((k3_scatter_lds<PNB, false>), gsc, dim3(SCT), 0, st, c);
         HIP_CHECK(hipGetLastError());
     }
     sort_groups();

@@ -659,7 +659,7 @@ uint64_t Decoder::decode(const uint8_t* d_in, uint64_t n, const uint8_t* h_in, h
         // 4. block CRCs of the output
         BlockDesc* d_bd = b_bd.as<BlockDesc>(nb);
         hipLaunchKernelGGL(k_dec_crc_desc, dim3((nb + 255) / 256), dim3(256), 0, st, d_blk, nb, d_bd);
-        rle_crc(d_out, d_bd, nb, reinterpret_cast<uint32_t*>(d_tt), st);
+        rle_crc(d_out, d_bd, nb, nullptr, reinterpret_cast<uint32_t*>(d_tt), st);
         HIP_CHECK(hipGetLastError());
         std::vector<BlockDesc> bd(nb);
         HIP_CHECK(hipMemcpyAsync(bd.data(), d_bd, nb * sizeof(BlockDesc), hipMemcpyDeviceToHost, st));

@@ -90,7 +90,7 @@ void Encoder::plan(const uint8_t* d_text, const std::vector<StreamIn>& streams, 
     uint32_t* d_carry = b_tile_carry.as<uint32_t>(ntiles + 1);
     uint32_t* d_tw = b_tile_w.as<uint32_t>(ntiles + 1);
     uint64_t* d_twpre = b_tile_wpre.as<uint64_t>(ntiles + 1);
-    uint8_t* d_tpos = b_tpos.as<uint8_t>(ntiles * kTB + 16);            // tile-aligned
+    uint8_t* d_tpos = b_tpos.as<uint8_t>(ntiles * (kTB / 4) + 64);      // 2-bit classes, tile-aligned
     uint64_t* d_scal = b_scal.as<uint64_t>(nstreams_ + 16);
     HIP_CHECK(hipMemsetAsync(d_twpre, 0, (ntiles + 1) * sizeof(uint64_t), st));
     if (ntiles) {
@@ -100,47 +100,51 @@ void Encoder::plan(const uint8_t* d_text, const std::vector<StreamIn>& streams, 
         rle_pos(d_text, d_tiles, ntiles, d_carry, d_tpos, d_tw, st);
         scan::excl_sum_u32_to_u64(d_tw, d_twpre, ntiles, d_twpre + ntiles, b_tmp, st);
     }
-    rle_stream_w(d_tile0, d_twpre, nstreams_, d_scal, st);
-    HIP_CHECK(hipGetLastError());
-    std::vector<uint64_t> wtot(nstreams_);
-    HIP_CHECK(hipMemcpyAsync(wtot.data(), d_scal, nstreams_ * sizeof(uint64_t), hipMemcpyDeviceToHost, st));
-    HIP_CHECK(hipStreamSynchronize(st));
-
+    // block-descriptor slots per stream from an upper bound on its RLE1 size
+    // (<= 5/4 of its text: a 4-byte run emits 5), so no read-back is needed here
     std::vector<uint64_t> slot0(nstreams_ + 1, 0);
-    for (uint32_t s = 0; s < nstreams_; ++s) slot0[s + 1] = slot0[s] + wtot[s] / nblock_max + 2;
+    for (uint32_t s = 0; s < nstreams_; ++s)
+        slot0[s + 1] = slot0[s] + (streams[s].text_len + streams[s].text_len / 4 + 1) / nblock_max + 2;
+    const uint64_t nb_max = slot0[nstreams_];
+    if (nb_max > 0xFFFFFFFFull) throw StarchError(-2, "too many blocks");
     uint64_t* d_slot0 = b_seg_nblk.as<uint64_t>(2 * nstreams_ + 2);
     uint32_t* d_nblk = reinterpret_cast<uint32_t*>(d_slot0 + nstreams_ + 1);
     HIP_CHECK(hipMemcpyAsync(d_slot0, slot0.data(), (nstreams_ + 1) * sizeof(uint64_t), hipMemcpyHostToDevice, st));
-    BlockDesc* d_btmp = b_blk_tmp.as<BlockDesc>(slot0[nstreams_] + 1);
+    BlockDesc* d_btmp = b_blk_tmp.as<BlockDesc>(nb_max + 1);
     rle_cut(d_streams, d_tile0, d_twpre, d_tpos, nstreams_, nblock_max, d_slot0, d_btmp, d_nblk, st);
+    // first block of every stream and the block count, on the device; the
+    // block arrays are sized by the bound, the counts read back once below
+    uint32_t* d_first = reinterpret_cast<uint32_t*>(b_souts.as<uint64_t>(nstreams_ + 2));
+    uint32_t* d_nb = d_first + nstreams_;
+    rle_block_first(d_nblk, nstreams_, d_first, d_nb, st);
+    BlockDesc* d_blocks = b_blk.as<BlockDesc>(nb_max + 1);
+    // tile -> block of its first byte, in the (dead after rle_pos) carry array
+    uint32_t* d_tile_block = d_carry;
+    rle_compact(d_btmp, d_slot0, d_nblk, d_first, nstreams_, d_blocks, d_streams, d_tile0, d_tile_block, st);
+    uint8_t* d_blkbytes = b_blkbytes.as<uint8_t>(nb_max * blk_stride_ + 64);
+    if (ntiles) {
+        rle_emit(d_text, d_tiles, ntiles, d_twpre, d_tile0, d_tpos, d_streams, d_first, d_nblk, d_tile_block, d_blocks,
+                 d_blkbytes, blk_stride_, st);
+    }
+    rle_crc(d_text, d_blocks, (uint32_t)nb_max, d_nb, b_crc.as<uint32_t>(nb_max * kCrcMaxChunks), st);
     HIP_CHECK(hipGetLastError());
-    std::vector<uint32_t> nblk(nstreams_);
-    HIP_CHECK(hipMemcpyAsync(nblk.data(), d_nblk, nstreams_ * sizeof(uint32_t), hipMemcpyDeviceToHost, st));
+    // one read-back: per-stream block counts, the total and every block's descriptor
+    uint32_t* nblk = h_nblk_.as<uint32_t>(nstreams_ + 1);
+    BlockDesc* hbp = h_blocks_.as<BlockDesc>(nb_max + 1);
+    HIP_CHECK(hipMemcpyAsync(nblk, d_nblk, nstreams_ * sizeof(uint32_t), hipMemcpyDeviceToHost, st));
+    HIP_CHECK(hipMemcpyAsync(nblk + nstreams_, d_nb, sizeof(uint32_t), hipMemcpyDeviceToHost, st));
+    HIP_CHECK(hipMemcpyAsync(hbp, d_blocks, nb_max * sizeof(BlockDesc), hipMemcpyDeviceToHost, st));
     HIP_CHECK(hipStreamSynchronize(st));
-    std::vector<uint32_t> first(nstreams_, 0);
+    t_rle.stop();
     uint32_t nb = 0;
     for (uint32_t s = 0; s < nstreams_; ++s) {
-        first[s] = nb;
         StreamOut& g = outs[streams[s].group];
         if (g.n_blocks == 0) g.first_block = nb;
         g.n_blocks += nblk[s];
         nb += nblk[s];
     }
+    if (nb != nblk[nstreams_]) throw StarchError(-10, "block count mismatch");
     nblocks_ = nb;
-    uint32_t* d_first = reinterpret_cast<uint32_t*>(b_souts.as<uint64_t>(nstreams_ + 1));
-    HIP_CHECK(hipMemcpyAsync(d_first, first.data(), nstreams_ * sizeof(uint32_t), hipMemcpyHostToDevice, st));
-    BlockDesc* d_blocks = b_blk.as<BlockDesc>(nb + 1);
-    // tile -> block of its first byte, in the (dead after rle_pos) carry array
-    uint32_t* d_tile_block = d_carry;
-    rle_compact(d_btmp, d_slot0, d_nblk, d_first, nstreams_, d_blocks, d_streams, d_tile0, d_tile_block, st);
-    uint8_t* d_blkbytes = b_blkbytes.as<uint8_t>((uint64_t)nb * blk_stride_ + 64);
-    if (ntiles) {
-        rle_emit(d_text, d_tiles, ntiles, d_twpre, d_tile0, d_tpos, d_streams, d_first, d_nblk, d_tile_block, d_blocks,
-                 d_blkbytes, blk_stride_, st);
-    }
-    rle_crc(d_text, d_blocks, nb, b_crc.as<uint32_t>((uint64_t)nb * kCrcMaxChunks), st);
-    HIP_CHECK(hipGetLastError());
-    t_rle.stop();
     if (stats) stats->n_blocks += nb;
     if (nb == 0) {
         for (uint32_t g = 0; g < ngroups_; ++g) outs[g].bytes = 14;   // header + trailer (bz:compress.c:622-666)
@@ -153,9 +157,7 @@ void Encoder::plan(const uint8_t* d_text, const std::vector<StreamIn>& streams, 
     // Group candidate duplicates by (nblock, blockCRC, inUse), confirm each with a
     // byte compare against its representative, and run the block sort, MTF and
     // tables once per distinct block.  STARCH_DEDUPE=0 disables it.
-    std::vector<BlockDesc> hb(nb);
-    HIP_CHECK(hipMemcpyAsync(hb.data(), d_blocks, nb * sizeof(BlockDesc), hipMemcpyDeviceToHost, st));
-    HIP_CHECK(hipStreamSynchronize(st));
+    std::vector<BlockDesc> hb(hbp, hbp + nb);
     const char* env_d = getenv("STARCH_DEDUPE");
     const bool dedupe_on = !(env_d && !strcmp(env_d, "0"));
     // STARCH_DEDUPE_KEY=n groups by nblock only (tests: forces byte-compare rejections)
@@ -280,7 +282,7 @@ void Encoder::plan(const uint8_t* d_text, const std::vector<StreamIn>& streams, 
     }
     unsigned long long* d_stats = reinterpret_cast<unsigned long long*>(d_scal);
     HIP_CHECK(hipMemsetAsync(d_stats, 0, 4 * sizeof(uint64_t), st));
-    std::vector<BlockDesc> hr(nr);
+    BlockDesc* hr = h_hr_.as<BlockDesc>(nr);
     uint32_t* d_which = reinterpret_cast<uint32_t*>(b_fallback.as<uint32_t>(batch + 1));
     for (uint32_t b0 = 0; b0 < nr; b0 += batch) {
         uint32_t cnt = std::min(batch, nr - b0);
@@ -301,8 +303,7 @@ void Encoder::plan(const uint8_t* d_text, const std::vector<StreamIn>& streams, 
             }
             if (lsd) launch_bwt(d_bl, b0, cnt, d_bytes, blk_stride_, scr, d_stats, st);
             else launch_bwt3(d_bl, b0, cnt, d_bytes, blk_stride_, scr, b_bwt3, h_ctr_.get(), d_stats, st, wide);
-            HIP_CHECK(hipMemcpyAsync(hr.data() + b0, d_bl + b0, cnt * sizeof(BlockDesc), hipMemcpyDeviceToHost,
-                                     st));
+            HIP_CHECK(hipMemcpyAsync(hr + b0, d_bl + b0, cnt * sizeof(BlockDesc), hipMemcpyDeviceToHost, st));
             HIP_CHECK(hipStreamSynchronize(st));
             std::vector<uint32_t> which, wn;
             for (uint32_t k = 0; k < cnt; ++k)
@@ -329,13 +330,13 @@ void Encoder::plan(const uint8_t* d_text, const std::vector<StreamIn>& streams, 
             launch_tables(d_bl, b0, cnt, d_mtfv, mtf_stride, d_tabs, d_sel, d_gbits, scr, st);
         }
     }
-    HIP_CHECK(hipMemcpyAsync(hr.data(), d_bl, nr * sizeof(BlockDesc), hipMemcpyDeviceToHost, st));
-    uint64_t hstats[4] = {0, 0, 0, 0};
-    HIP_CHECK(hipMemcpyAsync(hstats, d_stats, sizeof(hstats), hipMemcpyDeviceToHost, st));
+    HIP_CHECK(hipMemcpyAsync(hr, d_bl, nr * sizeof(BlockDesc), hipMemcpyDeviceToHost, st));
+    uint64_t* hstats = reinterpret_cast<uint64_t*>(h_wtot_.as<uint64_t>(std::max<uint64_t>(nstreams_, 4)));
+    HIP_CHECK(hipMemcpyAsync(hstats, d_stats, 4 * sizeof(uint64_t), hipMemcpyDeviceToHost, st));
     HIP_CHECK(hipStreamSynchronize(st));
     // every block takes the sort / MTF / table results of its data block; its
     // position fields (text range, stream, RLE offset) stay its own
-    if (!reuse) hb.swap(hr);
+    if (!reuse) memcpy(hb.data(), hr, nb * sizeof(BlockDesc));
     else {
         for (uint32_t b = 0; b < nb; ++b) {
             BlockDesc o = hr[src_of[b]];

@@ -168,6 +168,9 @@ void rle_emit(const uint8_t* text, const TileDesc* tiles, uint64_t ntiles, const
               const uint8_t* tpos, const StreamIn* streams, const uint32_t* first, const uint32_t* nblk,
               const uint32_t* tile_block, BlockDesc* blocks, uint8_t* blk, uint64_t stride, hipStream_t st);
 constexpr uint32_t kCrcMaxChunks = 128;       // per block (k_crc_chunks)
-void rle_crc(const uint8_t* text, BlockDesc* blocks, uint32_t nb, uint32_t* creg, hipStream_t st);
+void rle_block_first(const uint32_t* nblk, uint32_t ns, uint32_t* first, uint32_t* total, hipStream_t st);
+// nb_max: grid bound; nb_dev (nullable): the device's block count (blocks past it are skipped)
+void rle_crc(const uint8_t* text, BlockDesc* blocks, uint32_t nb_max, const uint32_t* nb_dev, uint32_t* creg,
+             hipStream_t st);
 
 }  // namespace bz

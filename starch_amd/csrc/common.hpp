@@ -47,6 +47,27 @@ struct DevBuf {
     ~DevBuf() { release(); }
 };
 
+// Grow-only pinned host buffer (hipHostMalloc): small device <-> host
+// transfers without pageable staging.  The caller orders reuse against the
+// copies that read or fill it (stream syncs).
+struct PinnedBuf {
+    void* p = nullptr;
+    size_t cap = 0;
+    void* get(size_t bytes) {
+        if (bytes == 0) bytes = 16;
+        if (bytes > cap) {
+            if (p) HIP_CHECK(hipHostFree(p));
+            p = nullptr;
+            size_t want = bytes + bytes / 2 + 4096;
+            HIP_CHECK(hipHostMalloc(&p, want, hipHostMallocDefault));
+            cap = want;
+        }
+        return p;
+    }
+    template <class T> T* as(size_t count) { return static_cast<T*>(get(count * sizeof(T))); }
+    ~PinnedBuf() { if (p) (void)hipHostFree(p); }
+};
+
 // ---------------------------------------------------------------------------
 // Wave / workgroup scan helpers (wave64).
 // ---------------------------------------------------------------------------

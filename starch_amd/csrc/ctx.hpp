@@ -124,6 +124,8 @@ struct starch_ctx {
     bz::Encoder enc;
     gz::Encoder genc;            // the gzip method (-g)
     DevBuf input, archive, part, raw_in, raw_out, text_all;
+    DevBuf names_dev;                // segment names gathered on the device (one D2H per encode)
+    PinnedBuf names_pin;             // ... their host copy, and the gather descriptors
     // decompression / unstarch: the last result is out_dev[0, out_bytes)
     bz::Decoder dec;
     ut::Untransform untf;

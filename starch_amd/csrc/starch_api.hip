@@ -256,6 +256,60 @@ const uint8_t* transform_units(starch_ctx* c, const uint8_t* d_base, const std::
     return all;
 }
 
+// Segment names (the chr tokens, in the input) -> c->names.  One gather
+// kernel packs them into a device buffer and ONE copy brings them to pinned
+// host memory (one copy per name costs a host round trip each: ~20 us per
+// segment).  fetch_names issues the work on c->st; finish_names fills
+// c->names once the stream has passed it (the caller syncs or waits on ev).
+struct NameDesc { uint64_t src, dst, len; };
+
+__global__ void k_gather_names(const uint8_t* __restrict__ base, const NameDesc* __restrict__ d, uint8_t* __restrict__ out)
+{
+    const NameDesc x = d[blockIdx.x];
+    for (uint64_t i = threadIdx.x; i < x.len; i += blockDim.x) out[x.dst + i] = base[x.src + i];
+}
+
+struct PendingNames {
+    std::vector<uint64_t> at;    // nseg + 1 offsets into the packed bytes
+    const uint8_t* host = nullptr;
+    hipEvent_t ev = nullptr;
+    ~PendingNames() { if (ev) (void)hipEventDestroy(ev); }
+};
+
+void fetch_names(starch_ctx* c, const uint8_t* d_base, const std::vector<SegInfo>& si, PendingNames& pn)
+{
+    const uint64_t nseg = si.size();
+    pn.at.assign(nseg + 1, 0);
+    for (uint64_t s = 0; s < nseg; ++s) pn.at[s + 1] = pn.at[s] + si[s].name_len;
+    const uint64_t total = pn.at[nseg];
+    if (!total) return;
+    uint8_t* hp = static_cast<uint8_t*>(c->names_pin.get(total + nseg * sizeof(NameDesc) + 64));
+    NameDesc* hd = reinterpret_cast<NameDesc*>(hp + align_up(total, 64));
+    for (uint64_t s = 0; s < nseg; ++s) hd[s] = NameDesc{si[s].name_off, pn.at[s], si[s].name_len};
+    uint8_t* dp = c->names_dev.as<uint8_t>(align_up(total, 64) + nseg * sizeof(NameDesc));
+    NameDesc* dd = reinterpret_cast<NameDesc*>(dp + align_up(total, 64));
+    HIP_CHECK(hipMemcpyAsync(dd, hd, nseg * sizeof(NameDesc), hipMemcpyHostToDevice, c->st));
+    hipLaunchKernelGGL(k_gather_names, dim3((unsigned)nseg), dim3(64), 0, c->st, d_base, dd, dp);
+    HIP_CHECK(hipGetLastError());
+    HIP_CHECK(hipMemcpyAsync(hp, dp, total, hipMemcpyDeviceToHost, c->st));
+    HIP_CHECK(hipEventCreateWithFlags(&pn.ev, hipEventDisableTiming));
+    HIP_CHECK(hipEventRecord(pn.ev, c->st));
+    pn.host = hp;
+}
+
+void finish_names(starch_ctx* c, PendingNames& pn)
+{
+    const uint64_t nseg = pn.at.empty() ? 0 : pn.at.size() - 1;
+    c->names.assign(nseg, std::string());
+    if (pn.ev) {
+        HIP_CHECK(hipEventSynchronize(pn.ev));
+        (void)hipEventDestroy(pn.ev);
+        pn.ev = nullptr;
+        for (uint64_t s = 0; s < nseg; ++s)
+            c->names[s].assign(reinterpret_cast<const char*>(pn.host) + pn.at[s], pn.at[s + 1] - pn.at[s]);
+    }
+}
+
 enum Layout { L_ARCHIVE, L_STREAMS };
 
 // transform + bzip2 over units.  L_ARCHIVE: magic + streams + index in
@@ -294,14 +348,9 @@ void encode_units(starch_ctx* c, const uint8_t* d_base, const std::vector<UnitIn
     c->stats.text_bytes = tbytes;
     c->text_bytes = tbytes;
     c->text_dev = text;
-    // segment names (small host copies of the chr tokens)
-    c->names.assign(nseg, std::string());
-    for (uint64_t s = 0; s < nseg; ++s) {
-        c->names[s].resize(si[s].name_len);
-        if (si[s].name_len)
-            HIP_CHECK(hipMemcpyAsync(&c->names[s][0], d_base + si[s].name_off, si[s].name_len, hipMemcpyDeviceToHost,
-                                     c->st));
-    }
+    // segment names: one gather + one copy, read once the encoder has synced
+    PendingNames pnames;
+    fetch_names(c, d_base, si, pnames);
     c->segs.assign(nseg, starch_segment{});
     for (uint64_t s = 0; s < nseg; ++s) {
         c->segs[s].line_count = si[s].line_count;
@@ -318,6 +367,7 @@ void encode_units(starch_ctx* c, const uint8_t* d_base, const std::vector<UnitIn
         uint8_t* out = c->archive.as<uint8_t>(64);
         HIP_CHECK(hipMemcpyAsync(out, kMagic, 4, hipMemcpyHostToDevice, c->st));
         HIP_CHECK(hipStreamSynchronize(c->st));
+        finish_names(c, pnames);
         c->archive_bytes = 4;
         c->have = true;
         (void)hipEventDestroy(e0);
@@ -337,6 +387,7 @@ void encode_units(starch_ctx* c, const uint8_t* d_base, const std::vector<UnitIn
     const bool gzip = opt.compression_method == STARCH_METHOD_GZIP;
     if (gzip) c->genc.plan(text, sin, c->st, outs, &bst);
     else c->enc.plan(text, sin, opt.block_size_100k, c->st, outs, &bst);
+    finish_names(c, pnames);
     uint64_t streams_bytes = 0;
     for (auto& o : outs) streams_bytes = std::max(streams_bytes, o.out_off + o.bytes);
     for (uint64_t s = 0; s < nseg; ++s) {
@@ -1319,17 +1370,15 @@ static void transform_only(starch_ctx* c, const uint8_t* d, uint64_t n)
                                  hipMemcpyDeviceToHost, c->st));
     HIP_CHECK(hipStreamSynchronize(c->st));
     c->segs.assign(tr.n_segments, starch_segment{});
-    c->names.assign(tr.n_segments, std::string());
+    PendingNames pnames;
+    fetch_names(c, d, si, pnames);
     for (uint64_t s = 0; s < tr.n_segments; ++s) {
         c->segs[s].line_count = si[s].line_count;
         c->segs[s].text_bytes = si[s].text_len;
         c->segs[s].stream_offset = si[s].text_off;   // transform-only: offset into the text
         c->segs[s].name_len = si[s].name_len;
-        c->names[s].resize(si[s].name_len);
-        if (si[s].name_len)
-            HIP_CHECK(hipMemcpyAsync(&c->names[s][0], d + si[s].name_off, si[s].name_len, hipMemcpyDeviceToHost, c->st));
     }
-    HIP_CHECK(hipStreamSynchronize(c->st));
+    finish_names(c, pnames);
     float ms = 0;
     HIP_CHECK(hipEventElapsedTime(&ms, e0, e1));
     (void)hipEventDestroy(e0);

@@ -509,14 +509,49 @@ __device__ __forceinline__ uint32_t next_bit(uint64_t lo, uint64_t hi, uint32_t 
     return m ? 64u + (uint32_t)__builtin_ctzll(m) : 128u;
 }
 
+// 8 bytes of LDS from byte offset b (any alignment): three aligned words, two
+// byte-aligns (first byte lowest)
+__device__ __forceinline__ uint64_t lds_u64(const uint8_t* tb, uint32_t b)
+{
+    const uint32_t* w = reinterpret_cast<const uint32_t*>(tb + (b & ~3u));
+    const uint32_t sh = b & 3u;
+    const uint32_t w0 = w[0], w1 = w[1], w2 = w[2];
+    return ((uint64_t)__builtin_amdgcn_alignbyte(w2, w1, sh) << 32) | __builtin_amdgcn_alignbyte(w1, w0, sh);
+}
+
+// value of the 1..8 ASCII digits in the low n bytes of x (first digit lowest);
+// false if one of them is not a digit.  SWAR: digit pairs, then quads, then
+// the 8-digit value, three multiplies in all.
+__device__ __forceinline__ bool swar8(uint64_t x, uint32_t n, uint64_t& v)
+{
+    const uint64_t keep = n >= 8u ? ~0ull : ((1ull << (8u * n)) - 1ull);
+    // a byte < '0' sets its top bit in x - '0', a byte > '9' in x + 0x46 (or, past 0xB9, in x - '0')
+    if (((x + 0x4646464646464646ull) | (x - 0x3030303030303030ull)) & 0x8080808080808080ull & keep) return false;
+    x = ((x - 0x3030303030303030ull) & keep) << (8u * (8u - n));    // leading zero digits
+    x = (x * 10u + (x >> 8)) & 0x00FF00FF00FF00FFull;
+    x = (x * 100u + (x >> 16)) & 0x0000FFFF0000FFFFull;
+    v = (uint32_t)(x * 10000u + (x >> 32));
+    return true;
+}
+
 // 1..18 plain digits at tb[b..b+n) -> v (sscanf gives the same value for them)
 __device__ __forceinline__ bool dig_fast(const uint8_t* tb, uint32_t b, uint32_t n, int64_t& v)
 {
     if (n - 1u >= 18u) return false;
-    // trip count = the wave's longest field (coordinates: <= 9 digits), not 18
+    if (n <= 8u) {
+        uint64_t x;
+        if (!swar8(lds_u64(tb, b), n, x)) return false;
+        v = (int64_t)x;
+        return true;
+    }
+    if (n <= 16u) {                                  // the first n - 8 digits, then the last 8
+        uint64_t hi, lo;
+        if (!swar8(lds_u64(tb, b), n - 8u, hi) || !swar8(lds_u64(tb, b + n - 8u), 8u, lo)) return false;
+        v = (int64_t)(hi * 100000000ull + lo);
+        return true;
+    }
     uint64_t acc = 0;
     uint32_t bad = 0;
-#pragma unroll 3
     for (uint32_t k = 0; k < n; ++k) {
         const uint32_t d = (uint32_t)tb[b + k] - 48u;
         bad |= (d > 9u) ? 1u : 0u;
@@ -567,6 +602,43 @@ __device__ __forceinline__ bool parse_fast(const uint8_t* tb, uint32_t r0, uint3
     if (t3 < 128u) {
         r.rem_b = ls + (t3 + 1u - off);
         r.rem_len = nlp - (t3 + 1u);
+    } else {
+        r.rem_b = ls + len;
+        r.rem_len = 0;
+    }
+    return true;
+}
+
+// parse_fast with the tab positions read from precomputed LDS bit masks
+// (tabm bit i of word c: staged byte 32c + i is a tab) instead of SWAR over the
+// line's bytes; for tiles with no NUL byte (C-string rules then never apply).
+// Same acceptance rules and results as parse_fast; line at stage offset r0,
+// len bytes incl. its newline (<= 128), bed offset ls.
+__device__ __forceinline__ bool parse_mask(const uint8_t* tb, const uint32_t* tabm, uint32_t r0, uint32_t len,
+                                           uint64_t ls, LineVals& r)
+{
+    if (len - 1u >= 128u) return false;
+    const uint32_t w = r0 >> 5, sh = r0 & 31u;
+    const uint32_t m0 = tabm[w], m1 = tabm[w + 1], m2 = tabm[w + 2], m3 = tabm[w + 3], m4 = tabm[w + 4];
+    const uint32_t e = len - 1u;                           // the newline, line-relative
+    uint64_t tl = ((uint64_t)__builtin_amdgcn_alignbit(m2, m1, sh) << 32) | __builtin_amdgcn_alignbit(m1, m0, sh);
+    uint64_t th = ((uint64_t)__builtin_amdgcn_alignbit(m4, m3, sh) << 32) | __builtin_amdgcn_alignbit(m3, m2, sh);
+    tl &= lowbits(e);
+    th &= lowbits(e > 64u ? e - 64u : 0u);
+    // the reference's scan does not test the byte after a tab for a tab (tokenize)
+    const uint32_t t1 = next_bit(tl, th, 0);
+    if (t1 >= 128u) return false;
+    const uint32_t t2 = next_bit(tl, th, t1 + 2u);
+    if (t2 >= 128u) return false;
+    const uint32_t t3 = next_bit(tl, th, t2 + 2u);
+    const uint32_t e2 = t3 < 128u ? t3 : e;
+    if (!dig_fast(tb, r0 + t1 + 1u, t2 - t1 - 1u, r.a)) return false;
+    if (!dig_fast(tb, r0 + t2 + 1u, e2 - t2 - 1u, r.b)) return false;
+    r.aok = r.bok = true;
+    r.chr_len = t1;
+    if (t3 < 128u) {
+        r.rem_b = ls + t3 + 1u;
+        r.rem_len = e - (t3 + 1u);
     } else {
         r.rem_b = ls + len;
         r.rem_len = 0;
@@ -939,11 +1011,12 @@ struct LineKey { int64_t a, b; uint32_t cls, clen; };   // what the next line ne
 struct FusedShared {
     uint4 tb4[(kFH + kFT + 32 + kStagePad) / 16];
     uint16_t nlp[kFMaxLines];                  // LDS position of each line's '\n'
+    uint32_t tabm[(kFH + kFT + 32 + kStagePad) / 32 + 8];   // tab bit masks of the staged bytes (parse_mask)
     uint32_t ob4[kFOut / 4];
     uint64_t scan[kThreads / 64 + 1];
     FusedSeg seg[kFSeg];
     LineKey wlast[kThreads / 64 + 1];          // [0]: carry into the chunk; [w+1]: wave w's last line
-    uint32_t tile, ffpos, p1, p2, over;
+    uint32_t tile, ffpos, p1, p2, over, nul;
     TileAgg excl;
 };
 
@@ -994,8 +1067,9 @@ __device__ __forceinline__ void fused_lines(FusedShared& S, const uint8_t* tb, u
                 ls[u] = k ? (uint32_t)S.nlp[k - 1] + 1u : first_ls;
                 const uint32_t le = (uint32_t)S.nlp[k] + 1u;
                 t[u].ls = a0 + ls[u];
-                if (!parse_fast(tb, ls[u], le - ls[u], t[u].ls, t[u].r))
-                    t[u].r = parse_line_at(lsrc, a0 + ls[u], a0 + le);
+                const bool fast = S.nul ? parse_fast(tb, ls[u], le - ls[u], t[u].ls, t[u].r)
+                                        : parse_mask(tb, S.tabm, ls[u], le - ls[u], t[u].ls, t[u].r);
+                if (!fast) t[u].r = parse_line_at(lsrc, a0 + ls[u], a0 + le);
                 if (!t[u].r.aok || !t[u].r.bok) atomicOr(xflags, FX_FAIL);
                 key[u] = LineKey{t[u].r.a, t[u].r.b, ls[u], t[u].r.chr_len};
             }
@@ -1015,12 +1089,10 @@ __device__ __forceinline__ void fused_lines(FusedShared& S, const uint8_t* tb, u
             if (!(c0 + 2 * tid + u == 0 && input_start)) {
                 const uint32_t cl = t[u].r.chr_len;
                 bool same = (p.clen == cl);
-                for (uint32_t q = 0; same && q < cl; q += 8) {
-#pragma unroll
-                    for (uint32_t j = 0; j < 8; ++j) {
-                        const bool e = tb[p.cls + q + j] == tb[ls[u] + q + j];
-                        if (q + j < cl) same = same && e;
-                    }
+                for (uint32_t q = 0; same && q < cl; q += 8) {   // 8 bytes of both names at a time
+                    const uint64_t x = lds_u64(tb, p.cls + q) ^ lds_u64(tb, ls[u] + q);
+                    const uint32_t k = cl - q;
+                    same = (k >= 8u ? x : (x & ((1ull << (8u * k)) - 1ull))) == 0;
                 }
                 newseg = !same;
             }
@@ -1070,6 +1142,7 @@ k_tf_fused(const uint8_t* __restrict__ bed, uint64_t n, uint32_t* __restrict__ t
         S.p1 = 0;
         S.p2 = 0;
         S.over = 0;
+        S.nul = 0;
     }
     __syncthreads();
     const uint32_t tile = S.tile;
@@ -1097,18 +1170,37 @@ k_tf_fused(const uint8_t* __restrict__ bed, uint64_t n, uint32_t* __restrict__ t
         const uint4* q = reinterpret_cast<const uint4*>(tb + ch * 32);
         const uint4 x = q[0], y = q[1];
         const uint32_t w[8] = {x.x, x.y, x.z, x.w, y.x, y.y, y.z, y.w};
-        uint32_t nm = 0, fm = 0;
+        uint32_t nm = 0, fm = 0, tm = 0, zf = 0;
 #pragma unroll
         for (int j = 0; j < 8; ++j) {
             nm |= eq4(w[j], 0x0a0a0a0au) << (4 * j);
+            tm |= eq4(w[j], 0x09090909u) << (4 * j);
+            zf |= (w[j] - 0x01010101u) & ~w[j] & 0x80808080u;   // some byte is NUL
             fm |= eq4(w[j], 0xffffffffu) << (4 * j);
         }
+        S.tabm[ch] = tm;
+        if (zf) S.nul = 1;
         const uint32_t lo = ch * 32 < Lt0 ? Lt0 - ch * 32 : 0u;
         const uint32_t hi = Lend - ch * 32 < 32u ? Lend - ch * 32 : 32u;
         const uint32_t keep = (hi >= 32u ? 0xFFFFFFFFu : ((1u << hi) - 1u)) & ~((1u << lo) - 1u);
         nlm[it] = nm & keep;
         fm &= keep;
         if (fm) atomicMin(&S.ffpos, ch * 32 + (uint32_t)__builtin_ctz(fm));
+    }
+    // tab masks and the NUL flag of the halo chunks as well (a tile's first
+    // line starts in its halo)
+    for (uint32_t ch = tid; ch < cbeg; ch += kThreads) {
+        const uint4* q = reinterpret_cast<const uint4*>(tb + ch * 32);
+        const uint4 x = q[0], y = q[1];
+        const uint32_t w[8] = {x.x, x.y, x.z, x.w, y.x, y.y, y.z, y.w};
+        uint32_t tm = 0, zf = 0;
+#pragma unroll
+        for (int j = 0; j < 8; ++j) {
+            tm |= eq4(w[j], 0x09090909u) << (4 * j);
+            zf |= (w[j] - 0x01010101u) & ~w[j] & 0x80808080u;
+        }
+        S.tabm[ch] = tm;
+        if (zf) S.nul = 1;
     }
     // the halo's last two newlines (wave 0, 64 bytes at a time, backwards):
     // the previous line is [p2, p1), the first line starts at p1
