@@ -119,6 +119,16 @@ void starch_options_init(starch_options* opt);
 int starch_encode_device(starch_ctx* ctx, const void* d_bed, uint64_t n, const starch_options* opt);
 /* Same, from host memory (copied to HBM first; the copy is not in ms_total). */
 int starch_encode_host(starch_ctx* ctx, const void* bed, uint64_t n, const starch_options* opt);
+/* Host bytes in, archive bytes out into the caller's host buffer out[0, cap)
+ * (*out_len = its size; STARCH_ERR_MEM if cap is short).  For large pinned
+ * inputs every chromosome batch's finished streams go device-to-host while
+ * later batches still cross PCIe / encode, so the archive's PCIe trip
+ * overlaps the work (pinned out recommended).  Same bytes as
+ * starch_encode_host + starch_archive_copy; the archive also stays readable
+ * through the accessors below.  (The reference writes its archive to stdout
+ * from starch3.cpp's main loop, hpp:758-776.) */
+int starch_encode_host_into(starch_ctx* ctx, const void* bed, uint64_t n, const starch_options* opt, void* out,
+                            uint64_t cap, uint64_t* out_len);
 
 /* ---- multi-GPU: per-chromosome units sharded across devices ----
  * Plan: split host BED bytes (up to the first 0xFF, hpp:181) into at most

@@ -120,6 +120,8 @@ def load():
         "starch_options_init": ([ctypes.POINTER(Options)], None),
         "starch_encode_device": ([vp, vp, u64, ctypes.POINTER(Options)], ctypes.c_int),
         "starch_encode_host": ([vp, ctypes.c_char_p, u64, ctypes.POINTER(Options)], ctypes.c_int),
+        "starch_encode_host_into": ([vp, vp, u64, ctypes.POINTER(Options), vp, u64, ctypes.POINTER(u64)],
+                                    ctypes.c_int),
         "starch_archive_size": ([vp, pu64], ctypes.c_int),
         "starch_archive_device": ([vp, ctypes.POINTER(vp)], ctypes.c_int),
         "starch_archive_copy": ([vp, vp, u64], ctypes.c_int),
@@ -277,6 +279,16 @@ class Starch:
         o = self._opts(emit_index)
         _check(self._L.starch_encode_host(self._h, ctypes.cast(ctypes.c_void_p(ptr), ctypes.c_char_p), n,
                                           ctypes.byref(o)), self._h)
+
+    def compress_host_into(self, ptr: int, n: int, out_ptr: int, cap: int, emit_index=True) -> int:
+        """BED bytes at a host address -> archive written to the host address
+        out_ptr (cap bytes); finished batches go device-to-host while later
+        ones encode (starch_encode_host_into).  Returns the archive size."""
+        o = self._opts(emit_index)
+        k = ctypes.c_uint64()
+        _check(self._L.starch_encode_host_into(self._h, ctypes.c_void_p(ptr), n, ctypes.byref(o),
+                                               ctypes.c_void_p(out_ptr), cap, ctypes.byref(k)), self._h)
+        return k.value
 
     # -- streaming ingestion (starch_stream_*) ----------------------------------
     def stream_begin(self, batch_bytes=0, emit_index=True, reference_compat=False):

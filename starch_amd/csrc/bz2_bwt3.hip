@@ -1282,7 +1282,13 @@ __device__ __forceinline__ void grp_finish_keys(GrpIn<E>& x)
 #ifndef STARCH_WPE_M2
 #define STARCH_WPE_M2 3
 #endif
-constexpr int sort_wpe(int NW, int E) { return NW == 4 && E == 8 ? STARCH_WPE_M2 : (NW == 1 ? STARCH_WPE_GRP : 1); }
+#ifndef STARCH_WPE_S
+#define STARCH_WPE_S STARCH_WPE_GRP   // the S class (one wave, E = 2)
+#endif
+constexpr int sort_wpe(int NW, int E)
+{
+    return NW == 4 && E == 8 ? STARCH_WPE_M2 : (NW == 1 ? (E == 2 ? STARCH_WPE_S : STARCH_WPE_GRP) : 1);
+}
 
 template <int NW, int E, bool DBL>
 __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(sort_wpe(NW, E))))

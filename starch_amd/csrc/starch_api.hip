@@ -515,12 +515,45 @@ void collect_append(starch_ctx* L, uint64_t& end, const void* src, uint64_t n)
     end += n;
 }
 
+// Host output of the pipelined encode (starch_encode_host_into): a batch's
+// archive offset is known once every earlier batch has finished, so each
+// finished batch whose predecessors are done goes device-to-host at once, on
+// its lane's stream (after the append that put it in the collect buffer).
+// Appends run under mu, so collect.p is read consistently, and a collect
+// reallocation syncs its stream before freeing, so a queued copy's source
+// stays valid.
+struct HostOut {
+    uint8_t* out = nullptr;
+    uint64_t cap = 0, off = 4;     // next batch's archive offset (after the magic)
+    size_t next = 0;               // first batch not yet written
+    bool overflow = false;
+    std::mutex mu;
+    std::vector<char> done;
+    std::vector<starch_ctx*> lane;
+    void finished(size_t k, const std::vector<LaneBatch>& res)
+    {
+        std::lock_guard<std::mutex> lk(mu);
+        done[k] = 1;
+        while (next < done.size() && done[next]) {
+            const LaneBatch& r = res[next];
+            if (off + r.bytes > cap) overflow = true;
+            else if (r.bytes) {
+                starch_ctx* L = lane[r.lane];
+                HIP_CHECK(hipMemcpyAsync(out + off, static_cast<uint8_t*>(L->collect.p) + r.coll_off, r.bytes,
+                                         hipMemcpyDeviceToHost, L->st));
+            }
+            off += r.bytes;
+            ++next;
+        }
+    }
+};
+
 // one lane: batches `mine` (indices into `batches`) in order, each once its
 // bytes are in HBM (ev[k], recorded on the shared copy stream after its H2D)
 void run_lane(starch_ctx* L, const uint8_t* d_in, const std::vector<shard::Unit>& plan,
               const std::vector<std::pair<size_t, size_t>>& batches, const std::vector<hipEvent_t>& ev,
               const std::vector<size_t>& mine, const starch_options& opt, std::vector<LaneBatch>& out, int lane,
-              const std::atomic<bool>& stop)
+              const std::atomic<bool>& stop, HostOut* hout)
 {
     uint64_t total = 0;
     for (size_t k : mine)
@@ -545,12 +578,21 @@ void run_lane(starch_ctx* L, const uint8_t* d_in, const std::vector<shard::Unit>
         r.segs = L->segs;
         r.names = L->names;
         r.stats = L->stats;
-        collect_append(L, cend, L->part.p, L->part_bytes);
+        if (hout) {   // appends (and collect reallocations) under the writer's lock: it reads collect.p
+            {
+                std::lock_guard<std::mutex> lk(hout->mu);
+                collect_append(L, cend, L->part.p, L->part_bytes);
+            }
+            hout->finished(k, out);
+        } else {
+            collect_append(L, cend, L->part.p, L->part_bytes);
+        }
     }
     HIP_CHECK(hipStreamSynchronize(L->st));
 }
 
-bool encode_host_pipelined(starch_ctx* c, const uint8_t* bed, uint64_t n, const starch_options& opt)
+bool encode_host_pipelined(starch_ctx* c, const uint8_t* bed, uint64_t n, const starch_options& opt,
+                           uint8_t* hout_p = nullptr, uint64_t hout_cap = 0, uint64_t* hout_len = nullptr)
 {
     using clk = std::chrono::steady_clock;
     const auto t0 = clk::now();
@@ -584,6 +626,14 @@ bool encode_host_pipelined(starch_ctx* c, const uint8_t* bed, uint64_t n, const 
     for (int i = 0; i < nl; ++i) lane[i] = lane_ctx(c, i);
     std::vector<LaneBatch> res(batches.size());
     std::atomic<bool> stop{false}, saw_ff{false};
+    std::unique_ptr<HostOut> hout;
+    if (hout_p) {
+        hout.reset(new HostOut());
+        hout->out = hout_p;
+        hout->cap = hout_cap;
+        hout->done.assign(batches.size(), 0);
+        hout->lane = lane;
+    }
     std::vector<int> codes(nl, 0);
     std::vector<std::string> errs(nl);
     // every batch crosses PCIe in input order on one copy stream, into one
@@ -607,7 +657,7 @@ bool encode_host_pipelined(starch_ctx* c, const uint8_t* bed, uint64_t n, const 
     auto work = [&](int i) {
         try {
             Ctx g(lane[i]);
-            run_lane(lane[i], d_in, plan, batches, ev, mine[i], opt, res, i, stop);
+            run_lane(lane[i], d_in, plan, batches, ev, mine[i], opt, res, i, stop, hout.get());
         } catch (const FFInBatch&) {
             saw_ff = true;
             stop = true;
@@ -628,6 +678,7 @@ bool encode_host_pipelined(starch_ctx* c, const uint8_t* bed, uint64_t n, const 
         for (auto& t : th) t.join();
     }
     (void)hipStreamSynchronize(c->cst);
+    for (int i = 0; i < nl; ++i) (void)hipStreamSynchronize(lane[i]->st);   // device-to-host writes queued by other lanes
     for (auto& e : ev) (void)hipEventDestroy(e);
     for (int i = 0; i < nl; ++i)
         if (codes[i]) throw StarchError(codes[i], errs[i]);
@@ -684,6 +735,15 @@ bool encode_host_pipelined(starch_ctx* c, const uint8_t* bed, uint64_t n, const 
         k = k2;
     }
     if (!idx.empty()) HIP_CHECK(hipMemcpyAsync(arch + end, idx.data(), idx.size(), hipMemcpyHostToDevice, c->st));
+    if (hout) {   // every batch went out already (all lanes finished); magic and index from the host
+        if (hout->overflow || hout->off != end || end + idx.size() > hout_cap) {
+            HIP_CHECK(hipStreamSynchronize(c->st));
+            throw StarchError(STARCH_ERR_MEM, "output buffer too small");
+        }
+        memcpy(hout_p, kMagic, 4);
+        memcpy(hout_p + end, idx.data(), idx.size());
+        *hout_len = end + idx.size();
+    }
     HIP_CHECK(hipStreamSynchronize(c->st));
     st.input_bytes = n;
     st.n_segments = segs.size();
@@ -1153,6 +1213,32 @@ static int units_in(const starch_unit* units, const uint64_t* ids, uint64_t nuni
     for (uint64_t k = 1; k < nunits; ++k)
         if (u[k].id <= u[k - 1].id) return STARCH_ERR_ARG;   // units in input order
     return STARCH_OK;
+}
+
+int starch_encode_host_into(starch_ctx* c, const void* bed, uint64_t n, const starch_options* opt, void* out,
+                            uint64_t cap, uint64_t* out_len)
+{
+    GUARD(c)
+    if ((n && !bed) || !out || !out_len) return STARCH_ERR_ARG;
+    starch_options o;
+    starch_options_init(&o);
+    if (opt) o = *opt;
+    if (o.block_size_100k < 1 || o.block_size_100k > 9 ||
+        (o.compression_method != STARCH_METHOD_BZIP2 && o.compression_method != STARCH_METHOD_GZIP)) return STARCH_ERR_ARG;
+    static const bool pipe_off = [] { const char* e = getenv("STARCH_PIPELINE"); return e && !strcmp(e, "0"); }();
+    if (!pipe_off && !o.reference_compat && n >= (256ull << 20) && host_is_pinned(bed) &&
+        encode_host_pipelined(c, static_cast<const uint8_t*>(bed), n, o, static_cast<uint8_t*>(out), cap, out_len))
+        return STARCH_OK;
+    uint8_t* d = c->input.as<uint8_t>(n + 64);
+    if (n) HIP_CHECK(hipMemcpyAsync(d, bed, n, hipMemcpyHostToDevice, c->st));
+    HIP_CHECK(hipStreamSynchronize(c->st));
+    encode_device(c, d, n, o);
+    if (cap < c->archive_bytes) return STARCH_ERR_MEM;
+    if (c->archive_bytes) HIP_CHECK(hipMemcpyAsync(out, c->archive.p, c->archive_bytes, hipMemcpyDeviceToHost, c->st));
+    HIP_CHECK(hipStreamSynchronize(c->st));
+    *out_len = c->archive_bytes;
+    return STARCH_OK;
+    END_GUARD(c)
 }
 
 int starch_encode_units_device(starch_ctx* c, const void* d_base, const starch_unit* units, const uint64_t* unit_ids,

@@ -173,6 +173,38 @@ def test_pipelined_host_encode_equals_device_encode():
     c.close()
 
 
+def test_host_into_equals_device_encode():
+    """starch_encode_host_into: the pipelined encode writes every finished
+    batch's streams straight into the caller's host buffer while later batches
+    encode; magic + streams + index equal the device-resident archive, a short
+    buffer is refused, and a pageable / small input takes the one-copy path."""
+    import ctypes
+    import torch
+    import starch_amd
+    n = sum(starch_amd.gen_bed_sizes(0, 12_000_000, seed=3))
+    host = torch.empty(n, dtype=torch.uint8, pin_memory=True)
+    starch_amd.gen_bed(0, 12_000_000, seed=3, into=ctypes.c_void_p(host.data_ptr()))
+    c = starch_amd.Starch(0)
+    dev = host.to("cuda")
+    c.compress_device(dev.data_ptr(), n)
+    want = c.archive()
+    out = torch.zeros(len(want) + 4096, dtype=torch.uint8, pin_memory=True)
+    for _ in range(2):
+        k = c.compress_host_into(host.data_ptr(), n, out.data_ptr(), out.numel())
+        assert k == len(want) and out[:k].numpy().tobytes() == want
+    assert c.archive() == want
+    with pytest.raises(starch_amd.StarchError):
+        c.compress_host_into(host.data_ptr(), n, out.data_ptr(), len(want) // 2)
+    small = bytes(host[:5_000_000].numpy())
+    small = small[:small.rfind(b"\n") + 1]
+    ref = c.compress(small)
+    buf = ctypes.create_string_buffer(len(ref) + 64)
+    sbuf = ctypes.create_string_buffer(small, len(small))
+    k = c.compress_host_into(ctypes.addressof(sbuf), len(small), ctypes.addressof(buf), len(buf))
+    assert buf.raw[:k] == ref
+    c.close()
+
+
 @pytest.mark.parametrize("lanes", ["1", "3"])
 def test_pipelined_lanes_and_batches(lanes):
     """The lane count and batch count of the pipelined path change only the

@@ -16,6 +16,7 @@ import csv
 import glob
 import json
 import os
+import re
 import sys
 
 sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
@@ -23,11 +24,14 @@ from bench import src_stamp  # noqa: E402
 from tools.pmc_bwt_traffic import is_bwt  # noqa: E402
 
 
+KSEL = os.environ.get("PMC_KERNELS", "")     # regex over kernel names (default: the block-sort kernels)
+
+
 def load(d):
     tot = collections.defaultdict(collections.Counter)
     for f in glob.glob(os.path.join(d, "**", "run_counter_collection.csv"), recursive=True):
         for r in csv.DictReader(open(f)):
-            if is_bwt(r["Kernel_Name"]):
+            if (re.search(KSEL, r["Kernel_Name"]) if KSEL else is_bwt(r["Kernel_Name"])):
                 k = r["Kernel_Name"].replace("(anonymous namespace)::", "").split("(")[0].replace("void ", "")
                 tot[k][r["Counter_Name"]] += float(r["Counter_Value"])
     return tot
