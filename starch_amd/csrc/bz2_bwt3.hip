@@ -179,6 +179,26 @@ __device__ __forceinline__ uint64_t lanemask_lt()
     return lane ? (~0ull >> (64 - lane)) : 0ull;
 }
 
+// Rotation values (SA / V) and last-column bytes stream through the sorts:
+// read once per group, written once.  Non-temporal access keeps them from
+// evicting the blocks' packed symbol streams (the random key gathers) from
+// the XCD's 4 MB L2.  STARCH_NT=0: plain accesses.
+#ifndef STARCH_NT
+#define STARCH_NT 0   // 1: non-temporal SA/LL/value streams (measured: cfg2 sort 23.5 -> 34.3 ms, cfg4 110 -> 130 ms)
+#endif
+template <class T>
+__device__ __forceinline__ T ld_nt(const T* p)
+{
+    if constexpr (STARCH_NT != 0) return __builtin_nontemporal_load(p);
+    else return *p;
+}
+template <class T>
+__device__ __forceinline__ void st_nt(T* p, T v)
+{
+    if constexpr (STARCH_NT != 0) __builtin_nontemporal_store(v, p);
+    else *p = v;
+}
+
 // Append `item` for every lane with pred to list/ctr; one atomic per wave.
 // Must be reached by all 64 lanes of the wave.
 __device__ __forceinline__ void wave_push(uint32_t* ctr, uint64_t* list, bool pred, uint64_t item)
@@ -736,7 +756,7 @@ __global__ void __launch_bounds__(SCT) k3_scatter_lds(Ctx c)
                 const uint32_t v = stage[j];
                 const uint32_t dg = v >> 15, r = t0 + (v & 0x7FFFu);
                 const uint32_t pos = cur[dg] + (j - lst[dg]);
-                SA[pos] = r;
+                st_nt(SA + pos, r);
                 uint32_t ls = 0;
                 if (mat && r) {   // (MAT: compile-time)
                     const uint64_t bit = (uint64_t)(r - 1) * B - (wbase << 6);
@@ -898,7 +918,7 @@ __global__ void __launch_bounds__(LT) k3_part_l(Ctx c, const uint64_t* __restric
             for (int u = 0; u < PU; ++u) {
                 const uint32_t i = i0 + u * LT + tid;
                 const uint32_t ic = i < m ? i : 0u;
-                d[u] = (uint32_t)((elem_key<DBL>(ks, s + ic, sv[ic]) >> sh2) & dmask);
+                d[u] = (uint32_t)((elem_key<DBL>(ks, s + ic, ld_nt(sv + ic)) >> sh2) & dmask);
                 if (!DBL && m <= PL_CAP && i < m) dcache[i] = (uint8_t)d[u];
             }
 #pragma unroll
@@ -919,7 +939,7 @@ __global__ void __launch_bounds__(LT) k3_part_l(Ctx c, const uint64_t* __restric
             for (int u = 0; u < PU; ++u) {
                 const uint32_t i = i0 + u * LT + tid;
                 const uint32_t ic = i < m ? i : 0u;
-                v[u] = sv[ic];
+                v[u] = ld_nt(sv + ic);
                 if (!DBL && m <= PL_CAP) k[u] = (uint64_t)dcache[ic] << sh2;   // only the digit is used below
                 else k[u] = elem_key<DBL>(ks, s + ic, v[u]);
                 lsy[u] = dl ? ks.l[s + ic] : (uint8_t)0;
@@ -928,7 +948,7 @@ __global__ void __launch_bounds__(LT) k3_part_l(Ctx c, const uint64_t* __restric
             for (int u = 0; u < PU; ++u) {
                 if (i0 + u * LT + tid < m) {
                     const uint32_t p = atomicAdd(&cur[(uint32_t)((k[u] >> sh2) & dmask)], 1u);
-                    dv[p] = v[u];
+                    st_nt(dv + p, v[u]);
                     if constexpr (DBL) dk[p] = k[u];
                     if (dl) dl[p] = lsy[u];
                 }
@@ -990,8 +1010,8 @@ __device__ __forceinline__ void emit_sorted(const Ctx& c, uint32_t slot, uint32_
 {
     const uint64_t so = (uint64_t)slot * c.scr.stride;
     if (valid) {
-        c.scr.SA[so + s + j] = v;
-        c.scr.LL[so + s + j] = (uint8_t)lsym;
+        st_nt(c.scr.SA + so + s + j, v);
+        st_nt(c.scr.LL + so + s + j, (uint8_t)lsym);
         if (c.mode) c.scr.RK[so + v] = s + hp;
         if (v == 0) c.blocks[c.b0 + slot].orig_ptr = s + j;
     }
@@ -1012,8 +1032,8 @@ __device__ __forceinline__ void emit_vals(const Ctx& c, uint32_t slot, uint32_t 
 {
     if (valid) {
         const uint64_t so = (uint64_t)slot * c.scr.stride;
-        c.scr.SA[so + s + j] = v;
-        c.scr.LL[so + s + j] = (uint8_t)lsym;
+        st_nt(c.scr.SA + so + s + j, v);
+        st_nt(c.scr.LL + so + s + j, (uint8_t)lsym);
         if (c.mode) c.scr.RK[so + v] = s + hp;
         if (v == 0) c.blocks[c.b0 + slot].orig_ptr = s + j;
     }
@@ -1099,7 +1119,7 @@ __global__ void __launch_bounds__(256) k3_sort_w(Ctx c, const uint64_t* __restri
             const uint32_t j = valid ? lane - gstart : 0u;
             const uint32_t* sv = (par ? c.scr.V : c.scr.SA) + (uint64_t)slot * c.scr.stride + s;
             const KeySrc ks = key_src(c, slot, par);
-            const uint32_t v = sv[j];
+            const uint32_t v = ld_nt(sv + j);
             uint32_t ls;
             uint64_t k = elem_key<DBL>(c, ks, slot, s + j, v, ls);
             if (!valid) k = ~0ull;
@@ -1186,6 +1206,7 @@ struct GrpIn {                 // one group's inputs, as loaded
     uint64_t kb[E];            // PSS rounds: the second raw key word
     uint32_t lb[E];            // ... and the second raw window word of the last-column symbol
     uint64_t k0b;
+    bool one;                  // PSS round 0, B in {1,2,4,5,6,8}: kx/kb = ONE 16-B load holding the symbol and the key
 };
 
 // loads of a group that does not exist (ok false) go to element 0 of slot 0's
@@ -1200,7 +1221,7 @@ __device__ __forceinline__ void grp_load_vals(const Ctx& c, GrpIn<E>& x, bool ok
 #pragma unroll
     for (int e = 0; e < E; ++e) {
         const uint32_t i = (uint32_t)(wid * 64 * E + e * 64 + lane);
-        x.v[e] = sv[i < m ? i : 0u];
+        x.v[e] = ld_nt(sv + (i < m ? i : 0u));
     }
     x.v0 = sv[0];
 }
@@ -1239,14 +1260,36 @@ __device__ __forceinline__ void grp_load_keys(const Ctx& c, GrpIn<E>& x, int wid
     } else {
         const uint64_t* __restrict__ w = x.ks.pss;
         const uint32_t* __restrict__ w32 = reinterpret_cast<const uint32_t*>(w);
+        const uint32_t B = x.ks.B;
+        // round 0: the last-column symbol's B bits sit right before the key's KB
+        // bits, and for these B the B + KB bits after the symbol's bit offset
+        // within its word (a multiple of B <= 64 - B ... 63) never pass the
+        // next word: one 16-byte load per element instead of four
+        x.one = x.ks.off == 0 && (B == 1 || B == 2 || B == 4 || B == 5 || B == 6 || B == 8);
+        if (x.one) {
 #pragma unroll
-        for (int e = 0; e < E; ++e) {
-            const uint64_t q = ((uint64_t)pss_rr(x.ks, x.v[e]) * x.ks.B) >> 6;
-            x.kx[e] = w[q];
-            x.kb[e] = w[q + 1];
-            const uint64_t j = ((uint64_t)pss_pr(x.ks, x.v[e]) * x.ks.B) >> 5;
-            x.ls[e] = w32[j ^ 1u];
-            x.lb[e] = w32[(j + 1u) ^ 1u];
+            for (int e = 0; e < E; ++e) {
+                const uint32_t r = x.v[e];
+                const uint64_t q = ((uint64_t)(r ? r - 1u : 0u) * B) >> 6;
+                const uint4 kv = *reinterpret_cast<const uint4*>(w + q);
+                x.kx[e] = ((uint64_t)kv.y << 32) | kv.x;
+                x.kb[e] = ((uint64_t)kv.w << 32) | kv.z;
+                if (r == 0) {                      // rotation 0: its symbol is the block's last
+                    const uint64_t j = ((uint64_t)(x.ks.n - 1u) * B) >> 5;
+                    x.ls[e] = w32[j ^ 1u];
+                    x.lb[e] = w32[(j + 1u) ^ 1u];
+                }
+            }
+        } else {
+#pragma unroll
+            for (int e = 0; e < E; ++e) {
+                const uint64_t q = ((uint64_t)pss_rr(x.ks, x.v[e]) * B) >> 6;
+                x.kx[e] = w[q];
+                x.kb[e] = w[q + 1];
+                const uint64_t j = ((uint64_t)pss_pr(x.ks, x.v[e]) * B) >> 5;
+                x.ls[e] = w32[j ^ 1u];
+                x.lb[e] = w32[(j + 1u) ^ 1u];
+            }
         }
         const uint64_t q0 = ((uint64_t)pss_rr(x.ks, x.v0) * x.ks.B) >> 6;
         x.k0 = w[q0];
@@ -1259,6 +1302,25 @@ __device__ __forceinline__ void grp_finish_keys(GrpIn<E>& x)
 {
     if constexpr (defer_keys<NW, DBL>()) {
         const KeySrc& ks = x.ks;
+        if (x.one) {
+            const uint32_t B = ks.B;
+#pragma unroll
+            for (int e = 0; e < E; ++e) {
+                const uint32_t r = x.v[e];
+                const uint64_t A = x.kx[e], W = x.kb[e];
+                if (r) {
+                    const uint32_t p0 = (uint32_t)(((uint64_t)(r - 1u) * B) & 63u), pk = p0 + B;
+                    x.ls[e] = (uint32_t)(((A << p0) | ((W >> 1) >> (63u - p0))) >> (64u - B));
+                    const uint64_t win = pk >= 64u ? (W << (pk - 64u)) : ((A << pk) | ((W >> 1) >> (63u - pk)));
+                    x.kx[e] = win >> (64u - ks.kbits);
+                } else {
+                    x.kx[e] = A >> (64u - ks.kbits);
+                    const uint32_t pl = (uint32_t)(((uint64_t)(ks.n - 1u) * B) & 31u);
+                    const uint64_t lw = ((uint64_t)x.ls[e] << 32) | x.lb[e];
+                    x.ls[e] = (uint32_t)((lw << pl) >> (64u - B));
+                }
+            }
+        } else {
 #pragma unroll
         for (int e = 0; e < E; ++e) {
             const uint32_t p = (uint32_t)(((uint64_t)pss_rr(ks, x.v[e]) * ks.B) & 63u);
@@ -1267,6 +1329,7 @@ __device__ __forceinline__ void grp_finish_keys(GrpIn<E>& x)
             const uint32_t pl = (uint32_t)(((uint64_t)pss_pr(ks, x.v[e]) * ks.B) & 31u);
             const uint64_t lw = ((uint64_t)x.ls[e] << 32) | x.lb[e];
             x.ls[e] = (uint32_t)((lw << pl) >> (64u - ks.B));
+        }
         }
         const uint32_t p0 = (uint32_t)(((uint64_t)pss_rr(ks, x.v0) * ks.B) & 63u);
         const uint64_t v0 = (x.k0 << p0) | ((x.k0b >> 1) >> (63u - p0));
@@ -1777,6 +1840,17 @@ k3_sort_lds(Ctx c, const uint64_t* __restrict__ items,
 #endif
 constexpr uint32_t HARD_Q = STARCH_HARD_Q;
 
+// STARCH_SORT_PROF (timing experiment, dev builds only): per-wave shader-clock
+// time of k3_sort_grp's phases, summed over the launch into g_sprof
+#ifdef STARCH_SORT_PROF
+__device__ unsigned long long g_sprof[16];
+#define SPROF(v) const uint64_t v = __builtin_readcyclecounter()
+#define SPACC(i, a, b) pacc[i] += (b) - (a)
+#else
+#define SPROF(v)
+#define SPACC(i, a, b)
+#endif
+
 template <int NW, int E, bool DBL>
 __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(sort_wpe(NW, E))))
 k3_sort_grp(Ctx c, const uint64_t* __restrict__ items,
@@ -1834,7 +1908,11 @@ k3_sort_grp(Ctx c, const uint64_t* __restrict__ items,
     grp_load_keys<NW, E, DBL>(c, cur, wid, lane);
     grp_load_vals<NW, E>(c, nxt, it1 != NONE, wid, lane);
     uint64_t nitem2 = it2 != NONE ? items[it2] : 0ull;
+#ifdef STARCH_SORT_PROF
+    uint64_t pacc[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+#endif
     while (it != NONE) {
+    SPROF(t0);
     const uint64_t item = cur.item;
     const uint32_t slot = it_slot(item), s = it_start(item), m = it_size(item);
     grp_finish_keys<NW, E, DBL>(cur);
@@ -1862,6 +1940,8 @@ k3_sort_grp(Ctx c, const uint64_t* __restrict__ items,
         for (int w = 0; w < NW; ++w) diff |= red_all[w0 + w];
     }
     if ((diff >> KEYB) && tg == 0) atomicOr(&c.L.ctr[C_ERR], 1u);   // top bits not shared
+    SPROF(t1);
+    SPACC(0, t0, t1);
 
     bool is_hard = false;
     const uint64_t kdiff = diff & KMASK;
@@ -1896,6 +1976,8 @@ k3_sort_grp(Ctx c, const uint64_t* __restrict__ items,
             for (int w = 0; w < NW; ++w) sq += wsq_all[w0 + w];
         }
         is_hard = sq > HARD_Q * m;                 // uniform per group
+        SPROF(t2);
+        SPACC(1, t1, t2);
 #ifdef STARCH_SORT_STATS
         if (tg == 0) { atomicAdd(&c.L.ctr[C_STG], 1u); atomicAdd(&c.L.ctr[C_STE], m); if (is_hard) atomicAdd(&c.L.ctr[C_STH], 1u); }
 #endif
@@ -1937,8 +2019,12 @@ k3_sort_grp(Ctx c, const uint64_t* __restrict__ items,
 #pragma unroll
         for (int e = 0; e < E; ++e) xk[wid * 64 * E + e * 64 + lane] = k[e];
     }
+    SPROF(t3);
+    SPACC(2, t1, t3);
     // next group's keys (its rotations were loaded one group ago), the item after it
     grp_load_keys<NW, E, DBL>(c, nxt, wid, lane);
+    SPROF(t4);
+    SPACC(3, t3, t4);
     const uint32_t it3 = it2 != NONE ? wq.next(c.qhead, qs, c.qseg, xs) : NONE;
     const uint64_t nitem3 = it3 != NONE ? items[it3] : 0ull;
     if (!is_hard) {
@@ -1983,6 +2069,8 @@ k3_sort_grp(Ctx c, const uint64_t* __restrict__ items,
             for (int e = 0; e < E; ++e) hp[e] = hp[e] > pre ? hp[e] : pre;
         }
     }
+    SPROF(t5);
+    SPACC(4, t4, t5);
     // the group's SA range was read (values consumed above) before any write
     uint32_t runs = 0, tcnt = 0;
     uint64_t tm[E];
@@ -2011,6 +2099,8 @@ k3_sort_grp(Ctx c, const uint64_t* __restrict__ items,
         }
     }
     }
+    SPROF(t6);
+    SPACC(5, t4, t6);
     // rotate the pipeline: next group's rotations, the one after it
     cur = nxt;
     nxt.item = nitem2;
@@ -2019,7 +2109,14 @@ k3_sort_grp(Ctx c, const uint64_t* __restrict__ items,
     it = it1;
     it1 = it2;
     it2 = it3;
+    SPROF(t7);
+    SPACC(6, t6, t7);
+    SPACC(7, t0, t7);
     }
+#ifdef STARCH_SORT_PROF
+    if (lane == 0)
+        for (int q = 0; q < 8; ++q) atomicAdd(&g_sprof[q + (E == 2 ? 0 : 8)], (unsigned long long)pacc[q]);
+#endif
     tacc = wave_reduce_add<uint32_t>(tacc);
     if (lane == 0 && tacc) atomicAdd(c.L.ctr + C_TS0 + c.tsel, tacc);
 }
@@ -2503,6 +2600,21 @@ void launch_bwt3(BlockDesc* blocks, uint32_t b0, uint32_t nb, const uint8_t* blk
     }
     hipLaunchKernelGGL(k3_finish, dim3((nb + 255) / 256), dim3(256), 0, st, c, nb, stats);
     HIP_CHECK(hipGetLastError());
+#ifdef STARCH_SORT_PROF
+    {
+        unsigned long long h[16];
+        HIP_CHECK(hipStreamSynchronize(st));
+        HIP_CHECK(hipMemcpyFromSymbol(h, HIP_SYMBOL(g_sprof), sizeof(h)));
+        static const unsigned long long zero[16] = {};
+        HIP_CHECK(hipMemcpyToSymbol(HIP_SYMBOL(g_sprof), zero, sizeof(zero)));
+        const char* nm[8] = {"keys-wait+finish", "digit+hist+scan", "digit..place", "next-keys-issue", "ties+heads",
+                             "tail(ties..emit)", "rotate+next-vals", "total"};
+        for (int e = 0; e < 2; ++e)
+            for (int q = 0; q < 8; ++q)
+                fprintf(stderr, "[sprof] E=%d %-18s %14llu (%.1f%%)\n", e ? 4 : 2, nm[q], h[8 * e + q],
+                        100.0 * (double)h[8 * e + q] / (double)(h[8 * e + 7] ? h[8 * e + 7] : 1));
+    }
+#endif
 }
 
 }  // namespace bz

@@ -90,7 +90,7 @@ void Encoder::plan(const uint8_t* d_text, const std::vector<StreamIn>& streams, 
     uint32_t* d_carry = b_tile_carry.as<uint32_t>(ntiles + 1);
     uint32_t* d_tw = b_tile_w.as<uint32_t>(ntiles + 1);
     uint64_t* d_twpre = b_tile_wpre.as<uint64_t>(ntiles + 1);
-    uint8_t* d_tpos = b_tpos.as<uint8_t>(ntiles * (kTB / 4) + 64);      // 2-bit classes, tile-aligned
+    uint8_t* d_tpos = b_tpos.as<uint8_t>(ntiles * kTB + 16);            // tile-aligned
     uint64_t* d_scal = b_scal.as<uint64_t>(nstreams_ + 16);
     HIP_CHECK(hipMemsetAsync(d_twpre, 0, (ntiles + 1) * sizeof(uint64_t), st));
     if (ntiles) {

@@ -17,11 +17,7 @@
 //                   CRC-32/BZIP2 of each block's input bytes: slice-by-4 CRC of
 //                   16-byte strips, GF(2) combine of strips -> chunks -> block
 // Every lane handles one 16-byte strip, loaded with one or two aligned 16-B
-// loads (any text alignment).  tpos keeps, per text byte, only the class of its
-// chunk position that the later passes read -- 0: t = 0 (chunk start), 1: t in
-// {1, 2}, 2: t = 3 (its chunk's count byte follows), 3: t > 3 -- 2 bits each,
-// one u32 per 16-byte strip, tile-aligned (tile t at word t * 256): a quarter
-// of the bytes of a per-byte array to write and read back.
+// loads (any text alignment); tpos is stored tile-aligned (tile t at t*4096).
 #include "bz2_int.hpp"
 
 namespace bz {
@@ -293,11 +289,6 @@ __global__ void __launch_bounds__(CT) k_rle_carry(const uint64_t* __restrict__ s
 }
 
 __device__ __forceinline__ uint32_t rle_w(uint32_t t) { return t < 3 ? 1u : (t == 3 ? 2u : 0u); }
-__device__ __forceinline__ uint32_t tcls(uint32_t t) { return t == 0 ? 0u : t < 3 ? 1u : t == 3 ? 2u : 3u; }
-__device__ __forceinline__ uint32_t cls_w(uint32_t c) { return c < 2 ? 1u : (c == 2 ? 2u : 0u); }
-// class of byte i of a stream whose tile-aligned words start at tw (i = byte
-// offset from the stream's first byte)
-__device__ __forceinline__ uint32_t cls_at(const uint32_t* tw, uint64_t i) { return (tw[i >> 4] >> (2 * (i & 15))) & 3u; }
 
 __global__ void __launch_bounds__(256) k_rle_pos(const uint8_t* __restrict__ text, const TileDesc* __restrict__ tiles,
                                                   const uint32_t* __restrict__ carry, uint8_t* __restrict__ tpos,
@@ -319,7 +310,7 @@ __global__ void __launch_bounds__(256) k_rle_pos(const uint8_t* __restrict__ tex
     uint32_t run = (P.len > 0 && S.len > 0 && P.last == S.first) ? P.trail : 0;
     uint32_t w = 0;
     int prev = -1;
-    uint32_t tw = 0;
+    uint32_t tw[4] = {0, 0, 0, 0};
 #pragma unroll
     for (int k = 0; k < 16; ++k) {
         if (k < cnt) {
@@ -327,11 +318,11 @@ __global__ void __launch_bounds__(256) k_rle_pos(const uint8_t* __restrict__ tex
             if (k > 0) run = (ch == prev) ? run + 1 : 0;
             prev = ch;
             const uint32_t t = run % 255u;
-            tw |= tcls(t) << (2 * k);
+            tw[k >> 2] |= t << (8 * (k & 3));
             w += rle_w(t);
         }
     }
-    reinterpret_cast<uint32_t*>(tpos)[(uint64_t)blockIdx.x * (kTB / 16) + threadIdx.x] = tw;
+    *reinterpret_cast<uint4*>(tpos + (uint64_t)blockIdx.x * kTB + off) = make_uint4(tw[0], tw[1], tw[2], tw[3]);
     uint32_t tot;
     (void)block_excl_scan_add<uint32_t>(w, wsh, &tot);
     if (threadIdx.x == 0) tile_w[blockIdx.x] = tot;
@@ -365,8 +356,8 @@ __global__ void __launch_bounds__(64) k_cut(const StreamIn* __restrict__ streams
     const int lane = threadIdx.x;
     const uint64_t beg = streams[s].text_off, end = beg + streams[s].text_len;
     const uint64_t t0 = seg_tile0[s], t1 = seg_tile0[s + 1];
-    // tile-aligned class words: stream byte i = y - beg -> bits 2 (i & 15) of word i >> 4
-    const uint32_t* tpw = reinterpret_cast<const uint32_t*>(tpos_t) + t0 * (kTB / 16);
+    // tile-aligned tpos: text position y of this stream -> tile t0 + (y-beg)/kTB
+    const uint8_t* tpos = tpos_t + t0 * kTB - beg;
     const uint64_t w0 = tile_wpre[t0], wend = tile_wpre[t1] - w0;
     const bool frj = streams[s].final_run_joins != 0;
     uint64_t bs = beg, wbs = 0;
@@ -412,17 +403,21 @@ __global__ void __launch_bounds__(64) k_cut(const StreamIn* __restrict__ streams
                 // each lane: one 64-byte aligned stretch of the tile's tpos, in
                 // registers (four 16-B loads); bytes outside [y0, tend) weigh 0
                 const uint64_t a = beg + ((y0 - beg) & ~63ull) + (uint64_t)lane * 64;
-                uint32_t tw[4];
+                uint32_t tw[16];
                 {
-                    const uint4 v = a < tend ? *reinterpret_cast<const uint4*>(tpw + ((a - beg) >> 4))
-                                             : make_uint4(0, 0, 0, 0);
-                    tw[0] = v.x; tw[1] = v.y; tw[2] = v.z; tw[3] = v.w;
+                    const uint4* p4 = reinterpret_cast<const uint4*>(tpos + a);
+                    const bool in = a < tend;
+#pragma unroll
+                    for (int k = 0; k < 4; ++k) {
+                        const uint4 v = in ? p4[k] : make_uint4(0, 0, 0, 0);
+                        tw[4 * k] = v.x; tw[4 * k + 1] = v.y; tw[4 * k + 2] = v.z; tw[4 * k + 3] = v.w;
+                    }
                 }
                 uint32_t ssum = 0;
 #pragma unroll
                 for (int k = 0; k < 64; ++k) {
                     const uint64_t y = a + (uint64_t)k;
-                    if (y >= y0 && y < tend) ssum += cls_w((tw[k >> 4] >> (2 * (k & 15))) & 3u);
+                    if (y >= y0 && y < tend) ssum += rle_w((tw[k >> 2] >> (8 * (k & 3))) & 0xffu);
                 }
                 const uint32_t incl = wave_incl_scan_add(ssum);
                 const uint64_t ball = __ballot(a < tend && W0 + incl >= target);
@@ -434,7 +429,7 @@ __global__ void __launch_bounds__(64) k_cut(const StreamIn* __restrict__ streams
                         for (int k = 0; k < 64; ++k) {
                             const uint64_t y = a + (uint64_t)k;
                             if (Wx < target) {
-                                if (y >= y0 && y < tend) Wx += cls_w((tw[k >> 4] >> (2 * (k & 15))) & 3u);
+                                if (y >= y0 && y < tend) Wx += rle_w((tw[k >> 2] >> (8 * (k & 3))) & 0xffu);
                                 x = y + 1;
                             }
                         }
@@ -449,14 +444,14 @@ __global__ void __launch_bounds__(64) k_cut(const StreamIn* __restrict__ streams
             uint64_t p = end;
             for (int r = 0; r < 4; ++r) {
                 const uint64_t pos = q + (uint64_t)r * 64 + lane;
-                const uint64_t hit = __ballot(pos < end && cls_at(tpw, pos - beg) == 0);
+                const uint64_t hit = __ballot(pos < end && tpos[pos] == 0);
                 if (hit) { p = q + (uint64_t)r * 64 + (__ffsll((unsigned long long)hit) - 1); break; }
                 if (q + (uint64_t)(r + 1) * 64 >= end) break;
             }
             uint32_t part = 0;
             for (int r = 0; r < 4; ++r) {
                 const uint64_t pos = q + (uint64_t)r * 64 + lane;
-                if (pos < p) part += cls_w(cls_at(tpw, pos - beg));
+                if (pos < p) part += rle_w(tpos[pos]);
             }
             const uint64_t Wp = Wq + wave_reduce_add(part);
             if (p < end && !(frj && p == end - 1)) { block_end = p; wblock_end = Wp; }
@@ -554,13 +549,13 @@ __global__ void __launch_bounds__(256) k_rle_emit(const uint8_t* __restrict__ te
     int off = threadIdx.x * 16;
     int cnt = (int)d.len - off;
     cnt = cnt < 0 ? 0 : (cnt > 16 ? 16 : cnt);
-    // class words of this tile (tiles of a stream are consecutive, tile-aligned)
-    const uint32_t* tpw = reinterpret_cast<const uint32_t*>(tpos) + (uint64_t)blockIdx.x * (kTB / 16);
-    const uint32_t tv = tpw[threadIdx.x];
+    // tpos of this stream, indexed by text position (tiles of a stream are consecutive)
+    const uint8_t* tp = tpos + (uint64_t)blockIdx.x * kTB - d.beg;
+    const uint4 tv = *reinterpret_cast<const uint4*>(tpos + (uint64_t)blockIdx.x * kTB + off);
     const uint4 xv = cnt > 0 ? load16u(text + d.beg + off, text + d.beg + d.len) : make_uint4(0, 0, 0, 0);
     uint32_t w = 0;
 #pragma unroll
-    for (int k = 0; k < 16; ++k) if (k < cnt) w += cls_w((tv >> (2 * k)) & 3u);
+    for (int k = 0; k < 16; ++k) if (k < cnt) w += rle_w(byte16(tv, k));
     uint32_t tot = 0;
     const uint32_t pre = block_excl_scan_add<uint32_t>(w, wsh, &tot);   // contains __syncthreads
     const uint32_t b0 = bsel;
@@ -574,23 +569,23 @@ __global__ void __launch_bounds__(256) k_rle_emit(const uint8_t* __restrict__ te
     const uint64_t wnext = b0 + 1 < bl ? blocks[b0 + 1].w_beg : ~0ull;
     uint32_t o = pre;
     for (int k = 0; k < cnt; ++k) {
-        const uint32_t t = (tv >> (2 * k)) & 3u;      // chunk-position class
+        const uint32_t t = byte16(tv, k);
         const uint8_t c = (uint8_t)byte16(xv, k);
         const int slot = (Wt + o >= wnext) ? 1 : 0;
-        if (t < 2) {
+        if (t < 3) {
             ob[o] = c;
             if (t == 0) ul[slot][c >> 5][threadIdx.x] |= 1u << (c & 31);
-        } else if (t == 2) {                          // chunk position 3: the count byte follows
+        } else if (t == 3) {
             const uint64_t i = d.beg + off + k;
             uint64_t j = i + 1;
-            while (j < send && cls_at(tpw, j - d.beg) != 0) ++j;
+            while (j < send && tp[j] != 0) ++j;
             const uint32_t L = (uint32_t)(j - i) + 3;
             const uint8_t cnt_byte = (uint8_t)(L - 4);
             ob[o] = c;
             ob[o + 1] = cnt_byte;
             ul[slot][cnt_byte >> 5][threadIdx.x] |= 1u << (cnt_byte & 31);
         }
-        o += cls_w(t);
+        o += rle_w(t);
     }
     __syncthreads();
     const uint32_t split = wnext > Wt ? (wnext - Wt < tot ? (uint32_t)(wnext - Wt) : tot) : 0u;

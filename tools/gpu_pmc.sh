@@ -2,7 +2,7 @@
 # GPU box: hardware-counter passes over a reduced bench run (one rocprofv3
 # --pmc pass per counter set, each under its own time limit; --kernel-trace
 # only, never combined with other trace domains).  Output: gpurun_out/pmc/<name>/
-#   PASSES="sq1 sq2 fetch write" (default all), LINES=<bench --lines> (default 20M)
+#   PASSES="sq1 sq2 fetch write" (default all), LINES=<bench --lines> (default 20M), KIND=<bench --kind>
 set -o pipefail
 mkdir -p gpurun_out/pmc
 ROOT=${GRAFT_REPO_ROOT:-$(pwd)}
@@ -12,7 +12,7 @@ PASSES=${PASSES:-sq1 sq2 fetch write}
 run() {   # name, counters...
   local name=$1; shift
   timeout -s KILL ${TP:-120} rocprofv3 --kernel-trace --pmc "$@" -d $ROOT/gpurun_out/pmc/$name -o run \
-      --output-format csv -- python3 $ROOT/bench.py --steps 1 --warmup 0 --lines $LINES --no-cpu-baseline --no-verify --no-e2e \
+      --output-format csv -- python3 $ROOT/bench.py --steps 1 --warmup 0 --kind ${KIND:-0} --lines $LINES --no-cpu-baseline --no-verify --no-e2e \
       > $ROOT/gpurun_out/pmc/$name.log 2>&1
 }
 rc=0
