@@ -72,6 +72,14 @@ public:
     // last bsW call in its bit buffer when a block ends (bz:compress.c:37-52),
     // which decides how many bytes a BZ_FLUSH makes readable.  0: no blocks.
     uint32_t last_write_bits(uint32_t g, const StreamOut& so, hipStream_t st);
+    // plan() and emit() record their stage timings as event pairs without
+    // waiting on them; once the stream has synchronised, this adds them to
+    // *stats (null: drops them).  plan() drops any left from an earlier call.
+    void resolve_timers(Stats* stats);
+    struct PendTimer {
+        hipEvent_t a, b;
+        int stage;                 // 0 rle, 1 bwt, 2 mtf, 3 tables, 4 emit
+    };
 
 private:
     DevBuf b_streams, b_tiles, b_tile_sum, b_tile_carry, b_tile_w, b_tile_wpre, b_tpos, b_seg_tile0, b_seg_nblk,
@@ -92,6 +100,7 @@ private:
     std::vector<uint32_t> src_of_host_;     // the same on the host (empty: identity)
     std::vector<StreamIn> streams_;
     std::vector<BlockDesc> host_blocks_;
+    std::vector<PendTimer> pend_;
 };
 
 }  // namespace bz

@@ -29,7 +29,8 @@ void launch_bwt(BlockDesc* blocks, uint32_t b0, uint32_t nb, const uint8_t* blkb
                 const BwtScratch& scr, unsigned long long* stats, hipStream_t st);
 // v3 (default): batch-wide segmented sort + doubling on ties (bz2_bwt3.hip).
 // hctr: pinned host memory of >= 16 u32; stats[0..2] += rounds, periodic, tied rotations.
-void launch_bwt3(BlockDesc* blocks, uint32_t b0, uint32_t nb, const uint8_t* blkbytes, uint64_t stride,
+// Returns false when no block needed prefix doubling (then none is periodic).
+bool launch_bwt3(BlockDesc* blocks, uint32_t b0, uint32_t nb, const uint8_t* blkbytes, uint64_t stride,
                  const BwtScratch& scr, DevBuf& meta, uint32_t* hctr, unsigned long long* stats, hipStream_t st,
                  bool wide = false);   // wide: some block has 17..20 symbols (8192-bin mixed-radix top digit)
 // periodic blocks: bzip2's exact fallbackSort tie order (bz:blocksort.c:211-329),

@@ -784,19 +784,27 @@ __global__ void __launch_bounds__(SCT) k3_scatter_lds(Ctx c)
 }
 
 // ---------------------------------------------------------------------------
-// binning of a work list by block into per-XCD segments (blocks x, x+8, ...)
+// binning of a work list by block into per-XCD segments (blocks x, x+8, ...).
+// A batch of few blocks (nb < 64) bins by (block, item mod 8) instead (vs = 3),
+// so its groups spread over all XCDs: one block's PSS fits every L2, and
+// binning by block alone would leave 7 of 8 XCDs idle.
 // ---------------------------------------------------------------------------
 constexpr uint32_t BIN_CH = 32768;    // items per binning workgroup (at least)
 constexpr uint32_t BIN_MAXWG = 512;
 
+__device__ __forceinline__ uint32_t bin_of(uint64_t it, uint32_t i, uint32_t vs)
+{
+    return (it_slot(it) << vs) | (i & ((1u << vs) - 1u));
+}
+
 __global__ void __launch_bounds__(256) k3_bin_hist(const uint64_t* __restrict__ in, uint32_t n, uint32_t nb,
-                                                    uint32_t ch, uint32_t* __restrict__ hist)
+                                                    uint32_t ch, uint32_t* __restrict__ hist, uint32_t vs)
 {
     __shared__ uint32_t h[4096];
     for (uint32_t i = threadIdx.x; i < nb; i += 256) h[i] = 0;
     __syncthreads();
     const uint32_t a = blockIdx.x * ch, e = a + ch < n ? a + ch : n;
-    for (uint32_t i = a + threadIdx.x; i < e; i += 256) atomicAdd(&h[it_slot(in[i])], 1u);
+    for (uint32_t i = a + threadIdx.x; i < e; i += 256) atomicAdd(&h[bin_of(in[i], i, vs)], 1u);
     __syncthreads();
     for (uint32_t i = threadIdx.x; i < nb; i += 256) hist[(uint64_t)blockIdx.x * nb + i] = h[i];
 }
@@ -848,7 +856,7 @@ __global__ void __launch_bounds__(1024) k3_bin_scan(uint32_t* __restrict__ hist,
 
 __global__ void __launch_bounds__(256) k3_bin_scatter(const uint64_t* __restrict__ in, uint32_t n, uint32_t nb,
                                                        uint32_t ch, const uint32_t* __restrict__ hist,
-                                                       uint64_t* __restrict__ out)
+                                                       uint64_t* __restrict__ out, uint32_t vs)
 {
     __shared__ uint32_t cur[4096];
     for (uint32_t i = threadIdx.x; i < nb; i += 256) cur[i] = hist[(uint64_t)blockIdx.x * nb + i];
@@ -856,7 +864,7 @@ __global__ void __launch_bounds__(256) k3_bin_scatter(const uint64_t* __restrict
     const uint32_t a = blockIdx.x * ch, e = a + ch < n ? a + ch : n;
     for (uint32_t i = a + threadIdx.x; i < e; i += 256) {
         const uint64_t it = in[i];
-        out[atomicAdd(&cur[it_slot(it)], 1u)] = it;
+        out[atomicAdd(&cur[bin_of(it, i, vs)], 1u)] = it;
     }
 }
 
@@ -1094,10 +1102,14 @@ __global__ void __launch_bounds__(256) k3_sort_w(Ctx c, const uint64_t* __restri
     const uint32_t lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
     // static assignment: workgroup L works segment L mod 8 (the XCD it runs on);
     // its waves take 64-item chunks of that segment in turn
+    // (chunks shrink when the segment has fewer than 64 items per wave, so a
+    // small batch spreads over all waves instead of queueing on a few)
     const uint32_t xs8 = blockIdx.x & 7u, wseg = (gridDim.x >> 3) * 4u, w_in = (blockIdx.x >> 3) * 4u + wid;
     const uint32_t seg0 = c.qseg[xs8], seg1 = c.qseg[xs8 + 1];
-    for (uint32_t cb = seg0 + w_in * 64u; cb < seg1; cb += wseg * 64u) {
-        const uint32_t cnt = seg1 - cb < 64u ? seg1 - cb : 64u;
+    const uint32_t per_w = (seg1 - seg0 + wseg - 1) / wseg;
+    const uint32_t ch = per_w >= 64u ? 64u : (per_w ? per_w : 1u);
+    for (uint32_t cb = seg0 + w_in * ch; cb < seg1; cb += wseg * ch) {
+        const uint32_t cnt = seg1 - cb < ch ? seg1 - cb : ch;
         const uint64_t myitem = lane < cnt ? items[cb + lane] : 0ull;
         const uint32_t msz = lane < cnt ? it_size(myitem) : 0u;
         for (uint32_t done = 0; done < cnt;) {
@@ -1365,7 +1377,10 @@ k3_sort_lds(Ctx c, const uint64_t* __restrict__ items,
     constexpr uint64_t KMASK = (1ull << KEYB) - 1ull;
     constexpr int DPT = 256 / (64 * NW);           // digits per thread in the offset scan
     static_assert(CAP <= (1 << IDXB), "index does not fit");
-    constexpr int DB = CAP <= 128 ? 7 : (CAP <= 256 ? 8 : (CAP <= 1024 ? 10 : 11));   // MSD digit bits
+#ifndef STARCH_M2_DB
+#define STARCH_M2_DB 11
+#endif
+    constexpr int DB = CAP <= 128 ? 7 : (CAP <= 256 ? 8 : (CAP <= 1024 ? 10 : (CAP == 2048 ? STARCH_M2_DB : 11)));   // MSD digit bits
     constexpr int NBIN = 1 << DB;
     constexpr int T = NW * 64;
     constexpr int BPT = NBIN / T;                  // bins per thread
@@ -1378,9 +1393,12 @@ k3_sort_lds(Ctx c, const uint64_t* __restrict__ items,
     constexpr uint32_t LIMIT = STARCH_LIM_NUM / E; // largest sub-bucket ranked by comparison
     __shared__ uint64_t xk_all[IPW][CAP];
     __shared__ uint32_t vb_all[IPW][CAP];          // rotations by group index
-    __shared__ uint32_t bst_all[IPW][NBIN + 1];   // sub-bucket starts
-    __shared__ uint32_t bcur_all[IPW][NBIN];      // scatter cursors
-    __shared__ uint32_t cnt_all[4][256];
+    // LDS is what caps residency here: sub-bucket starts as u16 (positions <=
+    // CAP), and the scatter cursors share their words with the LSD path's
+    // per-wave digit counters (the LSD path runs only after the MSD attempt)
+    __shared__ uint16_t bst_all[IPW][NBIN + 2];   // sub-bucket starts
+    constexpr int UR = NBIN > 256 * NW ? NBIN : 256 * NW;
+    __shared__ uint32_t ur_all[IPW][UR];          // scatter cursors | LSD digit counters
     __shared__ uint32_t sc_all[IPW][NW + 1];
     constexpr int NB2 = NW == 1 ? 256 : 1024;      // second-digit bins
     constexpr uint32_t LIMIT2 = STARCH_LIM2_NUM / E;   // largest second-level sub-bucket ranked by comparison
@@ -1394,7 +1412,7 @@ k3_sort_lds(Ctx c, const uint64_t* __restrict__ items,
     const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
     const int g = wave / NW, wid = wave % NW, w0 = g * NW;
     uint64_t* xk = xk_all[g];
-    uint32_t* wcnt = cnt_all[wave];
+    uint32_t* wcnt = ur_all[g] + wid * 256;
     uint32_t* sc = sc_all[g];
     const uint64_t lt = lanemask_lt();
     // binned list: dynamic pops from the XCD's queue (a workgroup per group for
@@ -1473,8 +1491,8 @@ k3_sort_lds(Ctx c, const uint64_t* __restrict__ items,
     bool moved = false;
     const uint64_t kdiff = diff & KMASK;
     if (kdiff) {
-        uint32_t* bst = bst_all[g];
-        uint32_t* bcur = bcur_all[g];
+        uint16_t* bst = bst_all[g];
+        uint32_t* bcur = ur_all[g];
         const int tg = wid * 64 + lane;
         const int hb = 63 - __clzll((long long)kdiff);
         const int lo = hb + 1 - DB > 0 ? hb + 1 - DB : 0;
@@ -1705,7 +1723,7 @@ k3_sort_lds(Ctx c, const uint64_t* __restrict__ items,
             for (int q = 0; q < DPT; ++q) {
                 uint32_t a = 0;
 #pragma unroll
-                for (int w = 0; w < NW; ++w) a += cnt_all[w0 + w][t * DPT + q];
+                for (int w = 0; w < NW; ++w) a += ur_all[g][w * 256 + t * DPT + q];
                 loc[q] = a;
                 sum += a;
             }
@@ -1721,8 +1739,8 @@ k3_sort_lds(Ctx c, const uint64_t* __restrict__ items,
                 uint32_t r = run;
 #pragma unroll
                 for (int w = 0; w < NW; ++w) {
-                    const uint32_t xx = cnt_all[w0 + w][t * DPT + q];
-                    cnt_all[w0 + w][t * DPT + q] = r;
+                    const uint32_t xx = ur_all[g][w * 256 + t * DPT + q];
+                    ur_all[g][w * 256 + t * DPT + q] = r;
                     r += xx;
                 }
                 run += loc[q];
@@ -1898,6 +1916,13 @@ k3_sort_grp(Ctx c, const uint64_t* __restrict__ items,
     load_qsizes_binned(c, qs);
     WaveQueue<STARCH_GRP_CHUNK> wq;
     constexpr uint32_t NONE = 0xFFFFFFFFu;
+    // software pipeline, three groups deep: while group n sorts, the keys of
+    // n + 1 are issued (its rotations arrived an iteration ago) and the
+    // rotations of n + 2 are in flight (STARCH_GRP_DEEP=0: two deep, the
+    // rotations of n + 1 issued only one iteration before its keys)
+#ifndef STARCH_GRP_DEEP
+#define STARCH_GRP_DEEP 0   // measured no faster (cfg2 sort 23.2 vs 23.3 ms, profiles/r03_v3/sweep_deep*.json)
+#endif
     uint32_t it = wq.next(c.qhead, qs, c.qseg, xs);
     uint32_t it1 = it != NONE ? wq.next(c.qhead, qs, c.qseg, xs) : NONE;
     uint32_t it2 = it1 != NONE ? wq.next(c.qhead, qs, c.qseg, xs) : NONE;
@@ -1907,7 +1932,15 @@ k3_sort_grp(Ctx c, const uint64_t* __restrict__ items,
     grp_load_vals<NW, E>(c, cur, it != NONE, wid, lane);
     grp_load_keys<NW, E, DBL>(c, cur, wid, lane);
     grp_load_vals<NW, E>(c, nxt, it1 != NONE, wid, lane);
+#if STARCH_GRP_DEEP
+    GrpIn<E> vst;                                  // group n + 2: rotations only
+    vst.item = it2 != NONE ? items[it2] : 0ull;
+    grp_load_vals<NW, E>(c, vst, it2 != NONE, wid, lane);
+    uint32_t it3 = it2 != NONE ? wq.next(c.qhead, qs, c.qseg, xs) : NONE;
+    uint64_t nitem3 = it3 != NONE ? items[it3] : 0ull;
+#else
     uint64_t nitem2 = it2 != NONE ? items[it2] : 0ull;
+#endif
 #ifdef STARCH_SORT_PROF
     uint64_t pacc[8] = {0, 0, 0, 0, 0, 0, 0, 0};
 #endif
@@ -2021,12 +2054,17 @@ k3_sort_grp(Ctx c, const uint64_t* __restrict__ items,
     }
     SPROF(t3);
     SPACC(2, t1, t3);
-    // next group's keys (its rotations were loaded one group ago), the item after it
+    // next group's keys (its rotations were loaded one or two groups ago), a new item
     grp_load_keys<NW, E, DBL>(c, nxt, wid, lane);
     SPROF(t4);
     SPACC(3, t3, t4);
+#if STARCH_GRP_DEEP
+    const uint32_t it4 = it3 != NONE ? wq.next(c.qhead, qs, c.qseg, xs) : NONE;
+    const uint64_t nitem4 = it4 != NONE ? items[it4] : 0ull;
+#else
     const uint32_t it3 = it2 != NONE ? wq.next(c.qhead, qs, c.qseg, xs) : NONE;
     const uint64_t nitem3 = it3 != NONE ? items[it3] : 0ull;
+#endif
     if (!is_hard) {
     gsync<NW>();
 #pragma unroll
@@ -2101,7 +2139,22 @@ k3_sort_grp(Ctx c, const uint64_t* __restrict__ items,
     }
     SPROF(t6);
     SPACC(5, t4, t6);
-    // rotate the pipeline: next group's rotations, the one after it
+    // rotate the pipeline
+#if STARCH_GRP_DEEP
+    cur = nxt;
+    nxt.item = vst.item;
+    nxt.ks = vst.ks;
+#pragma unroll
+    for (int e = 0; e < E; ++e) nxt.v[e] = vst.v[e];
+    nxt.v0 = vst.v0;
+    vst.item = nitem3;
+    nitem3 = nitem4;
+    grp_load_vals<NW, E>(c, vst, it3 != NONE, wid, lane);
+    it = it1;
+    it1 = it2;
+    it2 = it3;
+    it3 = it4;
+#else
     cur = nxt;
     nxt.item = nitem2;
     nitem2 = nitem3;
@@ -2109,6 +2162,7 @@ k3_sort_grp(Ctx c, const uint64_t* __restrict__ items,
     it = it1;
     it1 = it2;
     it2 = it3;
+#endif
     SPROF(t7);
     SPACC(6, t6, t7);
     SPACC(7, t0, t7);
@@ -2284,11 +2338,11 @@ bool bwt_kmat()
     return on;
 }
 
-void launch_bwt3(BlockDesc* blocks, uint32_t b0, uint32_t nb, const uint8_t* blkbytes, uint64_t stride,
+bool launch_bwt3(BlockDesc* blocks, uint32_t b0, uint32_t nb, const uint8_t* blkbytes, uint64_t stride,
                  const BwtScratch& scr, DevBuf& meta, uint32_t* hctr, unsigned long long* stats, hipStream_t st,
                  bool wide)
 {
-    if (nb == 0) return;
+    if (nb == 0) return false;
     if (nb > 4095) throw StarchError(-2, "bwt3: batch too large");
     // the tile histograms live in K after the PSS: [MAXT + 1][bins] words (small
     // blocks, -1 .. -2, have room for the 4096-bin binary digit only)
@@ -2301,8 +2355,9 @@ void launch_bwt3(BlockDesc* blocks, uint32_t b0, uint32_t nb, const uint8_t* blk
                    cap_m2 = N / (M1_MAX + 1) + 64,
                    cap_m3 = N / (M2_MAX + 1) + 64, cap_l = N / ((L_MIN < M3_MAX ? L_MIN : M3_MAX) + 1) + 64;
     const uint64_t nwg_bin = BIN_MAXWG;
+    const uint64_t nb_bins = nb < 64 ? 8ull * nb : nb;     // bins of k3_bin_* (see bin_of)
     constexpr uint32_t QSETS = 64, QSET = 8 * XQ_STRIDE + 32;   // queue heads (a line each) + segments per launch
-    const uint64_t words = 2 * C_N + 14ull * nb + QSETS * QSET + nwg_bin * nb +
+    const uint64_t words = 2 * C_N + 14ull * nb + QSETS * QSET + nwg_bin * nb_bins +
                            2 * (cap_s + cap_s2 + cap_m0 + cap_m1 + cap_m2 + cap_m3 + 2 * cap_l) + 64;
     uint32_t* mw = meta.as<uint32_t>(words);
     Ctx c;
@@ -2321,7 +2376,7 @@ void launch_bwt3(BlockDesc* blocks, uint32_t b0, uint32_t nb, const uint8_t* blk
     c.L.geo = reinterpret_cast<Geo*>(c.L.tied + nb);            // 8 words per slot
     uint32_t* qpool = reinterpret_cast<uint32_t*>(c.L.geo + nb);
     uint32_t* binh = qpool + QSETS * QSET;
-    uintptr_t p = reinterpret_cast<uintptr_t>(binh + nwg_bin * nb);
+    uintptr_t p = reinterpret_cast<uintptr_t>(binh + nwg_bin * nb_bins);
     p = (p + 7) & ~(uintptr_t)7;
     c.L.s = reinterpret_cast<uint64_t*>(p);
     c.L.s2 = c.L.s + cap_s;
@@ -2380,9 +2435,10 @@ void launch_bwt3(BlockDesc* blocks, uint32_t b0, uint32_t nb, const uint8_t* blk
         uint32_t nwg = (n + BIN_CH - 1) / BIN_CH;
         if (nwg > BIN_MAXWG) nwg = BIN_MAXWG;
         const uint32_t ch = (n + nwg - 1) / nwg;
-        hipLaunchKernelGGL(k3_bin_hist, dim3(nwg), dim3(256), 0, st, list, n, nb, ch, binh);
-        hipLaunchKernelGGL(k3_bin_scan, dim3(1), dim3(1024), 0, st, binh, nwg, nb, seg);
-        hipLaunchKernelGGL(k3_bin_scatter, dim3(nwg), dim3(256), 0, st, list, n, nb, ch, binh, out);
+        const uint32_t vs = nb_bins > nb ? 3u : 0u, nbv = nb << vs;
+        hipLaunchKernelGGL(k3_bin_hist, dim3(nwg), dim3(256), 0, st, list, n, nbv, ch, binh, vs);
+        hipLaunchKernelGGL(k3_bin_scan, dim3(1), dim3(1024), 0, st, binh, nwg, nbv, seg);
+        hipLaunchKernelGGL(k3_bin_scatter, dim3(nwg), dim3(256), 0, st, list, n, nbv, ch, binh, out, vs);
         HIP_CHECK(hipGetLastError());
         c.qhead = head;
         c.qseg = seg;
@@ -2615,6 +2671,7 @@ void launch_bwt3(BlockDesc* blocks, uint32_t b0, uint32_t nb, const uint8_t* blk
                         100.0 * (double)h[8 * e + q] / (double)(h[8 * e + 7] ? h[8 * e + 7] : 1));
     }
 #endif
+    return !done;   // prefix doubling ran: some block may be periodic (flags bit 0)
 }
 
 }  // namespace bz

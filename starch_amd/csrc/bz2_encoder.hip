@@ -12,31 +12,46 @@
 
 namespace bz {
 
+// stage timer: an event pair queued on the encoder, read by resolve_timers()
+// after the caller's synchronisation (no host wait per stage)
 struct EvTimer {
-    hipEvent_t a = nullptr, b = nullptr;
+    hipEvent_t a = nullptr;
     hipStream_t st;
-    float* out;
-    EvTimer(hipStream_t s, float* o) : st(s), out(o)
+    std::vector<Encoder::PendTimer>* q;
+    int stage;
+    EvTimer(hipStream_t s, Stats* stats, std::vector<Encoder::PendTimer>* pq, int stg) : st(s), q(pq), stage(stg)
     {
-        if (!out) return;
+        if (!stats) return;
         HIP_CHECK(hipEventCreate(&a));
-        HIP_CHECK(hipEventCreate(&b));
         HIP_CHECK(hipEventRecord(a, st));
     }
     void stop()
     {
-        if (!out || !a) return;
+        if (!a) return;
+        hipEvent_t b = nullptr;
+        HIP_CHECK(hipEventCreate(&b));
         HIP_CHECK(hipEventRecord(b, st));
-        HIP_CHECK(hipEventSynchronize(b));
-        float ms = 0;
-        HIP_CHECK(hipEventElapsedTime(&ms, a, b));
-        *out += ms;
-        (void)hipEventDestroy(a);
-        (void)hipEventDestroy(b);
-        a = b = nullptr;
+        q->push_back(Encoder::PendTimer{a, b, stage});
+        a = nullptr;
     }
     ~EvTimer() { if (a) stop(); }
 };
+
+void Encoder::resolve_timers(Stats* stats)
+{
+    for (auto& t : pend_) {
+        float ms = 0;
+        if (stats) {
+            HIP_CHECK(hipEventSynchronize(t.b));
+            HIP_CHECK(hipEventElapsedTime(&ms, t.a, t.b));
+            float* f[5] = {&stats->rle, &stats->bwt, &stats->mtf, &stats->tables, &stats->emit};
+            *f[t.stage] += ms;
+        }
+        (void)hipEventDestroy(t.a);
+        (void)hipEventDestroy(t.b);
+    }
+    pend_.clear();
+}
 
 static uint64_t round_up(uint64_t x, uint64_t m) { return (x + m - 1) / m * m; }
 
@@ -56,6 +71,7 @@ void Encoder::plan(const uint8_t* d_text, const std::vector<StreamIn>& streams, 
 {
     if (bs100k < 1 || bs100k > 9) throw StarchError(-2, "blockSize100k must be 1..9");
     upload_crc_constants();
+    resolve_timers(nullptr);
     text_ = d_text;
     bs100k_ = bs100k;
     streams_ = streams;
@@ -72,7 +88,7 @@ void Encoder::plan(const uint8_t* d_text, const std::vector<StreamIn>& streams, 
     nblocks_ = 0;
     if (nstreams_ == 0) return;
 
-    EvTimer t_rle(st, stats ? &stats->rle : nullptr);
+    EvTimer t_rle(st, stats, &pend_, 0);
     StreamIn* d_streams = b_streams.as<StreamIn>(nstreams_);
     HIP_CHECK(hipMemcpyAsync(d_streams, streams.data(), nstreams_ * sizeof(StreamIn), hipMemcpyHostToDevice, st));
     std::vector<uint64_t> tile0(nstreams_ + 1, 0);
@@ -287,7 +303,7 @@ void Encoder::plan(const uint8_t* d_text, const std::vector<StreamIn>& streams, 
     for (uint32_t b0 = 0; b0 < nr; b0 += batch) {
         uint32_t cnt = std::min(batch, nr - b0);
         {
-            EvTimer tb(st, stats ? &stats->bwt : nullptr);
+            EvTimer tb(st, stats, &pend_, 1);
             // STARCH_BWT=lsd selects the one-workgroup-per-block prefix-doubling sort of
             // bz2_bwt.hip (kept as an independent implementation for cross-checks)
             static const bool lsd = [] { const char* e = getenv("STARCH_BWT"); return e && !strcmp(e, "lsd"); }();
@@ -301,13 +317,16 @@ void Encoder::plan(const uint8_t* d_text, const std::vector<StreamIn>& streams, 
                 for (int j = 0; j < 8; ++j) nin += (uint32_t)__builtin_popcount(bd.in_use[j]);
                 wide = nin >= 17 && nin <= 20;
             }
+            bool doubled = true;
             if (lsd) launch_bwt(d_bl, b0, cnt, d_bytes, blk_stride_, scr, d_stats, st);
-            else launch_bwt3(d_bl, b0, cnt, d_bytes, blk_stride_, scr, b_bwt3, h_ctr_.get(), d_stats, st, wide);
-            HIP_CHECK(hipMemcpyAsync(hr + b0, d_bl + b0, cnt * sizeof(BlockDesc), hipMemcpyDeviceToHost, st));
-            HIP_CHECK(hipStreamSynchronize(st));
+            else doubled = launch_bwt3(d_bl, b0, cnt, d_bytes, blk_stride_, scr, b_bwt3, h_ctr_.get(), d_stats, st, wide);
             std::vector<uint32_t> which, wn;
-            for (uint32_t k = 0; k < cnt; ++k)
-                if (hr[b0 + k].flags & 1u) { which.push_back(k); wn.push_back(hr[b0 + k].n); }
+            if (doubled) {   // periodic blocks are found by the doubling rounds only
+                HIP_CHECK(hipMemcpyAsync(hr + b0, d_bl + b0, cnt * sizeof(BlockDesc), hipMemcpyDeviceToHost, st));
+                HIP_CHECK(hipStreamSynchronize(st));
+                for (uint32_t k = 0; k < cnt; ++k)
+                    if (hr[b0 + k].flags & 1u) { which.push_back(k); wn.push_back(hr[b0 + k].n); }
+            }
             if (!which.empty()) {
                 HIP_CHECK(hipMemcpyAsync(d_which, which.data(), which.size() * sizeof(uint32_t),
                                          hipMemcpyHostToDevice, st));
@@ -322,11 +341,11 @@ void Encoder::plan(const uint8_t* d_text, const std::vector<StreamIn>& streams, 
                 launch_last_col(d_bl, b0, d_which, (uint32_t)which.size(), d_bytes, blk_stride_, scr, st);
         }
         {
-            EvTimer tm(st, stats ? &stats->mtf : nullptr);
+            EvTimer tm(st, stats, &pend_, 2);
             launch_mtf(d_bl, b0, cnt, d_bytes, blk_stride_, scr, d_mtfv, mtf_stride, d_tabs, st);
         }
         {
-            EvTimer tt(st, stats ? &stats->tables : nullptr);
+            EvTimer tt(st, stats, &pend_, 3);
             launch_tables(d_bl, b0, cnt, d_mtfv, mtf_stride, d_tabs, d_sel, d_gbits, scr, st);
         }
     }
@@ -372,7 +391,7 @@ void Encoder::plan(const uint8_t* d_text, const std::vector<StreamIn>& streams, 
 void Encoder::emit(uint8_t* d_out, uint64_t out_cap, uint64_t out_base, std::vector<StreamOut>& outs,
                    hipStream_t st, Stats* stats)
 {
-    EvTimer te(st, stats ? &stats->emit : nullptr);
+    EvTimer te(st, stats, &pend_, 4);
     uint64_t total = 0;
     for (auto& o : outs) total = std::max(total, o.out_off + o.bytes);
     if (((uintptr_t)d_out & 3u) != 0) throw StarchError(-2, "output buffer must be 4-byte aligned");
@@ -436,6 +455,8 @@ uint64_t Encoder::plan_and_encode(const uint8_t* d_text, const std::vector<Strea
 {
     plan(d_text, streams, bs100k, st, outs, stats);
     emit(d_out, out_cap, out_base, outs, st, stats);
+    HIP_CHECK(hipStreamSynchronize(st));
+    resolve_timers(stats);
     uint64_t total = 0;
     for (auto& o : outs) total = std::max(total, o.out_off + o.bytes);
     return total;

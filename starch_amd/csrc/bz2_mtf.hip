@@ -146,7 +146,8 @@ __device__ __forceinline__ void put_run(Out16& out, uint32_t z)   // bijective b
 // registers: 16 nibbles of a u64 for <= 16 symbols (NibP, BED3 text), 32
 // bytes in four u64 for 17..32 symbols (ByteP, narrowPeak and other BED6+
 // text); both do the move-to-front branch-free with SWAR compares.
-constexpr uint32_t MCS = 512;                 // symbols per chunk (4 lines)
+constexpr uint32_t MCS = 512;                 // symbols per chunk (4 lines); batches of few blocks
+                                              // use shorter chunks (mtf_chunk)
 constexpr int MCT = 256;                      // threads of the chunk kernels
 constexpr int MST = 1024;                     // threads of the scan kernels
 
@@ -279,7 +280,7 @@ struct MtfScr {
     __device__ typename P::List* l0() const { return reinterpret_cast<typename P::List*>(base + (uint64_t)P::SW * C); }
     __device__ RunSum* rs() const { return reinterpret_cast<RunSum*>(base + (uint64_t)(P::SW + P::LW) * C); }
     __device__ uint2* zo() const { return reinterpret_cast<uint2*>(base + (uint64_t)(P::SW + P::LW + 2) * C); }
-    // the MTF indices of the whole block (P::IXB bits each, chunk c at c * MCS symbols)
+    // the MTF indices of the whole block (P::IXB bits each, chunk c at c * cs symbols)
     __device__ uint8_t* ix() const { return reinterpret_cast<uint8_t*>(base + (uint64_t)(P::SW + P::LW + 3) * C); }
 };
 
@@ -337,14 +338,14 @@ __device__ __forceinline__ void visit_chunk_lines(const uint8_t* ll, uint32_t a,
 template <class P>
 __global__ void __launch_bounds__(MCT) k_mtf_local(const BlockDesc* __restrict__ blocks, uint32_t b0,
                                                    const uint8_t* __restrict__ LL, uint64_t ll_stride,
-                                                   uint64_t* __restrict__ K, uint64_t kstride, uint32_t C)
+                                                   uint64_t* __restrict__ K, uint64_t kstride, uint32_t C, uint32_t cs)
 {
     const uint32_t slot = blockIdx.y, b = b0 + slot;
     const uint32_t n = blocks[b].n, nin = blocks[b].n_in_use;
     const uint32_t ch = blockIdx.x * MCT + threadIdx.x;
-    const uint32_t a = ch * MCS;
+    const uint32_t a = ch * cs;
     if (!mtf_mine<P>(nin) || a >= n) return;
-    const uint32_t e = a + MCS < n ? a + MCS : n;
+    const uint32_t e = a + cs < n ? a + cs : n;
     const uint8_t* ll = LL + (uint64_t)slot * ll_stride;
     // local(c): the chunk's symbols by last occurrence, most recent first;
     // backward, line by line, until every symbol of the block has been seen
@@ -366,15 +367,16 @@ __global__ void __launch_bounds__(MCT) k_mtf_local(const BlockDesc* __restrict__
 // start list of every chunk: exclusive scan of the local-list composition
 template <class P>
 __global__ void __launch_bounds__(MST) k_mtf_scan_lists(const BlockDesc* __restrict__ blocks, uint32_t b0,
-                                                        uint64_t* __restrict__ K, uint64_t kstride, uint32_t C)
+                                                        uint64_t* __restrict__ K, uint64_t kstride, uint32_t C,
+                                                        uint32_t cs)
 {
     __shared__ typename P::State sh[MST];
     const int tid = threadIdx.x;
     const uint32_t slot = blockIdx.x, b = b0 + slot;
     const uint32_t n = blocks[b].n, nin = blocks[b].n_in_use;
     if (!mtf_mine<P>(nin)) return;
-    const uint32_t nch = (n + MCS - 1) / MCS;
-    const uint32_t per = (nch + MST - 1) / MST;          // <= 2 for 900 KB blocks
+    const uint32_t nch = (n + cs - 1) / cs;
+    const uint32_t per = (nch + MST - 1) / MST;          // <= 2 for 900 KB blocks at 512-symbol chunks
     const MtfScr<P> ms = mtf_scr<P>(K, kstride, slot, C);
     const uint32_t c0 = tid * per;
     typename P::State agg = P::empty();
@@ -402,14 +404,14 @@ __global__ void __launch_bounds__(MST) k_mtf_scan_lists(const BlockDesc* __restr
 template <class P>
 __global__ void __launch_bounds__(MCT) k_mtf_runs(const BlockDesc* __restrict__ blocks, uint32_t b0,
                                                   const uint8_t* __restrict__ LL, uint64_t ll_stride,
-                                                  uint64_t* __restrict__ K, uint64_t kstride, uint32_t C)
+                                                  uint64_t* __restrict__ K, uint64_t kstride, uint32_t C, uint32_t cs)
 {
     const uint32_t slot = blockIdx.y, b = b0 + slot;
     const uint32_t n = blocks[b].n, nin = blocks[b].n_in_use;
     const uint32_t ch = blockIdx.x * MCT + threadIdx.x;
-    const uint32_t a = ch * MCS;
+    const uint32_t a = ch * cs;
     if (!mtf_mine<P>(nin) || a >= n) return;
-    const uint32_t e = a + MCS < n ? a + MCS : n;
+    const uint32_t e = a + cs < n ? a + cs : n;
     const MtfScr<P> ms = mtf_scr<P>(K, kstride, slot, C);
     typename P::List L = ms.l0()[ch];
     uint32_t z = 0, nz = 0, lz = 0, inner = 0;
@@ -463,14 +465,14 @@ __global__ void __launch_bounds__(MCT) k_mtf_runs(const BlockDesc* __restrict__ 
 template <class P>
 __global__ void __launch_bounds__(MST) k_mtf_scan_runs(BlockDesc* __restrict__ blocks, uint32_t b0,
                                                        uint64_t* __restrict__ K, uint64_t kstride, uint32_t C,
-                                                       uint16_t* __restrict__ mtfv_all, uint64_t mtf_stride)
+                                                       uint32_t cs, uint16_t* __restrict__ mtfv_all, uint64_t mtf_stride)
 {
     __shared__ RunSum sh[MST];
     const int tid = threadIdx.x;
     const uint32_t slot = blockIdx.x, b = b0 + slot;
     const uint32_t n = blocks[b].n, nin = blocks[b].n_in_use;
     if (!mtf_mine<P>(nin)) return;
-    const uint32_t nch = (n + MCS - 1) / MCS;
+    const uint32_t nch = (n + cs - 1) / cs;
     const uint32_t per = (nch + MST - 1) / MST;
     const MtfScr<P> ms = mtf_scr<P>(K, kstride, slot, C);
     const uint32_t c0 = tid * per;
@@ -517,14 +519,14 @@ template <class P>
 __global__ void __launch_bounds__(MCT) k_mtf_emit(const BlockDesc* __restrict__ blocks, uint32_t b0,
                                                   const uint8_t* __restrict__ LL, uint64_t ll_stride,
                                                   const uint64_t* __restrict__ K, uint64_t kstride, uint32_t C,
-                                                  uint16_t* __restrict__ mtfv_all, uint64_t mtf_stride)
+                                                  uint32_t cs, uint16_t* __restrict__ mtfv_all, uint64_t mtf_stride)
 {
     const uint32_t slot = blockIdx.y, b = b0 + slot;
     const uint32_t n = blocks[b].n, nin = blocks[b].n_in_use;
     const uint32_t ch = blockIdx.x * MCT + threadIdx.x;
-    const uint32_t a = ch * MCS;
+    const uint32_t a = ch * cs;
     if (!mtf_mine<P>(nin) || a >= n) return;
-    const uint32_t e = a + MCS < n ? a + MCS : n;
+    const uint32_t e = a + cs < n ? a + cs : n;
     const MtfScr<P> ms = mtf_scr<P>(const_cast<uint64_t*>(K), kstride, slot, C);
     const uint2 zo = ms.zo()[ch];
     Out16 out;
@@ -782,18 +784,22 @@ void launch_mtf(BlockDesc* blocks, uint32_t b0, uint32_t nb, const uint8_t* blkb
     (void)blkbytes;
     (void)stride;
     // alphabets <= 32: chunk passes over the key scratch (free after the sort)
-    const uint32_t C = (uint32_t)((scr.stride + MCS - 1) / MCS);
+    // chunk length: 512 symbols when the batch fills the GPU; a few blocks
+    // take shorter chunks (more lanes, shorter serial MTF chains per lane)
+    const uint32_t cs = nb >= 32 ? MCS : nb >= 8 ? 128u : 64u;
+    const uint32_t C = (uint32_t)((scr.stride + cs - 1) / cs);
     const uint64_t kstride = scr.stride;                     // u64 words per slot
     const dim3 gch((C + MCT - 1) / MCT, nb);
     auto run = [&](auto pol) {
         using P = decltype(pol);
-        hipLaunchKernelGGL(k_mtf_local<P>, gch, dim3(MCT), 0, st, blocks, b0, scr.LL, scr.stride, scr.K, kstride, C);
-        hipLaunchKernelGGL(k_mtf_scan_lists<P>, dim3(nb), dim3(MST), 0, st, blocks, b0, scr.K, kstride, C);
-        hipLaunchKernelGGL(k_mtf_runs<P>, gch, dim3(MCT), 0, st, blocks, b0, scr.LL, scr.stride, scr.K, kstride, C);
-        hipLaunchKernelGGL(k_mtf_scan_runs<P>, dim3(nb), dim3(MST), 0, st, blocks, b0, scr.K, kstride, C, mtfv,
+        hipLaunchKernelGGL(k_mtf_local<P>, gch, dim3(MCT), 0, st, blocks, b0, scr.LL, scr.stride, scr.K, kstride, C, cs);
+        hipLaunchKernelGGL(k_mtf_scan_lists<P>, dim3(nb), dim3(MST), 0, st, blocks, b0, scr.K, kstride, C, cs);
+        hipLaunchKernelGGL(k_mtf_runs<P>, gch, dim3(MCT), 0, st, blocks, b0, scr.LL, scr.stride, scr.K, kstride, C,
+                           cs);
+        hipLaunchKernelGGL(k_mtf_scan_runs<P>, dim3(nb), dim3(MST), 0, st, blocks, b0, scr.K, kstride, C, cs, mtfv,
                            mtf_stride);
         hipLaunchKernelGGL(k_mtf_emit<P>, gch, dim3(MCT), 0, st, blocks, b0, scr.LL, scr.stride, scr.K, kstride, C,
-                           mtfv, mtf_stride);
+                           cs, mtfv, mtf_stride);
     };
     run(NibP{});
     run(ByteP{});

@@ -19,17 +19,23 @@
 // Every lane handles one 16-byte strip, loaded with one or two aligned 16-B
 // loads (any text alignment); tpos is stored tile-aligned (tile t at t*4096).
 #include "bz2_int.hpp"
+#include <atomic>
 
 namespace bz {
 
 __constant__ uint32_t c_pow8[64];   // x^(8*2^k) mod P, P = 0x04c11db7 (MSB-first)
 __constant__ uint32_t c_crc_tab[256];
 __constant__ uint32_t c_crc_tab4[4][256];   // [k][i]: register after byte i then k zero bytes
+__constant__ uint32_t c_lane[64];           // x^(8*128*(63-i)): lane i's line shifted to the end of its 8 KB span
 
 void upload_crc_constants()
 {
-    static bool done = false;
-    if (done) return;
+    // __constant__ data is per device: upload once for every device used
+    static std::atomic<uint64_t> done{0};
+    int dev = 0;
+    HIP_CHECK(hipGetDevice(&dev));
+    const uint64_t bit = 1ull << (dev & 63);
+    if (done.load() & bit) return;
     uint32_t tab[256];
     for (uint32_t b = 0; b < 256; ++b) {
         uint32_t c = b << 24;
@@ -48,7 +54,11 @@ void upload_crc_constants()
         for (int k = 1; k < 4; ++k) { r = (r << 8) ^ tab[r >> 24]; tab4[k][i] = r; }
     }
     HIP_CHECK(hipMemcpyToSymbol(HIP_SYMBOL(c_crc_tab4), tab4, sizeof(tab4)));
-    done = true;
+    uint32_t cl[64];
+    cl[63] = 1u;                                  // x^0
+    for (int i = 62; i >= 0; --i) cl[i] = host_mulmod(cl[i + 1], pw[7]);   // pw[7] = x^(8*128)
+    HIP_CHECK(hipMemcpyToSymbol(HIP_SYMBOL(c_lane), cl, sizeof(cl)));
+    done.fetch_or(bit);
 }
 
 __device__ __forceinline__ uint32_t mulmod(uint32_t a, uint32_t b)
@@ -609,9 +619,11 @@ __global__ void __launch_bounds__(256) k_rle_emit(const uint8_t* __restrict__ te
 // R(A||B) = R(A)*x^(8|B|) + R(B) (mod P); crc = ~(0xffffffff*x^(8n) + R(all)).
 // k_crc_chunks: each wave takes one chunk of a block (up to CRC_MAXC chunks,
 // whole 8 KB spans); every lane runs slice-by-4 over its own 128-byte line of
-// a span (eight 16-B loads in flight), and the 64 line registers are folded by
-// a 6-level shuffle tree whose multipliers are the x^(8*128*2^l) constants.
-// k_crc_final: one wave per block combines the chunk registers.
+// a span (eight 16-B loads in flight); then R(span) = XOR_i R(line_i) *
+// x^(8 * bytes after line i): each lane shifts its own register (a constant
+// per lane for a full span) and one XOR reduction over the wave combines them
+// -- one multiplication deep instead of a six-level tree of them.
+// k_crc_final: one wave per block combines the chunk registers the same way.
 constexpr uint32_t CRC_LANE = 128;                // bytes per lane per span
 constexpr uint32_t CRC_SPAN = 64 * CRC_LANE;      // 8 KB per wave per span
 constexpr uint32_t CRC_MAXC = 128;
@@ -662,19 +674,13 @@ __global__ void __launch_bounds__(64 * CRC_WPB) k_crc_chunks(const uint8_t* __re
                 for (uint32_t q = 0; q < m; ++q) r = (r << 8) ^ t4[0][(r >> 24) ^ byte16(v[k], (int)q)];
             }
         }
-        uint32_t len = n;
+        const uint32_t slen = ce - c0 < CRC_SPAN ? (uint32_t)(ce - c0) : CRC_SPAN;
+        const uint32_t lend = (uint32_t)(lane + 1) * CRC_LANE;
+        uint32_t x = 0;
+        if (n) x = mulmod(r, slen == CRC_SPAN ? c_lane[lane] : xpow8(slen - (lend < slen ? lend : slen)));
 #pragma unroll
-        for (int l = 0; l < 6; ++l) {                // lane i absorbs lane i + 2^l
-            const int step = 1 << l;
-            const uint32_t ro = __shfl_down(r, step, 64);
-            const uint32_t lo = __shfl_down(len, step, 64);
-            if ((lane & (2 * step - 1)) == 0 && lo) {
-                const uint32_t mul = (lo == CRC_LANE * (uint32_t)step) ? c_pow8[7 + l] : xpow8(lo);
-                r = mulmod(r, mul) ^ ro;
-                len += lo;
-            }
-        }
-        if (lane == 0) acc = mulmod(acc, len == CRC_SPAN ? c_pow8[13] : xpow8(len)) ^ r;
+        for (int l = 1; l < 64; l <<= 1) x ^= __shfl_xor(x, l, 64);
+        if (lane == 0) acc = mulmod(acc, slen == CRC_SPAN ? c_pow8[13] : xpow8(slen)) ^ x;
     }
     if (lane == 0) creg[(uint64_t)b * CRC_MAXC + c] = acc;
 }
@@ -688,27 +694,23 @@ __global__ void __launch_bounds__(64) k_crc_final(const uint32_t* __restrict__ c
     const uint64_t beg = blocks[b].in_beg, end = blocks[b].in_end;
     const uint64_t csz = crc_chunk_bytes(end - beg);
     const uint32_t nch = (uint32_t)((end - beg + csz - 1) / csz);
-    // lane l folds chunks 2l, 2l+1 (CRC_MAXC = 128 = 2 * 64); then a wave tree
+    // lane l holds chunks 2l, 2l+1 (CRC_MAXC = 128 = 2 * 64), shifted by the
+    // bytes after them; one XOR reduction combines the lanes
     uint32_t r = 0;
-    uint64_t len = 0;
+    uint64_t pend = beg;                              // end of this lane's chunks
     for (int q = 0; q < 2; ++q) {
         const uint32_t k = 2u * lane + q;
         if (k < nch) {
             const uint64_t cb = beg + (uint64_t)k * csz;
             const uint64_t cl = (end - cb) < csz ? end - cb : csz;
-            r = mulmod(r, xpow8(cl)) ^ creg[(uint64_t)b * CRC_MAXC + k];
-            len += cl;
+            r = (q ? mulmod(r, xpow8(cl)) : 0u) ^ creg[(uint64_t)b * CRC_MAXC + k];
+            pend = cb + cl;
         }
     }
-    for (int step = 1; step < 64; step <<= 1) {
-        const uint32_t ro = __shfl_down(r, step, 64);
-        const uint64_t lo = __shfl_down(len, step, 64);
-        if ((lane & (2 * step - 1)) == 0 && lane + step < 64 && lo) {
-            r = mulmod(r, xpow8(lo)) ^ ro;
-            len += lo;
-        }
-    }
-    if (lane == 0) blocks[b].crc = ~(mulmod(0xffffffffu, xpow8(end - beg)) ^ r);
+    uint32_t x = 0;
+    if (2u * lane < nch) x = mulmod(r, xpow8(end - pend));
+    for (int l = 1; l < 64; l <<= 1) x ^= __shfl_xor(x, l, 64);
+    if (lane == 0) blocks[b].crc = ~(mulmod(0xffffffffu, xpow8(end - beg)) ^ x);
 }
 
 // ---------------------------------------------------------------------------

@@ -21,11 +21,6 @@ struct HuffSmem {
     int32_t weight[6][516];
     int32_t parent[6][516];
 };
-struct HuffSmem32 {                     // alphabets <= 32 (k_tables32)
-    int32_t heap[6][40];
-    int32_t weight[6][72];
-    int32_t parent[6][72];
-};
 
 __device__ void hb_make_lengths(uint8_t* len, const uint32_t* freq, int32_t alpha, int32_t max_len, int32_t* heap,
                                 int32_t* weight, int32_t* parent)
@@ -78,6 +73,88 @@ __device__ void hb_make_lengths(uint8_t* len, const uint32_t* freq, int32_t alph
         }
         if (!too_long) break;
         for (int32_t i = 1; i <= alpha; ++i) weight[i] = (1 + ((weight[i] >> 8) / 2)) << 8;
+    }
+}
+
+// The same algorithm for alphabets <= 32 run by one whole wave, with the heap,
+// the weights and the parents in registers: node k's weight and parent in
+// lane k (2 * alpha - 1 <= 63 nodes), heap position z in lane z.  The control
+// flow is wave-uniform and every heap step reads and writes single lanes
+// (v_readlane with scalar indices, one v_cndmask per write), so the serial heap runs on
+// scalar-latency steps instead of one lane's chain of LDS round trips; the
+// depth walk is lane-parallel.  Same heap, same ties, same lengths.
+__device__ __forceinline__ int32_t rl(int32_t v, int32_t i) { return __builtin_amdgcn_readlane(v, i); }
+__device__ __forceinline__ int32_t wl(int32_t v, int32_t x, int32_t i) { return (int32_t)(threadIdx.x & 63) == i ? x : v; }
+
+__device__ void hb_make_lengths_wave(uint8_t* len, const uint32_t* freq, int32_t alpha, int32_t max_len)
+{
+    const int32_t lane = (int32_t)(threadIdx.x & 63);
+    const bool sym = lane >= 1 && lane <= alpha;
+    int32_t W = 0;                                             // weight of node `lane`
+    if (sym) W = (int32_t)((freq[lane - 1] == 0 ? 1u : freq[lane - 1]) << 8);
+    for (;;) {
+        int32_t P = lane == 0 ? -2 : -1;                       // parent of node `lane`
+        int32_t H = 0;                                         // heap entry at position `lane`
+        W = lane == 0 ? 0 : W;
+        int32_t nodes = alpha, nheap = 0;
+        auto upheap = [&](int32_t t) {
+            const int32_t wt = rl(W, t);
+            int32_t zz = nheap;
+            for (;;) {
+                const int32_t hp = rl(H, zz >> 1);
+                if (!(wt < rl(W, hp))) break;
+                H = wl(H, hp, zz);
+                zz >>= 1;
+            }
+            H = wl(H, t, zz);
+        };
+        for (int32_t i = 1; i <= alpha; ++i) {
+            ++nheap;
+            upheap(i);
+        }
+        while (nheap > 1) {
+            int32_t pick[2];
+            for (int q = 0; q < 2; ++q) {
+                pick[q] = rl(H, 1);
+                const int32_t t = rl(H, nheap);
+                --nheap;
+                const int32_t wt = rl(W, t);
+                int32_t zz = 1;
+                for (;;) {
+                    int32_t yy = zz << 1;
+                    if (yy > nheap) break;
+                    int32_t hy = rl(H, yy), wy = rl(W, hy);
+                    if (yy < nheap) {
+                        const int32_t h1 = rl(H, yy + 1), w1 = rl(W, h1);
+                        if (w1 < wy) { ++yy; hy = h1; wy = w1; }
+                    }
+                    if (wt < wy) break;
+                    H = wl(H, hy, zz);
+                    zz = yy;
+                }
+                H = wl(H, t, zz);
+            }
+            ++nodes;
+            P = wl(P, nodes, pick[0]);
+            P = wl(P, nodes, pick[1]);
+            const int32_t wa = rl(W, pick[0]), wb = rl(W, pick[1]);
+            const int32_t da = wa & 0xff, db = wb & 0xff;
+            W = wl(W, (int32_t)(((uint32_t)wa & 0xffffff00u) + ((uint32_t)wb & 0xffffff00u)) | (1 + (da > db ? da : db)),
+                   nodes);
+            P = wl(P, -1, nodes);
+            ++nheap;
+            upheap(nodes);
+        }
+        // depth of every symbol: all lanes walk their parent chains at once
+        int32_t d = 0, k = lane;
+        bool walking = sym;
+        while (__ballot(walking)) {
+            const int32_t pk = __shfl(P, k, 64);
+            if (walking && pk >= 0) { k = pk; ++d; } else walking = false;
+        }
+        if (sym) len[lane - 1] = (uint8_t)d;
+        if (!__ballot(sym && d > max_len)) break;
+        if (sym) W = (1 + ((W >> 8) / 2)) << 8;
     }
 }
 
@@ -285,6 +362,13 @@ __global__ void __launch_bounds__(TT) k_tables(BlockDesc* __restrict__ blocks, u
 #endif
 constexpr int T32 = 256;
 constexpr int NW32 = T32 / 64;
+#ifdef STARCH_TABLES_PROF
+__device__ unsigned long long g_tprof[8];
+#define TPROF(k) do { __syncthreads(); if (threadIdx.x == 0) { const uint64_t t_ = wall_clock64(); \
+    atomicAdd(&g_tprof[k], (unsigned long long)(t_ - tp_last)); tp_last = t_; } } while (0)
+#else
+#define TPROF(k) do {} while (0)
+#endif
 
 __device__ __forceinline__ uint32_t byte_of(const uint32_t (&h)[8], int v)
 {
@@ -304,7 +388,7 @@ __global__ void __launch_bounds__(T32) __attribute__((amdgpu_waves_per_eu(STARCH
     // packed lengths, profiles/r01_v24_tables_wpe.json)
     union Scratch {
         uint32_t hl[8][T32];
-        struct { HuffSmem32 hs; uint32_t rf[NW32][6][32]; uint32_t rfreq[6][32]; } it;
+        struct { uint32_t rf[NW32][6][32]; uint32_t rfreq[6][32]; } it;
         NibState nst[T32];
     };
     __shared__ Scratch u;
@@ -314,7 +398,6 @@ __global__ void __launch_bounds__(T32) __attribute__((amdgpu_waves_per_eu(STARCH
     __shared__ uint8_t sel_l[kMaxSelectors];
     __shared__ unsigned long long hdr_bits, sbits_sh;
     auto& hl = u.hl;
-    auto& hs = u.it.hs;
     auto& rf = u.it.rf;
     auto& rfreq = u.it.rfreq;
     auto& nst = u.nst;
@@ -332,6 +415,9 @@ __global__ void __launch_bounds__(T32) __attribute__((amdgpu_waves_per_eu(STARCH
     const int ng = n_mtf < 200 ? 2 : n_mtf < 600 ? 3 : n_mtf < 1200 ? 4 : n_mtf < 2400 ? 5 : 6;
     const uint32_t nsel = (n_mtf + 49) / 50;
 
+#ifdef STARCH_TABLES_PROF
+    uint64_t tp_last = wall_clock64();
+#endif
     for (int i = tid; i < 258; i += T32) freq[i] = 0;
     for (int i = tid; i < 6 * 32; i += T32) (&len[0][0])[i] = 15;   // BZ_GREATER_ICOST
     __syncthreads();
@@ -375,13 +461,14 @@ __global__ void __launch_bounds__(T32) __attribute__((amdgpu_waves_per_eu(STARCH
         }
     }
     __syncthreads();
-    if (tid == 0) {   // initial equal-frequency bands (bz:compress.c:280-317)
+    if (wid == 0) {   // initial equal-frequency bands (bz:compress.c:280-317), wave-uniform
+        const int32_t fv = lane < alpha ? (int32_t)freq[lane] : 0;
         int32_t parts = ng, rem = (int32_t)n_mtf, gs = 0;
         while (parts > 0) {
             int32_t target = rem / parts, ge = gs - 1, acc = 0;
-            while (acc < target && ge < alpha - 1) { ++ge; acc += (int32_t)freq[ge]; }
-            if (ge > gs && parts != ng && parts != 1 && ((ng - parts) % 2 == 1)) { acc -= (int32_t)freq[ge]; --ge; }
-            for (int32_t v = 0; v < alpha; ++v) len[parts - 1][v] = (v >= gs && v <= ge) ? 0 : 15;
+            while (acc < target && ge < alpha - 1) { ++ge; acc += rl(fv, ge); }
+            if (ge > gs && parts != ng && parts != 1 && ((ng - parts) % 2 == 1)) { acc -= rl(fv, ge); --ge; }
+            if (lane < alpha) len[parts - 1][lane] = (lane >= gs && lane <= ge) ? 0 : 15;
             --parts;
             gs = ge + 1;
             rem -= acc;
@@ -389,6 +476,7 @@ __global__ void __launch_bounds__(T32) __attribute__((amdgpu_waves_per_eu(STARCH
     }
     for (int i = tid; i < 258; i += T32) tabs[b].freq[i] = freq[i];
     __syncthreads();
+    TPROF(0);
     for (int iter = 0; iter < 4; ++iter) {                         // BZ_N_ITERS
         if (tid < 48) {
             const int t = tid >> 3, q = tid & 7;
@@ -451,6 +539,7 @@ __global__ void __launch_bounds__(T32) __attribute__((amdgpu_waves_per_eu(STARCH
             }
         }
         __syncthreads();
+        TPROF(1);
         if (tid < 6 * 32) {
             const int t = tid >> 5, v = tid & 31;
             uint32_t a = 0;
@@ -458,8 +547,9 @@ __global__ void __launch_bounds__(T32) __attribute__((amdgpu_waves_per_eu(STARCH
             if (v < alpha) rfreq[t][v] = a;
         }
         __syncthreads();
-        if (tid < ng) hb_make_lengths(len[tid], rfreq[tid], alpha, 17, hs.heap[tid], hs.weight[tid], hs.parent[tid]);
+        for (int t = wid; t < ng; t += NW32) hb_make_lengths_wave(len[t], rfreq[t], alpha, 17);
         __syncthreads();
+        TPROF(2);
     }
     for (uint32_t g = tid; g < nsel; g += T32) sel[g] = sel_l[g];
     // selector MTF (bz:compress.c:461-478): contiguous ranges per thread, start
@@ -498,7 +588,8 @@ __global__ void __launch_bounds__(T32) __attribute__((amdgpu_waves_per_eu(STARCH
         if (lane == 0) atomicAdd(&sbits_sh, (unsigned long long)sb);
         __syncthreads();
     }
-    if (tid == 0) {
+    TPROF(3);
+    if (wid == 0) {   // header bits: the tables' delta-coded lengths summed across lanes
         const uint64_t sbits = sbits_sh;
         uint32_t used16 = 0;
         for (int i = 0; i < 16; ++i) {
@@ -506,35 +597,39 @@ __global__ void __launch_bounds__(T32) __attribute__((amdgpu_waves_per_eu(STARCH
             uint32_t half = (i & 1) ? (w >> 16) : (w & 0xffffu);
             if (half) ++used16;
         }
-        uint64_t tbits = 0;
+        uint32_t tb = 0;
         for (int t = 0; t < ng; ++t) {
-            int32_t cur = len[t][0];
-            tbits += 5;
-            for (int32_t i = 0; i < alpha; ++i) {
-                int32_t d = (int32_t)len[t][i] - cur;
-                tbits += 1 + 2 * (uint64_t)(d < 0 ? -d : d);
-                cur = len[t][i];
-            }
+            const int32_t l = lane < alpha ? (int32_t)len[t][lane] : 0;
+            const int32_t pv = lane == 0 ? l : (lane < alpha ? (int32_t)len[t][lane - 1] : 0);
+            const int32_t d = l - pv;
+            tb += lane < alpha ? 1u + 2u * (uint32_t)(d < 0 ? -d : d) : 0u;
         }
-        hdr_bits = 48 + 32 + 1 + 24 + 16 + 16ull * used16 + 3 + 15 + sbits + tbits;
-        blocks[b].hdr_bits = (uint32_t)hdr_bits;
+        const uint64_t tbits = 5ull * (uint64_t)ng + wave_reduce_add(tb);
+        if (lane == 0) {
+            hdr_bits = 48 + 32 + 1 + 24 + 16 + 16ull * used16 + 3 + 15 + sbits + tbits;
+            blocks[b].hdr_bits = (uint32_t)hdr_bits;
+        }
     }
-    // canonical codes (bz:huffman.c:152-166)
-    if (tid < ng) {
-        int32_t mn = 32, mx = 0;
-        for (int32_t i = 0; i < alpha; ++i) {
-            int32_t l = len[tid][i];
-            if (l > mx) mx = l;
-            if (l < mn) mn = l;
+    // canonical codes (bz:huffman.c:152-166): for each length in increasing
+    // order the symbols of that length take consecutive codes in symbol order
+    // -- a ballot per length, the rank inside it by popcount
+    for (int t = wid; t < ng; t += NW32) {
+        const bool in = lane < alpha;
+        const int32_t l = in ? (int32_t)len[t][lane] : 0;
+        const uint64_t lt = (1ull << lane) - 1ull;
+        uint32_t base = 0, code = 0;
+        for (int32_t L = 1; L <= 17; ++L) {
+            const uint64_t m = __ballot(in && l == L);
+            if (in && l == L) code = base + (uint32_t)__popcll(m & lt);
+            base = (base + (uint32_t)__popcll(m)) << 1;
         }
-        int32_t v = 0;
-        for (int32_t L = mn; L <= mx; ++L) {
-            for (int32_t i = 0; i < alpha; ++i) if (len[tid][i] == L) tabs[b].code[tid][i] = (uint32_t)v++;
-            v <<= 1;
+        if (in) {
+            tabs[b].code[t][lane] = code;
+            tabs[b].len[t][lane] = (uint8_t)l;
         }
-        for (int32_t i = 0; i < alpha; ++i) tabs[b].len[tid][i] = len[tid][i];
     }
     __syncthreads();
+    TPROF(4);
     // data bits per group with the final tables
     uint64_t local = 0;
     for (uint32_t g = tid; g < nsel; g += T32) {
@@ -550,6 +645,7 @@ __global__ void __launch_bounds__(T32) __attribute__((amdgpu_waves_per_eu(STARCH
     local = wave_reduce_add(local);
     if (lane == 0) atomicAdd(&hdr_bits, (unsigned long long)local);
     __syncthreads();
+    TPROF(5);
     if (tid == 0) {
         blocks[b].bits = hdr_bits;
         blocks[b].n_groups = (uint32_t)ng;
@@ -568,6 +664,17 @@ void launch_tables(BlockDesc* blocks, uint32_t b0, uint32_t nb, const uint16_t* 
     hipLaunchKernelGGL(k_tables, dim3(nb), dim3(TT), 0, st, blocks, b0, mtfv, mtf_stride, tabs, sel, gbits, hist,
                        hist_stride);
     HIP_CHECK(hipGetLastError());
+#ifdef STARCH_TABLES_PROF
+    {
+        unsigned long long h[8];
+        HIP_CHECK(hipStreamSynchronize(st));
+        HIP_CHECK(hipMemcpyFromSymbol(h, HIP_SYMBOL(g_tprof), sizeof(h)));
+        static const unsigned long long zero[8] = {};
+        HIP_CHECK(hipMemcpyToSymbol(HIP_SYMBOL(g_tprof), zero, sizeof(zero)));
+        const char* nm[6] = {"hist+bands", "iter:cost+rfreq", "iter:heap", "selmtf", "hdr+codes", "gbits"};
+        for (int q = 0; q < 6; ++q) fprintf(stderr, "[tprof] nb %u %-16s %.1f us/block\n", nb, nm[q], h[q] / 100.0 / nb);
+    }
+#endif
 }
 
 }  // namespace bz

@@ -28,6 +28,7 @@
 // A block is one deflate block (BFINAL on the segment's last), so blocks are
 // bit-contiguous and need no alignment; matches never cross a sub-chunk.
 #include "gz.hpp"
+#include <atomic>
 
 #include <algorithm>
 
@@ -568,8 +569,12 @@ __global__ void k_gz_frame(const MemberOut* __restrict__ mo, const uint32_t* __r
 
 void upload_tables()
 {
-    static bool done = false;
-    if (done) return;
+    // __constant__ data is per device: upload once for every device used
+    static std::atomic<uint64_t> done{0};
+    int dev = 0;
+    HIP_CHECK(hipGetDevice(&dev));
+    const uint64_t bit = 1ull << (dev & 63);
+    if (done.load() & bit) return;
     FixedTables ft{};
     for (uint32_t s = 0; s < 288; ++s) {
         uint32_t code, n;
@@ -602,7 +607,7 @@ void upload_tables()
     }
     HIP_CHECK(hipMemcpyToSymbol(HIP_SYMBOL(c_ft), &ft, sizeof(ft)));
     HIP_CHECK(hipMemcpyToSymbol(HIP_SYMBOL(c_crc_tab), tab, sizeof(tab)));
-    done = true;
+    done.fetch_or(bit);
 }
 
 }  // namespace

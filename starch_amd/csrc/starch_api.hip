@@ -421,6 +421,7 @@ void encode_units(starch_ctx* c, const uint8_t* d_base, const std::vector<UnitIn
     }
     HIP_CHECK(hipEventRecord(e2, c->st));
     HIP_CHECK(hipStreamSynchronize(c->st));
+    if (!gzip) c->enc.resolve_timers(&bst);
     float ms_t = 0, ms_all = 0;
     HIP_CHECK(hipEventElapsedTime(&ms_t, e0, e1));
     HIP_CHECK(hipEventElapsedTime(&ms_all, e0, e2));
