@@ -17,6 +17,16 @@ struct StreamIn {          // one RLE1 piece: a stream, or the part of a stream 
     uint64_t text_len;
     uint32_t final_run_joins;  // 1: its last byte arrived with the FLUSH/FINISH call (bz:bzlib.c:393-397)
     uint32_t group;        // output stream it belongs to (pieces of a stream are consecutive)
+    // a stream encoded in pieces (streaming ingestion inside a chromosome):
+    // all zero for a whole stream.  cont: not the stream's first piece (no
+    // header; its bits start at bit `phase` of the first output byte, the
+    // bits before belong to the previous piece).  open: the stream goes on
+    // after this piece: its last, incomplete block is not encoded (its text
+    // from Encoder::open_rest() on goes first in the next piece; a block
+    // starts a fresh RLE1 run, bz:bzlib.c:266-280) and no trailer is written.
+    // comb_in: combined CRC of the blocks before this piece.  Only the last
+    // piece of a call may be open.
+    uint32_t cont, open, phase, comb_in;
 };
 
 struct BlockDesc {         // one bzip2 block (bz:compress.c:602-667)
@@ -39,10 +49,10 @@ struct BlockDesc {         // one bzip2 block (bz:compress.c:602-667)
 
 struct StreamOut {
     uint64_t out_off;          // byte offset of the stream in the output buffer
-    uint64_t bytes;            // stream length in bytes
+    uint64_t bytes;            // stream length in bytes (a piece: its bytes, the last one partial unless closed)
     uint32_t first_block, n_blocks;
-    uint32_t combined_crc;
-    uint32_t pad;
+    uint32_t combined_crc;     // (emit: the CRC entering the piece; after emit: over all blocks so far)
+    uint32_t frame;            // bit 0: header, bit 1: trailer, bits 8..10: phase (see StreamIn)
     uint64_t block_bits;       // bits of the blocks alone (no header, trailer or padding)
 };
 
@@ -76,6 +86,9 @@ public:
     // waiting on them; once the stream has synchronised, this adds them to
     // *stats (null: drops them).  plan() drops any left from an earlier call.
     void resolve_timers(Stats* stats);
+    // text offset (in the plan's d_text) where an open last piece's unencoded
+    // rest starts; its end is the piece's end
+    uint64_t open_rest() const { return open_rest_; }
     struct PendTimer {
         hipEvent_t a, b;
         int stage;                 // 0 rle, 1 bwt, 2 mtf, 3 tables, 4 emit
@@ -101,6 +114,7 @@ private:
     std::vector<StreamIn> streams_;
     std::vector<BlockDesc> host_blocks_;
     std::vector<PendTimer> pend_;
+    uint64_t open_rest_ = 0;
 };
 
 }  // namespace bz

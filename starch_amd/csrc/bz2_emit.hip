@@ -275,16 +275,20 @@ __global__ void k_stream_frame(const StreamOut* __restrict__ souts, const BlockD
     uint32_t s = blockIdx.x * blockDim.x + threadIdx.x;
     if (s >= nstreams) return;
     const StreamOut so = souts[s];
-    uint64_t pos = (out_base + so.out_off) * 8;
+    uint64_t pos = (out_base + so.out_off) * 8 + ((so.frame >> 8) & 7u);   // a piece may start mid-byte
     BitOut o;
-    o.init(out32, pos);
-    o.put(8, 'B');
-    o.put(8, 'Z');
-    o.put(8, 'h');
-    o.put(8, (uint32_t)('0' + bs100k));
-    o.finish();
-    uint32_t comb = 0;
-    uint64_t end = pos + 32;
+    if (so.frame & 1u) {
+        o.init(out32, pos);
+        o.put(8, 'B');
+        o.put(8, 'Z');
+        o.put(8, 'h');
+        o.put(8, (uint32_t)('0' + bs100k));
+        o.finish();
+        pos += 32;
+    }
+    if (!(so.frame & 2u)) return;                  // an open piece: the stream goes on
+    uint32_t comb = so.combined_crc;               // blocks of earlier pieces
+    uint64_t end = pos;
     for (uint32_t k = 0; k < so.n_blocks; ++k) {
         const BlockDesc& bd = blocks[so.first_block + k];
         comb = ((comb << 1) | (comb >> 31)) ^ bd.crc;                   // bz:compress.c:606-608

@@ -154,16 +154,44 @@ void Encoder::plan(const uint8_t* d_text, const std::vector<StreamIn>& streams, 
     t_rle.stop();
     uint32_t nb = 0;
     for (uint32_t s = 0; s < nstreams_; ++s) {
+        if (streams[s].open && s + 1 != nstreams_) throw StarchError(-2, "only the last piece may be open");
         StreamOut& g = outs[streams[s].group];
         if (g.n_blocks == 0) g.first_block = nb;
         g.n_blocks += nblk[s];
         nb += nblk[s];
     }
     if (nb != nblk[nstreams_]) throw StarchError(-10, "block count mismatch");
+    open_rest_ = 0;
+    if (streams.back().open) {   // the open piece's last block waits for more text
+        const StreamIn& o = streams.back();
+        open_rest_ = o.text_off + o.text_len;
+        if (nblk[nstreams_ - 1]) {
+            open_rest_ = hbp[nb - 1].in_beg;
+            --nb;
+            --outs[o.group].n_blocks;
+        }
+    }
     nblocks_ = nb;
     if (stats) stats->n_blocks += nb;
+    // frame of each output stream (whole stream: header + trailer, phase 0)
+    for (uint32_t s = 0; s < nstreams_; ++s) {
+        StreamOut& g = outs[streams[s].group];
+        const bool first = s == 0 || streams[s - 1].group != streams[s].group;
+        const bool last = s + 1 == nstreams_ || streams[s + 1].group != streams[s].group;
+        if (first) {
+            g.frame = (streams[s].cont ? 0u : 1u) | ((streams[s].phase & 7u) << 8);
+            g.combined_crc = streams[s].comb_in;
+        }
+        if (last && !streams[s].open) g.frame |= 2u;
+    }
+    auto frame_bits = [](const StreamOut& o) {
+        return (uint64_t)((o.frame >> 8) & 7u) + ((o.frame & 1u) ? 32u : 0u) + ((o.frame & 2u) ? 80u : 0u);
+    };
     if (nb == 0) {
-        for (uint32_t g = 0; g < ngroups_; ++g) outs[g].bytes = 14;   // header + trailer (bz:compress.c:622-666)
+        for (uint32_t g = 0; g < ngroups_; ++g) {   // header + trailer (bz:compress.c:622-666)
+            outs[g].block_bits = 0;
+            outs[g].bytes = (frame_bits(outs[g]) + 7) / 8;
+        }
         uint64_t off = 0;
         for (uint32_t g = 0; g < ngroups_; ++g) { outs[g].out_off = off; off += outs[g].bytes; }
         return;
@@ -374,13 +402,13 @@ void Encoder::plan(const uint8_t* d_text, const std::vector<StreamIn>& streams, 
         stats->bwt_tied += hstats[2];
         for (auto& b : hb) stats->rle_bytes += b.n;
     }
-    // stream sizes: 32 header bits + blocks + 80 trailer bits, padded to a byte
+    // stream sizes: (phase) + 32 header bits + blocks + 80 trailer bits, padded to a byte
     uint64_t off = 0;
     for (uint32_t s = 0; s < ngroups_; ++s) {
         uint64_t bits = 0;
         for (uint32_t k = 0; k < outs[s].n_blocks; ++k) bits += hb[outs[s].first_block + k].bits;
         outs[s].block_bits = bits;
-        bits += 32 + 80;
+        bits += frame_bits(outs[s]);
         outs[s].bytes = (bits + 7) / 8;
         outs[s].out_off = off;
         off += outs[s].bytes;
@@ -400,7 +428,7 @@ void Encoder::emit(uint8_t* d_out, uint64_t out_cap, uint64_t out_base, std::vec
     HIP_CHECK(hipMemsetAsync(d_out + out_base, 0, total, st));
     // absolute bit offsets of every block
     for (uint32_t s = 0; s < ngroups_; ++s) {
-        uint64_t pos = (out_base + outs[s].out_off) * 8 + 32;
+        uint64_t pos = (out_base + outs[s].out_off) * 8 + ((outs[s].frame >> 8) & 7u) + ((outs[s].frame & 1u) ? 32u : 0u);
         for (uint32_t k = 0; k < outs[s].n_blocks; ++k) {
             BlockDesc& b = host_blocks_[outs[s].first_block + k];
             b.bit_off = pos;
@@ -422,7 +450,7 @@ void Encoder::emit(uint8_t* d_out, uint64_t out_cap, uint64_t out_base, std::vec
                        src_of_dev_, out32, st);
     launch_stream_frame(d_souts, d_blocks, ngroups_, bs100k_, out_base, out32, st);
     for (uint32_t s = 0; s < ngroups_; ++s) {
-        uint32_t comb = 0;
+        uint32_t comb = outs[s].combined_crc;      // the CRC entering the piece (0: a whole stream)
         for (uint32_t k = 0; k < outs[s].n_blocks; ++k) {
             uint32_t c = host_blocks_[outs[s].first_block + k].crc;
             comb = ((comb << 1) | (comb >> 31)) ^ c;

@@ -166,14 +166,36 @@ struct starch_ctx {
         double t_copy = 0, t_commit = 0;   // STARCH_TRACE: feed-side time
         uint64_t fed = 0;
         int64_t init_start = 0, init_stop = 0;   // sscanf values current before buf[cur][0]
+        // buf[cur] starts with ctx_len bytes of context: the last line of a
+        // batch cut inside a chromosome, re-parsed for the transform state of
+        // the lines after it (its own output is dropped)
+        uint64_t ctx_len = 0;
         // encoder thread and its one job slot
         std::thread worker;
         std::mutex mu;                // guards the job slot, ready, segs/names/stats, err
         std::condition_variable cv;
         bool job = false, busy = false, stop = false;
         const uint8_t* job_buf = nullptr;   // device (dbuf)
-        uint64_t job_n = 0;
+        uint64_t job_n = 0, job_ctx = 0;
+        bool job_open = false;          // the batch ends inside a chromosome
         int64_t job_is = 0, job_ip = 0;
+        struct OpenStream {             // a chromosome's bzip2 stream encoded batch by batch (encoder thread)
+            bool active = false;
+            std::string name;
+            DevBuf rest;                // its text after the last complete block
+            uint64_t rest_len = 0;
+            uint32_t phase = 0, comb = 0, n_blocks = 0;
+            uint8_t carry = 0;          // the first `phase` bits of its next byte
+            uint64_t lines = 0, text_bytes = 0, off = 0, bytes = 0;
+            void clear()                // everything but the rest's allocation and length
+            {
+                active = false;
+                name.clear();
+                phase = comb = n_blocks = 0;
+                carry = 0;
+                lines = text_bytes = off = bytes = 0;
+            }
+        } os;
         int err = 0;
         std::string err_msg;
         std::vector<uint8_t> ready;   // archive bytes not yet read, from ready_off on

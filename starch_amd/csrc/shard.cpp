@@ -193,6 +193,21 @@ void plan_units_upto(const uint8_t* b, uint64_t lim, uint64_t max_units, std::ve
     }
 }
 
+void values_before(const uint8_t* b, uint64_t lo, uint64_t pos, int64_t* start, int64_t* stop)
+{
+    bool hs = false, hp = false;
+    uint64_t le = pos;
+    while (le > lo && !(hs && hp)) {
+        const uint64_t ls = line_start(b, lo, le - 1);
+        int64_t a = 0, c = 0;
+        bool oa = false, oc = false;
+        parse_line(b, ls, le, &a, &oa, &c, &oc);
+        if (!hs && oa) { *start = a; hs = true; }
+        if (!hp && oc) { *stop = c; hp = true; }
+        le = ls;
+    }
+}
+
 void assign_lpt(const std::vector<Unit>& units, int nshards, std::vector<int32_t>& shard_of)
 {
     shard_of.assign(units.size(), 0);

@@ -941,12 +941,194 @@ void stream_reserve(starch_ctx* c, int i, uint64_t need)
     std::swap(m.dbuf[i].cap, nb.cap);
 }
 
+// Streaming inside a chromosome (bzip2): a batch may end inside a chromosome
+// (open) and the next one then starts with the last line of it (ctx bytes of
+// context).  The chromosome's stream is encoded in pieces: every batch
+// encodes the complete bzip2 blocks of its text and carries the text after
+// the last block boundary (a block starts a fresh RLE1 run, so the rest
+// encodes the same in front of the next batch's text), the bits of the last
+// partial byte, the combined CRC and the block count to the next piece; the
+// header goes with the first piece, the trailer with the last one.  The
+// context line is transformed on its own as well, and that output (the line
+// as a segment's first) is dropped from the batch's first segment.
+void stream_encode_pieces(starch_ctx* c, const uint8_t* d, uint64_t n, int64_t is, int64_t ip, uint64_t ctx,
+                          bool open)
+{
+    auto& m = c->sm;
+    auto& os = m.os;
+    hipEvent_t e0, e1, e2;
+    HIP_CHECK(hipEventCreate(&e0));
+    HIP_CHECK(hipEventCreate(&e1));
+    HIP_CHECK(hipEventCreate(&e2));
+    HIP_CHECK(hipEventRecord(e0, c->st));
+    c->stats = starch_stats{};
+    c->stats.input_bytes = n - ctx;
+    uint64_t o_ctx = 0;
+    if (ctx) {
+        TransformResult tc;
+        c->tf.run(d, ctx, c->st, tc, is, ip);
+        if (tc.n_lines != 1 || tc.n_segments != 1) throw StarchError(STARCH_ERR_INTERNAL, "stream: context line");
+        o_ctx = tc.text_bytes;
+    }
+    TransformResult tr;
+    c->tf.run(d, n, c->st, tr, is, ip);
+    std::vector<SegInfo> si(tr.n_segments);
+    if (tr.n_segments)
+        HIP_CHECK(hipMemcpyAsync(si.data(), c->tf.seg_info_dev, tr.n_segments * sizeof(SegInfo), hipMemcpyDeviceToHost,
+                                 c->st));
+    HIP_CHECK(hipStreamSynchronize(c->st));
+    if (ctx) {
+        if (si.empty() || si[0].line_count < 1 || si[0].text_len < o_ctx)
+            throw StarchError(STARCH_ERR_INTERNAL, "stream: context segment");
+        si[0].text_off += o_ctx;
+        si[0].text_len -= o_ctx;
+        si[0].line_count -= 1;
+        si[0].first_line += 1;
+    }
+    HIP_CHECK(hipEventRecord(e1, c->st));
+    const uint64_t nseg = si.size();
+    const bool cont = os.active;
+    if (cont != (ctx > 0) || nseg == 0) throw StarchError(STARCH_ERR_INTERNAL, "stream: piece state");
+    PendingNames pn;
+    fetch_names(c, d, si, pn);
+    // the open stream's rest, then the batch's text from segment 0 on
+    const uint8_t* T = c->tf.text;
+    const uint64_t new0 = si[0].text_len;
+    if (cont && os.rest_len) {
+        const uint64_t R = os.rest_len, t0 = si[0].text_off, span = tr.text_bytes - t0;
+        uint8_t* Tb = c->text_all.as<uint8_t>(R + span + 64);
+        HIP_CHECK(hipMemcpyAsync(Tb, os.rest.p, R, hipMemcpyDeviceToDevice, c->st));
+        if (span) HIP_CHECK(hipMemcpyAsync(Tb + R, c->tf.text + t0, span, hipMemcpyDeviceToDevice, c->st));
+        for (auto& x : si) x.text_off = x.text_off - t0 + R;
+        si[0].text_off = 0;
+        si[0].text_len += R;
+        T = Tb;
+    }
+    std::vector<bz::StreamIn> sin(nseg);
+    for (uint64_t s = 0; s < nseg; ++s) {
+        sin[s].text_off = si[s].text_off;
+        sin[s].text_len = si[s].text_len;
+        sin[s].final_run_joins = 1;
+        sin[s].group = (uint32_t)s;
+    }
+    if (cont) {
+        sin[0].cont = 1;
+        sin[0].phase = os.phase;
+        sin[0].comb_in = os.comb;
+    }
+    if (open) {
+        sin[nseg - 1].open = 1;
+        sin[nseg - 1].final_run_joins = 0;
+    }
+    std::vector<bz::StreamOut> outs;
+    bz::Stats bst;
+    c->enc.plan(T, sin, m.opt.block_size_100k, c->st, outs, &bst);
+    finish_names(c, pn);
+    if (cont && c->names[0] != os.name) throw StarchError(STARCH_ERR_INTERNAL, "stream: continued chromosome");
+    uint64_t total = 0;
+    for (auto& o : outs) total = std::max(total, o.out_off + o.bytes);
+    const uint64_t cap = align_up(total + 64, 256);
+    uint8_t* out = c->part.as<uint8_t>(cap);
+    c->enc.emit(out, cap, 0, outs, c->st, &bst);
+    std::vector<uint8_t> part(total);
+    if (total) HIP_CHECK(hipMemcpyAsync(part.data(), out, total, hipMemcpyDeviceToHost, c->st));
+    if (open) {   // the text after the last complete block waits for the next batch
+        const uint64_t r0 = c->enc.open_rest(), r1 = sin[nseg - 1].text_off + sin[nseg - 1].text_len;
+        os.rest_len = r1 - r0;
+        if (os.rest.cap < os.rest_len + 64) HIP_CHECK(hipStreamSynchronize(c->st));   // T may hold the old rest
+        uint8_t* rp = os.rest.as<uint8_t>(os.rest_len + 64);
+        if (os.rest_len) HIP_CHECK(hipMemcpyAsync(rp, T + r0, os.rest_len, hipMemcpyDeviceToDevice, c->st));
+    }
+    HIP_CHECK(hipEventRecord(e2, c->st));
+    HIP_CHECK(hipStreamSynchronize(c->st));
+    c->enc.resolve_timers(&bst);
+    float ms_t = 0, ms_all = 0;
+    HIP_CHECK(hipEventElapsedTime(&ms_t, e0, e1));
+    HIP_CHECK(hipEventElapsedTime(&ms_all, e0, e2));
+    (void)hipEventDestroy(e0);
+    (void)hipEventDestroy(e1);
+    (void)hipEventDestroy(e2);
+    STRACE("stream batch %llu: %llu bytes in %llu segments (%s%s), device %.3f ms", (unsigned long long)m.batches,
+           (unsigned long long)(n - ctx), (unsigned long long)nseg, cont ? "continues a chromosome" : "",
+           open ? (cont ? ", open" : "open") : "", ms_all);
+    std::lock_guard<std::mutex> lk(m.mu);
+    for (uint64_t s = 0; s < nseg; ++s) {
+        const bz::StreamOut& o = outs[s];
+        const bool is_cont = s == 0 && cont, is_open = s + 1 == nseg && open;
+        const uint8_t* b = part.data() + o.out_off;
+        const uint64_t bits = ((o.frame >> 8) & 7u) + ((o.frame & 1u) ? 32u : 0u) + o.block_bits +
+                              ((o.frame & 2u) ? 80u : 0u);
+        const uint64_t full = is_open ? bits / 8 : o.bytes;   // an open piece keeps its last partial byte
+        const size_t at = m.ready.size();
+        m.ready.insert(m.ready.end(), b, b + full);
+        if (is_cont && full) m.ready[at] |= os.carry;   // the previous piece's bits of this byte
+        uint8_t carry = 0;
+        if (is_open && (bits & 7u)) carry = (uint8_t)(b[full] | ((is_cont && full == 0) ? os.carry : 0u));
+        const uint64_t off = m.stream_end;
+        m.stream_end += full;
+        if (!is_cont) {               // a stream starts here
+            os.clear();
+            if (is_open) {
+                os.active = true;
+                os.name = c->names[s];
+                os.off = off;
+            }
+        }
+        if (is_cont || is_open) {     // a piece of a stream encoded in pieces
+            os.bytes += full;
+            os.n_blocks += o.n_blocks;
+            os.comb = o.combined_crc;
+            os.lines += si[s].line_count;
+            os.text_bytes += s == 0 ? new0 : si[s].text_len;
+            if (is_open) {
+                os.phase = (uint32_t)(bits & 7u);
+                os.carry = carry;
+                continue;
+            }
+        }
+        starch_segment g{};
+        g.line_count = is_cont ? os.lines : si[s].line_count;
+        g.text_bytes = is_cont ? os.text_bytes : si[s].text_len;
+        g.name_len = c->names[s].size();
+        g.stream_offset = is_cont ? os.off : off;
+        g.stream_bytes = is_cont ? os.bytes : o.bytes;
+        g.n_blocks = is_cont ? os.n_blocks : o.n_blocks;
+        g.combined_crc = o.combined_crc;
+        g.unit = m.batches;
+        m.segs.push_back(g);
+        m.names.push_back(c->names[s]);
+        if (is_cont) os.clear();
+    }
+    if (!open) os.rest_len = 0;
+    ++m.batches;
+    starch_stats& t = m.stats;
+    t.n_lines += tr.n_lines - (ctx ? 1 : 0);
+    t.text_bytes += tr.text_bytes - o_ctx;
+    t.n_blocks += bst.n_blocks;
+    t.rle_bytes += bst.rle_bytes;
+    t.bwt_rounds += bst.bwt_rounds;
+    t.periodic_blocks += bst.periodic_blocks;
+    t.bwt_tied += bst.bwt_tied;
+    t.dedup_blocks += bst.dedup_blocks;
+    t.ms_transform += ms_t;
+    t.ms_rle += bst.rle;
+    t.ms_bwt += bst.bwt;
+    t.ms_mtf += bst.mtf;
+    t.ms_tables += bst.tables;
+    t.ms_emit += bst.emit;
+    t.ms_total += ms_all;
+}
+
 // encoder thread: encode b[0, n) (segment boundary to segment boundary, or to
 // the end) with the given initial values and append its streams
-void stream_encode(starch_ctx* c, const uint8_t* d, uint64_t n, int64_t is, int64_t ip)
+void stream_encode(starch_ctx* c, const uint8_t* d, uint64_t n, int64_t is, int64_t ip, uint64_t ctx, bool open)
 {
     auto& m = c->sm;
     if (m.opt.reference_compat) return;   // the reference writes only the magic (hpp:765-769)
+    if (ctx || open || m.os.active) {
+        stream_encode_pieces(c, d, n, is, ip, ctx, open);
+        return;
+    }
     STRACE("stream batch %llu: %llu bytes, encode", (unsigned long long)m.batches, (unsigned long long)n);
     HIP_CHECK(hipStreamWaitEvent(c->st, m.job_ev, 0));   // the batch's H2D (copy stream) is done
     std::vector<UnitIn> u(1, UnitIn{0, n, is, ip, 0});
@@ -993,7 +1175,8 @@ void stream_worker(starch_ctx* c)
     (void)hipSetDevice(c->device);
     for (;;) {
         const uint8_t* b;
-        uint64_t n;
+        uint64_t n, ctx;
+        bool open;
         int64_t is, ip;
         {
             std::unique_lock<std::mutex> lk(m.mu);
@@ -1001,6 +1184,8 @@ void stream_worker(starch_ctx* c)
             if (!m.job) return;
             b = m.job_buf;
             n = m.job_n;
+            ctx = m.job_ctx;
+            open = m.job_open;
             is = m.job_is;
             ip = m.job_ip;
             m.job = false;
@@ -1009,7 +1194,7 @@ void stream_worker(starch_ctx* c)
         int code = 0;
         std::string msg;
         try {
-            stream_encode(c, b, n, is, ip);
+            stream_encode(c, b, n, is, ip, ctx, open);
         } catch (const StarchError& e) {
             code = e.code;
             msg = e.what();
@@ -1035,17 +1220,21 @@ void stream_wait(starch_ctx* c)
     if (m.err) throw StarchError(m.err, m.err_msg);
 }
 
-// hand buf[cur][0, n) to the encoder thread (the caller has waited for idle)
-void stream_submit(starch_ctx* c, uint64_t n)
+// hand buf[cur][0, n) to the encoder thread (the caller has waited for idle);
+// its first m.ctx_len bytes are context (already counted), open: it ends
+// inside a chromosome
+void stream_submit(starch_ctx* c, uint64_t n, bool open = false)
 {
     auto& m = c->sm;
-    m.stats.input_bytes += n;
+    m.stats.input_bytes += n - m.ctx_len;
     HIP_CHECK(hipEventRecord(m.job_ev, c->cst));
     {
         std::lock_guard<std::mutex> lk(m.mu);
         m.job = true;
         m.job_buf = static_cast<const uint8_t*>(m.dbuf[m.cur].p);
         m.job_n = n;
+        m.job_ctx = m.ctx_len;
+        m.job_open = open;
         m.job_is = m.init_start;
         m.job_ip = m.init_stop;
     }
@@ -1064,8 +1253,40 @@ void stream_cut(starch_ctx* c)
         const uint64_t lim = (uint64_t)(static_cast<const uint8_t*>(nl) - h) + 1;
         shard::plan_units_upto(h, lim, 4096, u, m.init_start, m.init_stop);   // commit cut the bytes at any 0xFF
     }
-    if (u.size() < 2) {   // no boundary yet: the held run continues
-        m.try_at = m.held_n + m.batch / 2;
+    if (u.size() < 2) {   // no chromosome boundary among the complete lines
+        // bzip2 streams encode in pieces: a whole batch of one chromosome is
+        // cut at its last complete line (STARCH_STREAM_HOLD=1: held whole)
+        static const bool hold = [] { const char* e = getenv("STARCH_STREAM_HOLD"); return e && !strcmp(e, "1"); }();
+        const bool pieces = !hold && m.opt.compression_method == STARCH_METHOD_BZIP2 && !m.opt.base_counts &&
+                            !m.opt.reference_compat;
+        uint64_t ls = 0, cut = 0;
+        if (pieces && nl && m.held_n >= m.batch) {
+            cut = (uint64_t)(static_cast<const uint8_t*>(nl) - h) + 1;
+            ls = cut - 1;
+            while (ls > 0 && h[ls - 1] != '\n') --ls;   // the last complete line [ls, cut): the next context
+        }
+        if (!pieces || ls <= m.ctx_len || ls == 0) {   // the held run continues
+            m.try_at = m.held_n + m.batch / 2;
+            return;
+        }
+        int64_t st = m.init_start, sp = m.init_stop;
+        shard::values_before(h, 0, ls, &st, &sp);      // sscanf values current before the context line
+        const uint64_t tail = m.held_n - ls;
+        STRACE("stream cut inside a chromosome at %llu of %llu held", (unsigned long long)cut,
+               (unsigned long long)m.held_n);
+        stream_wait(c);
+        const int o = 1 - m.cur;
+        stream_reserve(c, o, std::max<uint64_t>(tail + m.batch + (m.batch >> 2), 1ull << 20));
+        m.pool.copy(m.buf[o], h + ls, tail);
+        HIP_CHECK(hipMemcpyAsync(m.dbuf[o].p, static_cast<uint8_t*>(m.dbuf[m.cur].p) + ls, tail,
+                                 hipMemcpyDeviceToDevice, c->cst));
+        stream_submit(c, cut, true);
+        m.cur = o;
+        m.held_n = tail;
+        m.ctx_len = cut - ls;
+        m.init_start = st;
+        m.init_stop = sp;
+        m.try_at = std::max(m.batch, tail + m.batch / 2);
         return;
     }
     const uint64_t cut = u.back().offset, tail = m.held_n - cut;
@@ -1081,6 +1302,7 @@ void stream_cut(starch_ctx* c)
     stream_submit(c, cut);
     m.cur = o;
     m.held_n = tail;
+    m.ctx_len = 0;
     m.init_start = u.back().init_start;
     m.init_stop = u.back().init_stop;
     m.try_at = std::max(m.batch, tail + m.batch / 2);
@@ -1594,6 +1816,9 @@ int starch_stream_begin(starch_ctx* c, const starch_options* opt, uint64_t batch
     m.opt.note = o.note ? m.note.c_str() : nullptr;
     m.cur = 0;
     m.held_n = 0;
+    m.ctx_len = 0;
+    m.os.clear();                                // a session left open may have left a piece behind
+    m.os.rest_len = 0;
     m.batch = batch_bytes ? batch_bytes : (256ull << 20);
     m.try_at = m.batch;
     m.batches = 0;
@@ -1685,7 +1910,7 @@ int starch_stream_end(starch_ctx* c)
     if (!m.active) return STARCH_ERR_STATE;
     try {
         stream_wait(c);
-        if (m.held_n) {
+        if (m.held_n > m.ctx_len || m.os.active) {
             stream_submit(c, m.held_n);
             stream_wait(c);
         }
@@ -1699,6 +1924,7 @@ int starch_stream_end(starch_ctx* c)
     m.t_copy = m.t_commit = 0;
     m.fed = 0;
     m.held_n = 0;
+    m.ctx_len = 0;
     if (m.opt.emit_index && !m.opt.reference_compat) {
         std::vector<const char*> np(m.segs.size());
         std::vector<uint64_t> nl(m.segs.size());

@@ -253,3 +253,57 @@ again = c.archive()
 c.close()
 print("same" if got == want and again == want else "differ")
 '''
+
+
+@pytest.mark.parametrize("batch", [1 << 20, 3_000_000, 7_777_777])
+def test_stream_inside_one_chromosome(batch):
+    """A single chromosome run longer than a batch is not held whole: batches
+    are cut at a complete line inside it and its bzip2 stream is encoded in
+    pieces (complete blocks per batch, the rest of the text, the last partial
+    byte and the combined CRC carried to the next piece).  The archive equals
+    the one-call archive byte for byte."""
+    import starch_amd
+    data = starch_amd.gen_bed(0, 1_500_000, chroms=[0])
+    ref = _one_call(data)
+    got, st = _streamed(data, 1 << 20, batch)
+    assert got == ref
+    assert st["n_segments"] == 1
+    assert st["input_bytes"] == len(data)
+
+
+def test_stream_inside_chromosome_runs_and_revisits():
+    """Pieces whose cuts fall inside long byte runs (RLE1 chunks of 255), a
+    chromosome revisited later, lines that do not parse (stale values carried
+    across an inside cut) and a multi-block tail."""
+    import random
+    rnd = random.Random(7)
+    lines = []
+    pos = 1000
+    for i in range(60_000):
+        pos += rnd.randrange(0, 50)
+        rem = "\t" + "A" * rnd.choice([0, 3, 4, 5, 254, 255, 256, 600]) if i % 7 == 0 else ""
+        if i % 501 == 0:
+            lines.append("chr1\tx\t%d%s\n" % (pos + 5, rem))
+        else:
+            lines.append("chr1\t%d\t%d%s\n" % (pos, pos + rnd.randrange(1, 400), rem))
+    data = "".join(lines).encode() + b"chr2\t5\t9\n" * 3000 + "".join(lines[:20_000]).encode()
+    ref = _one_call(data)
+    for piece, batch in ((1 << 16, 200_000), (12_345, 1_000_000), (1 << 20, 1)):
+        got, _ = _streamed(data, piece, batch)
+        assert got == ref, (piece, batch)
+
+
+def test_stream_inside_chromosome_hold_knob():
+    """STARCH_STREAM_HOLD=1 keeps the chromosome-boundary-only cuts (the same
+    archive, one batch per chromosome run)."""
+    import starch_amd
+    data = starch_amd.gen_bed(0, 300_000, chroms=[0, 1])
+    ref = _one_call(data)
+    code = ("import sys; sys.path.insert(0, %r); import starch_amd\n"
+            "d = starch_amd.gen_bed(0, 300_000, chroms=[0, 1])\n"
+            "c = starch_amd.Starch(0)\n"
+            "a = c.compress_stream([d[i:i + 65536] for i in range(0, len(d), 65536)], batch_bytes=1 << 20)\n"
+            "sys.stdout.buffer.write(a)\n") % ROOT
+    env = dict(os.environ, STARCH_STREAM_HOLD="1")
+    out = subprocess.run([sys.executable, "-c", code], env=env, capture_output=True, timeout=300, check=True).stdout
+    assert out == ref
