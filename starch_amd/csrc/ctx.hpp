@@ -46,25 +46,35 @@ struct CopyPool {
                 if (stop) return;
                 seen = gen;
             }
-            for (;;) {
-                const uint64_t k = next.fetch_add(1);
-                const uint64_t o = k * chunk;
-                if (o >= n) break;
-                const uint64_t len = std::min(chunk, n - o);
-                memcpy(dst + o, src + o, len);
-                if (find_ff) {   // while the chunk is in cache: its first 0xFF
-                    const void* f = memchr(dst + o, 0xFF, len);
-                    if (f) {
-                        const uint64_t at = o + (uint64_t)(static_cast<const uint8_t*>(f) - (dst + o));
-                        uint64_t cur = ff.load();
-                        while (at < cur && !ff.compare_exchange_weak(cur, at)) {}
-                    }
-                }
-            }
+            work();
             std::lock_guard<std::mutex> lk(mu);
             if (--pending == 0) done.notify_all();
         }
     }
+    // take chunks until none is left; each chunk goes in 256 KiB steps, its
+    // 0xFF search right after each step's copy (the bytes still in cache)
+    void work()
+    {
+        for (;;) {
+            const uint64_t k = next.fetch_add(1);
+            const uint64_t o = k * chunk;
+            if (o >= n) break;
+            const uint64_t e = std::min(o + chunk, n);
+            for (uint64_t p = o; p < e; p += kStep) {
+                const uint64_t len = std::min(kStep, e - p);
+                memcpy(dst + p, src + p, len);
+                if (!find_ff) continue;
+                const void* f = memchr(dst + p, 0xFF, len);
+                if (f) {
+                    const uint64_t at = p + (uint64_t)(static_cast<const uint8_t*>(f) - (dst + p));
+                    uint64_t cur = ff.load();
+                    while (at < cur && !ff.compare_exchange_weak(cur, at)) {}
+                    break;   // a later 0xFF in this chunk cannot be the first
+                }
+            }
+        }
+    }
+    static constexpr uint64_t kStep = 256ull << 10;
     // copy and return the offset of the first 0xFF in the bytes (len if none)
     uint64_t copy_find_ff(uint8_t* d, const uint8_t* s, uint64_t len)
     {
@@ -82,22 +92,25 @@ struct CopyPool {
     void copy(uint8_t* d, const uint8_t* s, uint64_t len)
     {
         if (len < (8ull << 20)) { memcpy(d, s, len); return; }
-        if (th.empty()) {
+        if (th.empty()) {   // the caller copies too: threads = the CPU share (OMP_NUM_THREADS) - 1
             unsigned hw = std::thread::hardware_concurrency();
-            const int k = (int)std::max(1u, std::min(8u, hw / 2));
-            for (int i = 0; i < k; ++i) th.emplace_back(&CopyPool::run, this, i, (uint64_t)0);
+            const char* e = getenv("OMP_NUM_THREADS");
+            unsigned want = e && atoi(e) > 0 ? (unsigned)atoi(e) : std::min(16u, std::max(1u, hw / 2));
+            want = std::min(want, 32u);
+            for (unsigned i = 1; i < want; ++i) th.emplace_back(&CopyPool::run, this, (int)i, (uint64_t)0);
         }
         {
             std::lock_guard<std::mutex> lk(mu);
             dst = d;
             src = s;
             n = len;
-            chunk = 4ull << 20;
+            chunk = 1ull << 20;
             next = 0;
             pending = (int)th.size();
             ++gen;
         }
         cv.notify_all();
+        work();
         std::unique_lock<std::mutex> lk(mu);
         done.wait(lk, [&] { return pending == 0; });
     }
