@@ -785,18 +785,22 @@ __global__ void __launch_bounds__(SCT) k3_scatter_lds(Ctx c)
 
 // ---------------------------------------------------------------------------
 // binning of a work list by block into per-XCD segments (blocks x, x+8, ...).
-// A batch of few blocks (nb < 64) bins by (block, item mod 8) instead (vs = 3),
-// so its groups spread over all XCDs: one block's PSS fits every L2, and
-// binning by block alone would leave 7 of 8 XCDs idle.
+// A batch of few blocks (nb < 64) bins by (block, 64-item run mod 8) instead
+// (vs = 3), so its groups spread over all XCDs: one block's PSS fits every
+// L2, and binning by block alone would leave 7 of 8 XCDs idle.  Lists come
+// out of the sorts mostly grouped by block: a wave whose 64 items share a bin
+// counts / places them with one LDS atomic (one atomic per item serialised
+// the wave on one address).
 // ---------------------------------------------------------------------------
-constexpr uint32_t BIN_CH = 32768;    // items per binning workgroup (at least)
-constexpr uint32_t BIN_MAXWG = 512;
+constexpr uint32_t BIN_CH = 4096;     // items per binning workgroup (at least)
+constexpr uint32_t BIN_MAXWG = 128;
 
 __device__ __forceinline__ uint32_t bin_of(uint64_t it, uint32_t i, uint32_t vs)
 {
-    return (it_slot(it) << vs) | (i & ((1u << vs) - 1u));
+    return (it_slot(it) << vs) | ((i >> 6) & ((1u << vs) - 1u));
 }
 
+// chunks are multiples of 64 items, so every wave's 64 items share i >> 6
 __global__ void __launch_bounds__(256) k3_bin_hist(const uint64_t* __restrict__ in, uint32_t n, uint32_t nb,
                                                     uint32_t ch, uint32_t* __restrict__ hist, uint32_t vs)
 {
@@ -804,7 +808,20 @@ __global__ void __launch_bounds__(256) k3_bin_hist(const uint64_t* __restrict__ 
     for (uint32_t i = threadIdx.x; i < nb; i += 256) h[i] = 0;
     __syncthreads();
     const uint32_t a = blockIdx.x * ch, e = a + ch < n ? a + ch : n;
-    for (uint32_t i = a + threadIdx.x; i < e; i += 256) atomicAdd(&h[bin_of(in[i], i, vs)], 1u);
+    for (uint32_t i0 = a; i0 < e; i0 += 256) {     // wave-uniform trip count
+        const uint32_t i = i0 + threadIdx.x;
+        const bool ok = i < e;
+        const uint32_t b = ok ? bin_of(in[i], i, vs) : 0u;
+        const uint64_t act = __ballot(ok);
+        if (!act) continue;
+        const int lead = __ffsll((unsigned long long)act) - 1;
+        const uint32_t b0 = (uint32_t)__shfl((int)b, lead, 64);
+        if (__ballot(ok && b == b0) == act) {
+            if ((int)(threadIdx.x & 63) == lead) atomicAdd(&h[b0], (uint32_t)__popcll(act));
+        } else if (ok) {
+            atomicAdd(&h[b], 1u);
+        }
+    }
     __syncthreads();
     for (uint32_t i = threadIdx.x; i < nb; i += 256) hist[(uint64_t)blockIdx.x * nb + i] = h[i];
 }
@@ -862,9 +879,25 @@ __global__ void __launch_bounds__(256) k3_bin_scatter(const uint64_t* __restrict
     for (uint32_t i = threadIdx.x; i < nb; i += 256) cur[i] = hist[(uint64_t)blockIdx.x * nb + i];
     __syncthreads();
     const uint32_t a = blockIdx.x * ch, e = a + ch < n ? a + ch : n;
-    for (uint32_t i = a + threadIdx.x; i < e; i += 256) {
-        const uint64_t it = in[i];
-        out[atomicAdd(&cur[bin_of(it, i, vs)], 1u)] = it;
+    for (uint32_t i0 = a; i0 < e; i0 += 256) {     // wave-uniform trip count
+        const uint32_t i = i0 + threadIdx.x;
+        const bool ok = i < e;
+        const uint64_t it = ok ? in[i] : 0ull;
+        const uint32_t b = ok ? bin_of(it, i, vs) : 0u;
+        const uint64_t act = __ballot(ok);
+        if (!act) continue;
+        const int lane = (int)(threadIdx.x & 63), lead = __ffsll((unsigned long long)act) - 1;
+        const uint32_t b0 = (uint32_t)__shfl((int)b, lead, 64);
+        uint32_t pos;
+        if (__ballot(ok && b == b0) == act) {          // one bin: one atomic, items in lane order
+            uint32_t base = 0;
+            if (lane == lead) base = atomicAdd(&cur[b0], (uint32_t)__popcll(act));
+            base = (uint32_t)__shfl((int)base, lead, 64);
+            pos = base + (uint32_t)__popcll(act & ((1ull << lane) - 1ull));
+        } else {
+            pos = ok ? atomicAdd(&cur[b], 1u) : 0u;
+        }
+        if (ok) out[pos] = it;
     }
 }
 
@@ -2434,7 +2467,7 @@ bool launch_bwt3(BlockDesc* blocks, uint32_t b0, uint32_t nb, const uint8_t* blk
         next_q(head, seg);
         uint32_t nwg = (n + BIN_CH - 1) / BIN_CH;
         if (nwg > BIN_MAXWG) nwg = BIN_MAXWG;
-        const uint32_t ch = (n + nwg - 1) / nwg;
+        const uint32_t ch = ((n + nwg - 1) / nwg + 63) & ~63u;   // whole waves of items
         const uint32_t vs = nb_bins > nb ? 3u : 0u, nbv = nb << vs;
         hipLaunchKernelGGL(k3_bin_hist, dim3(nwg), dim3(256), 0, st, list, n, nbv, ch, binh, vs);
         hipLaunchKernelGGL(k3_bin_scan, dim3(1), dim3(1024), 0, st, binh, nwg, nbv, seg);

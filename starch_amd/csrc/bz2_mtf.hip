@@ -786,7 +786,7 @@ void launch_mtf(BlockDesc* blocks, uint32_t b0, uint32_t nb, const uint8_t* blkb
     // alphabets <= 32: chunk passes over the key scratch (free after the sort)
     // chunk length: 512 symbols when the batch fills the GPU; a few blocks
     // take shorter chunks (more lanes, shorter serial MTF chains per lane)
-    const uint32_t cs = nb >= 32 ? MCS : nb >= 8 ? 128u : 64u;
+    const uint32_t cs = nb >= 256 ? MCS : nb >= 64 ? 256u : nb >= 8 ? 128u : 64u;
     const uint32_t C = (uint32_t)((scr.stride + cs - 1) / cs);
     const uint64_t kstride = scr.stride;                     // u64 words per slot
     const dim3 gch((C + MCT - 1) / MCT, nb);

@@ -360,8 +360,6 @@ __global__ void __launch_bounds__(TT) k_tables(BlockDesc* __restrict__ blocks, u
 #ifndef STARCH_TABLES_WPE
 #define STARCH_TABLES_WPE 4
 #endif
-constexpr int T32 = 256;
-constexpr int NW32 = T32 / 64;
 #ifdef STARCH_TABLES_PROF
 __device__ unsigned long long g_tprof[8];
 #define TPROF(k) do { __syncthreads(); if (threadIdx.x == 0) { const uint64_t t_ = wall_clock64(); \
@@ -375,12 +373,17 @@ __device__ __forceinline__ uint32_t byte_of(const uint32_t (&h)[8], int v)
     return (h[v >> 2] >> (8 * (v & 3))) & 0xffu;
 }
 
+// T32 threads per block: 256 when the batch fills the GPU with blocks (their
+// serial phases overlap other blocks'), 1024 for a batch of few blocks (each
+// block's group loops and its six heaps spread over 16 waves: per-block latency)
+template <int T32>
 __global__ void __launch_bounds__(T32) __attribute__((amdgpu_waves_per_eu(STARCH_TABLES_WPE))) k_tables32(BlockDesc* __restrict__ blocks, uint32_t b0,
                                                    const uint16_t* __restrict__ mtfv_all, uint64_t mtf_stride,
                                                    Tables* __restrict__ tabs, uint8_t* __restrict__ sel_all,
                                                    uint32_t* __restrict__ gbits_all, uint4* __restrict__ hist_all,
                                                    uint64_t hist_stride)
 {
+    constexpr int NW32 = T32 / 64;
     // phase-disjoint scratch shares one LDS region (histograms, then the four
     // refinement passes, then the selector MTF) and the per-table rows are
     // alpha <= 32 wide: ~27 KB, so LDS no longer caps residency; registers do
@@ -659,8 +662,15 @@ void launch_tables(BlockDesc* blocks, uint32_t b0, uint32_t nb, const uint16_t* 
     // per-group histograms live in the (now free) block-sort key scratch
     uint8_t* hist = reinterpret_cast<uint8_t*>(scr.K);
     const uint64_t hist_stride = scr.stride * sizeof(uint64_t);
-    hipLaunchKernelGGL(k_tables32, dim3(nb), dim3(T32), 0, st, blocks, b0, mtfv, mtf_stride, tabs, sel, gbits,
-                       reinterpret_cast<uint4*>(scr.K), hist_stride / sizeof(uint4));
+#ifndef STARCH_TABLES_WIDE_NB
+#define STARCH_TABLES_WIDE_NB 512
+#endif
+    if (nb < STARCH_TABLES_WIDE_NB)
+        hipLaunchKernelGGL(k_tables32<1024>, dim3(nb), dim3(1024), 0, st, blocks, b0, mtfv, mtf_stride, tabs, sel, gbits,
+                           reinterpret_cast<uint4*>(scr.K), hist_stride / sizeof(uint4));
+    else
+        hipLaunchKernelGGL(k_tables32<256>, dim3(nb), dim3(256), 0, st, blocks, b0, mtfv, mtf_stride, tabs, sel, gbits,
+                           reinterpret_cast<uint4*>(scr.K), hist_stride / sizeof(uint4));
     hipLaunchKernelGGL(k_tables, dim3(nb), dim3(TT), 0, st, blocks, b0, mtfv, mtf_stride, tabs, sel, gbits, hist,
                        hist_stride);
     HIP_CHECK(hipGetLastError());
