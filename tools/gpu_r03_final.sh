@@ -30,6 +30,11 @@ timeout -k 10 600 python bench.py > $O/bench_cfg2.json 2> $O/bench_cfg2.err || {
 cat $O/bench_cfg2.json
 timeout -k 10 600 python bench.py --kind 1 --lines 50000000 --no-cpu-baseline --no-e2e > $O/bench_cfg4.json 2> $O/bench_cfg4.err || { tail -20 $O/bench_cfg4.err; exit 1; }
 cat $O/bench_cfg4.json
+timeout -k 10 300 python bench.py --lines 12500000 --steps 10 --warmup 3 --no-cpu-baseline --no-e2e > $O/bench_eighth.json 2> $O/bench_eighth.err || { tail -20 $O/bench_eighth.err; exit 1; }
+timeout -k 10 120 python tools/small_cost.py 300 > $O/cfg1_small_cost.json 2> $O/cfg1_small_cost.err || { tail -20 $O/cfg1_small_cost.err; exit 1; }
+if [ -n "${CFG5:-}" ]; then
+  timeout -k 10 900 python bench.py --kind 2 --steps 1 --warmup 1 --no-cpu-baseline --no-e2e > $O/bench_cfg5.json 2> $O/bench_cfg5.err || { tail -20 $O/bench_cfg5.err; exit 1; }
+fi
 BENCH_ARGS="--steps 2 --warmup 1" TP=300 bash tools/gpu_prof.sh > /dev/null || exit 1
 cp gpurun_out/prof/run_kernel_stats.csv $O/cfg2_kernel_stats.csv
 BENCH_ARGS="--steps 2 --warmup 1 --kind 1 --lines 50000000" TP=300 bash tools/gpu_prof.sh > /dev/null || exit 1
