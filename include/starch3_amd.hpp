@@ -314,16 +314,51 @@ public:
     }
 
     // Read the in stream to EOF and write everything after the magic (which
-    // initialize_out_stream wrote) to the out stream.
+    // initialize_out_stream wrote) to the out stream.  One device: the
+    // streaming session (starch_stream_*) -- the input is read in 16 MiB
+    // pieces straight into the session's pinned window and the archive bytes
+    // are written as they finish, so memory stays at about two batches
+    // (hpp:158-199 reads line by line).  Several devices: read whole, then
+    // starch_encode_multi_host.
     int compress_in_stream(void)
     {
-        std::vector<unsigned char> in, arch;
-        std::vector<unsigned char> buf(1 << 24);
-        size_t k;
-        while ((k = std::fread(&buf[0], 1, buf.size(), _in_stream)) > 0) in.insert(in.end(), buf.begin(), buf.begin() + k);
-        int rc = compress(in.empty() ? NULL : &in[0], in.size(), &arch);
+        int rc = open_devices();
         if (rc) return rc;
-        if (arch.size() > 4) std::fwrite(&arch[4], 1, arch.size() - 4, _out_stream);
+        if (_ctx.size() > 1) {
+            std::vector<unsigned char> in, arch;
+            std::vector<unsigned char> buf(1 << 24);
+            size_t k;
+            while ((k = std::fread(&buf[0], 1, buf.size(), _in_stream)) > 0)
+                in.insert(in.end(), buf.begin(), buf.begin() + k);
+            if ((rc = compress(in.empty() ? NULL : &in[0], in.size(), &arch))) return rc;
+            if (arch.size() > 4) std::fwrite(&arch[4], 1, arch.size() - 4, _out_stream);
+            std::fflush(_out_stream);
+            return STARCH_OK;
+        }
+        starch_ctx* c = _ctx[0];
+        starch_options o = options();
+        if ((rc = starch_stream_begin(c, &o, 0))) return rc;
+        std::vector<unsigned char> out(1 << 24);
+        uint64_t skip = 4;   // the magic, already written
+        auto drain = [&]() -> int {
+            for (;;) {
+                uint64_t got = 0;
+                const int r = starch_stream_read(c, &out[0], out.size(), &got);
+                if (r || !got) return r;
+                const uint64_t off = skip < got ? skip : got;
+                skip -= off;
+                if (got > off) std::fwrite(&out[off], 1, got - off, _out_stream);
+            }
+        };
+        for (;;) {
+            void* w = NULL;
+            uint64_t cap = 0;
+            if ((rc = starch_stream_window(c, 1 << 24, &w, &cap))) return rc;
+            const size_t k = std::fread(w, 1, cap < (1u << 24) ? (size_t)cap : (size_t)(1u << 24), _in_stream);
+            if (k == 0) break;
+            if ((rc = starch_stream_commit(c, k)) || (rc = drain())) return rc;
+        }
+        if ((rc = starch_stream_end(c)) || (rc = drain())) return rc;
         std::fflush(_out_stream);
         return STARCH_OK;
     }
