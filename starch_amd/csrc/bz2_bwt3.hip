@@ -1399,16 +1399,17 @@ constexpr int sort_wpe(int NW, int E)
 }
 
 template <int NW, int E, bool DBL>
-__global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(sort_wpe(NW, E))))
+__global__ void __launch_bounds__(NW > 4 ? 64 * NW : 256) __attribute__((amdgpu_waves_per_eu(sort_wpe(NW, E))))
 k3_sort_lds(Ctx c, const uint64_t* __restrict__ items,
                                                     const uint32_t* __restrict__ hard_n)
 {
-    constexpr int IPW = 4 / NW;                    // groups per workgroup
+    constexpr int IPW = NW >= 4 ? 1 : 4 / NW;      // groups per workgroup
+    constexpr int NWV = IPW * NW;                  // waves per workgroup
     constexpr int CAP = NW * 64 * E;
     constexpr int IDXB = CAP <= 256 ? 8 : 12;      // packed local index bits
     constexpr int KEYB = 64 - IDXB;
     constexpr uint64_t KMASK = (1ull << KEYB) - 1ull;
-    constexpr int DPT = 256 / (64 * NW);           // digits per thread in the offset scan
+    constexpr int DPT = NW >= 4 ? 1 : 256 / (64 * NW);   // digits per thread in the offset scan (NW > 4: threads 0..255)
     static_assert(CAP <= (1 << IDXB), "index does not fit");
 #ifndef STARCH_M2_DB
 #define STARCH_M2_DB 11
@@ -1437,10 +1438,10 @@ k3_sort_lds(Ctx c, const uint64_t* __restrict__ items,
     constexpr uint32_t LIMIT2 = STARCH_LIM2_NUM / E;   // largest second-level sub-bucket ranked by comparison
     __shared__ uint32_t c2_all[IPW][NB2 + 1];
     __shared__ uint32_t sc2_all[IPW][NW + 1];
-    __shared__ uint64_t red_all[4];
-    __shared__ uint32_t wmax_all[4];
-    __shared__ uint32_t flag_all[4];
-    __shared__ uint32_t tc_all[5];
+    __shared__ uint64_t red_all[NWV];
+    __shared__ uint32_t wmax_all[NWV];
+    __shared__ uint32_t flag_all[NWV];
+    __shared__ uint32_t tc_all[NW + 1 > 5 ? NW + 1 : 5];
     uint32_t tacc = 0;                             // tied elements pushed (flushed at exit)
     const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
     const int g = wave / NW, wid = wave % NW, w0 = g * NW;
@@ -1751,12 +1752,13 @@ k3_sort_lds(Ctx c, const uint64_t* __restrict__ items,
         gsync<NW>();
         {   // digit offsets: base(d) + counts of earlier waves, in place
             const int t = wid * 64 + lane;
+            const bool has = t * DPT < 256;
             uint32_t loc[DPT], sum = 0;
 #pragma unroll
             for (int q = 0; q < DPT; ++q) {
                 uint32_t a = 0;
 #pragma unroll
-                for (int w = 0; w < NW; ++w) a += ur_all[g][w * 256 + t * DPT + q];
+                for (int w = 0; w < NW; ++w) a += has ? ur_all[g][w * 256 + t * DPT + q] : 0u;
                 loc[q] = a;
                 sum += a;
             }
@@ -1768,7 +1770,7 @@ k3_sort_lds(Ctx c, const uint64_t* __restrict__ items,
                 for (int w = 0; w < wid; ++w) run += sc[w];
             }
 #pragma unroll
-            for (int q = 0; q < DPT; ++q) {
+            for (int q = 0; q < DPT && has; ++q) {
                 uint32_t r = run;
 #pragma unroll
                 for (int w = 0; w < NW; ++w) {
@@ -2509,9 +2511,9 @@ bool launch_bwt3(BlockDesc* blocks, uint32_t b0, uint32_t nb, const uint8_t* blk
         auto g8 = [](uint32_t x) { return dim3((x + 7) / 8 * 8); };
         // static assignment needs every workgroup resident at once: one wave of
         // workgroups, sized by the kernel's occupancy
-        auto resident = [&](const void* f) {
+        auto resident = [&](const void* f, int threads = 256) {
             int per_cu = 0;
-            HIP_CHECK(hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, f, 256, 0));
+            HIP_CHECK(hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, f, threads, 0));
             return g8((uint32_t)ncu * (uint32_t)(per_cu > 0 ? per_cu : 1));
         };
         // M classes: k3_sort_lds (MSD digit(s) + compare, LSD fallback); S: k3_sort_grp,
@@ -2534,8 +2536,15 @@ bool launch_bwt3(BlockDesc* blocks, uint32_t b0, uint32_t nb, const uint8_t* blk
         };
         auto leaf = [&](auto dbl) {
             constexpr bool D = decltype(dbl)::value;
-            static const dim3 gm3 = resident(reinterpret_cast<const void*>(&k3_sort_lds<4, 16, D>));
-            static const dim3 gm2 = resident(reinterpret_cast<const void*>(&k3_sort_lds<4, 8, D>));
+            // M2 / M3: 8 / 16 waves of 4 rotations per lane (the 4-wave, 8 / 16
+            // per lane forms held 168 / 294 VGPRs: 3 / 1 waves per SIMD)
+#ifndef STARCH_M_WIDE
+#define STARCH_M_WIDE 1
+#endif
+            constexpr int M2W = STARCH_M_WIDE ? 8 : 4, M2E = STARCH_M_WIDE ? 4 : 8;
+            constexpr int M3W = STARCH_M_WIDE ? 16 : 4, M3E = STARCH_M_WIDE ? 4 : 16;
+            static const dim3 gm3 = resident(reinterpret_cast<const void*>(&k3_sort_lds<M3W, M3E, D>), 64 * M3W);
+            static const dim3 gm2 = resident(reinterpret_cast<const void*>(&k3_sort_lds<M2W, M2E, D>), 64 * M2W);
             static const dim3 gm1 = resident(reinterpret_cast<const void*>(&k3_sort_lds<4, 4, D>));
             static const dim3 gm0 = resident(reinterpret_cast<const void*>(&k3_sort_lds<4, 2, D>));
             static const dim3 gs = resident(reinterpret_cast<const void*>(&k3_sort_grp<1, 2, D>));
@@ -2543,12 +2552,12 @@ bool launch_bwt3(BlockDesc* blocks, uint32_t b0, uint32_t nb, const uint8_t* blk
             static const dim3 gw = resident(reinterpret_cast<const void*>(&k3_sort_w<D>));
             if (n3) {
                 bin(c.L.m3, n3, bout);
-                hipLaunchKernelGGL((k3_sort_lds<4, 16, D>), gm3, dim3(256), 0, st, c, bout, nullptr);
+                hipLaunchKernelGGL((k3_sort_lds<M3W, M3E, D>), gm3, dim3(64 * M3W), 0, st, c, bout, nullptr);
                 sstat("M3");
             }
             if (n2) {
                 bin(c.L.m2, n2, bout);
-                hipLaunchKernelGGL((k3_sort_lds<4, 8, D>), gm2, dim3(256), 0, st, c, bout, nullptr);
+                hipLaunchKernelGGL((k3_sort_lds<M2W, M2E, D>), gm2, dim3(64 * M2W), 0, st, c, bout, nullptr);
                 sstat("M2");
             }
             if (n0) {
