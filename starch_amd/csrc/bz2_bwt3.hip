@@ -1393,9 +1393,18 @@ __device__ __forceinline__ void grp_finish_keys(GrpIn<E>& x)
 #ifndef STARCH_WPE_S
 #define STARCH_WPE_S STARCH_WPE_GRP   // the S class (one wave, E = 2)
 #endif
+#ifndef STARCH_WPE_M1
+#define STARCH_WPE_M1 1
+#endif
+#ifndef STARCH_WPE_M0
+#define STARCH_WPE_M0 6   // M0 (257..512): 6 waves per SIMD (cfg2 sort -0.5 ms, cfg4 -3 ms; profiles/r03_v5/sweep_*_m0w6.json)
+#endif
 constexpr int sort_wpe(int NW, int E)
 {
-    return NW == 4 && E == 8 ? STARCH_WPE_M2 : (NW == 1 ? (E == 2 ? STARCH_WPE_S : STARCH_WPE_GRP) : 1);
+    return NW == 4 && E == 8   ? STARCH_WPE_M2
+           : NW == 4 && E == 4 ? STARCH_WPE_M1
+           : NW == 4 && E == 2 ? STARCH_WPE_M0
+           : (NW == 1 ? (E == 2 ? STARCH_WPE_S : STARCH_WPE_GRP) : 1);
 }
 
 template <int NW, int E, bool DBL>
