@@ -2501,8 +2501,11 @@ bool launch_bwt3(BlockDesc* blocks, uint32_t b0, uint32_t nb, const uint8_t* blk
             bin(c.L.l[lsel], nl, bout);
             c.lsel = lsel ^ 1u;
             HIP_CHECK(hipMemsetAsync(c.L.ctr + C_L0 + (lsel ^ 1u), 0, sizeof(uint32_t), st));
-            if (c.keysrc) hipLaunchKernelGGL(k3_part_l<true>, dim3(ncu * 2), dim3(LT), 0, st, c, bout);
-            else hipLaunchKernelGGL(k3_part_l<false>, dim3(ncu * 2), dim3(LT), 0, st, c, bout);
+#ifndef STARCH_PL_WG
+#define STARCH_PL_WG 2   // k3_part_l workgroups per CU
+#endif
+            if (c.keysrc) hipLaunchKernelGGL(k3_part_l<true>, dim3(ncu * STARCH_PL_WG), dim3(LT), 0, st, c, bout);
+            else hipLaunchKernelGGL(k3_part_l<false>, dim3(ncu * STARCH_PL_WG), dim3(LT), 0, st, c, bout);
             HIP_CHECK(hipGetLastError());
             HIP_CHECK(hipMemsetAsync(c.L.ctr + C_L0 + lsel, 0, sizeof(uint32_t), st));
             lsel ^= 1u;
@@ -2596,11 +2599,17 @@ bool launch_bwt3(BlockDesc* blocks, uint32_t b0, uint32_t nb, const uint8_t* blk
             }
             if (ns2) {
                 bin(c.L.s2, ns2, bout);
+#ifdef STARCH_S2_LDS   // experiment: S2 groups by four waves of one rotation per lane
+                static const dim3 gs2l = resident(reinterpret_cast<const void*>(&k3_sort_lds<4, 1, D>));
+                hipLaunchKernelGGL((k3_sort_lds<4, 1, D>), gs2l, dim3(256), 0, st, c, bout, nullptr);
+                sstat("S2");
+#else
                 clear_h();
                 hipLaunchKernelGGL((k3_sort_grp<1, 4, D>), gs2, dim3(256), 0, st, c, bout, c.L.s2);
                 sstat("S2");
                 hipLaunchKernelGGL((k3_sort_lds<1, 4, D>), dim3(ncu / 2), dim3(256), 0, st, c, c.L.s2, hard_n);
                 sstat("S2-hard");
+#endif
             }
             if (nw) {
                 bin(c.L.w, nw, bout);
