@@ -491,6 +491,80 @@ __global__ void __launch_bounds__(BT) k_fb_init(const uint8_t* __restrict__ blk,
     for (int c = tid; c < 256; c += BT) if (sm.hist[c]) head[sm.base[c]] = 1;
 }
 
+// The same 1-byte bucket sort over the whole GPU (the one-workgroup radix
+// sort above took most of a period-2 block's time): per-tile byte counts, one
+// scan, then per tile one wave places its bytes in order -- a byte's rank
+// among its equals from the tile's offset, the 8-ballot peer set of its
+// 64-byte step and the step's running counters -- at bucket end - 1 - rank
+// (indices descending inside a bucket, bz:blocksort.c:240-249).
+constexpr uint32_t FB_TILE = 4096;
+
+__global__ void __launch_bounds__(256) k_fb_cnt(const uint8_t* __restrict__ blk, uint32_t n, uint32_t* __restrict__ cnt)
+{
+    __shared__ uint32_t h[256];
+    h[threadIdx.x] = 0;
+    __syncthreads();
+    const uint32_t a = blockIdx.x * FB_TILE, e = a + FB_TILE < n ? a + FB_TILE : n;
+    for (uint32_t i = a + threadIdx.x; i < e; i += 256) atomicAdd(&h[blk[i]], 1u);
+    __syncthreads();
+    cnt[(uint64_t)blockIdx.x * 256 + threadIdx.x] = h[threadIdx.x];
+}
+
+// one workgroup of 256: bucket starts and totals, per-tile offsets in place
+__global__ void __launch_bounds__(256) k_fb_cscan(uint32_t* __restrict__ cnt, uint32_t ntile, uint32_t* __restrict__ bstart,
+                                                   uint32_t* __restrict__ btot, uint32_t* __restrict__ head, uint32_t n)
+{
+    __shared__ uint32_t sh[256 / 64 + 1];
+    const uint32_t c = threadIdx.x;
+    uint32_t t = 0;
+    for (uint32_t k = 0; k < ntile; ++k) {
+        uint32_t& x = cnt[(uint64_t)k * 256 + c];
+        const uint32_t v = x;
+        x = t;
+        t += v;
+    }
+    uint32_t tot = 0;
+    const uint32_t st = block_excl_scan_add<uint32_t>(t, sh, &tot);
+    bstart[c] = st;
+    btot[c] = t;
+    if (t && st < n) head[st] = 1;
+}
+
+__global__ void __launch_bounds__(64) k_fb_place(const uint8_t* __restrict__ blk, uint32_t n,
+                                                  const uint32_t* __restrict__ cnt, const uint32_t* __restrict__ bstart,
+                                                  const uint32_t* __restrict__ btot, uint32_t* __restrict__ fmap)
+{
+    __shared__ uint32_t run[256];
+    const int lane = threadIdx.x;
+    for (int c = lane; c < 256; c += 64) run[c] = cnt[(uint64_t)blockIdx.x * 256 + c];
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_ACQ_REL, "workgroup");
+    const uint64_t lt = lanemask_lt();
+    const uint32_t a = blockIdx.x * FB_TILE, e = a + FB_TILE < n ? a + FB_TILE : n;
+    for (uint32_t i0 = a; i0 < e; i0 += 64) {
+        const uint32_t i = i0 + lane;
+        const bool ok = i < e;
+        const uint32_t c = ok ? blk[i] : 0u;
+        uint64_t peers = __ballot(ok);
+#pragma unroll
+        for (int bb = 0; bb < 8; ++bb) {
+            const uint64_t bal = __ballot((c >> bb) & 1u);
+            peers &= ((c >> bb) & 1u) ? bal : ~bal;
+        }
+        const uint32_t below = (uint32_t)__popcll(peers & lt);
+        const uint32_t base = ok ? run[c] : 0u;     // all peers read the same counter
+        __builtin_amdgcn_wave_barrier();
+        __builtin_amdgcn_fence(__ATOMIC_ACQ_REL, "workgroup");
+        if (ok && below == 0) run[c] = base + (uint32_t)__popcll(peers);   // the first peer advances it
+        __builtin_amdgcn_wave_barrier();
+        __builtin_amdgcn_fence(__ATOMIC_ACQ_REL, "workgroup");
+        if (ok) {
+            const uint32_t r = base + below;             // rank among the bucket's bytes, ascending index
+            fmap[bstart[c] + btot[c] - 1u - r] = i;
+        }
+    }
+}
+
 __global__ void k_fb_hp(const uint32_t* __restrict__ head, uint64_t* __restrict__ hp, uint32_t n)
 {
     const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
@@ -641,7 +715,17 @@ void launch_fallback(BlockDesc* blocks, uint32_t b0, const uint32_t* which_host,
         uint64_t* hp = scr.K + so;
         uint64_t* list = scr.K2 + so;
         uint32_t* ctr = scr.V2 + so;                      // [0] not done, [1] mixed buckets, [2] next bucket
-        hipLaunchKernelGGL(k_fb_init, dim3(1), dim3(BT), 0, st, blkbytes + (uint64_t)b * stride, n, scr, so);
+        {   // 1-byte bucket sort and the first heads, over the whole GPU
+            const uint8_t* blk = blkbytes + (uint64_t)b * stride;
+            const uint32_t ntile = (n + FB_TILE - 1) / FB_TILE;
+            uint32_t* cnt = reinterpret_cast<uint32_t*>(scr.K2 + so);             // ntile x 256 (free until the rounds)
+            uint32_t* bst = ecls;                                                  // bucket starts / totals in RK
+            HIP_CHECK(hipMemsetAsync(head, 0, (uint64_t)n * sizeof(uint32_t), st));
+            hipLaunchKernelGGL(k_fb_cnt, dim3(ntile), dim3(256), 0, st, blk, n, cnt);
+            hipLaunchKernelGGL(k_fb_cscan, dim3(1), dim3(256), 0, st, cnt, ntile, bst, bst + 256, head, n);
+            hipLaunchKernelGGL(k_fb_place, dim3(ntile), dim3(64), 0, st, blk, n, cnt, bst, bst + 256, fmap);
+            HIP_CHECK(hipGetLastError());
+        }
         HIP_CHECK(hipMemsetAsync(mixed, 0, (uint64_t)n * sizeof(uint32_t), st));
         const dim3 g((n + 255) / 256), g1((n + 256) / 256);
         uint32_t stamp = 0;
