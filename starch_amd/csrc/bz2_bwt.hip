@@ -16,6 +16,7 @@
 // fallbackSort's tie order, so k_fallback_exact re-runs a restatement of
 // fallbackSort (bz:blocksort.c:30-329) for that block only, with the
 // all-equal-key buckets (whose 3-way partition is the identity) skipped.
+#include <string.h>
 #include "bz2_int.hpp"
 #include "bz2_bwt.hpp"
 
@@ -614,10 +615,163 @@ __global__ void k_fb_list(const uint32_t* __restrict__ head, const uint64_t* __r
     list[atomicAdd(ctr, 1u)] = ((uint64_t)l << 32) | (i - 1);
 }
 
+// One fallbackQSort3 partition step (fbp_partition, same pivot `med`) on a
+// range too large for the wave's LDS, computed by the whole wave as a
+// permutation instead of lane 0's serial scan.  The serial loop decomposes:
+// * the left scan stops at the k-th '>' (g_k), the right scan at the k-th '<'
+//   from the right (l_k), and the two swap while g_k < l_k; the scans meet at
+//   p = the first non-'=' position with (# non-'=' before it) >= n('<'); the
+//   left scan owns [lo, p), the right [p, hi], every '>' left of p is paired;
+// * in the left part the '=' keys collect at lo in arrival order and the
+//   '<' run [ltLo, unLo) behaves as a queue on the positions themselves: cell
+//   c receives the arriving '<' (own or paired element), or, for a '=' of rank
+//   h (h '=' before it), the element cell h received -- chains resolved by
+//   pointer jumping; the right part is the mirror image;
+// * the two vswaps are a fixed block exchange.
+// Scratch: A (list of '<' then '>' offsets, then the gather indices) and B
+// (the pointer array, then a staging copy), m words each, indexed by offset.
+constexpr uint32_t FB_RES = 0x80000000u;
+
+__device__ __forceinline__ void fbw_sync()
+{
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+}
+
+__device__ bool fbw_partition(uint32_t* __restrict__ key, uint32_t* __restrict__ fm, int32_t lo, int32_t hi, uint32_t med,
+                              uint32_t* __restrict__ A, uint32_t* __restrict__ B, int32_t& alo, int32_t& ahi, int32_t& blo,
+                              int32_t& bhi)
+{
+    const uint32_t lane = threadIdx.x & 63;
+    const uint64_t lt = lanemask_lt();
+    const uint32_t m = (uint32_t)(hi - lo + 1);
+    uint32_t* kk = key + lo;
+    uint32_t* ff = fm + lo;
+    uint32_t cl = 0, cg = 0;
+    for (uint32_t j = lane; j < m; j += 64) {
+        const uint32_t k = kk[j];
+        cl += k < med;
+        cg += k > med;
+    }
+    const uint32_t nL = wave_reduce_add<uint32_t>(cl), nG = wave_reduce_add<uint32_t>(cg), nE = m - nL - nG;
+    if (nL + nG == 0) return false;                      // every key equals the pivot: nothing moves
+    // lists of '<' and '>' offsets; the meeting point p
+    uint32_t rL = 0, rG = 0, p = m, lbp = nL, gbp = nG;
+    for (uint32_t j0 = 0; j0 < m; j0 += 64) {
+        const uint32_t j = j0 + lane;
+        const bool ok = j < m;
+        const uint32_t k = ok ? kk[j] : med;
+        const bool isL = k < med, isG = k > med;
+        const uint64_t bL = __ballot(isL), bG = __ballot(isG);
+        const uint32_t lb = rL + (uint32_t)__popcll(bL & lt), gb = rG + (uint32_t)__popcll(bG & lt);
+        if (isL) A[lb] = j;
+        if (isG) A[nL + gb] = j;
+        if (p == m) {
+            const uint64_t hit = __ballot((isL || isG) && lb + gb >= nL);
+            if (hit) {
+                const int h = __ffsll((unsigned long long)hit) - 1;
+                p = j0 + (uint32_t)h;
+                lbp = (uint32_t)__shfl((int)lb, h, 64);
+                gbp = (uint32_t)__shfl((int)gb, h, 64);
+            }
+        }
+        rL += (uint32_t)__popcll(bL);
+        rG += (uint32_t)__popcll(bG);
+    }
+    const uint32_t nEL = p - lbp - gbp, nER = nE - nEL;
+    fbw_sync();
+    // the pointer array: resolved cells carry FB_RES | source offset
+    rL = rG = 0;
+    uint32_t rE = 0;
+    for (uint32_t j0 = 0; j0 < m; j0 += 64) {
+        const uint32_t j = j0 + lane;
+        const bool ok = j < m;
+        const uint32_t k = ok ? kk[j] : 0u;
+        const bool isL = ok && k < med, isG = ok && k > med, isE = ok && k == med;
+        const uint64_t bL = __ballot(isL), bG = __ballot(isG), bE = __ballot(isE);
+        const uint32_t lb = rL + (uint32_t)__popcll(bL & lt), gb = rG + (uint32_t)__popcll(bG & lt),
+                       eb = rE + (uint32_t)__popcll(bE & lt);
+        if (ok) {
+            uint32_t v;
+            if (j < p) {
+                if (isE) v = eb == j ? FB_RES : eb;                  // eb == j: no '<' queued yet, stays put
+                else if (isL) v = FB_RES | j;
+                else v = FB_RES | A[nL - 1 - gb];                   // paired with the (gb+1)-th '<' from the right
+            } else {
+                const uint32_t ea = nE - eb - 1;                    // '=' after it (for a '=')
+                if (isE) v = ea == m - 1 - j ? FB_RES : m - 1 - ea;
+                else if (isG) v = FB_RES | j;
+                else v = FB_RES | A[2 * nL - lb - 1];               // paired with the (nL-lb)-th '>' from the left
+            }
+            B[j] = v;
+        }
+        rL += (uint32_t)__popcll(bL);
+        rG += (uint32_t)__popcll(bG);
+        rE += (uint32_t)__popcll(bE);
+    }
+    for (;;) {                                                       // pointer jumping (chains only go down)
+        fbw_sync();
+        bool un = false;
+        for (uint32_t j = lane; j < m; j += 64) {
+            const uint32_t v = B[j];
+            if (!(v & FB_RES)) {
+                const uint32_t w = B[v];
+                B[j] = w;
+                un |= !(w & FB_RES);
+            }
+        }
+        if (!__any(un)) break;
+    }
+    fbw_sync();
+    // gather indices after the vswaps (bz:blocksort.c:166-167)
+    const uint32_t n1 = nEL < p - nEL ? nEL : p - nEL;
+    const uint32_t ul = m - p, m1 = nER < ul - nER ? nER : ul - nER;
+    auto phi = [&](uint32_t q) -> uint32_t {
+        if (q < n1) return q + (p - n1);
+        if (q < p && q >= p - n1) return q - (p - n1);
+        if (q >= p && q < p + m1) return q + (m - m1 - p);
+        if (q >= m - m1) return q - (m - m1 - p);
+        return q;
+    };
+    rE = 0;
+    for (uint32_t j0 = 0; j0 < m; j0 += 64) {
+        const uint32_t j = j0 + lane;
+        const bool ok = j < m;
+        const bool isE = ok && kk[j] == med;
+        const uint64_t bE = __ballot(isE);
+        const uint32_t eb = rE + (uint32_t)__popcll(bE & lt);
+        if (ok) {
+            if (j < p) {
+                if (isE) A[phi(eb)] = j;
+                if (j >= nEL) A[phi(j)] = B[j] & ~FB_RES;
+            } else {
+                if (isE) A[phi(m - 1 - (nE - eb - 1))] = j;
+                if (m - 1 - j >= nER) A[phi(j)] = B[j] & ~FB_RES;
+            }
+        }
+        rE += (uint32_t)__popcll(bE);
+    }
+    fbw_sync();
+    for (uint32_t j = lane; j < m; j += 64) B[j] = kk[A[j]];
+    fbw_sync();
+    for (uint32_t j = lane; j < m; j += 64) kk[j] = B[j];
+    fbw_sync();
+    for (uint32_t j = lane; j < m; j += 64) B[j] = ff[A[j]];
+    fbw_sync();
+    for (uint32_t j = lane; j < m; j += 64) ff[j] = B[j];
+    fbw_sync();
+    const int32_t nn = lo + (int32_t)nL - 1, mm = hi - (int32_t)nG + 1;
+    if (nn - lo > hi - mm) { alo = lo; ahi = nn; blo = mm; bhi = hi; }   // larger pushed first
+    else { alo = mm; ahi = hi; blo = lo; bhi = nn; }
+    return true;
+}
+
 // fallbackQSort3 on every listed bucket: one wave per bucket (persistent)
 __global__ void __launch_bounds__(64 * FB_WAVES) k_fb_sort(uint32_t* __restrict__ fmap, uint32_t* __restrict__ key,
                                                            const uint64_t* __restrict__ list,
-                                                           const uint32_t* __restrict__ nlist, uint32_t* __restrict__ next)
+                                                           const uint32_t* __restrict__ nlist, uint32_t* __restrict__ next,
+                                                           uint32_t* __restrict__ sa, uint32_t* __restrict__ sb, int wave_part)
 {
     __shared__ uint32_t sk_all[FB_WAVES][FB_CAP], sf_all[FB_WAVES][FB_CAP];
     __shared__ int32_t cmd_all[FB_WAVES][4];
@@ -646,16 +800,33 @@ __global__ void __launch_bounds__(64 * FB_WAVES) k_fb_sort(uint32_t* __restrict_
                     const int32_t lo = slo[sp], hi = shi[sp];
                     if (hi - lo < 10) { fbp_simple(key, fmap, lo, hi); continue; }
                     if ((uint32_t)(hi - lo + 1) <= FB_CAP) { cmd[0] = 1; cmd[1] = lo; cmd[2] = hi; break; }
+                    if (wave_part) {     // a large range: the wave partitions it (fbw_partition)
+                        lcg = (lcg * 7621u + 1u) % 32768u;                   // as fbp_partition
+                        const uint32_t r3 = lcg % 3u;
+                        cmd[0] = 3; cmd[1] = lo; cmd[2] = hi;
+                        cmd[3] = (int32_t)(r3 == 0 ? key[lo] : r3 == 1 ? key[(lo + hi) >> 1] : key[hi]);
+                        break;
+                    }
                     int32_t alo, ahi, blo, bhi;
                     if (!fbp_partition(key, fmap, lo, hi, lcg, alo, ahi, blo, bhi)) continue;
                     slo[sp] = alo; shi[sp] = ahi; ++sp;
                     slo[sp] = blo; shi[sp] = bhi; ++sp;
                 }
             }
-            __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
-            __builtin_amdgcn_wave_barrier();
-            __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+            fbw_sync();
             if (cmd[0] == 0) break;                                // the call is done
+            if (cmd[0] == 3) {
+                const int32_t lo = cmd[1], hi = cmd[2];
+                const uint32_t med = (uint32_t)cmd[3];
+                int32_t alo = 0, ahi = 0, blo = 0, bhi = 0;
+                const bool split = fbw_partition(key, fmap, lo, hi, med, sa + lo, sb + lo, alo, ahi, blo, bhi);
+                if (lane == 0 && split) {
+                    slo[sp] = alo; shi[sp] = ahi; ++sp;
+                    slo[sp] = blo; shi[sp] = bhi; ++sp;
+                }
+                fbw_sync();
+                continue;
+            }
             const int32_t lo = cmd[1], hi = cmd[2], m = hi - lo + 1;
             for (int32_t q = lane; q < m; q += 64) { sk[q] = key[lo + q]; sf[q] = fmap[lo + q]; }
             __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
@@ -728,6 +899,9 @@ void launch_fallback(BlockDesc* blocks, uint32_t b0, const uint32_t* which_host,
         }
         HIP_CHECK(hipMemsetAsync(mixed, 0, (uint64_t)n * sizeof(uint32_t), st));
         const dim3 g((n + 255) / 256), g1((n + 256) / 256);
+        // scratch of the wave partitions: ecls (consumed by k_fb_key, rewritten by the
+        // next round's k_fb_eclass) and the list's second half (<= n/2 buckets listed)
+        static const bool wave_part = [] { const char* e = getenv("STARCH_FB_WAVE"); return !(e && !strcmp(e, "0")); }();
         uint32_t stamp = 0;
         for (uint64_t H = 1;; H *= 2) {
             ++stamp;
@@ -743,7 +917,8 @@ void launch_fallback(BlockDesc* blocks, uint32_t b0, const uint32_t* which_host,
             const uint32_t not_done = hctr[0], nmixed = hctr[1];
             if (nmixed) {
                 const uint32_t wg = std::min<uint32_t>((nmixed + FB_WAVES - 1) / FB_WAVES, (uint32_t)ncu);
-                hipLaunchKernelGGL(k_fb_sort, dim3(wg), dim3(64 * FB_WAVES), 0, st, fmap, key, list, ctr + 1, ctr + 2);
+                hipLaunchKernelGGL(k_fb_sort, dim3(wg), dim3(64 * FB_WAVES), 0, st, fmap, key, list, ctr + 1, ctr + 2,
+                                   ecls, reinterpret_cast<uint32_t*>(list) + n, wave_part ? 1 : 0);
                 hipLaunchKernelGGL(k_fb_heads, g, dim3(256), 0, st, key, hp, mixed, head, n, stamp);
                 HIP_CHECK(hipGetLastError());
             }

@@ -2373,6 +2373,47 @@ __global__ void k3_finish(Ctx c, uint32_t nb, unsigned long long* stats)
     if (slot == 0) atomicAdd(stats + 2, (unsigned long long)c.L.ctr[C_TIE_ELEMS]);
 }
 
+// Periodic blocks up front: a cyclic block has equal rotations iff its minimal
+// period divides n and is < n, iff block[i] == block[i + n/q] (i < n - n/q)
+// for a prime q of n.  Flagged blocks take no doubling round (k3_gather drops
+// their groups); the flag is the one the rounds would reach.  One workgroup per
+// block, 4 KiB steps, so a non-periodic block stops after its first step.
+__global__ void __launch_bounds__(256) k3_period(Ctx c)
+{
+    __shared__ uint32_t q_sh[16];
+    __shared__ uint32_t nq_sh;
+    const uint32_t slot = blockIdx.x, b = c.b0 + slot;
+    const uint32_t n = c.blocks[b].n;
+    if (n < 2) return;
+    if (threadIdx.x == 0) {
+        uint32_t m = n, k = 0;
+        for (uint32_t d = 2; d * d <= m; ++d)
+            if (m % d == 0) {
+                q_sh[k++] = d;
+                while (m % d == 0) m /= d;
+            }
+        if (m > 1) q_sh[k++] = m;
+        nq_sh = k;
+    }
+    __syncthreads();
+    const uint8_t* blk = c.blkbytes + (uint64_t)b * c.stride;
+    const uint32_t nq = nq_sh;
+    for (uint32_t j = 0; j < nq; ++j) {
+        const uint32_t p = n / q_sh[j], e = n - p;
+        int bad = 0;
+        for (uint32_t a = 0; a < e && !bad; a += 4096) {
+            const uint32_t z = a + 4096 < e ? a + 4096 : e;
+            int mis = 0;
+            for (uint32_t i = a + threadIdx.x; i < z; i += 256) mis |= blk[i] != blk[i + p];
+            bad = __syncthreads_or(mis);
+        }
+        if (!bad) {
+            if (threadIdx.x == 0) c.L.periodic[slot] = 1;
+            return;
+        }
+    }
+}
+
 }  // namespace
 
 // Host orchestration.  A handful of host round trips per batch (list sizes).
@@ -2445,6 +2486,8 @@ bool launch_bwt3(BlockDesc* blocks, uint32_t b0, uint32_t nb, const uint8_t* blk
     c.qseg = nullptr;
     c.nbins = wide ? PNB_WIDE : PNB;
     HIP_CHECK(hipMemsetAsync(mw, 0, (2 * C_N + 14ull * nb + QSETS * QSET) * sizeof(uint32_t), st));
+    static const bool period_off = [] { const char* e = getenv("STARCH_PERIOD_CHECK"); return e && !strcmp(e, "0"); }();
+    if (!period_off) hipLaunchKernelGGL(k3_period, dim3(nb), dim3(256), 0, st, c);
 
     uint32_t qnext = 0;
     auto next_q = [&](uint32_t*& head, uint32_t*& seg) {
