@@ -1127,6 +1127,23 @@ __device__ __forceinline__ uint64_t shfl64(uint64_t v, uint32_t src)
     return ((uint64_t)hi << 32) | lo;
 }
 
+// arr[slot] += v over the wave's active lanes, one atomic per distinct slot
+// (per-group atomics on one block's counter serialise: a block of 450k tied
+// pairs spent ~5 ms per doubling round in them).  Wave-uniform call.
+__device__ __forceinline__ void wave_add_slot(uint32_t* arr, bool act, uint32_t slot, uint32_t v)
+{
+    const uint32_t lane = threadIdx.x & 63;
+    uint64_t pend = __ballot(act);
+    while (pend) {
+        const int l = __ffsll((unsigned long long)pend) - 1;
+        const uint32_t s0 = (uint32_t)__shfl((int)slot, l, 64);
+        const bool mine = act && slot == s0;
+        const uint32_t tot = wave_reduce_add<uint32_t>(mine ? v : 0u);
+        if (lane == (uint32_t)l && tot) atomicAdd(&arr[s0], tot);
+        pend &= ~__ballot(mine);
+    }
+}
+
 template <bool DBL>
 __global__ void __launch_bounds__(256) k3_sort_w(Ctx c, const uint64_t* __restrict__ items)
 {
@@ -1199,7 +1216,7 @@ __global__ void __launch_bounds__(256) k3_sort_w(Ctx c, const uint64_t* __restri
             if (c.mode) {                                // runs per group, by its first lane
                 const uint64_t em = __ballot(end);
                 const uint64_t gm = (m >= 64 ? ~0ull : ((1ull << m) - 1ull)) << gstart;
-                if (valid && j == 0) atomicAdd(&c.L.runs[slot], (uint32_t)__popcll(em & gm));
+                wave_add_slot(c.L.runs, valid && j == 0, slot, (uint32_t)__popcll(em & gm));
             }
             done += ng;
         }
@@ -2316,7 +2333,7 @@ __global__ void __launch_bounds__(256) k3_gather(Ctx c, const uint64_t* __restri
     }
     __shared__ uint32_t cls_sh[16];
     wg_classify(c, cls_sh, active, slot, s, m, RBITS, 0);
-    if (active) atomicAdd(&c.L.gin[slot], 1u);
+    wave_add_slot(c.L.gin, active, slot, 1u);
     const uint32_t tied = wave_reduce_add<uint32_t>(active ? m : 0u);
     if (lane == 0 && tied) atomicAdd(&c.L.ctr[C_TIE_ELEMS], tied);
 }

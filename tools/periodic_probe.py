@@ -26,6 +26,7 @@ CASES = {
     "p5_text": lambda: periodic(b"p1\n0\n"),
     "p997": lambda: periodic(rand_unit(1, 997, b"0123456789\n-p")),
     "p_half": lambda: periodic(rand_unit(3, N // 2, b"ACGTN")),
+    "p_third": lambda: periodic(rand_unit(4, N // 3, b"ab")),
 }
 
 names = sys.argv[1].split(",") if len(sys.argv) > 1 else list(CASES)
@@ -39,5 +40,8 @@ for nm in names:
         t0 = time.perf_counter()
         c.bz2_compress(d, 9)
         ts.append((time.perf_counter() - t0) * 1e3)
-    print("%s: %s ms" % (nm, " ".join("%.1f" % t for t in ts)), flush=True)
+    st = c.stats()
+    print("%s: %s ms  (blocks %s, periodic %s, rounds %s, tied %s, rle %s)" % (
+        nm, " ".join("%.1f" % t for t in ts), st.get("n_blocks"), st.get("periodic_blocks"), st.get("bwt_rounds"),
+        st.get("bwt_tied"), st.get("rle_bytes")), flush=True)
 c.close()
