@@ -120,7 +120,9 @@ int starch_encode_device(starch_ctx* ctx, const void* d_bed, uint64_t n, const s
 /* Same, from host memory (copied to HBM first; the copy is not in ms_total). */
 int starch_encode_host(starch_ctx* ctx, const void* bed, uint64_t n, const starch_options* opt);
 /* Host bytes in, archive bytes out into the caller's host buffer out[0, cap)
- * (*out_len = its size; STARCH_ERR_MEM if cap is short).  For large pinned
+ * (*out_len = its size; STARCH_ERR_MEM if cap is short, with *out_len = the
+ * size needed and out's contents undefined -- finished batches may already
+ * have been written into it).  For large pinned
  * inputs every chromosome batch's finished streams go device-to-host while
  * later batches still cross PCIe / encode, so the archive's PCIe trip
  * overlaps the work (pinned out recommended).  Same bytes as
@@ -183,6 +185,10 @@ int starch_comm_create(int device, int rank, int world, const void* id, starch_c
  * the others connect to host:port, retrying for up to 10 minutes) */
 int starch_comm_create_tcp(int device, int rank, int world, const char* host, int port, starch_comm** out);
 void starch_comm_destroy(starch_comm* comm);
+/* Path of the librccl the gather uses (loaded on first use; "" when RCCL is
+ * unavailable).  In a process that already loaded torch-ROCm's RCCL this is
+ * that library: both resolve SONAME librccl.so.1 to one object. */
+const char* starch_rccl_library(void);
 const char* starch_comm_last_error(void);   /* detail of the last failed starch_comm_* / starch_gather_host */
 int starch_gather_archive(starch_ctx* ctx, starch_comm* comm, const starch_options* opt);
 

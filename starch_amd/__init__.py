@@ -177,6 +177,7 @@ def load():
         "starch_comm_create_tcp": ([ctypes.c_int, ctypes.c_int, ctypes.c_int, ctypes.c_char_p, ctypes.c_int,
                                     ctypes.POINTER(vp)], ctypes.c_int),
         "starch_comm_destroy": ([vp], None),
+        "starch_rccl_library": ([], ctypes.c_char_p),
         "starch_comm_last_error": ([], ctypes.c_char_p),
         "starch_gather_archive": ([vp, vp, ctypes.POINTER(Options)], ctypes.c_int),
         "starch_gather_host": ([ctypes.POINTER(HostComm), ctypes.POINTER(Segment), ctypes.POINTER(ctypes.c_char_p),
@@ -615,6 +616,11 @@ class Comm:
             raise StarchError(rc, L.starch_comm_last_error().decode(errors="replace"))
         self._h, self._L, self.rank, self.world = h, L, rank, world
         return self
+
+    @staticmethod
+    def rccl_library() -> str:
+        """Path of the librccl the gather runs on (dladdr of its symbols)."""
+        return (load().starch_rccl_library() or b"").decode(errors="replace")
 
     def close(self):
         if getattr(self, "_h", None):

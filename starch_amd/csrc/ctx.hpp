@@ -159,6 +159,14 @@ struct starch_ctx {
     std::vector<std::string> names;
     starch_stats stats{};
     bool streamed = false;            // the last result went out through starch_stream_read
+    bool gathered = false;            // rank 0 after starch_gather_archive: segs are archive-order records
+    hipEvent_t tev[3] = {nullptr, nullptr, nullptr};   // encode timers (created once, reused)
+    hipEvent_t* timers()
+    {
+        for (auto& e : tev)
+            if (!e && hipEventCreate(&e) != hipSuccess) { e = nullptr; throw StarchError(STARCH_ERR_DEVICE, "hipEventCreate"); }
+        return tev;
+    }
     struct Streaming {                // starch_stream_* session
         bool active = false, eof = false;
         starch_options opt{};
@@ -244,6 +252,8 @@ struct starch_ctx {
         for (int i = 0; i < 2; ++i)
             if (sm.buf[i]) (void)hipHostFree(sm.buf[i]);
         if (sm.job_ev) (void)hipEventDestroy(sm.job_ev);
+        for (auto& e : tev)
+            if (e) (void)hipEventDestroy(e);
     }
 };
 

@@ -53,6 +53,7 @@ namespace {
 struct Rccl {
     bool tried = false, ok = false;
     std::string why;
+    std::string path;   // the file the symbols came from (dladdr)
     ncclResult_t (*GetUniqueId)(ncclUniqueId*) = nullptr;
     ncclResult_t (*CommInitRank)(ncclComm_t*, int, ncclUniqueId, int) = nullptr;
     ncclResult_t (*CommDestroy)(ncclComm_t) = nullptr;
@@ -100,6 +101,10 @@ const Rccl& rccl()
     sym(r.GetErrorString, "ncclGetErrorString");
     r.ok = all;
     if (!all) throw StarchError(STARCH_ERR_DEVICE, "RCCL unavailable:" + r.why);
+    // which librccl answered: a process that already holds torch-ROCm's RCCL
+    // (SONAME librccl.so.1) gets that same object back from dlopen
+    Dl_info di{};
+    if (dladdr(reinterpret_cast<void*>(r.GetUniqueId), &di) && di.dli_fname) r.path = di.dli_fname;
     return r;
 }
 
@@ -521,6 +526,15 @@ int starch_comm_create_tcp(int device, int rank, int world, const char* host, in
     }
 }
 
+const char* starch_rccl_library(void)
+{
+    try {
+        return rccl().path.c_str();
+    } catch (const std::exception&) {
+        return "";
+    }
+}
+
 void starch_comm_destroy(starch_comm* m)
 {
     if (!m) return;
@@ -537,7 +551,8 @@ int starch_gather_archive(starch_ctx* c, starch_comm* m, const starch_options* o
 {
     if (!c || !m) return STARCH_ERR_ARG;
     if (m->device != c->device) return STARCH_ERR_ARG;
-    if (!c->have || c->streamed) return STARCH_ERR_STATE;
+    // a second gather would read archive offsets as offsets into the shard streams
+    if (!c->have || c->streamed || c->gathered) return STARCH_ERR_STATE;
     starch_options o;
     starch_options_init(&o);
     if (opt) o = *opt;
@@ -550,6 +565,7 @@ int starch_gather_archive(starch_ctx* c, starch_comm* m, const starch_options* o
             c->segs.swap(r.segs);
             c->names.swap(r.names);
             c->archive_bytes = r.bytes;
+            c->gathered = true;
         } else {
             c->archive_bytes = 0;   // rank 0 holds the archive; this rank keeps its own segments
         }

@@ -318,13 +318,12 @@ enum Layout { L_ARCHIVE, L_STREAMS };
 void encode_units(starch_ctx* c, const uint8_t* d_base, const std::vector<UnitIn>& units, const starch_options& opt,
                   Layout lay, bool planned = false)
 {
-    hipEvent_t e0, e1, e2;
-    HIP_CHECK(hipEventCreate(&e0));
-    HIP_CHECK(hipEventCreate(&e1));
-    HIP_CHECK(hipEventCreate(&e2));
+    hipEvent_t* tv = c->timers();   // owned by the context: nothing to release on a throw
+    hipEvent_t e0 = tv[0], e1 = tv[1], e2 = tv[2];
     HIP_CHECK(hipEventRecord(e0, c->st));
     c->have = false;
     c->streamed = false;
+    c->gathered = false;
     c->stats = starch_stats{};
     for (auto& u : units) c->stats.input_bytes += u.len;
     std::vector<SegInfo> si;
@@ -370,9 +369,6 @@ void encode_units(starch_ctx* c, const uint8_t* d_base, const std::vector<UnitIn
         finish_names(c, pnames);
         c->archive_bytes = 4;
         c->have = true;
-        (void)hipEventDestroy(e0);
-        (void)hipEventDestroy(e1);
-        (void)hipEventDestroy(e2);
         return;
     }
     std::vector<bz::StreamIn> sin(nseg);
@@ -425,9 +421,6 @@ void encode_units(starch_ctx* c, const uint8_t* d_base, const std::vector<UnitIn
     float ms_t = 0, ms_all = 0;
     HIP_CHECK(hipEventElapsedTime(&ms_t, e0, e1));
     HIP_CHECK(hipEventElapsedTime(&ms_all, e0, e2));
-    (void)hipEventDestroy(e0);
-    (void)hipEventDestroy(e1);
-    (void)hipEventDestroy(e2);
     if (lay == L_ARCHIVE) c->archive_bytes = total;
     else c->part_bytes = total;
     c->stats.archive_bytes = total;
@@ -739,6 +732,7 @@ bool encode_host_pipelined(starch_ctx* c, const uint8_t* bed, uint64_t n, const 
     if (hout) {   // every batch went out already (all lanes finished); magic and index from the host
         if (hout->overflow || hout->off != end || end + idx.size() > hout_cap) {
             HIP_CHECK(hipStreamSynchronize(c->st));
+            *hout_len = end + idx.size();   // the size needed; the buffer's contents are undefined
             throw StarchError(STARCH_ERR_MEM, "output buffer too small");
         }
         memcpy(hout_p, kMagic, 4);
@@ -956,10 +950,8 @@ void stream_encode_pieces(starch_ctx* c, const uint8_t* d, uint64_t n, int64_t i
 {
     auto& m = c->sm;
     auto& os = m.os;
-    hipEvent_t e0, e1, e2;
-    HIP_CHECK(hipEventCreate(&e0));
-    HIP_CHECK(hipEventCreate(&e1));
-    HIP_CHECK(hipEventCreate(&e2));
+    hipEvent_t* tv = c->timers();   // owned by the context: nothing to release on a throw
+    hipEvent_t e0 = tv[0], e1 = tv[1], e2 = tv[2];
     HIP_CHECK(hipEventRecord(e0, c->st));
     c->stats = starch_stats{};
     c->stats.input_bytes = n - ctx;
@@ -1045,9 +1037,6 @@ void stream_encode_pieces(starch_ctx* c, const uint8_t* d, uint64_t n, int64_t i
     float ms_t = 0, ms_all = 0;
     HIP_CHECK(hipEventElapsedTime(&ms_t, e0, e1));
     HIP_CHECK(hipEventElapsedTime(&ms_all, e0, e2));
-    (void)hipEventDestroy(e0);
-    (void)hipEventDestroy(e1);
-    (void)hipEventDestroy(e2);
     STRACE("stream batch %llu: %llu bytes in %llu segments (%s%s), device %.3f ms", (unsigned long long)m.batches,
            (unsigned long long)(n - ctx), (unsigned long long)nseg, cont ? "continues a chromosome" : "",
            open ? (cont ? ", open" : "open") : "", ms_all);
@@ -1125,12 +1114,14 @@ void stream_encode(starch_ctx* c, const uint8_t* d, uint64_t n, int64_t is, int6
 {
     auto& m = c->sm;
     if (m.opt.reference_compat) return;   // the reference writes only the magic (hpp:765-769)
+    // the batch's H2D (copy stream) must be done before any kernel on c->st
+    // reads it -- the piece path (context line + open stream) included
+    HIP_CHECK(hipStreamWaitEvent(c->st, m.job_ev, 0));
     if (ctx || open || m.os.active) {
         stream_encode_pieces(c, d, n, is, ip, ctx, open);
         return;
     }
     STRACE("stream batch %llu: %llu bytes, encode", (unsigned long long)m.batches, (unsigned long long)n);
-    HIP_CHECK(hipStreamWaitEvent(c->st, m.job_ev, 0));   // the batch's H2D (copy stream) is done
     std::vector<UnitIn> u(1, UnitIn{0, n, is, ip, 0});
     encode_units(c, d, u, m.opt, L_STREAMS);
     STRACE("stream batch %llu: encoded, device %.3f ms", (unsigned long long)m.batches, c->stats.ms_total);
@@ -1456,7 +1447,7 @@ int starch_encode_host_into(starch_ctx* c, const void* bed, uint64_t n, const st
     if (n) HIP_CHECK(hipMemcpyAsync(d, bed, n, hipMemcpyHostToDevice, c->st));
     HIP_CHECK(hipStreamSynchronize(c->st));
     encode_device(c, d, n, o);
-    if (cap < c->archive_bytes) return STARCH_ERR_MEM;
+    if (cap < c->archive_bytes) { *out_len = c->archive_bytes; return STARCH_ERR_MEM; }
     if (c->archive_bytes) HIP_CHECK(hipMemcpyAsync(out, c->archive.p, c->archive_bytes, hipMemcpyDeviceToHost, c->st));
     HIP_CHECK(hipStreamSynchronize(c->st));
     *out_len = c->archive_bytes;
@@ -1513,7 +1504,7 @@ int starch_encode_units_host(starch_ctx* c, const void* bed, const starch_unit* 
 int starch_streams_device(starch_ctx* c, const void** d_ptr, uint64_t* n)
 {
     if (!c || !d_ptr || !n) return STARCH_ERR_ARG;
-    if (!c->have) return STARCH_ERR_STATE;
+    if (!c->have || c->gathered) return STARCH_ERR_STATE;
     *d_ptr = c->part.p;
     *n = c->part_bytes;
     return STARCH_OK;
@@ -1522,7 +1513,7 @@ int starch_streams_device(starch_ctx* c, const void** d_ptr, uint64_t* n)
 int starch_streams_copy(starch_ctx* c, void* dst, uint64_t cap)
 {
     GUARD(c)
-    if (!c->have) return STARCH_ERR_STATE;
+    if (!c->have || c->gathered) return STARCH_ERR_STATE;
     if (cap < c->part_bytes || (c->part_bytes && !dst)) return STARCH_ERR_MEM;
     if (c->part_bytes) HIP_CHECK(hipMemcpyAsync(dst, c->part.p, c->part_bytes, hipMemcpyDeviceToHost, c->st));
     HIP_CHECK(hipStreamSynchronize(c->st));
@@ -1690,8 +1681,6 @@ static void transform_only(starch_ctx* c, const uint8_t* d, uint64_t n)
     finish_names(c, pnames);
     float ms = 0;
     HIP_CHECK(hipEventElapsedTime(&ms, e0, e1));
-    (void)hipEventDestroy(e0);
-    (void)hipEventDestroy(e1);
     c->stats = starch_stats{};
     c->stats.input_bytes = n;
     c->stats.n_lines = tr.n_lines;

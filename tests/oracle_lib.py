@@ -158,3 +158,31 @@ def untransform(text: bytes, chromosome: bytes):
     if n == ctypes.c_size_t(-1).value:
         return None
     return out.raw[:n]
+
+
+POOL_SO = os.path.join(ROOT, "oracle", "_build", "libcpu_pool.so")
+_pool = None
+
+
+def cpu_pool(buf, spans, threads, level=9, use_ref=True):
+    """CPU baseline (oracle/cpu_pool.c): transform + bzip2 of every (offset,
+    length) piece of `buf` (bytes, or an int host address) on a C pthread
+    pool, largest piece first, the reference libbz2 when built ->
+    (seconds, [seconds per piece], [bz2 bytes per piece], codec kind)."""
+    global _pool
+    if _pool is None:
+        if not os.path.exists(POOL_SO):
+            subprocess.check_call(["make", "-s", "-C", os.path.join(ROOT, "oracle"), POOL_SO])
+        _pool = ctypes.CDLL(POOL_SO)
+        _pool.cpu_pool_run.restype = ctypes.c_int
+    n = len(spans)
+    offs = (ctypes.c_uint64 * max(1, n))(*[o for o, _ in spans])
+    lens = (ctypes.c_uint64 * max(1, n))(*[l for _, l in spans])
+    secs = (ctypes.c_double * max(1, n))()
+    outb = (ctypes.c_uint64 * max(1, n))()
+    tot = ctypes.c_double(0)
+    ref_path = REF_SO if (use_ref and os.path.exists(REF_SO)) else ""
+    ptr = ctypes.c_void_p(buf) if isinstance(buf, int) else ctypes.c_char_p(buf)
+    rc = _pool.cpu_pool_run(ptr, offs, lens, n, threads, level, ref_path.encode(), ctypes.byref(tot), secs, outb)
+    assert rc == 0, rc
+    return tot.value, list(secs[:n]), list(outb[:n]), ("reference" if ref_path else "port")

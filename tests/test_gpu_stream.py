@@ -307,3 +307,18 @@ def test_stream_inside_chromosome_hold_knob():
     env = dict(os.environ, STARCH_STREAM_HOLD="1")
     out = subprocess.run([sys.executable, "-c", code], env=env, capture_output=True, timeout=300, check=True).stdout
     assert out == ref
+
+
+def test_stream_large_open_pieces_wait_for_their_copy():
+    """Batches cut inside one large chromosome (the piece path, with a context
+    line) must not be read by the encoder before their H2D copy on the copy
+    stream has landed (starch_api.hip stream_encode waits on the batch's copy
+    event before both paths).  chr1 of cfg2 (~190 MB) in 48 MiB pieces and
+    64 MiB batches: every batch is an open piece whose copy is tens of MB."""
+    import starch_amd
+    data = starch_amd.gen_bed(0, 100_000_000, chroms=[0])
+    ref = _one_call(data)
+    for piece, batch in ((48 << 20, 64 << 20), (96 << 20, 32 << 20)):
+        got, st = _streamed(data, piece, batch)
+        assert got == ref, (piece, batch)
+        assert st["n_segments"] == 1
