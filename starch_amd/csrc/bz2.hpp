@@ -62,6 +62,19 @@ struct Stats {                 // per-stage device timings (ms) from HIP events
     uint64_t dedup_blocks = 0;     // blocks that reused a byte-identical block's results
 };
 
+// Every periodic block of a batch replays at once: one HIP stream per block
+// (from the pool, round-robin), each block's round issued on its stream, one
+// host read-back per round for all of them.
+struct FbPool {
+    static constexpr int kStreams = 8;
+    hipStream_t st[kStreams] = {};
+    hipEvent_t ev[kStreams + 1] = {};
+    DevBuf tmp[kStreams];          // scan scratch per stream
+    PinnedBuf ctr;                 // per block: not-done, mixed-bucket count
+    int dev = -1;
+    void init(int device);
+    ~FbPool();
+};
 class Encoder {
 public:
     // Compress `streams` whose bytes live in d_text (device).  The result is
@@ -82,6 +95,15 @@ public:
     // last bsW call in its bit buffer when a block ends (bz:compress.c:37-52),
     // which decides how many bytes a BZ_FLUSH makes readable.  0: no blocks.
     uint32_t last_write_bits(uint32_t g, const StreamOut& so, hipStream_t st);
+    // Per-block results of the last plan() + emit(), in block order: text
+    // range (plan's d_text offsets), absolute bit offset and length in the
+    // emitted buffer, block CRC, and the bit length of its last code (its
+    // EOB: what libbz2's bit buffer keeps when the block ends).  One read-back.
+    struct BlockOut {
+        uint64_t in_beg, in_end, bit_off, bits;
+        uint32_t crc, last_bits;
+    };
+    void block_results(std::vector<BlockOut>& out, hipStream_t st);
     // plan() and emit() record their stage timings as event pairs without
     // waiting on them; once the stream has synchronised, this adds them to
     // *stats (null: drops them).  plan() drops any left from an earlier call.
@@ -97,8 +119,9 @@ public:
 private:
     DevBuf b_streams, b_tiles, b_tile_sum, b_tile_carry, b_tile_w, b_tile_wpre, b_tpos, b_seg_tile0, b_seg_nblk,
         b_blk_tmp, b_blk, b_blkbytes, b_scal, b_tmp, b_bwt, b_mtfv, b_freq, b_sel, b_tabs, b_gbits, b_souts,
-        b_fallback, b_bwt3, b_crc, b_dedupe, b_rep_bytes, b_rep_blk;
-    PinnedBuf h_wtot_, h_nblk_, h_blocks_, h_hr_;   // read-back targets (pinned)
+        b_fallback, b_bwt3, b_crc, b_dedupe, b_rep_bytes, b_rep_blk, b_last;
+    PinnedBuf h_wtot_, h_nblk_, h_blocks_, h_hr_, h_last_;
+    FbPool fb_pool_;                        // periodic blocks' concurrent replays   // read-back targets (pinned)
     struct PinnedCtr {
         uint32_t* p = nullptr;
         uint32_t* get();

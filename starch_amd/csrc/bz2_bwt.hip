@@ -866,66 +866,134 @@ void launch_bwt(BlockDesc* blocks, uint32_t b0, uint32_t nb, const uint8_t* blkb
     HIP_CHECK(hipGetLastError());
 }
 
+void FbPool::init(int device)
+{
+    if (dev == device) return;
+    if (dev >= 0) throw StarchError(-10, "FbPool: device changed");
+    for (int i = 0; i < kStreams; ++i) HIP_CHECK(hipStreamCreateWithFlags(&st[i], hipStreamNonBlocking));
+    for (int i = 0; i <= kStreams; ++i) HIP_CHECK(hipEventCreateWithFlags(&ev[i], hipEventDisableTiming));
+    dev = device;
+}
+
+FbPool::~FbPool()
+{
+    for (int i = 0; i < kStreams; ++i)
+        if (st[i]) { (void)hipStreamSynchronize(st[i]); (void)hipStreamDestroy(st[i]); }
+    for (int i = 0; i <= kStreams; ++i)
+        if (ev[i]) (void)hipEventDestroy(ev[i]);
+}
+
 void launch_fallback(BlockDesc* blocks, uint32_t b0, const uint32_t* which_host, const uint32_t* n_host,
-                     uint32_t nwhich, const uint8_t* blkbytes, uint64_t stride, const BwtScratch& scr, DevBuf& tmp,
-                     uint32_t* hctr, hipStream_t st)
+                     uint32_t nwhich, const uint8_t* blkbytes, uint64_t stride, const BwtScratch& scr, FbPool& pool,
+                     hipStream_t st)
 {
     int dev = 0, ncu = 256;
     HIP_CHECK(hipGetDevice(&dev));
     hipDeviceProp_t prop;
     if (hipGetDeviceProperties(&prop, dev) == hipSuccess && prop.multiProcessorCount > 0) ncu = prop.multiProcessorCount;
+    pool.init(dev);
+    static const bool wave_part = [] { const char* e = getenv("STARCH_FB_WAVE"); return !(e && !strcmp(e, "0")); }();
+    struct Blk {
+        uint32_t slot, b, n;
+        uint64_t so;
+        hipStream_t s;
+        DevBuf* tmp;
+        uint64_t H;
+        uint32_t stamp;
+        bool active;
+    };
+    std::vector<Blk> bl;
     for (uint32_t q = 0; q < nwhich; ++q) {
-        const uint32_t slot = which_host[q], b = b0 + slot, n = n_host[q];
-        if (n == 0) continue;
-        const uint64_t so = (uint64_t)slot * scr.stride;
-        uint32_t* fmap = scr.SA + so;
-        uint32_t* ecls = scr.RK + so;
-        uint32_t* key = scr.V + so;
-        uint32_t* head = scr.U + so;
-        uint32_t* mixed = scr.U2 + so;
-        uint64_t* hp = scr.K + so;
-        uint64_t* list = scr.K2 + so;
-        uint32_t* ctr = scr.V2 + so;                      // [0] not done, [1] mixed buckets, [2] next bucket
-        {   // 1-byte bucket sort and the first heads, over the whole GPU
-            const uint8_t* blk = blkbytes + (uint64_t)b * stride;
-            const uint32_t ntile = (n + FB_TILE - 1) / FB_TILE;
-            uint32_t* cnt = reinterpret_cast<uint32_t*>(scr.K2 + so);             // ntile x 256 (free until the rounds)
-            uint32_t* bst = ecls;                                                  // bucket starts / totals in RK
-            HIP_CHECK(hipMemsetAsync(head, 0, (uint64_t)n * sizeof(uint32_t), st));
-            hipLaunchKernelGGL(k_fb_cnt, dim3(ntile), dim3(256), 0, st, blk, n, cnt);
-            hipLaunchKernelGGL(k_fb_cscan, dim3(1), dim3(256), 0, st, cnt, ntile, bst, bst + 256, head, n);
-            hipLaunchKernelGGL(k_fb_place, dim3(ntile), dim3(64), 0, st, blk, n, cnt, bst, bst + 256, fmap);
+        if (n_host[q] == 0) continue;
+        const int k = (int)(bl.size() % FbPool::kStreams);
+        bl.push_back(Blk{which_host[q], b0 + which_host[q], n_host[q], (uint64_t)which_host[q] * scr.stride,
+                         pool.st[k], &pool.tmp[k], 1, 0, true});
+    }
+    if (bl.empty()) return;
+    const int nst = (int)std::min<size_t>(bl.size(), FbPool::kStreams);
+    // the sort's results on st come first
+    HIP_CHECK(hipEventRecord(pool.ev[FbPool::kStreams], st));
+    for (int k = 0; k < nst; ++k) HIP_CHECK(hipStreamWaitEvent(pool.st[k], pool.ev[FbPool::kStreams], 0));
+    uint32_t* hc = static_cast<uint32_t*>(pool.ctr.get(bl.size() * 2 * sizeof(uint32_t) + 64));
+    for (auto& x : bl) {   // 1-byte bucket sort and the first heads, over the whole GPU
+        const uint32_t n = x.n;
+        uint32_t* fmap = scr.SA + x.so;
+        uint32_t* ecls = scr.RK + x.so;
+        uint32_t* head = scr.U + x.so;
+        uint32_t* mixed = scr.U2 + x.so;
+        const uint8_t* blk = blkbytes + (uint64_t)x.b * stride;
+        const uint32_t ntile = (n + FB_TILE - 1) / FB_TILE;
+        uint32_t* cnt = reinterpret_cast<uint32_t*>(scr.K2 + x.so);             // ntile x 256 (free until the rounds)
+        uint32_t* bst = ecls;                                                     // bucket starts / totals in RK
+        HIP_CHECK(hipMemsetAsync(head, 0, (uint64_t)n * sizeof(uint32_t), x.s));
+        hipLaunchKernelGGL(k_fb_cnt, dim3(ntile), dim3(256), 0, x.s, blk, n, cnt);
+        hipLaunchKernelGGL(k_fb_cscan, dim3(1), dim3(256), 0, x.s, cnt, ntile, bst, bst + 256, head, n);
+        hipLaunchKernelGGL(k_fb_place, dim3(ntile), dim3(64), 0, x.s, blk, n, cnt, bst, bst + 256, fmap);
+        HIP_CHECK(hipMemsetAsync(mixed, 0, (uint64_t)n * sizeof(uint32_t), x.s));
+        HIP_CHECK(hipGetLastError());
+    }
+    // rounds H = 1, 2, 4, ... (bz:blocksort.c:252-327): every active block's
+    // round is issued on its stream, then one wait for all of them
+    for (;;) {
+        bool any = false;
+        for (size_t q = 0; q < bl.size(); ++q) {
+            Blk& x = bl[q];
+            if (!x.active) continue;
+            any = true;
+            const uint32_t n = x.n;
+            uint32_t* fmap = scr.SA + x.so;
+            uint32_t* ecls = scr.RK + x.so;
+            uint32_t* key = scr.V + x.so;
+            uint32_t* head = scr.U + x.so;
+            uint32_t* mixed = scr.U2 + x.so;
+            uint64_t* hp = scr.K + x.so;
+            uint64_t* list = scr.K2 + x.so;
+            uint32_t* ctr = scr.V2 + x.so;                      // [0] not done, [1] mixed buckets, [2] next bucket
+            const dim3 g((n + 255) / 256), g1((n + 256) / 256);
+            ++x.stamp;
+            HIP_CHECK(hipMemsetAsync(ctr, 0, 4 * sizeof(uint32_t), x.s));
+            hipLaunchKernelGGL(k_fb_hp, g, dim3(256), 0, x.s, head, hp, n);
+            scan::incl_max_u64(hp, n, *x.tmp, x.s);
+            hipLaunchKernelGGL(k_fb_eclass, g, dim3(256), 0, x.s, fmap, hp, ecls, n, (uint32_t)(x.H % n));
+            hipLaunchKernelGGL(k_fb_key, g, dim3(256), 0, x.s, fmap, ecls, head, hp, key, mixed, ctr, n, x.stamp);
+            hipLaunchKernelGGL(k_fb_list, g1, dim3(256), 0, x.s, head, hp, mixed, list, ctr + 1, n, x.stamp);
             HIP_CHECK(hipGetLastError());
+            HIP_CHECK(hipMemcpyAsync(hc + 2 * q, ctr, 2 * sizeof(uint32_t), hipMemcpyDeviceToHost, x.s));
         }
-        HIP_CHECK(hipMemsetAsync(mixed, 0, (uint64_t)n * sizeof(uint32_t), st));
-        const dim3 g((n + 255) / 256), g1((n + 256) / 256);
-        // scratch of the wave partitions: ecls (consumed by k_fb_key, rewritten by the
-        // next round's k_fb_eclass) and the list's second half (<= n/2 buckets listed)
-        static const bool wave_part = [] { const char* e = getenv("STARCH_FB_WAVE"); return !(e && !strcmp(e, "0")); }();
-        uint32_t stamp = 0;
-        for (uint64_t H = 1;; H *= 2) {
-            ++stamp;
-            HIP_CHECK(hipMemsetAsync(ctr, 0, 4 * sizeof(uint32_t), st));
-            hipLaunchKernelGGL(k_fb_hp, g, dim3(256), 0, st, head, hp, n);
-            scan::incl_max_u64(hp, n, tmp, st);
-            hipLaunchKernelGGL(k_fb_eclass, g, dim3(256), 0, st, fmap, hp, ecls, n, (uint32_t)(H % n));
-            hipLaunchKernelGGL(k_fb_key, g, dim3(256), 0, st, fmap, ecls, head, hp, key, mixed, ctr, n, stamp);
-            hipLaunchKernelGGL(k_fb_list, g1, dim3(256), 0, st, head, hp, mixed, list, ctr + 1, n, stamp);
-            HIP_CHECK(hipGetLastError());
-            HIP_CHECK(hipMemcpyAsync(hctr, ctr, 2 * sizeof(uint32_t), hipMemcpyDeviceToHost, st));
-            HIP_CHECK(hipStreamSynchronize(st));
-            const uint32_t not_done = hctr[0], nmixed = hctr[1];
+        if (!any) break;
+        for (int k = 0; k < nst; ++k) HIP_CHECK(hipStreamSynchronize(pool.st[k]));
+        for (size_t q = 0; q < bl.size(); ++q) {
+            Blk& x = bl[q];
+            if (!x.active) continue;
+            const uint32_t n = x.n, not_done = hc[2 * q], nmixed = hc[2 * q + 1];
+            uint32_t* fmap = scr.SA + x.so;
+            uint32_t* ecls = scr.RK + x.so;
+            uint32_t* key = scr.V + x.so;
+            uint32_t* head = scr.U + x.so;
+            uint32_t* mixed = scr.U2 + x.so;
+            uint64_t* hp = scr.K + x.so;
+            uint64_t* list = scr.K2 + x.so;
+            uint32_t* ctr = scr.V2 + x.so;
+            const dim3 g((n + 255) / 256);
             if (nmixed) {
                 const uint32_t wg = std::min<uint32_t>((nmixed + FB_WAVES - 1) / FB_WAVES, (uint32_t)ncu);
-                hipLaunchKernelGGL(k_fb_sort, dim3(wg), dim3(64 * FB_WAVES), 0, st, fmap, key, list, ctr + 1, ctr + 2,
+                hipLaunchKernelGGL(k_fb_sort, dim3(wg), dim3(64 * FB_WAVES), 0, x.s, fmap, key, list, ctr + 1, ctr + 2,
                                    ecls, reinterpret_cast<uint32_t*>(list) + n, wave_part ? 1 : 0);
-                hipLaunchKernelGGL(k_fb_heads, g, dim3(256), 0, st, key, hp, mixed, head, n, stamp);
+                hipLaunchKernelGGL(k_fb_heads, g, dim3(256), 0, x.s, key, hp, mixed, head, n, x.stamp);
                 HIP_CHECK(hipGetLastError());
             }
-            if (2 * H > n || not_done == 0) break;         // H *= 2; if (H > nblock || nNotDone == 0) break
+            if (2 * x.H > n || not_done == 0) {                 // H *= 2; if (H > nblock || nNotDone == 0) break
+                hipLaunchKernelGGL(k_fb_origptr, g, dim3(256), 0, x.s, fmap, blocks, x.b, n);
+                HIP_CHECK(hipGetLastError());
+                x.active = false;
+            }
+            x.H *= 2;
         }
-        hipLaunchKernelGGL(k_fb_origptr, g, dim3(256), 0, st, fmap, blocks, b, n);
-        HIP_CHECK(hipGetLastError());
+    }
+    // st continues after every block's replay
+    for (int k = 0; k < nst; ++k) {
+        HIP_CHECK(hipEventRecord(pool.ev[k], pool.st[k]));
+        HIP_CHECK(hipStreamWaitEvent(st, pool.ev[k], 0));
     }
 }
 

@@ -37,8 +37,8 @@ bool launch_bwt3(BlockDesc* blocks, uint32_t b0, uint32_t nb, const uint8_t* blk
 // round by round on the GPU; which_host / n_host: batch slots and block sizes;
 // hctr: pinned host memory (>= 2 u32)
 void launch_fallback(BlockDesc* blocks, uint32_t b0, const uint32_t* which_host, const uint32_t* n_host,
-                     uint32_t nwhich, const uint8_t* blkbytes, uint64_t stride, const BwtScratch& scr, DevBuf& tmp,
-                     uint32_t* hctr, hipStream_t st);
+                     uint32_t nwhich, const uint8_t* blkbytes, uint64_t stride, const BwtScratch& scr, FbPool& pool,
+                     hipStream_t st);
 // last column for blocks whose SA was produced elsewhere (fallback / LSD path)
 void launch_last_col(const BlockDesc* blocks, uint32_t b0, const uint32_t* which, uint32_t nwhich,
                      const uint8_t* blkbytes, uint64_t stride, const BwtScratch& scr, hipStream_t st);

@@ -81,12 +81,15 @@ constexpr uint32_t W_MAX = 64, S1_MAX = 128, S_MAX = 256, M0_MAX = 512, M1_MAX =
 #define STARCH_L_MIN 4096
 #endif
 constexpr uint32_t L_MIN = STARCH_L_MIN;
+constexpr uint32_t GB_MIN = 16384;      // doubling: tie groups above this are gathered by the whole grid
+constexpr uint32_t GB_MAXN = 4096;
+constexpr uint32_t HG_MIN_PUSH = 32768;  // (= HG_MIN) L groups above it are partitioned by the whole grid
 constexpr uint32_t RBITS = 20;          // rank bits (n <= 899,985 < 2^20)
 constexpr uint32_t TEXT_ROUNDS = 4;     // max text-extension rounds before doubling
 
 // counters (u32) in the meta buffer
 enum { C_W = 0, C_S, C_S2, C_M1, C_M2, C_M3, C_L0, C_L1, C_T0, C_T1, C_TIE_ELEMS, C_ERR, C_TS0, C_TS1, C_H, C_DBG2,
-       C_DBGL, C_M0, C_STG, C_STA, C_STW, C_STE, C_STLP, C_STH, C_N = 24 };
+       C_DBGL, C_M0, C_STG, C_STA, C_STW, C_STE, C_STLP, C_STH, C_HG, C_HGC, C_GB, C_LM0, C_LM1, C_N = 30 };
 
 // item = slot[63:52] | start[51:32] | size[31:12] | parity[7] | shift[6:0]
 __device__ __forceinline__ uint64_t mk_item(uint32_t slot, uint32_t s, uint32_t m, uint32_t shift, uint32_t par)
@@ -140,6 +143,12 @@ struct Lists {
     uint32_t* periodic;     // per slot
     uint32_t* rounds;       // per slot: doubling rounds with work
     uint32_t* tied;         // per slot: still tied when doubling starts
+    uint64_t* hg;           // huge groups of the current partition level (k3_hg_*), HG_MAXN
+    uint32_t* hg_base;      // ... their first chunk row
+    uint32_t* hg_hist;      // [HG_MAXCH][256] chunk digit counts -> chunk write cursors
+    uint32_t* hg_info;      // [HG_MAXN][256] bin start | final flags
+    uint64_t* gb;           // doubling: tie groups gathered by the whole grid (k3_gather_big), GB_MAXN
+    uint32_t* gb_h;         // ... their key offset h mod n
 };
 
 struct Ctx {
@@ -248,6 +257,7 @@ __device__ __forceinline__ void wg_classify(const Ctx& c, uint32_t* sh, bool pre
     if (threadIdx.x < 8 && sh[threadIdx.x]) sh[8 + threadIdx.x] = atomicAdd(class_ctr(c, (int)threadIdx.x), sh[threadIdx.x]);
     __syncthreads();
     if (cls >= 0) class_list(c, cls)[sh[8 + cls] + loff] = mk_item(slot, s, m, shift, par);
+    if (cls == 6 && m > HG_MIN_PUSH) atomicMax(&c.L.ctr[C_LM0 + c.lsel], m);   // the host launches k3_hg_* only then
     __syncthreads();
 }
 
@@ -933,6 +943,7 @@ __global__ void __launch_bounds__(LT) k3_part_l(Ctx c, const uint64_t* __restric
         const uint64_t item = items[c.qseg[job >> 28] + (job & 0x0FFFFFFFu)];
         const uint32_t slot = it_slot(item), s = it_start(item), m = it_size(item), shift = it_shift(item),
                        par = it_par(item);
+        if (m == 0) continue;                          // taken by the grid-wide path (k3_hg_pick); uniform
         const uint32_t b = c.b0 + slot;
         const uint64_t so = (uint64_t)slot * c.scr.stride;
         const uint64_t base = so + s;
@@ -1039,6 +1050,228 @@ __global__ void __launch_bounds__(LT) k3_part_l(Ctx c, const uint64_t* __restric
             }
         }
         __syncthreads();
+    }
+}
+
+// ---------------------------------------------------------------------------
+// Huge groups (> HG_MIN rotations): k3_part_l's MSD partition step spread over
+// the whole grid.  One k3_part_l workgroup per group left a group of
+// hundreds of thousands of tied rotations -- every doubling round of a
+// near-periodic block (per-position BED: "0\n" repeated, broken once) -- to
+// one CU for the whole round.  Here a group is cut into HG_CH-element chunks:
+// per-chunk digit histograms (k3_hg_hist), one workgroup per group scans them
+// into per-chunk cursors and classifies the sub-buckets exactly as k3_part_l
+// does (k3_hg_scan), every chunk scatters its elements (k3_hg_scatter), and
+// sub-buckets that are final (singletons, or all-equal keys with no key bits
+// left) are written out by k3_hg_final -- after the scatter, so no chunk's
+// source reads race the final SA writes.
+// ---------------------------------------------------------------------------
+constexpr uint32_t HG_MIN = HG_MIN_PUSH;
+constexpr uint32_t HG_CH = 8192;
+constexpr uint32_t HG_MAXCH = 16384;
+constexpr uint32_t HG_MAXN = 256;
+constexpr uint32_t HG_FINAL = 1u << 31;
+
+// L-list items above HG_MIN whose chunks fit go to the huge list; their
+// L-list entry gets size 0 (k3_part_l skips it)
+__global__ void k3_hg_pick(Ctx c, uint64_t* __restrict__ list, uint32_t n)
+{
+    const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= n) return;
+    const uint64_t item = list[i];
+    const uint32_t m = it_size(item);
+    if (m <= HG_MIN) return;
+    const uint32_t nch = (m + HG_CH - 1) / HG_CH;
+    const uint32_t k = atomicAdd(&c.L.ctr[C_HG], 1u);
+    if (k >= HG_MAXN) return;
+    const uint32_t base = atomicAdd(&c.L.ctr[C_HGC], nch);
+    if (base + nch > HG_MAXCH) {            // no hist rows left: k3_part_l keeps it
+        c.L.hg[k] = 0;
+        return;
+    }
+    c.L.hg[k] = item;
+    c.L.hg_base[k] = base;
+    list[i] = mk_item(it_slot(item), it_start(item), 0, it_shift(item), it_par(item));
+}
+
+struct HgGroup {
+    uint32_t slot, s, m, shift, par, db, sh2, nch;
+    uint64_t dmask;
+};
+__device__ __forceinline__ HgGroup hg_group(uint64_t item)
+{
+    HgGroup g;
+    g.slot = it_slot(item);
+    g.s = it_start(item);
+    g.m = it_size(item);
+    g.shift = it_shift(item);
+    g.par = it_par(item);
+    g.db = g.shift < 8 ? g.shift : 8;
+    g.sh2 = g.shift - g.db;
+    g.dmask = (1ull << g.db) - 1ull;
+    g.nch = (g.m + HG_CH - 1) / HG_CH;
+    return g;
+}
+
+// count[d] += 1 for a wave's lanes (one LDS atomic when they share a digit:
+// a skewed group sends most elements to one bin)
+__device__ __forceinline__ uint32_t wave_bin_add(uint32_t* cnt, bool act, uint32_t d)
+{
+    const uint64_t a = __ballot(act);
+    if (!a) return 0;
+    const int lead = __ffsll((unsigned long long)a) - 1;
+    const uint32_t d0 = (uint32_t)__shfl((int)d, lead, 64);
+    const int lane = threadIdx.x & 63;
+    if (__ballot(act && d == d0) == a) {
+        uint32_t b = 0;
+        if (lane == lead) b = atomicAdd(&cnt[d0], (uint32_t)__popcll(a));
+        b = (uint32_t)__shfl((int)b, lead, 64);
+        return b + (uint32_t)__popcll(a & lanemask_lt());
+    }
+    return act ? atomicAdd(&cnt[d], 1u) : 0u;
+}
+
+template <bool DBL>
+__global__ void __launch_bounds__(256) k3_hg_hist(Ctx c)
+{
+    __shared__ uint32_t h[256];
+    const uint32_t tid = threadIdx.x;
+    const uint32_t nh = min(c.L.ctr[C_HG], HG_MAXN);
+    for (uint32_t q = 0; q < nh; ++q) {
+        const uint64_t item = c.L.hg[q];
+        if (it_size(item) == 0) continue;
+        const HgGroup g = hg_group(item);
+        const KeySrc ks = key_src(c, g.slot, g.par);
+        const uint32_t* sv = (g.par ? c.scr.V : c.scr.SA) + (uint64_t)g.slot * c.scr.stride + g.s;
+        uint32_t* rows = c.L.hg_hist + (uint64_t)c.L.hg_base[q] * 256;
+        for (uint32_t ch = blockIdx.x; ch < g.nch; ch += gridDim.x) {
+            h[tid] = 0;
+            __syncthreads();
+            const uint32_t a = ch * HG_CH, e = min(g.m, a + HG_CH);
+            for (uint32_t i0 = a; i0 < e; i0 += 256) {   // uniform trip count
+                const uint32_t i = i0 + tid;
+                const bool ok = i < e;
+                const uint32_t ic = ok ? i : a;
+                const uint32_t d = (uint32_t)((elem_key<DBL>(ks, g.s + ic, sv[ic]) >> g.sh2) & g.dmask);
+                (void)wave_bin_add(h, ok, d);
+            }
+            __syncthreads();
+            rows[(uint64_t)ch * 256 + tid] = h[tid];
+            __syncthreads();
+        }
+    }
+}
+
+// one workgroup per huge group: bin starts, per-chunk cursors (in place),
+// sub-bucket classes (k3_part_l's rules)
+__global__ void __launch_bounds__(256) k3_hg_scan(Ctx c)
+{
+    __shared__ uint32_t scan_sh[5];
+    __shared__ uint32_t cls_sh[16];
+    const uint32_t q = blockIdx.x, tid = threadIdx.x;
+    if (q >= min(c.L.ctr[C_HG], HG_MAXN)) return;
+    const uint64_t item = c.L.hg[q];
+    if (it_size(item) == 0) return;                   // uniform
+    const HgGroup g = hg_group(item);
+    uint32_t* rows = c.L.hg_hist + (uint64_t)c.L.hg_base[q] * 256;
+    uint32_t cc = 0;
+    for (uint32_t ch = 0; ch < g.nch; ++ch) cc += rows[(uint64_t)ch * 256 + tid];
+    const uint32_t ss = block_excl_scan_add<uint32_t>(cc, scan_sh, (uint32_t*)nullptr);
+    uint32_t run = ss;
+    for (uint32_t ch = 0; ch < g.nch; ++ch) {
+        uint32_t& x = rows[(uint64_t)ch * 256 + tid];
+        const uint32_t t = x;
+        x = run;
+        run += t;
+    }
+    const bool alleq = cc >= 2 && size_class(cc) == 6 && g.sh2 == 0;   // one tie group
+    const bool fin = cc == 1 || alleq;
+    c.L.hg_info[(uint64_t)q * 256 + tid] = ss | (fin ? HG_FINAL : 0u);
+    if (alleq) {
+        const uint32_t o = atomicAdd(c.L.ctr + C_T0 + c.tsel, 1u);
+        c.L.t[c.tsel][o] = mk_item(g.slot, g.s + ss, cc, 0, 0);
+        atomicAdd(c.L.ctr + C_TS0 + c.tsel, cc);
+    }
+    wg_classify(c, cls_sh, cc >= 2 && !alleq, g.slot, g.s + ss, cc, g.sh2, g.par ^ 1u);
+    const uint32_t r = wave_reduce_add<uint32_t>(fin ? 1u : 0u);
+    if (c.mode && (tid & 63) == 0 && r) atomicAdd(&c.L.runs[g.slot], r);
+}
+
+template <bool DBL>
+__global__ void __launch_bounds__(256) k3_hg_scatter(Ctx c)
+{
+    __shared__ uint32_t cur[256];
+    const uint32_t tid = threadIdx.x;
+    const uint32_t nh = min(c.L.ctr[C_HG], HG_MAXN);
+    for (uint32_t q = 0; q < nh; ++q) {
+        const uint64_t item = c.L.hg[q];
+        if (it_size(item) == 0) continue;
+        const HgGroup g = hg_group(item);
+        const KeySrc ks = key_src(c, g.slot, g.par);
+        const uint64_t base = (uint64_t)g.slot * c.scr.stride + g.s;
+        const uint32_t* sv = (g.par ? c.scr.V : c.scr.SA) + base;
+        uint32_t* dv = (g.par ? c.scr.SA : c.scr.V) + base;
+        uint64_t* dk = (g.par ? c.kA : c.kB) + base;
+        uint8_t* dl = DBL && ks.l ? (g.par ? c.lA : c.lB) + base : nullptr;
+        const uint32_t* rows = c.L.hg_hist + (uint64_t)c.L.hg_base[q] * 256;
+        for (uint32_t ch = blockIdx.x; ch < g.nch; ch += gridDim.x) {
+            cur[tid] = rows[(uint64_t)ch * 256 + tid];
+            __syncthreads();
+            const uint32_t a = ch * HG_CH, e = min(g.m, a + HG_CH);
+            for (uint32_t i0 = a; i0 < e; i0 += 256) {
+                const uint32_t i = i0 + tid;
+                const bool ok = i < e;
+                const uint32_t ic = ok ? i : a;
+                const uint32_t v = sv[ic];
+                const uint64_t k = elem_key<DBL>(ks, g.s + ic, v);
+                const uint32_t d = (uint32_t)((k >> g.sh2) & g.dmask);
+                const uint32_t p = wave_bin_add(cur, ok, d);
+                if (ok) {
+                    dv[p] = v;
+                    if constexpr (DBL) dk[p] = k;
+                    if (dl) dl[p] = ks.l[g.s + ic];
+                }
+            }
+            __syncthreads();
+        }
+    }
+}
+
+// final sub-buckets of every huge group: SA, last column, RK, origPtr
+__global__ void __launch_bounds__(256) k3_hg_final(Ctx c)
+{
+    __shared__ uint32_t info[256];
+    const uint32_t tid = threadIdx.x;
+    const uint32_t nh = min(c.L.ctr[C_HG], HG_MAXN);
+    for (uint32_t q = 0; q < nh; ++q) {
+        const uint64_t item = c.L.hg[q];
+        if (it_size(item) == 0) continue;
+        const HgGroup g = hg_group(item);
+        const uint64_t so = (uint64_t)g.slot * c.scr.stride, base = so + g.s;
+        const uint32_t* dv = (g.par ? c.scr.SA : c.scr.V) + base;
+        const KeySrc ks = key_src(c, g.slot, g.par);
+        const uint8_t* dl = ks.l ? (g.par ? c.lA : c.lB) + base : nullptr;
+        __syncthreads();
+        info[tid] = c.L.hg_info[(uint64_t)q * 256 + tid];
+        __syncthreads();
+        for (uint32_t ch = blockIdx.x; ch < g.nch; ch += gridDim.x) {
+            const uint32_t a = ch * HG_CH, e = min(g.m, a + HG_CH);
+            for (uint32_t p = a + tid; p < e; p += 256) {
+                // the bin holding position p: the last start <= p (starts ascend)
+                uint32_t lo = 0, hi = 255;
+                while (lo < hi) {
+                    const uint32_t mid = (lo + hi + 1) >> 1;
+                    if ((info[mid] & ~HG_FINAL) <= p) lo = mid; else hi = mid - 1;
+                }
+                const uint32_t f = info[lo];
+                if (!(f & HG_FINAL)) continue;
+                const uint32_t v = dv[p];
+                if (!g.par) c.scr.SA[base + p] = v;
+                c.scr.LL[base + p] = dl ? dl[p] : last_sym(c, g.slot, v);
+                if (c.mode) c.scr.RK[so + v] = g.s + (f & ~HG_FINAL);
+                if (v == 0) c.blocks[c.b0 + g.slot].orig_ptr = g.s + p;
+            }
+        }
     }
 }
 
@@ -2280,6 +2513,7 @@ __global__ void __launch_bounds__(256) k3_classify_text(Ctx c, const uint64_t* _
             for (int q = 0; q < 8; ++q) if (q == cls) o = off[q]++;
             const Geo g = c.L.geo[slot];
             class_list(c, cls)[cls_base[cls] + o] = mk_item(slot, it_start(it[k]), m, g.Dp * g.B, 0);
+            if (cls == 6 && m > HG_MIN_PUSH) atomicMax(&c.L.ctr[C_LM0 + c.lsel], m);
         }
     }
     tied = wave_reduce_add<uint32_t>(tied);
@@ -2318,7 +2552,26 @@ __global__ void __launch_bounds__(256) k3_gather(Ctx c, const uint64_t* __restri
             c.scr.K2[so + q] = c.scr.RK[so + t];
         }
     }
-    uint64_t bigm = __ballot(active && m > 64);
+    // groups above GB_MIN: gathered by the whole grid (k3_gather_big) -- one
+    // wave walking a group of 450k tied rotations took most of a round
+    bool taken = false;
+    {
+        const bool huge = active && m > GB_MIN;
+        const uint64_t hb = __ballot(huge);
+        if (hb) {
+            const int lead = __ffsll((unsigned long long)hb) - 1;
+            uint32_t b0 = 0;
+            if (lane == lead) b0 = atomicAdd(&c.L.ctr[C_GB], (uint32_t)__popcll(hb));
+            b0 = (uint32_t)__shfl((int)b0, lead, 64);
+            const uint32_t o = b0 + (uint32_t)__popcll(hb & lanemask_lt());
+            taken = huge && o < GB_MAXN;
+            if (taken) {
+                c.L.gb[o] = mk_item(slot, s, m, 0, 0);
+                c.L.gb_h[o] = hm;
+            }
+        }
+    }
+    uint64_t bigm = __ballot(active && m > 64 && !taken);
     while (bigm) {
         const int l = __ffsll((unsigned long long)bigm) - 1;
         bigm &= bigm - 1;
@@ -2336,6 +2589,23 @@ __global__ void __launch_bounds__(256) k3_gather(Ctx c, const uint64_t* __restri
     wave_add_slot(c.L.gin, active, slot, 1u);
     const uint32_t tied = wave_reduce_add<uint32_t>(active ? m : 0u);
     if (lane == 0 && tied) atomicAdd(&c.L.ctr[C_TIE_ELEMS], tied);
+}
+
+__global__ void __launch_bounds__(256) k3_gather_big(Ctx c)
+{
+    const uint32_t ng = min(c.L.ctr[C_GB], GB_MAXN);
+    const uint32_t step = gridDim.x * 256u;
+    for (uint32_t q = 0; q < ng; ++q) {
+        const uint64_t item = c.L.gb[q];
+        const uint32_t slot = it_slot(item), s = it_start(item), m = it_size(item), hm = c.L.gb_h[q];
+        const uint32_t n = c.blocks[c.b0 + slot].n;
+        const uint64_t so = (uint64_t)slot * c.scr.stride;
+        for (uint32_t i = blockIdx.x * 256u + threadIdx.x; i < m; i += step) {
+            uint32_t t = c.scr.SA[so + s + i] + hm;
+            if (t >= n) t -= n;
+            c.scr.K2[so + s + i] = c.scr.RK[so + t];
+        }
+    }
 }
 
 // ---- switch to doubling: dense ranks for the blocks that are still tied ----
@@ -2459,8 +2729,10 @@ bool launch_bwt3(BlockDesc* blocks, uint32_t b0, uint32_t nb, const uint8_t* blk
     const uint64_t nwg_bin = BIN_MAXWG;
     const uint64_t nb_bins = nb < 64 ? 8ull * nb : nb;     // bins of k3_bin_* (see bin_of)
     constexpr uint32_t QSETS = 64, QSET = 8 * XQ_STRIDE + 32;   // queue heads (a line each) + segments per launch
+    const uint64_t hg_words = 2ull * HG_MAXN + HG_MAXN + (uint64_t)HG_MAXCH * 256 + (uint64_t)HG_MAXN * 256 +
+                              3ull * GB_MAXN + 64;
     const uint64_t words = 2 * C_N + 14ull * nb + QSETS * QSET + nwg_bin * nb_bins +
-                           2 * (cap_s + cap_s2 + cap_m0 + cap_m1 + cap_m2 + cap_m3 + 2 * cap_l) + 64;
+                           2 * (cap_s + cap_s2 + cap_m0 + cap_m1 + cap_m2 + cap_m3 + 2 * cap_l) + 64 + hg_words;
     uint32_t* mw = meta.as<uint32_t>(words);
     Ctx c;
     c.blocks = blocks;
@@ -2488,6 +2760,19 @@ bool launch_bwt3(BlockDesc* blocks, uint32_t b0, uint32_t nb, const uint8_t* blk
     c.L.m3 = c.L.m2 + cap_m2;
     c.L.l[0] = c.L.m3 + cap_m3;
     c.L.l[1] = c.L.l[0] + cap_l;
+    {   // huge-group path (k3_hg_*, k3_gather_big): after the class lists
+        uintptr_t q = reinterpret_cast<uintptr_t>(c.L.l[1] + cap_l);
+        q = (q + 7) & ~(uintptr_t)7;
+        c.L.hg = reinterpret_cast<uint64_t*>(q);
+        c.L.gb = c.L.hg + HG_MAXN;
+        c.L.hg_base = reinterpret_cast<uint32_t*>(c.L.gb + GB_MAXN);
+        c.L.gb_h = c.L.hg_base + HG_MAXN;
+        c.L.hg_info = c.L.gb_h + GB_MAXN;
+        c.L.hg_hist = c.L.hg_info + (uint64_t)HG_MAXN * 256;
+        if (reinterpret_cast<uintptr_t>(c.L.hg_hist + (uint64_t)HG_MAXCH * 256) >
+            reinterpret_cast<uintptr_t>(mw + words))
+            throw StarchError(-10, "bwt3: meta layout");
+    }
     c.L.w = reinterpret_cast<uint64_t*>(scr.U);
     c.L.t[0] = reinterpret_cast<uint64_t*>(scr.U2);
     c.L.t[1] = reinterpret_cast<uint64_t*>(scr.V2);
@@ -2558,9 +2843,25 @@ bool launch_bwt3(BlockDesc* blocks, uint32_t b0, uint32_t nb, const uint8_t* blk
             const uint32_t nl = hctr[C_L0 + lsel];
             if (nl == 0) break;
             if (level > 64) throw StarchError(-10, "bwt3: partition did not converge");
+            const bool huge = hctr[C_LM0 + lsel] > HG_MIN;
+            if (huge) {   // groups above HG_MIN: partitioned by the whole grid
+                HIP_CHECK(hipMemsetAsync(c.L.ctr + C_HG, 0, 2 * sizeof(uint32_t), st));
+                hipLaunchKernelGGL(k3_hg_pick, dim3((nl + 255) / 256), dim3(256), 0, st, c, c.L.l[lsel], nl);
+            }
             bin(c.L.l[lsel], nl, bout);
             c.lsel = lsel ^ 1u;
             HIP_CHECK(hipMemsetAsync(c.L.ctr + C_L0 + (lsel ^ 1u), 0, sizeof(uint32_t), st));
+            HIP_CHECK(hipMemsetAsync(c.L.ctr + C_LM0 + (lsel ^ 1u), 0, sizeof(uint32_t), st));
+            if (huge) {
+                const dim3 gh(ncu * 4);
+                if (c.keysrc) hipLaunchKernelGGL(k3_hg_hist<true>, gh, dim3(256), 0, st, c);
+                else hipLaunchKernelGGL(k3_hg_hist<false>, gh, dim3(256), 0, st, c);
+                hipLaunchKernelGGL(k3_hg_scan, dim3(HG_MAXN), dim3(256), 0, st, c);
+                if (c.keysrc) hipLaunchKernelGGL(k3_hg_scatter<true>, gh, dim3(256), 0, st, c);
+                else hipLaunchKernelGGL(k3_hg_scatter<false>, gh, dim3(256), 0, st, c);
+                hipLaunchKernelGGL(k3_hg_final, gh, dim3(256), 0, st, c);
+                HIP_CHECK(hipGetLastError());
+            }
 #ifndef STARCH_PL_WG
 #define STARCH_PL_WG 2   // k3_part_l workgroups per CU
 #endif
@@ -2568,6 +2869,7 @@ bool launch_bwt3(BlockDesc* blocks, uint32_t b0, uint32_t nb, const uint8_t* blk
             else hipLaunchKernelGGL(k3_part_l<false>, dim3(ncu * STARCH_PL_WG), dim3(LT), 0, st, c, bout);
             HIP_CHECK(hipGetLastError());
             HIP_CHECK(hipMemsetAsync(c.L.ctr + C_L0 + lsel, 0, sizeof(uint32_t), st));
+            HIP_CHECK(hipMemsetAsync(c.L.ctr + C_LM0 + lsel, 0, sizeof(uint32_t), st));
             lsel ^= 1u;
         }
         c.lsel = 0;
@@ -2767,7 +3069,9 @@ bool launch_bwt3(BlockDesc* blocks, uint32_t b0, uint32_t nb, const uint8_t* blk
             c.tsel ^= 1u;
             HIP_CHECK(hipMemsetAsync(c.L.ctr + C_T0 + c.tsel, 0, sizeof(uint32_t), st));
             HIP_CHECK(hipMemsetAsync(c.L.ctr + C_TS0 + c.tsel, 0, sizeof(uint32_t), st));
+            HIP_CHECK(hipMemsetAsync(c.L.ctr + C_GB, 0, sizeof(uint32_t), st));
             hipLaunchKernelGGL(k3_gather, dim3((n2 + 255) / 256), dim3(256), 0, st, c, c.L.t[cur], n2, round, rtext);
+            hipLaunchKernelGGL(k3_gather_big, dim3(ncu * 4), dim3(256), 0, st, c);
             HIP_CHECK(hipGetLastError());
             HIP_CHECK(hipMemsetAsync(c.L.ctr + C_T0 + cur, 0, sizeof(uint32_t), st));
             sort_groups();

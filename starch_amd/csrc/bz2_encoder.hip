@@ -359,7 +359,7 @@ void Encoder::plan(const uint8_t* d_text, const std::vector<StreamIn>& streams, 
                 HIP_CHECK(hipMemcpyAsync(d_which, which.data(), which.size() * sizeof(uint32_t),
                                          hipMemcpyHostToDevice, st));
                 launch_fallback(d_bl, b0, which.data(), wn.data(), (uint32_t)which.size(), d_bytes, blk_stride_, scr,
-                                b_tmp, h_ctr_.get(), st);
+                                fb_pool_, st);
                 if (stats) stats->periodic_blocks += which.size();
             }
             // the v3 sort writes the last column next to SA; the v1 sort and the
@@ -475,6 +475,38 @@ uint32_t Encoder::last_write_bits(uint32_t g, const StreamOut& so, hipStream_t s
     HIP_CHECK(hipMemcpyAsync(&len, &tab->len[t][bd.n_in_use + 1], 1, hipMemcpyDeviceToHost, st));   // EOB = nInUse + 1
     HIP_CHECK(hipStreamSynchronize(st));
     return len;
+}
+
+// EOB code length of every block (bz:compress.c:580-593: the last symbol of
+// the last group): its table is the last selector's
+__global__ void k_last_bits(const BlockDesc* __restrict__ blocks, uint32_t nb, const uint8_t* __restrict__ sel,
+                            const Tables* __restrict__ tabs, const uint32_t* __restrict__ src_of,
+                            uint32_t* __restrict__ out)
+{
+    const uint32_t b = blockIdx.x * blockDim.x + threadIdx.x;
+    if (b >= nb) return;
+    const BlockDesc& bd = blocks[b];
+    const uint32_t src = src_of ? src_of[b] : b;
+    const uint32_t t = sel[(uint64_t)src * 2 * kMaxSelectors + (bd.n_sel - 1)];
+    out[b] = tabs[src].len[t][bd.n_in_use + 1];
+}
+
+void Encoder::block_results(std::vector<BlockOut>& out, hipStream_t st)
+{
+    out.assign(nblocks_, BlockOut{});
+    if (!nblocks_) return;
+    uint32_t* d_last = b_last.as<uint32_t>(nblocks_ + 16);
+    hipLaunchKernelGGL(k_last_bits, dim3((nblocks_ + 255) / 256), dim3(256), 0, st, static_cast<BlockDesc*>(b_blk.p),
+                       nblocks_, static_cast<const uint8_t*>(b_sel.p), static_cast<const Tables*>(b_tabs.p),
+                       src_of_dev_, d_last);
+    HIP_CHECK(hipGetLastError());
+    uint32_t* h = static_cast<uint32_t*>(h_last_.get((nblocks_ + 16) * sizeof(uint32_t)));
+    HIP_CHECK(hipMemcpyAsync(h, d_last, nblocks_ * sizeof(uint32_t), hipMemcpyDeviceToHost, st));
+    HIP_CHECK(hipStreamSynchronize(st));
+    for (uint32_t b = 0; b < nblocks_; ++b) {
+        const BlockDesc& bd = host_blocks_[b];
+        out[b] = BlockOut{bd.in_beg, bd.in_end, bd.bit_off, bd.bits, bd.crc, h[b]};
+    }
 }
 
 uint64_t Encoder::plan_and_encode(const uint8_t* d_text, const std::vector<StreamIn>& streams, int bs100k,

@@ -1,23 +1,31 @@
 // starch_amd/csrc/bzlib_abi.hip -- the patched-libbz2 streaming ABI
 // (include/starch_bzlib.h) on top of the GPU encoder.
 //
-// Mirrors the state machine of bz:bzlib.c:148-500 (modes RUNNING / FLUSHING /
-// FINISHING / IDLE, avail_in_expect, return codes, total_in/out counters,
-// block_close_functor at BZ_STREAM_END).  Input is recorded until the caller
-// ends a piece with BZ_FLUSH or BZ_FINISH; the piece is then RLE1-coded,
-// block-cut, sorted and coded on the GPU on its own (flush_RL resets the run
-// state, bz:bzlib.c:393-397; its final single-byte run joins a full block
-// only when the terminating call supplied input), and its blocks' bits are
-// appended to the stream's bit string: at BZ_FLUSH every whole byte so far is
-// output, the last 0..7 bits stay pending (the library's bsBuff/bsLive carry
-// across BZ2_compressBlock, bz:compress.c:609); BZ_FINISH appends the trailer
-// with the combined CRC and pads to a byte (bz:compress.c:657-666).  The
-// bytes and the total_out after every call are those of the patched library
-// for the same call sequence; only BZ_RUN differs in timing (the library emits
-// a block as soon as 900 k are buffered, here at the next FLUSH/FINISH).
+// A step-for-step emulation of libbz2's compression state machine
+// (bz:bzlib.c:148-500): modes RUNNING / FLUSHING / FINISHING / IDLE, the
+// INPUT / OUTPUT states of handle_compress, avail_in_expect, return codes,
+// total_in / total_out, block_close_functor at BZ_STREAM_END.  The input side
+// keeps libbz2's RLE1 bookkeeping (state_in_ch / state_in_len / nblock,
+// ADD_CHAR_TO_BLOCK bz:bzlib.c:269-293) so every block closes where the
+// library closes it: under BZ_RUN as soon as nblockMAX RLE1 bytes are in it
+// (bz:bzlib.c:297-338, 399-402), the pending run carried into the next block;
+// at FLUSH / FINISH with the pending run flushed in (flush_RL).  Only the
+// current block's input is held on the host (<= nblockMAX + a run).  Where
+// the library calls BZ2_compressBlock the block's text is coded on the GPU
+// and its bits are appended to the stream's bit string; the bytes that call
+// makes readable (numZ) follow the library's bit buffer, which keeps the
+// bits of its last bsW when a block ends (bz:compress.c:37-52, 609), so
+// total_out after every call -- BZ_RUN included -- equals the library's.
+//
+// Blocks are coded ahead in batches (one GPU plan for many blocks) where the
+// input they cover is certain to be consumed: FLUSH / FINISH input (the
+// caller has committed it: avail_in_expect) and BZ_RUN input when avail_out
+// is large enough that the library would drain every block of the call.
+// Otherwise one block is coded when it closes.
 #include <string.h>
 
 #include <condition_variable>
+#include <deque>
 #include <memory>
 #include <mutex>
 #include <new>
@@ -30,27 +38,48 @@
 namespace {
 
 enum Mode { M_IDLE = 1, M_RUNNING = 2, M_FLUSHING = 3, M_FINISHING = 4, M_FAILED = 5 };
+enum State { S_OUTPUT = 1, S_INPUT = 2 };
+
+// a block coded ahead: its text is input [beg, end) (absolute offsets); a
+// block closed by nblockMAX also consumed its closing byte `end` (the first
+// byte of the run it left pending); a flushed block ends the committed input
+struct Coded {
+    uint64_t beg, end;
+    uint64_t bit_off, bits;     // in GpuStreamState::enc
+    uint32_t crc, last_bits;
+    bool flushed;
+};
 
 struct GpuStreamState {
     bz_stream* strm;
     int bs100k;
     int mode;
-    std::vector<uint8_t> input;         // bytes of the open piece
-    std::vector<uint8_t> output;        // whole bytes not yet drained
-    uint64_t out_pos = 0;
-    uint64_t released = 0;              // output[0, released) may be drained (the library's numZ)
+    int state = S_INPUT;
+    uint32_t expect = 0;                // avail_in_expect
+    uint32_t nblock_max = 0;
+    // RLE1 bookkeeping of the current block (EState, bz:bzlib.c:116-126, 269-293)
+    uint32_t in_ch = 256, in_len = 0, nblock = 0;
+    std::vector<uint8_t> blk;           // the block's input bytes, the pending run included
+    uint64_t blk_beg = 0;               // absolute input offset of blk[0]
+    uint64_t consumed = 0;              // input bytes consumed (total_in)
+    // blocks coded ahead
+    std::deque<Coded> ahead;
+    std::vector<uint8_t> enc;           // their GPU output
+    // the stream's bits
+    std::vector<uint8_t> output;        // whole bytes from stream offset out_base on
+    uint64_t out_base = 0;              // stream offset of output[0] (drained bytes are dropped)
+    uint64_t out_pos = 0;               // stream offset of the next byte to drain
+    uint64_t released = 0;              // stream bytes [0, released) may be drained (the library's numZ)
     uint64_t total_bits = 0;            // bits of the stream so far
     uint32_t last_n = 0;                // bits of the last write (bsW) so far
     uint32_t tail = 0, tail_bits = 0;   // bits not yet a whole byte (right-aligned, < 8)
     bool header = false;                // "BZh<level>" written (first BZ2_compressBlock)
-    bool pending_piece = false;         // a FINISH failed: the closed piece is still to encode
-    bool pending_supplied = false, pending_finish = false;
     uint32_t n_blocks = 0, combined = 0;
 };
 
-// Encoder slots: each stream borrows one for its BZ_FINISH encode, so
-// streams of different threads encode concurrently (up to kSlots at once per
-// process) on their own HIP streams.  A slot belongs to one device.
+// Encoder slots: a stream borrows one to code blocks, so streams of different
+// threads encode concurrently (up to kSlots at once per process) on their
+// own HIP streams.  A slot belongs to one device.
 constexpr int kSlots = 4;
 struct Slot {
     int device = 0;
@@ -58,6 +87,7 @@ struct Slot {
     hipStream_t st = nullptr;
     bz::Encoder enc;
     DevBuf in, out;
+    PinnedBuf stage;
 };
 struct Pool {
     std::mutex mu;
@@ -114,6 +144,11 @@ void release(Slot* s)
     g_pool.cv.notify_all();
 }
 
+struct SlotGuard {
+    Slot* s;
+    ~SlotGuard() { if (s) release(s); }
+};
+
 void* default_bzalloc(void*, int items, int size) { return malloc((size_t)items * (size_t)size); }   // bz:bzlib.c:151-156
 void default_bzfree(void*, void* addr) { free(addr); }
 
@@ -128,17 +163,6 @@ void add_out(bz_stream* s, uint64_t n)
     uint64_t t = ((uint64_t)s->total_out_hi32 << 32 | s->total_out_lo32) + n;
     s->total_out_lo32 = (unsigned)t;
     s->total_out_hi32 = (unsigned)(t >> 32);
-}
-
-void consume(GpuStreamState* g)
-{
-    bz_stream* s = g->strm;
-    if (s->avail_in) {
-        g->input.insert(g->input.end(), (uint8_t*)s->next_in, (uint8_t*)s->next_in + s->avail_in);
-        s->next_in += s->avail_in;
-        add_in(s, s->avail_in);
-        s->avail_in = 0;
-    }
 }
 
 void put_bits(GpuStreamState* g, uint32_t v, uint32_t n)   // n <= 24, MSB first
@@ -193,42 +217,115 @@ void release(GpuStreamState* g)
     g->released = (g->total_bits - keep) / 8;
 }
 
-// BZ2_compressBlock for the open piece (bz:compress.c:602-667): encode it on
-// the GPU as a stream of its own and append its blocks' bits
-int encode_piece(GpuStreamState* g, bool supplied)
+// ---- RLE1 bookkeeping (ADD_CHAR_TO_BLOCK, bz:bzlib.c:269-293) --------------
+inline void add_char(GpuStreamState* g, uint32_t c)
 {
-    std::vector<uint8_t> tmp;
-    bz::StreamOut so{};
-    uint32_t last = 0;
-    if (!g->input.empty()) {
-        Slot* sl = nullptr;
-        try {
-            const int dev = target_device();
-            DeviceGuard guard(dev);
-            sl = acquire(dev);
-            if (!sl->st) HIP_CHECK(hipStreamCreateWithFlags(&sl->st, hipStreamNonBlocking));
-            const uint64_t n = g->input.size();
-            uint8_t* d_in = sl->in.as<uint8_t>(n + 64);
-            HIP_CHECK(hipMemcpyAsync(d_in, g->input.data(), n, hipMemcpyHostToDevice, sl->st));
-            std::vector<bz::StreamIn> pieces(1);
-            pieces[0].text_off = 0;
-            pieces[0].text_len = n;
-            pieces[0].final_run_joins = supplied ? 1u : 0u;
-            pieces[0].group = 0;
-            std::vector<bz::StreamOut> outs;
-            sl->enc.plan(d_in, pieces, g->bs100k, sl->st, outs, nullptr);
-            const uint64_t cap = (outs[0].bytes + 64 + 255) / 256 * 256;
-            uint8_t* d_out = sl->out.as<uint8_t>(cap);
-            sl->enc.emit(d_out, cap, 0, outs, sl->st, nullptr);
-            so = outs[0];
-            last = sl->enc.last_write_bits(0, so, sl->st);
-            tmp.resize(so.bytes);
-            HIP_CHECK(hipMemcpyAsync(tmp.data(), d_out, so.bytes, hipMemcpyDeviceToHost, sl->st));
-            HIP_CHECK(hipStreamSynchronize(sl->st));
-            release(sl);
-        } catch (const std::exception&) {
-            if (sl) release(sl);
-            return BZ_CONFIG_ERROR;
+    if (c != g->in_ch && g->in_len == 1) {           // fast track: the pending single byte goes in
+        ++g->nblock;
+        g->in_ch = c;
+    } else if (c != g->in_ch || g->in_len == 255) {  // add_pair_to_block (bz:bzlib.c:224-256)
+        if (g->in_ch < 256) g->nblock += g->in_len <= 3 ? g->in_len : 5u;
+        g->in_ch = c;
+        g->in_len = 1;
+    } else {
+        ++g->in_len;
+    }
+}
+
+bool empty_rl(const GpuStreamState* g) { return !(g->in_ch < 256 && g->in_len > 0); }   // isempty_RL
+
+// consume input bytes [p, p + n) into the block, through the RLE1 bookkeeping,
+// stopping once the block is full (copy_input_until_stop); returns the count
+uint64_t track(GpuStreamState* g, const uint8_t* p, uint64_t n)
+{
+    uint64_t i = 0;
+    while (i < n && g->nblock < g->nblock_max) {
+        // eight bytes at a time while each differs from its predecessor: each
+        // only pushes the pending single byte in (the fast track)
+        if (g->in_len == 1 && n - i >= 8 && g->nblock + 8 < g->nblock_max) {
+            uint64_t x;
+            memcpy(&x, p + i, 8);
+            const uint64_t prev = (x << 8) | (uint64_t)g->in_ch;
+            const uint64_t d = x ^ prev;                  // a zero byte: a byte equal to its predecessor
+            if (!((d - 0x0101010101010101ull) & ~d & 0x8080808080808080ull)) {
+                g->nblock += 8;
+                g->in_ch = (uint32_t)(x >> 56);
+                i += 8;
+                continue;
+            }
+        }
+        add_char(g, p[i]);
+        ++i;
+    }
+    return i;
+}
+
+// re-derive the bookkeeping of the current block from its bytes (after a
+// partial consumption on the coded-ahead path)
+void retrack(GpuStreamState* g)
+{
+    g->in_ch = 256;
+    g->in_len = 0;
+    g->nblock = 0;
+    (void)track(g, g->blk.data(), g->blk.size());
+}
+
+// ---- GPU coding -------------------------------------------------------------
+// Code text (host) as one piece on the GPU: closed (its last run flushed, the
+// final block included) or open (complete blocks only).  Appends one Coded
+// per block to g->ahead, with absolute offsets from `beg`.
+void code_text(GpuStreamState* g, const uint8_t* a, uint64_t na, const uint8_t* b, uint64_t nb, uint64_t beg,
+               bool closed)
+{
+    const uint64_t n = na + nb;
+    if (n == 0) return;
+    const int dev = target_device();
+    DeviceGuard guard(dev);
+    SlotGuard sg{acquire(dev)};
+    Slot* sl = sg.s;
+    if (!sl->st) HIP_CHECK(hipStreamCreateWithFlags(&sl->st, hipStreamNonBlocking));
+    uint8_t* h = static_cast<uint8_t*>(sl->stage.get(n + 64));
+    if (na) memcpy(h, a, na);
+    if (nb) memcpy(h + na, b, nb);
+    uint8_t* d_in = sl->in.as<uint8_t>(n + 64);
+    HIP_CHECK(hipMemcpyAsync(d_in, h, n, hipMemcpyHostToDevice, sl->st));
+    std::vector<bz::StreamIn> pieces(1);
+    pieces[0].text_off = 0;
+    pieces[0].text_len = n;
+    pieces[0].final_run_joins = 1;   // flush_RL adds the pending run to the block, full or not
+    pieces[0].group = 0;
+    pieces[0].open = closed ? 0u : 1u;
+    std::vector<bz::StreamOut> outs;
+    sl->enc.plan(d_in, pieces, g->bs100k, sl->st, outs, nullptr);
+    const uint64_t cap = (outs[0].bytes + 64 + 255) / 256 * 256;
+    uint8_t* d_out = sl->out.as<uint8_t>(cap);
+    sl->enc.emit(d_out, cap, 0, outs, sl->st, nullptr);
+    std::vector<bz::Encoder::BlockOut> res;
+    sl->enc.block_results(res, sl->st);
+    g->enc.resize(outs[0].bytes);
+    if (outs[0].bytes) HIP_CHECK(hipMemcpyAsync(g->enc.data(), d_out, outs[0].bytes, hipMemcpyDeviceToHost, sl->st));
+    HIP_CHECK(hipStreamSynchronize(sl->st));
+    for (size_t k = 0; k < res.size(); ++k) {
+        const bool fl = closed && k + 1 == res.size();
+        g->ahead.push_back(Coded{beg + res[k].in_beg, beg + res[k].in_end, res[k].bit_off, res[k].bits, res[k].crc,
+                                 res[k].last_bits, fl});
+    }
+}
+
+// BZ2_compressBlock (bz:compress.c:602-667) at the current block: its text is
+// the whole of blk when the pending run is flushed in (flush), else blk
+// without the pending run (a block closed by nblockMAX)
+void compress_block(GpuStreamState* g, bool flush, bool last)
+{
+    const uint64_t text = flush ? g->blk.size() : g->blk.size() - g->in_len;
+    if (text) {
+        const bool have = !g->ahead.empty() && g->ahead.front().beg == g->blk_beg &&
+                          g->ahead.front().end == g->blk_beg + text && g->ahead.front().flushed == flush;
+        if (!have) {   // code this block alone
+            g->ahead.clear();
+            code_text(g, g->blk.data(), text, nullptr, 0, g->blk_beg, true);
+            if (g->ahead.size() != 1 || g->ahead.front().end != g->blk_beg + text)
+                throw StarchError(-10, "bzlib: block cut differs from the RLE1 bookkeeping");
         }
     }
     if (!g->header) {   // the first compressBlock writes the stream header, data or not
@@ -239,49 +336,149 @@ int encode_piece(GpuStreamState* g, bool supplied)
         g->header = true;
         g->last_n = 8;
     }
-    if (so.n_blocks) {
-        put_stream_bits(g, tmp.data(), 32, so.block_bits);   // after the piece stream's own header
-        // combined CRC over all blocks: c = rotl1(c) ^ blockCRC per block, so a
-        // piece of k blocks folds in as rotl_k(c) ^ (its own combined CRC)
-        const uint32_t k = so.n_blocks & 31u;
-        g->combined = (k ? (g->combined << k) | (g->combined >> (32 - k)) : g->combined) ^ so.combined_crc;
-        g->n_blocks += so.n_blocks;
-        g->last_n = last;
+    if (text) {
+        const Coded c = g->ahead.front();
+        g->ahead.pop_front();
+        put_stream_bits(g, g->enc.data(), c.bit_off, c.bits);
+        g->combined = ((g->combined << 1) | (g->combined >> 31)) ^ c.crc;   // bz:compress.c:606-608
+        ++g->n_blocks;
+        g->last_n = c.last_bits;
     }
-    release(g);
-    g->input.clear();
-    return BZ_OK;
+    if (last) {        // trailer + combined CRC + byte pad (bz:compress.c:657-666)
+        put_bits(g, 0x177245u, 24);
+        put_bits(g, 0x385090u, 24);
+        put_bits(g, g->combined >> 16, 16);
+        put_bits(g, g->combined & 0xFFFFu, 16);
+        if (g->tail_bits) put_bits(g, 0, 8 - g->tail_bits);
+        g->released = g->out_base + g->output.size();   // bsFinishWrite
+    } else {
+        release(g);
+    }
+    // the next block starts with the pending run (none after a flush: init_RL)
+    if (flush) {
+        g->blk.clear();
+        g->blk_beg = g->consumed;
+        g->in_ch = 256;
+        g->in_len = 0;
+    } else {
+        g->blk.erase(g->blk.begin(), g->blk.begin() + (std::ptrdiff_t)text);
+        g->blk_beg += text;
+    }
+    g->nblock = 0;
+    if (g->blk.capacity() > (4u << 20)) g->blk.shrink_to_fit();
 }
 
-void finish_stream(GpuStreamState* g)   // trailer + combined CRC + byte pad
+// code the blocks of input that is certain to be consumed in one GPU plan
+// (see the header comment); at most kAhead bytes of new input at a time
+constexpr uint64_t kAhead = 64ull << 20;
+void code_ahead(GpuStreamState* g)
 {
-    put_bits(g, 0x177245u, 24);
-    put_bits(g, 0x385090u, 24);
-    put_bits(g, g->combined >> 16, 16);
-    put_bits(g, g->combined & 0xFFFFu, 16);
-    if (g->tail_bits) put_bits(g, 0, 8 - g->tail_bits);
-    g->released = g->output.size();   // bsFinishWrite
-    g->input.shrink_to_fit();
+    if (!g->ahead.empty()) return;
+    bz_stream* s = g->strm;
+    uint64_t avail = s->avail_in;
+    bool closed = false;
+    if (g->mode == M_RUNNING) {
+        const uint64_t text = g->blk.size() + avail;
+        if (text < 2ull * g->nblock_max) return;                // at most one block closes: code it when it does
+        const uint64_t nbk = text / g->nblock_max + 2;
+        const uint64_t worst = text + text / 3 + 1024 * nbk;    // > any bzip2 output of that text
+        if ((uint64_t)s->avail_out + g->out_pos < g->released + worst) return;   // the library might stop early
+        avail = std::min<uint64_t>(avail, kAhead);
+    } else {
+        avail = g->expect;
+        if (g->blk.size() + avail < g->nblock_max && avail) return;   // one block: coded at the flush anyway
+        if (avail <= kAhead) closed = true;
+        else avail = kAhead;
+    }
+    code_text(g, g->blk.data(), g->blk.size(), reinterpret_cast<const uint8_t*>(s->next_in), avail, g->blk_beg,
+              closed);
 }
 
+// copy_input_until_stop (bz:bzlib.c:297-338)
+bool copy_input(GpuStreamState* g)
+{
+    bz_stream* s = g->strm;
+    const bool running = g->mode == M_RUNNING;
+    uint64_t lim = s->avail_in;
+    if (!running) lim = std::min<uint64_t>(lim, g->expect);
+    if (lim == 0 || g->nblock >= g->nblock_max) return false;
+    const uint8_t* p = reinterpret_cast<const uint8_t*>(s->next_in);
+    uint64_t took;
+    if (!g->ahead.empty() && g->ahead.front().beg == g->blk_beg) {
+        // the block's end is known: consume to its closing byte (or the end)
+        const Coded& c = g->ahead.front();
+        const uint64_t target = c.flushed ? c.end : c.end + 1;
+        took = std::min<uint64_t>(lim, target - g->consumed);
+        g->blk.insert(g->blk.end(), p, p + took);
+        if (g->consumed + took == target) {
+            // closed by nblockMAX: full, its closing byte pending; flushed:
+            // the committed input is in (the flush follows at once)
+            g->in_ch = g->blk.back();
+            g->in_len = 1;
+            g->nblock = c.flushed ? 0u : g->nblock_max;
+        } else {
+            retrack(g);
+        }
+    } else {
+        took = track(g, p, lim);
+        g->blk.insert(g->blk.end(), p, p + took);
+    }
+    s->next_in += took;
+    s->avail_in -= (unsigned)took;
+    add_in(s, took);
+    g->consumed += took;
+    if (!running) g->expect -= (uint32_t)took;
+    return took > 0;
+}
+
+// copy_output_until_stop (bz:bzlib.c:342-365)
 bool drain(GpuStreamState* g)
 {
     bz_stream* s = g->strm;
     uint64_t left = g->released - g->out_pos;
     uint64_t k = left < s->avail_out ? left : s->avail_out;
     if (k) {
-        memcpy(s->next_out, g->output.data() + g->out_pos, k);
+        memcpy(s->next_out, g->output.data() + (g->out_pos - g->out_base), k);
         s->next_out += k;
         s->avail_out -= (unsigned)k;
         g->out_pos += k;
         add_out(s, k);
     }
-    if (g->out_pos == g->released && g->out_pos > (1u << 20)) {   // compact the drained prefix
-        g->output.erase(g->output.begin(), g->output.begin() + (std::ptrdiff_t)g->out_pos);
-        g->released -= g->out_pos;
-        g->out_pos = 0;
+    if (g->out_pos - g->out_base > (1u << 20)) {   // drop the drained prefix
+        g->output.erase(g->output.begin(), g->output.begin() + (std::ptrdiff_t)(g->out_pos - g->out_base));
+        g->out_base = g->out_pos;
     }
     return k > 0;
+}
+
+// handle_compress (bz:bzlib.c:369-412)
+bool handle_compress(GpuStreamState* g)
+{
+    bz_stream* s = g->strm;
+    bool pin = false, pout = false;
+    for (;;) {
+        if (g->state == S_OUTPUT) {
+            pout |= drain(g);
+            if (g->out_pos < g->released) break;
+            if (g->mode == M_FINISHING && g->expect == 0 && empty_rl(g)) break;
+            g->state = S_INPUT;                          // prepare_new_block
+            if (g->mode == M_FLUSHING && g->expect == 0 && empty_rl(g)) break;
+        }
+        if (g->state == S_INPUT) {
+            code_ahead(g);
+            pin |= copy_input(g);
+            if (g->mode != M_RUNNING && g->expect == 0) {
+                compress_block(g, true, g->mode == M_FINISHING);
+                g->state = S_OUTPUT;
+            } else if (g->nblock >= g->nblock_max) {
+                compress_block(g, false, false);
+                g->state = S_OUTPUT;
+            } else if (s->avail_in == 0) {
+                break;
+            }
+        }
+    }
+    return pin || pout;
 }
 
 GpuStreamState* state_of(bz_stream* s)
@@ -308,6 +505,7 @@ int BZ2_bzCompressInit(bz_stream* strm, int blockSize100k, int verbosity, int wo
     g->strm = strm;
     g->bs100k = blockSize100k;
     g->mode = M_RUNNING;
+    g->nblock_max = 100000u * (uint32_t)blockSize100k - 19u;   // bz:bzlib.c:194
     strm->state = g;
     strm->total_in_lo32 = strm->total_in_hi32 = 0;
     strm->total_out_lo32 = strm->total_out_hi32 = 0;
@@ -320,68 +518,51 @@ int BZ2_bzCompress(bz_stream* strm, int action)
 {
     GpuStreamState* g = state_of(strm);
     if (!g) return BZ_PARAM_ERROR;
-    switch (g->mode) {
-        case M_IDLE:
-            return BZ_SEQUENCE_ERROR;
-        case M_RUNNING:
-            if (action == BZ_RUN) {
-                bool progress = strm->avail_in > 0;
-                consume(g);
-                return progress ? BZ_RUN_OK : BZ_PARAM_ERROR;           // bz:bzlib.c:432-434
-            }
-            if (action == BZ_FLUSH || action == BZ_FINISH) {
-                const bool supplied = strm->avail_in > 0;
-                consume(g);
-                if (int rc = encode_piece(g, supplied)) {   // input kept: the same call may be retried
-                    g->mode = M_FAILED;
-                    g->pending_piece = true;
-                    g->pending_supplied = supplied;
-                    g->pending_finish = action == BZ_FINISH;
-                    return rc;
-                }
-                if (action == BZ_FLUSH) {
-                    drain(g);
-                    if (g->out_pos < g->released) { g->mode = M_FLUSHING; return BZ_FLUSH_OK; }   // bz:bzlib.c:451-459
+    try {
+        for (;;) {   // preswitch (bz:bzlib.c:420-471)
+            switch (g->mode) {
+                case M_IDLE:
+                    return BZ_SEQUENCE_ERROR;
+                case M_RUNNING:
+                    if (action == BZ_RUN) {
+                        const bool progress = handle_compress(g);
+                        if (!g->ahead.empty()) { g->ahead.clear(); g->enc.clear(); }   // BZ_RUN input is not committed
+                        return progress ? BZ_RUN_OK : BZ_PARAM_ERROR;                 // bz:bzlib.c:432-434
+                    }
+                    if (action == BZ_FLUSH || action == BZ_FINISH) {
+                        g->expect = strm->avail_in;
+                        g->mode = action == BZ_FLUSH ? M_FLUSHING : M_FINISHING;
+                        continue;
+                    }
+                    return BZ_PARAM_ERROR;
+                case M_FLUSHING: {
+                    if (action != BZ_FLUSH) return BZ_SEQUENCE_ERROR;
+                    if (g->expect != strm->avail_in) return BZ_SEQUENCE_ERROR;
+                    handle_compress(g);
+                    if (g->expect > 0 || !empty_rl(g) || g->out_pos < g->released) return BZ_FLUSH_OK;
+                    g->mode = M_RUNNING;
                     return BZ_RUN_OK;
                 }
-                finish_stream(g);
-                g->mode = M_FINISHING;
-                break;
+                case M_FINISHING: {
+                    if (action != BZ_FINISH) return BZ_SEQUENCE_ERROR;
+                    if (g->expect != strm->avail_in) return BZ_SEQUENCE_ERROR;
+                    if (!handle_compress(g)) return BZ_SEQUENCE_ERROR;
+                    if (g->expect > 0 || !empty_rl(g) || g->out_pos < g->released) return BZ_FINISH_OK;
+                    g->mode = M_IDLE;
+                    g->ahead.clear();
+                    std::vector<uint8_t>().swap(g->enc);
+                    std::vector<uint8_t>().swap(g->blk);
+                    if (strm->block_close_functor) strm->block_close_functor(strm->handler);   // bz:bzlib.c:470
+                    return BZ_STREAM_END;
+                }
+                default:
+                    return BZ_SEQUENCE_ERROR;   // a GPU failure ended the stream
             }
-            return BZ_PARAM_ERROR;
-        case M_FLUSHING:   // avail_in_expect is 0: everything was consumed by the first FLUSH call
-            if (action != BZ_FLUSH || strm->avail_in != 0) return BZ_SEQUENCE_ERROR;
-            drain(g);
-            if (g->out_pos < g->released) return BZ_FLUSH_OK;
-            g->mode = M_RUNNING;
-            return BZ_RUN_OK;
-        case M_FINISHING:
-            if (action != BZ_FINISH) return BZ_SEQUENCE_ERROR;
-            if (strm->avail_in != 0) return BZ_SEQUENCE_ERROR;          // avail_in_expect mismatch
-            break;
-        case M_FAILED:   // the piece is still held: the same action retries its encode
-            if ((action == BZ_FINISH) != g->pending_finish || action == BZ_RUN || strm->avail_in != 0)
-                return BZ_SEQUENCE_ERROR;
-            if (int rc = encode_piece(g, g->pending_supplied)) return rc;
-            g->pending_piece = false;
-            if (!g->pending_finish) {
-                g->mode = M_RUNNING;
-                drain(g);
-                if (g->out_pos < g->released) { g->mode = M_FLUSHING; return BZ_FLUSH_OK; }
-                return BZ_RUN_OK;
-            }
-            finish_stream(g);
-            g->mode = M_FINISHING;
-            break;
-        default:
-            return BZ_SEQUENCE_ERROR;
+        }
+    } catch (const std::exception&) {
+        g->mode = M_FAILED;
+        return BZ_CONFIG_ERROR;
     }
-    // FINISHING: drain the encoded stream
-    bool progress = drain(g);
-    if (g->out_pos < g->released) return progress ? BZ_FINISH_OK : BZ_SEQUENCE_ERROR;
-    g->mode = M_IDLE;
-    if (strm->block_close_functor) strm->block_close_functor(strm->handler);   // bz:bzlib.c:470
-    return BZ_STREAM_END;
 }
 
 int BZ2_bzCompressEnd(bz_stream* strm)
