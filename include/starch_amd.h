@@ -275,6 +275,13 @@ int starch_bz2_compress_many_device(starch_ctx* ctx, const void* d_in, const uin
  * size. */
 int starch_gen_bed(int kind, uint64_t seed, uint64_t total_lines, const int32_t* chroms, int nchroms, void* dst,
                    uint64_t cap, uint64_t* len);
+/* The per-position input (kind 2: "<chr>\t<p>\t<p+1>\n" for p in [first,
+ * first + count)) of one chromosome written by the GPU into device memory
+ * d_dst (cap bytes) on `stream` (asynchronous); *len = its byte count, which
+ * d_dst = NULL returns alone (no GPU needed).  Same bytes as starch_gen_bed
+ * kind 2 for that chromosome (cfg5's 73.6 GB input without the host). */
+int starch_gen_perpos_device(int chrom, uint64_t first, uint64_t count, void* d_dst, uint64_t cap, uint64_t* len,
+                             void* stream);
 /* Per-chromosome byte counts of starch_gen_bed's output (sizes[k] for chroms[k]). */
 int starch_gen_bed_sizes(int kind, uint64_t seed, uint64_t total_lines, const int32_t* chroms, int nchroms,
                          uint64_t* sizes);

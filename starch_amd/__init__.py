@@ -138,6 +138,7 @@ def load():
                                             ctypes.c_int),
         "starch_gen_bed": ([ctypes.c_int, u64, u64, ctypes.POINTER(ctypes.c_int32), ctypes.c_int, vp, u64, pu64],
                            ctypes.c_int),
+        "starch_gen_perpos_device": ([ctypes.c_int, u64, u64, vp, u64, pu64, vp], ctypes.c_int),
         "starch_build_index": ([ctypes.POINTER(Segment), ctypes.POINTER(ctypes.c_char_p), pu64, u64, u64,
                                 ctypes.c_char_p, ctypes.c_int, vp, u64, pu64], ctypes.c_int),
         "starch_build_index_opt": ([ctypes.POINTER(Segment), ctypes.POINTER(ctypes.c_char_p), pu64, u64, u64,
@@ -511,6 +512,17 @@ def gen_bed(kind, total_lines, chroms=None, seed=20261015, into=None):
     buf = ctypes.create_string_buffer(max(1, n.value))
     _check(L.starch_gen_bed(kind, seed, total_lines, C, len(chroms), buf, n.value, ctypes.byref(n)))
     return buf.raw[:n.value]
+
+
+def gen_perpos_device(chrom, d_ptr=None, cap=0, first=0, count=None, stream=None):
+    """Per-position lines of one chromosome written by the GPU at d_ptr (or,
+    d_ptr None, just the byte count) -> byte count."""
+    L = load()
+    count = HG38_LEN[chrom] - first if count is None else count
+    n = ctypes.c_uint64()
+    _check(L.starch_gen_perpos_device(chrom, first, count, ctypes.c_void_p(d_ptr) if d_ptr else None, cap,
+                                      ctypes.byref(n), ctypes.c_void_p(stream) if stream else None))
+    return n.value
 
 
 def gen_bed_sizes(kind, total_lines, chroms=None, seed=20261015):

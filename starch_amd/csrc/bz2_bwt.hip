@@ -566,9 +566,12 @@ __global__ void __launch_bounds__(64) k_fb_place(const uint8_t* __restrict__ blk
     }
 }
 
-__global__ void k_fb_hp(const uint32_t* __restrict__ head, uint64_t* __restrict__ hp, uint32_t n)
+// (and the round's counters zeroed: no separate memset launch per round)
+__global__ void k_fb_hp(const uint32_t* __restrict__ head, uint64_t* __restrict__ hp, uint32_t n,
+                        uint32_t* __restrict__ ctr)
 {
     const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
+    if (i < 4) ctr[i] = 0;
     if (i < n) hp[i] = head[i] ? i : 0u;
 }
 
@@ -951,8 +954,7 @@ void launch_fallback(BlockDesc* blocks, uint32_t b0, const uint32_t* which_host,
             uint32_t* ctr = scr.V2 + x.so;                      // [0] not done, [1] mixed buckets, [2] next bucket
             const dim3 g((n + 255) / 256), g1((n + 256) / 256);
             ++x.stamp;
-            HIP_CHECK(hipMemsetAsync(ctr, 0, 4 * sizeof(uint32_t), x.s));
-            hipLaunchKernelGGL(k_fb_hp, g, dim3(256), 0, x.s, head, hp, n);
+            hipLaunchKernelGGL(k_fb_hp, g, dim3(256), 0, x.s, head, hp, n, ctr);
             scan::incl_max_u64(hp, n, *x.tmp, x.s);
             hipLaunchKernelGGL(k_fb_eclass, g, dim3(256), 0, x.s, fmap, hp, ecls, n, (uint32_t)(x.H % n));
             hipLaunchKernelGGL(k_fb_key, g, dim3(256), 0, x.s, fmap, ecls, head, hp, key, mixed, ctr, n, x.stamp);

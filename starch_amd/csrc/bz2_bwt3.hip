@@ -144,9 +144,7 @@ struct Lists {
     uint32_t* rounds;       // per slot: doubling rounds with work
     uint32_t* tied;         // per slot: still tied when doubling starts
     uint64_t* hg;           // huge groups of the current partition level (k3_hg_*), HG_MAXN
-    uint32_t* hg_base;      // ... their first chunk row
-    uint32_t* hg_hist;      // [HG_MAXCH][256] chunk digit counts -> chunk write cursors
-    uint32_t* hg_info;      // [HG_MAXN][256] bin start | final flags
+    uint32_t* hg_info;      // [HG_MAXN][512]: bin start | final flag; bin totals -> scatter cursors
     uint64_t* gb;           // doubling: tie groups gathered by the whole grid (k3_gather_big), GB_MAXN
     uint32_t* gb_h;         // ... their key offset h mod n
 };
@@ -1067,8 +1065,8 @@ __global__ void __launch_bounds__(LT) k3_part_l(Ctx c, const uint64_t* __restric
 // source reads race the final SA writes.
 // ---------------------------------------------------------------------------
 constexpr uint32_t HG_MIN = HG_MIN_PUSH;
-constexpr uint32_t HG_CH = 8192;
-constexpr uint32_t HG_MAXCH = 16384;
+constexpr uint32_t HG_CH = 1024;        // elements per chunk: 4 per thread, every chunk in flight at once
+constexpr uint32_t HG_MAXCH = 16384;    // chunks per level (the pick's budget)
 constexpr uint32_t HG_MAXN = 256;
 constexpr uint32_t HG_FINAL = 1u << 31;
 
@@ -1085,12 +1083,11 @@ __global__ void k3_hg_pick(Ctx c, uint64_t* __restrict__ list, uint32_t n)
     const uint32_t k = atomicAdd(&c.L.ctr[C_HG], 1u);
     if (k >= HG_MAXN) return;
     const uint32_t base = atomicAdd(&c.L.ctr[C_HGC], nch);
-    if (base + nch > HG_MAXCH) {            // no hist rows left: k3_part_l keeps it
+    if (base + nch > HG_MAXCH) {            // over budget: k3_part_l keeps it
         c.L.hg[k] = 0;
         return;
     }
     c.L.hg[k] = item;
-    c.L.hg_base[k] = base;
     list[i] = mk_item(it_slot(item), it_start(item), 0, it_shift(item), it_par(item));
 }
 
@@ -1114,7 +1111,7 @@ __device__ __forceinline__ HgGroup hg_group(uint64_t item)
 }
 
 // count[d] += 1 for a wave's lanes (one LDS atomic when they share a digit:
-// a skewed group sends most elements to one bin)
+// a skewed group sends most elements to one bin); returns the lane's slot
 __device__ __forceinline__ uint32_t wave_bin_add(uint32_t* cnt, bool act, uint32_t d)
 {
     const uint64_t a = __ballot(act);
@@ -1131,39 +1128,69 @@ __device__ __forceinline__ uint32_t wave_bin_add(uint32_t* cnt, bool act, uint32
     return act ? atomicAdd(&cnt[d], 1u) : 0u;
 }
 
+// the chunks of every huge group as one flat index space: chunk j of the
+// launch -> (group q, chunk in group); groups' chunk counts prefix-summed in LDS
+struct HgMap {
+    uint32_t nh, total;
+    uint32_t pre[HG_MAXN + 1];
+};
+__device__ __forceinline__ void hg_map_load(const Ctx& c, HgMap& mp)
+{
+    if (threadIdx.x == 0) {
+        const uint32_t nh = min(c.L.ctr[C_HG], HG_MAXN);
+        uint32_t t = 0;
+        for (uint32_t q = 0; q < nh; ++q) {
+            mp.pre[q] = t;
+            t += hg_group(c.L.hg[q]).nch;   // 0 for a group left to k3_part_l
+        }
+        mp.pre[nh] = t;
+        mp.nh = nh;
+        mp.total = t;
+    }
+    __syncthreads();
+}
+__device__ __forceinline__ uint32_t hg_group_of(const HgMap& mp, uint32_t j)
+{
+    uint32_t lo = 0, hi = mp.nh - 1;
+    while (lo < hi) {                      // last q with pre[q] <= j (empty groups share a start)
+        const uint32_t mid = (lo + hi + 1) >> 1;
+        if (mp.pre[mid] <= j) lo = mid; else hi = mid - 1;
+    }
+    return lo;
+}
+
+// per-chunk digit counts, added into the group's 256 bin totals
 template <bool DBL>
 __global__ void __launch_bounds__(256) k3_hg_hist(Ctx c)
 {
     __shared__ uint32_t h[256];
+    __shared__ HgMap mp;
     const uint32_t tid = threadIdx.x;
-    const uint32_t nh = min(c.L.ctr[C_HG], HG_MAXN);
-    for (uint32_t q = 0; q < nh; ++q) {
-        const uint64_t item = c.L.hg[q];
-        if (it_size(item) == 0) continue;
-        const HgGroup g = hg_group(item);
+    hg_map_load(c, mp);
+    for (uint32_t j = blockIdx.x; j < mp.total; j += gridDim.x) {
+        const uint32_t q = hg_group_of(mp, j), ch = j - mp.pre[q];
+        const HgGroup g = hg_group(c.L.hg[q]);
         const KeySrc ks = key_src(c, g.slot, g.par);
         const uint32_t* sv = (g.par ? c.scr.V : c.scr.SA) + (uint64_t)g.slot * c.scr.stride + g.s;
-        uint32_t* rows = c.L.hg_hist + (uint64_t)c.L.hg_base[q] * 256;
-        for (uint32_t ch = blockIdx.x; ch < g.nch; ch += gridDim.x) {
-            h[tid] = 0;
-            __syncthreads();
-            const uint32_t a = ch * HG_CH, e = min(g.m, a + HG_CH);
-            for (uint32_t i0 = a; i0 < e; i0 += 256) {   // uniform trip count
-                const uint32_t i = i0 + tid;
-                const bool ok = i < e;
-                const uint32_t ic = ok ? i : a;
-                const uint32_t d = (uint32_t)((elem_key<DBL>(ks, g.s + ic, sv[ic]) >> g.sh2) & g.dmask);
-                (void)wave_bin_add(h, ok, d);
-            }
-            __syncthreads();
-            rows[(uint64_t)ch * 256 + tid] = h[tid];
-            __syncthreads();
+        h[tid] = 0;
+        __syncthreads();
+        const uint32_t a = ch * HG_CH, e = min(g.m, a + HG_CH);
+        uint32_t d[HG_CH / 256];
+#pragma unroll
+        for (uint32_t u = 0; u < HG_CH / 256; ++u) {   // all loads issued first
+            const uint32_t i = a + u * 256 + tid, ic = i < e ? i : a;
+            d[u] = (uint32_t)((elem_key<DBL>(ks, g.s + ic, sv[ic]) >> g.sh2) & g.dmask);
         }
+#pragma unroll
+        for (uint32_t u = 0; u < HG_CH / 256; ++u) (void)wave_bin_add(h, a + u * 256 + tid < e, d[u]);
+        __syncthreads();
+        if (h[tid]) atomicAdd(&c.L.hg_info[(uint64_t)q * 512 + 256 + tid], h[tid]);   // bin totals
+        __syncthreads();
     }
 }
 
-// one workgroup per huge group: bin starts, per-chunk cursors (in place),
-// sub-bucket classes (k3_part_l's rules)
+// one workgroup per huge group: bin starts -> the group's global cursors,
+// sub-bucket classes (k3_part_l's rules), final-bin flags
 __global__ void __launch_bounds__(256) k3_hg_scan(Ctx c)
 {
     __shared__ uint32_t scan_sh[5];
@@ -1173,20 +1200,13 @@ __global__ void __launch_bounds__(256) k3_hg_scan(Ctx c)
     const uint64_t item = c.L.hg[q];
     if (it_size(item) == 0) return;                   // uniform
     const HgGroup g = hg_group(item);
-    uint32_t* rows = c.L.hg_hist + (uint64_t)c.L.hg_base[q] * 256;
-    uint32_t cc = 0;
-    for (uint32_t ch = 0; ch < g.nch; ++ch) cc += rows[(uint64_t)ch * 256 + tid];
+    uint32_t* info = c.L.hg_info + (uint64_t)q * 512;   // [0,256) start | flags, [256,512) totals -> cursors
+    const uint32_t cc = info[256 + tid];
     const uint32_t ss = block_excl_scan_add<uint32_t>(cc, scan_sh, (uint32_t*)nullptr);
-    uint32_t run = ss;
-    for (uint32_t ch = 0; ch < g.nch; ++ch) {
-        uint32_t& x = rows[(uint64_t)ch * 256 + tid];
-        const uint32_t t = x;
-        x = run;
-        run += t;
-    }
+    info[256 + tid] = ss;                             // scatter cursor
     const bool alleq = cc >= 2 && size_class(cc) == 6 && g.sh2 == 0;   // one tie group
     const bool fin = cc == 1 || alleq;
-    c.L.hg_info[(uint64_t)q * 256 + tid] = ss | (fin ? HG_FINAL : 0u);
+    info[tid] = ss | (fin ? HG_FINAL : 0u);
     if (alleq) {
         const uint32_t o = atomicAdd(c.L.ctr + C_T0 + c.tsel, 1u);
         c.L.t[c.tsel][o] = mk_item(g.slot, g.s + ss, cc, 0, 0);
@@ -1197,50 +1217,65 @@ __global__ void __launch_bounds__(256) k3_hg_scan(Ctx c)
     if (c.mode && (tid & 63) == 0 && r) atomicAdd(&c.L.runs[g.slot], r);
 }
 
+// every chunk: its elements to their bins (one global reservation per bin
+// and chunk, then LDS cursors)
 template <bool DBL>
 __global__ void __launch_bounds__(256) k3_hg_scatter(Ctx c)
 {
-    __shared__ uint32_t cur[256];
+    __shared__ uint32_t cnt[256];
+    __shared__ HgMap mp;
     const uint32_t tid = threadIdx.x;
-    const uint32_t nh = min(c.L.ctr[C_HG], HG_MAXN);
-    for (uint32_t q = 0; q < nh; ++q) {
-        const uint64_t item = c.L.hg[q];
-        if (it_size(item) == 0) continue;
-        const HgGroup g = hg_group(item);
+    hg_map_load(c, mp);
+    constexpr uint32_t U = HG_CH / 256;
+    for (uint32_t j = blockIdx.x; j < mp.total; j += gridDim.x) {
+        const uint32_t q = hg_group_of(mp, j), ch = j - mp.pre[q];
+        const HgGroup g = hg_group(c.L.hg[q]);
         const KeySrc ks = key_src(c, g.slot, g.par);
         const uint64_t base = (uint64_t)g.slot * c.scr.stride + g.s;
         const uint32_t* sv = (g.par ? c.scr.V : c.scr.SA) + base;
         uint32_t* dv = (g.par ? c.scr.SA : c.scr.V) + base;
         uint64_t* dk = (g.par ? c.kA : c.kB) + base;
         uint8_t* dl = DBL && ks.l ? (g.par ? c.lA : c.lB) + base : nullptr;
-        const uint32_t* rows = c.L.hg_hist + (uint64_t)c.L.hg_base[q] * 256;
-        for (uint32_t ch = blockIdx.x; ch < g.nch; ch += gridDim.x) {
-            cur[tid] = rows[(uint64_t)ch * 256 + tid];
-            __syncthreads();
-            const uint32_t a = ch * HG_CH, e = min(g.m, a + HG_CH);
-            for (uint32_t i0 = a; i0 < e; i0 += 256) {
-                const uint32_t i = i0 + tid;
-                const bool ok = i < e;
-                const uint32_t ic = ok ? i : a;
-                const uint32_t v = sv[ic];
-                const uint64_t k = elem_key<DBL>(ks, g.s + ic, v);
-                const uint32_t d = (uint32_t)((k >> g.sh2) & g.dmask);
-                const uint32_t p = wave_bin_add(cur, ok, d);
-                if (ok) {
-                    dv[p] = v;
-                    if constexpr (DBL) dk[p] = k;
-                    if (dl) dl[p] = ks.l[g.s + ic];
-                }
-            }
-            __syncthreads();
+        uint32_t* cur = c.L.hg_info + (uint64_t)q * 512 + 256;
+        cnt[tid] = 0;
+        __syncthreads();
+        const uint32_t a = ch * HG_CH, e = min(g.m, a + HG_CH);
+        uint32_t v[U], d[U], r[U];
+        uint64_t k[U];
+#pragma unroll
+        for (uint32_t u = 0; u < U; ++u) {
+            const uint32_t i = a + u * 256 + tid, ic = i < e ? i : a;
+            v[u] = sv[ic];
+            k[u] = elem_key<DBL>(ks, g.s + ic, v[u]);
+            d[u] = (uint32_t)((k[u] >> g.sh2) & g.dmask);
         }
+#pragma unroll
+        for (uint32_t u = 0; u < U; ++u) r[u] = wave_bin_add(cnt, a + u * 256 + tid < e, d[u]);
+        __syncthreads();
+        const uint32_t mine = cnt[tid];
+        __syncthreads();
+        if (mine) cnt[tid] = atomicAdd(&cur[tid], mine);   // this chunk's range of bin tid
+        __syncthreads();
+#pragma unroll
+        for (uint32_t u = 0; u < U; ++u) {
+            const uint32_t i = a + u * 256 + tid;
+            if (i < e) {
+                const uint32_t p = cnt[d[u]] + r[u];
+                dv[p] = v[u];
+                if constexpr (DBL) dk[p] = k[u];
+                if (dl) dl[p] = ks.l[g.s + i];
+            }
+        }
+        __syncthreads();
     }
 }
 
-// final sub-buckets of every huge group: SA, last column, RK, origPtr
+// final sub-buckets of every huge group: SA, last column, RK, origPtr; the
+// work is the flat list of (group, final bin, 1024-element piece)
 __global__ void __launch_bounds__(256) k3_hg_final(Ctx c)
 {
-    __shared__ uint32_t info[256];
+    __shared__ uint32_t fin_pre[257];
+    __shared__ uint32_t scan_sh[5];
     const uint32_t tid = threadIdx.x;
     const uint32_t nh = min(c.L.ctr[C_HG], HG_MAXN);
     for (uint32_t q = 0; q < nh; ++q) {
@@ -1251,27 +1286,31 @@ __global__ void __launch_bounds__(256) k3_hg_final(Ctx c)
         const uint32_t* dv = (g.par ? c.scr.SA : c.scr.V) + base;
         const KeySrc ks = key_src(c, g.slot, g.par);
         const uint8_t* dl = ks.l ? (g.par ? c.lA : c.lB) + base : nullptr;
+        const uint32_t* info = c.L.hg_info + (uint64_t)q * 512;
+        // final bins' sizes (bin end = next bin's start; the last ends at m)
+        const uint32_t st = info[tid] & ~HG_FINAL;
+        const uint32_t en = tid < 255 ? (info[tid + 1] & ~HG_FINAL) : g.m;
+        const uint32_t fsz = (info[tid] & HG_FINAL) ? en - st : 0u;
+        uint32_t ftot = 0;
+        const uint32_t fp = block_excl_scan_add<uint32_t>(fsz, scan_sh, &ftot);
+        fin_pre[tid] = fp;
+        if (tid == 255) fin_pre[256] = ftot;
         __syncthreads();
-        info[tid] = c.L.hg_info[(uint64_t)q * 256 + tid];
-        __syncthreads();
-        for (uint32_t ch = blockIdx.x; ch < g.nch; ch += gridDim.x) {
-            const uint32_t a = ch * HG_CH, e = min(g.m, a + HG_CH);
-            for (uint32_t p = a + tid; p < e; p += 256) {
-                // the bin holding position p: the last start <= p (starts ascend)
-                uint32_t lo = 0, hi = 255;
-                while (lo < hi) {
-                    const uint32_t mid = (lo + hi + 1) >> 1;
-                    if ((info[mid] & ~HG_FINAL) <= p) lo = mid; else hi = mid - 1;
-                }
-                const uint32_t f = info[lo];
-                if (!(f & HG_FINAL)) continue;
-                const uint32_t v = dv[p];
-                if (!g.par) c.scr.SA[base + p] = v;
-                c.scr.LL[base + p] = dl ? dl[p] : last_sym(c, g.slot, v);
-                if (c.mode) c.scr.RK[so + v] = g.s + (f & ~HG_FINAL);
-                if (v == 0) c.blocks[c.b0 + g.slot].orig_ptr = g.s + p;
+        for (uint32_t x = blockIdx.x * 256u + tid; x < ftot; x += gridDim.x * 256u) {
+            uint32_t lo = 0, hi = 255;                 // the final bin holding flat index x
+            while (lo < hi) {
+                const uint32_t mid = (lo + hi + 1) >> 1;
+                if (fin_pre[mid] <= x) lo = mid; else hi = mid - 1;
             }
+            const uint32_t b0 = info[lo] & ~HG_FINAL;
+            const uint32_t p = b0 + (x - fin_pre[lo]);
+            const uint32_t v = dv[p];
+            if (!g.par) c.scr.SA[base + p] = v;
+            c.scr.LL[base + p] = dl ? dl[p] : last_sym(c, g.slot, v);
+            if (c.mode) c.scr.RK[so + v] = g.s + b0;
+            if (v == 0) c.blocks[c.b0 + g.slot].orig_ptr = g.s + p;
         }
+        __syncthreads();
     }
 }
 
@@ -2633,7 +2672,28 @@ __global__ void __launch_bounds__(256) k3_rk_groups(Ctx c, const uint64_t* __res
     const uint64_t item = items[gi];
     const uint32_t slot = it_slot(item), s = it_start(item), m = it_size(item);
     const uint64_t so = (uint64_t)slot * c.scr.stride;
+    if (m > GB_MIN) {                     // the whole grid takes it (k3_rk_big) unless the list is full
+        uint32_t o = 0;
+        if (lane == 0) o = atomicAdd(&c.L.ctr[C_GB], 1u);
+        o = (uint32_t)__shfl((int)o, 0, 64);
+        if (o < GB_MAXN) {
+            if (lane == 0) c.L.gb[o] = item;
+            return;
+        }
+    }
     for (uint32_t q = s + lane; q < s + m; q += 64) c.scr.RK[so + c.scr.SA[so + q]] = s;
+}
+
+__global__ void __launch_bounds__(256) k3_rk_big(Ctx c)
+{
+    const uint32_t ng = min(c.L.ctr[C_GB], GB_MAXN);
+    const uint32_t step = gridDim.x * 256u;
+    for (uint32_t q = 0; q < ng; ++q) {
+        const uint64_t item = c.L.gb[q];
+        const uint32_t slot = it_slot(item), s = it_start(item), m = it_size(item);
+        const uint64_t so = (uint64_t)slot * c.scr.stride;
+        for (uint32_t i = blockIdx.x * 256u + threadIdx.x; i < m; i += step) c.scr.RK[so + c.scr.SA[so + s + i]] = s;
+    }
 }
 
 __global__ void k3_round_end(Ctx c, uint32_t nb)
@@ -2703,6 +2763,13 @@ __global__ void __launch_bounds__(256) k3_period(Ctx c)
 
 }  // namespace
 
+// zero the counters whose bits are set (one launch instead of a memset each)
+__global__ void k3_zero(uint32_t* __restrict__ ctr, uint64_t mask)
+{
+    const uint32_t i = threadIdx.x;
+    if (i < 64 && ((mask >> i) & 1ull)) ctr[i] = 0;
+}
+
 // Host orchestration.  A handful of host round trips per batch (list sizes).
 bool bwt_kmat()
 {
@@ -2729,8 +2796,7 @@ bool launch_bwt3(BlockDesc* blocks, uint32_t b0, uint32_t nb, const uint8_t* blk
     const uint64_t nwg_bin = BIN_MAXWG;
     const uint64_t nb_bins = nb < 64 ? 8ull * nb : nb;     // bins of k3_bin_* (see bin_of)
     constexpr uint32_t QSETS = 64, QSET = 8 * XQ_STRIDE + 32;   // queue heads (a line each) + segments per launch
-    const uint64_t hg_words = 2ull * HG_MAXN + HG_MAXN + (uint64_t)HG_MAXCH * 256 + (uint64_t)HG_MAXN * 256 +
-                              3ull * GB_MAXN + 64;
+    const uint64_t hg_words = 2ull * HG_MAXN + (uint64_t)HG_MAXN * 512 + 3ull * GB_MAXN + 64;
     const uint64_t words = 2 * C_N + 14ull * nb + QSETS * QSET + nwg_bin * nb_bins +
                            2 * (cap_s + cap_s2 + cap_m0 + cap_m1 + cap_m2 + cap_m3 + 2 * cap_l) + 64 + hg_words;
     uint32_t* mw = meta.as<uint32_t>(words);
@@ -2765,12 +2831,9 @@ bool launch_bwt3(BlockDesc* blocks, uint32_t b0, uint32_t nb, const uint8_t* blk
         q = (q + 7) & ~(uintptr_t)7;
         c.L.hg = reinterpret_cast<uint64_t*>(q);
         c.L.gb = c.L.hg + HG_MAXN;
-        c.L.hg_base = reinterpret_cast<uint32_t*>(c.L.gb + GB_MAXN);
-        c.L.gb_h = c.L.hg_base + HG_MAXN;
+        c.L.gb_h = reinterpret_cast<uint32_t*>(c.L.gb + GB_MAXN);
         c.L.hg_info = c.L.gb_h + GB_MAXN;
-        c.L.hg_hist = c.L.hg_info + (uint64_t)HG_MAXN * 256;
-        if (reinterpret_cast<uintptr_t>(c.L.hg_hist + (uint64_t)HG_MAXCH * 256) >
-            reinterpret_cast<uintptr_t>(mw + words))
+        if (reinterpret_cast<uintptr_t>(c.L.hg_info + (uint64_t)HG_MAXN * 512) > reinterpret_cast<uintptr_t>(mw + words))
             throw StarchError(-10, "bwt3: meta layout");
     }
     c.L.w = reinterpret_cast<uint64_t*>(scr.U);
@@ -2791,6 +2854,9 @@ bool launch_bwt3(BlockDesc* blocks, uint32_t b0, uint32_t nb, const uint8_t* blk
     static const bool period_off = [] { const char* e = getenv("STARCH_PERIOD_CHECK"); return e && !strcmp(e, "0"); }();
     if (!period_off) hipLaunchKernelGGL(k3_period, dim3(nb), dim3(256), 0, st, c);
 
+    static_assert(C_N <= 64, "k3_zero masks");
+    auto zero = [&](uint64_t mask) { hipLaunchKernelGGL(k3_zero, dim3(1), dim3(64), 0, st, c.L.ctr, mask); };
+    auto bit = [](uint32_t i) { return 1ull << i; };
     uint32_t qnext = 0;
     auto next_q = [&](uint32_t*& head, uint32_t*& seg) {
         if (qnext == QSETS) {
@@ -2845,13 +2911,13 @@ bool launch_bwt3(BlockDesc* blocks, uint32_t b0, uint32_t nb, const uint8_t* blk
             if (level > 64) throw StarchError(-10, "bwt3: partition did not converge");
             const bool huge = hctr[C_LM0 + lsel] > HG_MIN;
             if (huge) {   // groups above HG_MIN: partitioned by the whole grid
-                HIP_CHECK(hipMemsetAsync(c.L.ctr + C_HG, 0, 2 * sizeof(uint32_t), st));
+                zero(bit(C_HG) | bit(C_HGC));
+                HIP_CHECK(hipMemsetAsync(c.L.hg_info, 0, (uint64_t)HG_MAXN * 512 * sizeof(uint32_t), st));
                 hipLaunchKernelGGL(k3_hg_pick, dim3((nl + 255) / 256), dim3(256), 0, st, c, c.L.l[lsel], nl);
             }
             bin(c.L.l[lsel], nl, bout);
             c.lsel = lsel ^ 1u;
-            HIP_CHECK(hipMemsetAsync(c.L.ctr + C_L0 + (lsel ^ 1u), 0, sizeof(uint32_t), st));
-            HIP_CHECK(hipMemsetAsync(c.L.ctr + C_LM0 + (lsel ^ 1u), 0, sizeof(uint32_t), st));
+            zero(bit(C_L0 + (lsel ^ 1u)) | bit(C_LM0 + (lsel ^ 1u)));
             if (huge) {
                 const dim3 gh(ncu * 4);
                 if (c.keysrc) hipLaunchKernelGGL(k3_hg_hist<true>, gh, dim3(256), 0, st, c);
@@ -2868,8 +2934,7 @@ bool launch_bwt3(BlockDesc* blocks, uint32_t b0, uint32_t nb, const uint8_t* blk
             if (c.keysrc) hipLaunchKernelGGL(k3_part_l<true>, dim3(ncu * STARCH_PL_WG), dim3(LT), 0, st, c, bout);
             else hipLaunchKernelGGL(k3_part_l<false>, dim3(ncu * STARCH_PL_WG), dim3(LT), 0, st, c, bout);
             HIP_CHECK(hipGetLastError());
-            HIP_CHECK(hipMemsetAsync(c.L.ctr + C_L0 + lsel, 0, sizeof(uint32_t), st));
-            HIP_CHECK(hipMemsetAsync(c.L.ctr + C_LM0 + lsel, 0, sizeof(uint32_t), st));
+            zero(bit(C_L0 + lsel) | bit(C_LM0 + lsel));
             lsel ^= 1u;
         }
         c.lsel = 0;
@@ -2894,7 +2959,7 @@ bool launch_bwt3(BlockDesc* blocks, uint32_t b0, uint32_t nb, const uint8_t* blk
         // then the groups it listed as hard (k3_sort_lds) from the class list it consumed.
         // Doubling rounds (keys in K/K2) run their own instantiations.
         const uint32_t* hard_n = c.L.ctr + C_H;
-        auto clear_h = [&]() { HIP_CHECK(hipMemsetAsync(c.L.ctr + C_H, 0, sizeof(uint32_t), st)); };
+        auto clear_h = [&]() { zero(bit(C_H)); };
         auto sstat = [&](const char* name) {
 #ifdef STARCH_SORT_STATS
             HIP_CHECK(hipMemcpyAsync(hctr, c.L.ctr, C_N * sizeof(uint32_t), hipMemcpyDeviceToHost, st));
@@ -2982,8 +3047,7 @@ bool launch_bwt3(BlockDesc* blocks, uint32_t b0, uint32_t nb, const uint8_t* blk
         if (c.keysrc) leaf(std::true_type{});
         else leaf(std::false_type{});
         HIP_CHECK(hipGetLastError());
-        HIP_CHECK(hipMemsetAsync(c.L.ctr + C_W, 0, 6 * sizeof(uint32_t), st));
-        HIP_CHECK(hipMemsetAsync(c.L.ctr + C_M0, 0, sizeof(uint32_t), st));
+        zero((0x3Full << C_W) | bit(C_M0));
     };
 
     // ---- round 0: packed prefix keys gathered from the PSS by every sort, as
@@ -3042,12 +3106,11 @@ bool launch_bwt3(BlockDesc* blocks, uint32_t b0, uint32_t nb, const uint8_t* blk
         c.rtext = rtext;
         const uint32_t cur = c.tsel;
         c.tsel ^= 1u;
-        HIP_CHECK(hipMemsetAsync(c.L.ctr + C_T0 + c.tsel, 0, sizeof(uint32_t), st));
-        HIP_CHECK(hipMemsetAsync(c.L.ctr + C_TS0 + c.tsel, 0, sizeof(uint32_t), st));
+        zero(bit(C_T0 + c.tsel) | bit(C_TS0 + c.tsel));
         hipLaunchKernelGGL(k3_classify_text, dim3((nt + 256 * CT_IPT - 1) / (256 * CT_IPT)), dim3(256), 0, st, c,
                            c.L.t[cur], nt);
         HIP_CHECK(hipGetLastError());
-        HIP_CHECK(hipMemsetAsync(c.L.ctr + C_T0 + cur, 0, sizeof(uint32_t), st));
+        zero(bit(C_T0 + cur));
         sort_groups();
     }
     // ---- prefix doubling on the blocks still tied ----
@@ -3056,7 +3119,9 @@ bool launch_bwt3(BlockDesc* blocks, uint32_t b0, uint32_t nb, const uint8_t* blk
         const uint64_t* T = c.L.t[c.tsel];
         hipLaunchKernelGGL(k3_mark_tied, dim3((nt + 255) / 256), dim3(256), 0, st, c, T, nt);
         hipLaunchKernelGGL(k3_rk_dense, dim3(64, nb), dim3(256), 0, st, c);
+        zero(bit(C_GB));
         hipLaunchKernelGGL(k3_rk_groups, dim3((nt + 3) / 4), dim3(256), 0, st, c, T, nt);
+        hipLaunchKernelGGL(k3_rk_big, dim3(ncu * 4), dim3(256), 0, st, c);
         HIP_CHECK(hipGetLastError());
         c.mode = 1;
         c.keysrc = 1;
@@ -3067,13 +3132,11 @@ bool launch_bwt3(BlockDesc* blocks, uint32_t b0, uint32_t nb, const uint8_t* blk
             if (round > 40) throw StarchError(-10, "bwt3: doubling did not converge");
             const uint32_t cur = c.tsel;
             c.tsel ^= 1u;
-            HIP_CHECK(hipMemsetAsync(c.L.ctr + C_T0 + c.tsel, 0, sizeof(uint32_t), st));
-            HIP_CHECK(hipMemsetAsync(c.L.ctr + C_TS0 + c.tsel, 0, sizeof(uint32_t), st));
-            HIP_CHECK(hipMemsetAsync(c.L.ctr + C_GB, 0, sizeof(uint32_t), st));
+            zero(bit(C_T0 + c.tsel) | bit(C_TS0 + c.tsel) | bit(C_GB));
             hipLaunchKernelGGL(k3_gather, dim3((n2 + 255) / 256), dim3(256), 0, st, c, c.L.t[cur], n2, round, rtext);
             hipLaunchKernelGGL(k3_gather_big, dim3(ncu * 4), dim3(256), 0, st, c);
             HIP_CHECK(hipGetLastError());
-            HIP_CHECK(hipMemsetAsync(c.L.ctr + C_T0 + cur, 0, sizeof(uint32_t), st));
+            zero(bit(C_T0 + cur));
             sort_groups();
             hipLaunchKernelGGL(k3_round_end, dim3((nb + 255) / 256), dim3(256), 0, st, c, nb);
         }

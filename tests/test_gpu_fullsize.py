@@ -63,40 +63,41 @@ def test_fullsize_unstarch_round_trip(cfg):
     c.close()
 
 
-def test_cfg5_chr1_chr21_chrY_fullsize():
-    """cfg5 (per-position BED, every base of hg38) at full size for chr1
-    (248,956,422 lines, 6.0 GB -- the largest stream), chr21 and chrY:
-    each stream's SHA-256 equals the CPU path's (tests/golden/
-    fullsize_cfg5.json), and the byte-identical "0\\n" blocks are sorted once
-    (exact block reuse: at most a handful of distinct blocks per stream, the
-    rest dedup'd -- the BWT of bz:blocksort.c:1031-1089 is a pure function of
-    the block bytes)."""
-    import ctypes
+def test_cfg5_all_24_fullsize():
+    """cfg5 (per-position BED, every base of hg38: 3.09 G lines, 73.6 GB) at
+    full size, all 24 chromosomes: each chromosome's input is generated in HBM
+    by the GPU (starch_gen_perpos_device, the same bytes as starch_gen_bed
+    kind 2) and encoded; every stream's SHA-256 equals the CPU path's
+    (tests/golden/fullsize_cfg5.json), and the byte-identical "0\\n" blocks
+    are sorted once (exact block reuse: a handful of distinct blocks per
+    stream -- the BWT of bz:blocksort.c:1031-1089 is a pure function of the
+    block bytes)."""
     import torch
     import starch_amd
     g = json.load(open(os.path.join(GOLDEN, "fullsize_cfg5.json")))
     want = {s["chromosome"]: s for s in g["streams"]}
-    chroms = [starch_amd.HG38.index(c) for c in ("chr1", "chr21", "chrY")]
-    sizes = starch_amd.gen_bed_sizes(2, 0, chroms, seed=g["seed"])
-    for c, sz in zip(("chr1", "chr21", "chrY"), sizes):
-        assert sz == want[c]["input_bytes"], c
-    n = sum(sizes)
-    host = torch.empty(n, dtype=torch.uint8, pin_memory=True)
-    starch_amd.gen_bed(2, 0, chroms, seed=g["seed"], into=ctypes.c_void_p(host.data_ptr()))
-    dev = host.to("cuda")
-    del host
+    assert len(want) == 24
+    cap = max(starch_amd.gen_perpos_device(c) for c in range(24))
+    dev = torch.empty(cap + 64, dtype=torch.uint8, device="cuda")
     c = starch_amd.Starch(0)
-    c.compress_device(dev.data_ptr(), n)
-    st = c.stats()
-    idx, streams = starch_amd.parse_archive(c.archive())
-    assert [m["chromosome"] for m in idx["streams"]] == ["chr1", "chr21", "chrY"]
-    for s, meta in zip(streams, idx["streams"]):
-        w = want[meta["chromosome"]]
+    stream = torch.cuda.current_stream()
+    c.set_stream(stream.cuda_stream)
+    done = 0
+    for ci, name in enumerate(starch_amd.HG38):
+        n = starch_amd.gen_perpos_device(ci, dev.data_ptr(), cap + 64, stream=stream.cuda_stream)
+        w = want[name]
+        assert n == w["input_bytes"], name
+        c.compress_device(dev.data_ptr(), n)
+        st = c.stats()
+        idx, streams = starch_amd.parse_archive(c.archive())
+        assert [m["chromosome"] for m in idx["streams"]] == [name]
+        meta, s = idx["streams"][0], streams[0]
         assert meta["uncompressedLineCount"] == w["lines"]
         assert meta["transformedBytes"] == w["text_bytes"]
-        assert len(s) == w["stream_bytes"], meta["chromosome"]
-        assert hashlib.sha256(s).hexdigest() == w["sha256"], meta["chromosome"]
-    nblk = sum(m["blocks"] for m in idx["streams"])
-    assert st["n_blocks"] == nblk and nblk > 700   # 553 + 104 + 127 full blocks + tails
-    assert 0 < st["dedup_blocks"] and st["dedup_blocks"] >= nblk - 4 * 3, (st["dedup_blocks"], nblk)
+        assert len(s) == w["stream_bytes"], name
+        assert hashlib.sha256(s).hexdigest() == w["sha256"], name
+        assert st["n_blocks"] == meta["blocks"]
+        assert st["n_blocks"] - st["dedup_blocks"] <= 4, (name, st["n_blocks"], st["dedup_blocks"])
+        done += 1
+    assert done == 24
     c.close()

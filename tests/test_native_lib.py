@@ -75,3 +75,17 @@ def test_build_index_roundtrip():
     j = json.loads(blob[:-32])
     assert j["streams"][0]["chromosome"] == "ch\"1"
     assert j["archive"]["note"] == "n"
+
+
+def test_gen_perpos_sizes_match_host_generator():
+    """starch_gen_perpos_device's byte count (closed-form digit sums, no GPU
+    needed to size) equals the host generator's (tests/golden/fullsize_cfg5.json
+    holds all 24 input sizes; the GPU test checks those)."""
+    import starch_amd
+    chroms = [13, 14, 23]                     # chr21, chr22, chrY (the host sizer walks every line)
+    host = starch_amd.gen_bed_sizes(2, 0, chroms)
+    for c, h in zip(chroms, host):
+        assert starch_amd.gen_perpos_device(c) == h, c
+    assert starch_amd.gen_perpos_device(0, first=0, count=0) == 0
+    # a piece: lines [9, 11) of chr1 = "chr1\t9\t10\n" + "chr1\t10\t11\n"
+    assert starch_amd.gen_perpos_device(0, first=9, count=2) == len(b"chr1\t9\t10\nchr1\t10\t11\n")
