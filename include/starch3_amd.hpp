@@ -51,6 +51,7 @@
 #include <cstdlib>
 #include <cstring>
 #include <string>
+#include <thread>
 #include <vector>
 
 #include "starch_amd.h"
@@ -318,23 +319,16 @@ public:
     // streaming session (starch_stream_*) -- the input is read in 16 MiB
     // pieces straight into the session's pinned window and the archive bytes
     // are written as they finish, so memory stays at about two batches
-    // (hpp:158-199 reads line by line).  Several devices: read whole, then
-    // starch_encode_multi_host.
+    // (hpp:158-199 reads line by line).  Several devices: batches of whole
+    // chromosome runs (for_each_run_batch), each batch's runs sharded over the
+    // devices (LPT), encoded concurrently and their streams written in input
+    // order; the index of all of them at the end.  Host memory: one batch (or
+    // the longest chromosome run, which one device must encode whole).
     int compress_in_stream(void)
     {
         int rc = open_devices();
         if (rc) return rc;
-        if (_ctx.size() > 1) {
-            std::vector<unsigned char> in, arch;
-            std::vector<unsigned char> buf(1 << 24);
-            size_t k;
-            while ((k = std::fread(&buf[0], 1, buf.size(), _in_stream)) > 0)
-                in.insert(in.end(), buf.begin(), buf.begin() + k);
-            if ((rc = compress(in.empty() ? NULL : &in[0], in.size(), &arch))) return rc;
-            if (arch.size() > 4) std::fwrite(&arch[4], 1, arch.size() - 4, _out_stream);
-            std::fflush(_out_stream);
-            return STARCH_OK;
-        }
+        if (_ctx.size() > 1) return compress_in_stream_multi();
         starch_ctx* c = _ctx[0];
         starch_options o = options();
         if ((rc = starch_stream_begin(c, &o, 0))) return rc;
@@ -363,6 +357,147 @@ public:
         return STARCH_OK;
     }
 
+    // The in stream in batches of whole chromosome runs (units of
+    // starch_plan_units_from): 16 MiB pieces are read until at least `batch`
+    // bytes are held; every run but the last (which may go on) is handed to
+    // f(bytes, units, count); the last run carries over with the sscanf values
+    // current before it (hpp:306-307).  A run longer than a batch is held
+    // whole.  At EOF, or at a 0xFF (which reads as EOF, hpp:181), every run
+    // goes.  Returns the first nonzero status of f.
+    template <class F>
+    int for_each_run_batch(uint64_t batch, F f)
+    {
+        const char* eb = std::getenv("STARCH_HPP_BATCH");   // tests: small batches
+        if (eb && std::atoll(eb) > 0) batch = (uint64_t)std::atoll(eb);
+        std::vector<unsigned char> buf;
+        std::vector<starch_unit> units(4096);
+        int64_t is = 0, ip = 0;
+        bool eof = false;
+        uint64_t want = batch;
+        uint64_t scanned = 0;      // bytes of buf known to hold no newline after the last complete line
+        for (;;) {
+            while (!eof && buf.size() < want) {
+                const size_t o = buf.size();
+                buf.resize(o + (1u << 24));
+                const size_t k = std::fread(&buf[o], 1, 1u << 24, _in_stream);
+                buf.resize(o + k);
+                if (k == 0) eof = true;
+            }
+            uint64_t lim = buf.size();
+            if (!eof) {            // complete lines only
+                while (lim > scanned && buf[lim - 1] != '\n') --lim;
+                if (lim == scanned && (scanned == 0 || buf[scanned - 1] != '\n')) lim = 0;
+            }
+            uint64_t nu = 0;
+            int rc = lim ? starch_plan_units_from(&buf[0], lim, units.size(), is, ip, &units[0], &nu) : STARCH_OK;
+            if (rc) return rc;
+            uint64_t covered = 0;
+            for (uint64_t k = 0; k < nu; ++k) covered = units[k].offset + units[k].length;
+            if (covered < lim) eof = true;        // a 0xFF: the input ends there
+            const uint64_t take = eof ? nu : (nu ? nu - 1 : 0);
+            if (take == 0 && !eof) {              // one run so far: read on
+                scanned = lim;
+                want = buf.size() + batch;
+                continue;
+            }
+            if (take && (rc = f(&buf[0], &units[0], take))) return rc;
+            if (eof) return STARCH_OK;
+            const starch_unit& last = units[nu - 1];
+            is = last.init_start;
+            ip = last.init_stop;
+            buf.erase(buf.begin(), buf.begin() + (std::ptrdiff_t)last.offset);
+            scanned = 0;
+            want = batch;
+        }
+    }
+
+    int compress_in_stream_multi(void)
+    {
+        const starch_options o = options();
+        const int nd = (int)_ctx.size();
+        std::vector<starch_segment> all;
+        std::vector<std::string> all_names;
+        uint64_t end = 4, next_unit = 0;
+        int rc = for_each_run_batch(1ull << 30, [&](const unsigned char* bed, const starch_unit* u, uint64_t n) -> int {
+            std::vector<int32_t> shard(n);
+            int r = starch_assign_shards(u, n, nd, &shard[0]);
+            if (r) return r;
+            std::vector<std::vector<starch_unit> > mine(nd);
+            std::vector<std::vector<uint64_t> > ids(nd);
+            for (uint64_t k = 0; k < n; ++k) {
+                mine[shard[k]].push_back(u[k]);
+                ids[shard[k]].push_back(next_unit + k);
+            }
+            std::vector<int> codes(nd, 0);
+            std::vector<std::thread> th;
+            for (int d = 0; d < nd; ++d)
+                th.push_back(std::thread([&, d]() {
+                    starch_options od = o;
+                    od.emit_index = 0;
+                    codes[d] = mine[d].empty() ? STARCH_OK
+                                               : starch_encode_units_host(_ctx[d], bed, &mine[d][0], &ids[d][0],
+                                                                          mine[d].size(), &od);
+                }));
+            for (size_t t = 0; t < th.size(); ++t) th[t].join();
+            for (int d = 0; d < nd; ++d) if (codes[d]) return codes[d];
+            // every device's segments and streams, then the batch's layout in unit order
+            std::vector<starch_segment> segs;
+            std::vector<std::string> names;
+            std::vector<std::vector<unsigned char> > streams(nd);
+            std::vector<int> dev_of;
+            for (int d = 0; d < nd; ++d) {
+                if (mine[d].empty()) continue;
+                uint64_t ns = 0, sb = 0;
+                const void* dp = NULL;
+                if ((r = starch_segment_count(_ctx[d], &ns)) || (r = starch_streams_device(_ctx[d], &dp, &sb))) return r;
+                streams[d].resize(sb);
+                if (sb && (r = starch_streams_copy(_ctx[d], &streams[d][0], sb))) return r;
+                std::vector<starch_segment> sd(ns + 1);
+                if (ns && (r = starch_segments(_ctx[d], &sd[0], ns))) return r;
+                for (uint64_t k = 0; k < ns; ++k) {
+                    std::string nm(sd[k].name_len, '\0');
+                    uint64_t len = 0;
+                    if ((r = starch_segment_name(_ctx[d], k, nm.empty() ? NULL : &nm[0], nm.size(), &len))) return r;
+                    segs.push_back(sd[k]);
+                    names.push_back(nm);
+                    dev_of.push_back(d);
+                }
+            }
+            const uint64_t ns = segs.size();
+            std::vector<uint64_t> unit_of(ns + 1), bytes(ns + 1), order(ns + 1), off(ns + 1);
+            for (uint64_t k = 0; k < ns; ++k) { unit_of[k] = segs[k].unit; bytes[k] = segs[k].stream_bytes; }
+            uint64_t nend = end;
+            if (ns && (r = starch_archive_layout(&unit_of[0], &bytes[0], ns, end, &order[0], &off[0], &nend))) return r;
+            for (uint64_t j = 0; j < ns; ++j) {
+                const uint64_t k = order[j];
+                const std::vector<unsigned char>& sv = streams[dev_of[k]];
+                if (segs[k].stream_bytes) std::fwrite(&sv[segs[k].stream_offset], 1, segs[k].stream_bytes, _out_stream);
+                starch_segment g = segs[k];
+                g.stream_offset = off[j];
+                all.push_back(g);
+                all_names.push_back(names[k]);
+            }
+            end = nend;
+            next_unit += n;
+            return STARCH_OK;
+        });
+        if (rc) return rc;
+        if (o.emit_index && !o.reference_compat) {
+            std::vector<const char*> np(all.size() + 1);
+            std::vector<uint64_t> nl(all.size() + 1);
+            for (size_t k = 0; k < all.size(); ++k) { np[k] = all_names[k].data(); nl[k] = all_names[k].size(); }
+            uint64_t n = 0;
+            rc = starch_build_index_opt(all.empty() ? NULL : &all[0], &np[0], &nl[0], all.size(), end, &o, NULL, 0, &n);
+            if (rc) return rc;
+            std::vector<char> idx(n + 1);
+            rc = starch_build_index_opt(all.empty() ? NULL : &all[0], &np[0], &nl[0], all.size(), end, &o, &idx[0], n, &n);
+            if (rc) return rc;
+            std::fwrite(&idx[0], 1, n, _out_stream);
+        }
+        std::fflush(_out_stream);
+        return STARCH_OK;
+    }
+
     // The per-chromosome hand-off (hpp:393-407), static as in the reference:
     // the chromosome's transformed text goes through starch3::self's bz_stream
     // (BZ2_bzCompress with BZ_FINISH, on the GPU), its stream to the out stream;
@@ -371,17 +506,28 @@ public:
     static void process_tf_buffer(shared_buffer_t* sb);
 
     // consume_tf_buffer's loop (hpp:371-391) over the GPU transform: the in
-    // stream is transformed on the GPU and every chromosome segment handed to
-    // process_tf_buffer in input order.
+    // stream is read in batches of whole chromosome runs (for_each_run_batch;
+    // memory: one batch, or the longest run -- the reference's tf_buffer
+    // holds a whole chromosome's text too, hpp:409-426), each batch is
+    // transformed on the GPU with the sscanf values current before it, and
+    // every chromosome segment is handed to process_tf_buffer in input order.
     int transform_and_flush_in_stream(void)
     {
-        std::vector<unsigned char> in, buf(1 << 24);
-        size_t k;
-        while ((k = std::fread(&buf[0], 1, buf.size(), _in_stream)) > 0) in.insert(in.end(), buf.begin(), buf.begin() + k);
         int rc = open_devices();
         if (rc) return rc;
         starch_ctx* c = _ctx[0];
-        if ((rc = starch_transform_host(c, in.empty() ? NULL : &in[0], in.size()))) return rc;
+        return for_each_run_batch(256ull << 20, [&](const unsigned char* bed, const starch_unit* u, uint64_t n) -> int {
+            const uint64_t beg = u[0].offset, len = u[n - 1].offset + u[n - 1].length - beg;
+            int r = starch_transform_host_init(c, bed + beg, len, u[0].init_start, u[0].init_stop);
+            if (r) return r;
+            return flush_transformed(c);
+        });
+    }
+
+    // hand every segment of the context's last transform to process_tf_buffer
+    int flush_transformed(starch_ctx* c)
+    {
+        int rc;
         uint64_t nseg = 0, tb = 0;
         if ((rc = starch_segment_count(c, &nseg)) || (rc = starch_text_size(c, &tb))) return rc;
         std::vector<char> text(tb + 1);

@@ -137,6 +137,11 @@ int starch_encode_host_into(starch_ctx* ctx, const void* bed, uint64_t n, const 
  * max_units units (out must hold max_units entries) by galloping + bisection
  * over line starts -- the chromosome runs of a sorted BED, never a full scan. */
 int starch_plan_units(const void* bed, uint64_t n, uint64_t max_units, starch_unit* out, uint64_t* nunits);
+/* The same for bytes that continue an input: (init_start, init_stop) are the
+ * sscanf values current before byte 0 (hpp:306-307; a batch that starts at a
+ * chromosome change whose first lines do not parse keeps them). */
+int starch_plan_units_from(const void* bed, uint64_t n, uint64_t max_units, int64_t init_start, int64_t init_stop,
+                           starch_unit* out, uint64_t* nunits);
 /* Longest-processing-time assignment of units to nshards (by byte length). */
 int starch_assign_shards(const starch_unit* units, uint64_t nunits, int nshards, int32_t* shard_of);
 /* One shard: encode units resident in HBM (offsets relative to d_base, in
@@ -249,6 +254,9 @@ int starch_get_stats(starch_ctx* ctx, starch_stats* out);
 /* Transform stage only: afterwards starch_text_size/starch_text_copy give the
  * concatenated segment texts and starch_segments the per-segment counts. */
 int starch_transform_host(starch_ctx* ctx, const void* bed, uint64_t n);
+/* The same for bytes that start a segment of a longer input, with the sscanf
+ * values current before them (a batch of whole chromosome runs). */
+int starch_transform_host_init(starch_ctx* ctx, const void* bed, uint64_t n, int64_t init_start, int64_t init_stop);
 int starch_transform_device(starch_ctx* ctx, const void* d_bed, uint64_t n);   /* BED bytes in HBM */
 int starch_text_size(starch_ctx* ctx, uint64_t* n);
 int starch_text_copy(starch_ctx* ctx, void* dst, uint64_t cap);

@@ -1696,6 +1696,20 @@ constexpr int sort_wpe(int NW, int E)
            : (NW == 1 ? (E == 2 ? STARCH_WPE_S : STARCH_WPE_GRP) : 1);
 }
 
+// STARCH_SORT_PROF (timing experiment, dev builds only): per-wave shader-clock
+// time of the sorts' phases, summed over the launch: k3_sort_grp into
+// g_sprof, the workgroup sorts k3_sort_lds<8|16, 4> (M2/M3) and <4, 4> (M1)
+// into g_sprof2
+#ifdef STARCH_SORT_PROF
+__device__ unsigned long long g_sprof[16];
+__device__ unsigned long long g_sprof2[16];
+#define SPROF(v) const uint64_t v = __builtin_readcyclecounter()
+#define SPACC(i, a, b) pacc[i] += (b) - (a)
+#else
+#define SPROF(v)
+#define SPACC(i, a, b)
+#endif
+
 template <int NW, int E, bool DBL>
 __global__ void __launch_bounds__(NW > 4 ? 64 * NW : 256) __attribute__((amdgpu_waves_per_eu(sort_wpe(NW, E))))
 k3_sort_lds(Ctx c, const uint64_t* __restrict__ items,
@@ -1790,7 +1804,11 @@ k3_sort_lds(Ctx c, const uint64_t* __restrict__ items,
     grp_load_keys<NW, E, DBL>(c, cur, wid, lane);
     nxt.item = it1 != NONE ? items[it1] : 0ull;
     grp_load_vals<NW, E>(c, nxt, it1 != NONE, wid, lane);
+#ifdef STARCH_SORT_PROF
+    uint64_t pacc[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+#endif
     while (it != NONE) {
+    SPROF(t0);
     const uint64_t item = cur.item;
     const uint32_t slot = it_slot(item), s = it_start(item), m = it_size(item);
     grp_finish_keys<NW, E, DBL>(cur);
@@ -1819,6 +1837,8 @@ k3_sort_lds(Ctx c, const uint64_t* __restrict__ items,
         for (int w = 0; w < NW; ++w) diff |= red_all[w0 + w];
     }
     if ((diff >> KEYB) && tid % (64 * NW) == 0) atomicOr(&c.L.ctr[C_ERR], 1u);   // top bits not shared
+    SPROF(t1);
+    SPACC(0, t0, t1);
 
     bool moved = false;
     const uint64_t kdiff = diff & KMASK;
@@ -1882,6 +1902,9 @@ k3_sort_lds(Ctx c, const uint64_t* __restrict__ items,
 #pragma unroll
             for (int e = 0; e < E; ++e) k[e] = xk[wid * 64 * E + e * 64 + lane];
         };
+#ifdef STARCH_SORT_PROF
+        pacc[1] += __builtin_readcyclecounter() - t1;
+#endif
         if (mx <= LIMIT) {                         // uniform per group
 #pragma unroll
             for (int q = 0; q < BPT; ++q) { bst[tg * BPT + q] = run; bcur[tg * BPT + q] = run; run += loc[q]; }
@@ -2019,6 +2042,8 @@ k3_sort_lds(Ctx c, const uint64_t* __restrict__ items,
             gsync<NW>();                           // bcur/sc reads done before the LSD passes
         }
     }
+    SPROF(t3);
+    SPACC(2, t1, t3);
     if (!moved && kdiff && tid % (64 * NW) == 0) atomicAdd(&c.L.ctr[C_DBGL], 1u);
 #ifdef STARCH_SORT_STATS
     if (tid % (64 * NW) == 0) { atomicAdd(&c.L.ctr[C_STG], 1u); atomicAdd(&c.L.ctr[C_STE], m); }
@@ -2134,6 +2159,8 @@ k3_sort_lds(Ctx c, const uint64_t* __restrict__ items,
             for (int e = 0; e < E; ++e) hp[e] = hp[e] > pre ? hp[e] : pre;
         }
     }
+    SPROF(t4);
+    SPACC(3, t3, t4);
     // the group's rotations and keys were consumed into registers/LDS (their
     // loads complete) before any write of its SA range; the loads in flight
     // now belong to other groups' disjoint ranges
@@ -2163,6 +2190,8 @@ k3_sort_lds(Ctx c, const uint64_t* __restrict__ items,
             tb += (uint32_t)__popcll(tm[e]);
         }
     }
+    SPROF(t5);
+    SPACC(4, t4, t5);
     // rotate the pipeline
     const uint32_t it2 = it1 != NONE ? next_item() : NONE;
     cur = nxt;
@@ -2170,7 +2199,14 @@ k3_sort_lds(Ctx c, const uint64_t* __restrict__ items,
     grp_load_vals<NW, E>(c, nxt, it2 != NONE, wid, lane);
     it = it1;
     it1 = it2;
+    SPROF(t6);
+    SPACC(5, t5, t6);
+    SPACC(7, t0, t6);
     }
+#ifdef STARCH_SORT_PROF
+    if (lane == 0 && E == 4 && NW >= 4 && !DBL)
+        for (int q = 0; q < 8; ++q) atomicAdd(&g_sprof2[q + (NW == 4 ? 8 : 0)], (unsigned long long)pacc[q]);
+#endif
     tacc = wave_reduce_add<uint32_t>(tacc);
     if (lane == 0 && tacc) atomicAdd(c.L.ctr + C_TS0 + c.tsel, tacc);
 }
@@ -2191,16 +2227,6 @@ k3_sort_lds(Ctx c, const uint64_t* __restrict__ items,
 #endif
 constexpr uint32_t HARD_Q = STARCH_HARD_Q;
 
-// STARCH_SORT_PROF (timing experiment, dev builds only): per-wave shader-clock
-// time of k3_sort_grp's phases, summed over the launch into g_sprof
-#ifdef STARCH_SORT_PROF
-__device__ unsigned long long g_sprof[16];
-#define SPROF(v) const uint64_t v = __builtin_readcyclecounter()
-#define SPACC(i, a, b) pacc[i] += (b) - (a)
-#else
-#define SPROF(v)
-#define SPACC(i, a, b)
-#endif
 
 template <int NW, int E, bool DBL>
 __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(sort_wpe(NW, E))))
@@ -3156,6 +3182,15 @@ bool launch_bwt3(BlockDesc* blocks, uint32_t b0, uint32_t nb, const uint8_t* blk
             for (int q = 0; q < 8; ++q)
                 fprintf(stderr, "[sprof] E=%d %-18s %14llu (%.1f%%)\n", e ? 4 : 2, nm[q], h[8 * e + q],
                         100.0 * (double)h[8 * e + q] / (double)(h[8 * e + 7] ? h[8 * e + 7] : 1));
+        unsigned long long h2[16];
+        HIP_CHECK(hipMemcpyFromSymbol(h2, HIP_SYMBOL(g_sprof2), sizeof(h2)));
+        HIP_CHECK(hipMemcpyToSymbol(HIP_SYMBOL(g_sprof2), zero, sizeof(zero)));
+        const char* nm2[8] = {"finish-keys+diff", "digit count+scan", "scatter+rank", "ties+heads", "emit",
+                              "rotate+next-vals", "-", "total"};
+        for (int e = 0; e < 2; ++e)
+            for (int q = 0; q < 8; ++q)
+                fprintf(stderr, "[sprof2] %s %-18s %14llu (%.1f%%)\n", e ? "M1" : "M2/M3", nm2[q], h2[8 * e + q],
+                        100.0 * (double)h2[8 * e + q] / (double)(h2[8 * e + 7] ? h2[8 * e + 7] : 1));
     }
 #endif
     return !done;   // prefix doubling ran: some block may be periodic (flags bit 0)

@@ -1549,10 +1549,16 @@ int starch_encode_multi_host(starch_ctx* const* ctxs, int nctx, const void* bed,
 
 int starch_plan_units(const void* bed, uint64_t n, uint64_t max_units, starch_unit* out, uint64_t* nunits)
 {
+    return starch_plan_units_from(bed, n, max_units, 0, 0, out, nunits);
+}
+
+int starch_plan_units_from(const void* bed, uint64_t n, uint64_t max_units, int64_t init_start, int64_t init_stop,
+                           starch_unit* out, uint64_t* nunits)
+{
     if (!nunits || !out || max_units < 1 || (n && !bed)) return STARCH_ERR_ARG;
     try {
         std::vector<shard::Unit> u;
-        shard::plan_units(static_cast<const uint8_t*>(bed), n, max_units, u);
+        shard::plan_units(static_cast<const uint8_t*>(bed), n, max_units, u, init_start, init_stop);
         for (size_t k = 0; k < u.size(); ++k)
             out[k] = starch_unit{u[k].offset, u[k].length, u[k].init_start, u[k].init_stop};
         *nunits = u.size();
@@ -1655,14 +1661,13 @@ int starch_get_stats(starch_ctx* c, starch_stats* out)
 
 // transform stage only on device-resident BED bytes (segments: stream_offset =
 // offset of the segment's text in the text buffer)
-static void transform_only(starch_ctx* c, const uint8_t* d, uint64_t n)
+static void transform_only(starch_ctx* c, const uint8_t* d, uint64_t n, int64_t init_start = 0, int64_t init_stop = 0)
 {
-    hipEvent_t e0, e1;
-    HIP_CHECK(hipEventCreate(&e0));
-    HIP_CHECK(hipEventCreate(&e1));
+    hipEvent_t* tv = c->timers();
+    hipEvent_t e0 = tv[0], e1 = tv[1];
     HIP_CHECK(hipEventRecord(e0, c->st));
     TransformResult tr;
-    c->tf.run(d, n, c->st, tr);
+    c->tf.run(d, n, c->st, tr, init_start, init_stop);
     HIP_CHECK(hipEventRecord(e1, c->st));
     std::vector<SegInfo> si(tr.n_segments);
     if (tr.n_segments)
@@ -1696,11 +1701,16 @@ static void transform_only(starch_ctx* c, const uint8_t* d, uint64_t n)
 
 int starch_transform_host(starch_ctx* c, const void* bed, uint64_t n)
 {
+    return starch_transform_host_init(c, bed, n, 0, 0);
+}
+
+int starch_transform_host_init(starch_ctx* c, const void* bed, uint64_t n, int64_t init_start, int64_t init_stop)
+{
     GUARD(c)
     if (n && !bed) return STARCH_ERR_ARG;
     uint8_t* d = c->input.as<uint8_t>(n + 64);
     if (n) HIP_CHECK(hipMemcpyAsync(d, bed, n, hipMemcpyHostToDevice, c->st));
-    transform_only(c, d, n);
+    transform_only(c, d, n, init_start, init_stop);
     return STARCH_OK;
     END_GUARD(c)
 }

@@ -1133,6 +1133,14 @@ __device__ __forceinline__ void fused_lines(FusedShared& S, const uint8_t* tb, u
 #ifndef STARCH_TF_WPE
 #define STARCH_TF_WPE 6
 #endif
+// STARCH_TF_PROF (timing experiment, dev builds only): per-wave shader-clock
+// time of k_tf_fused's phases, summed into g_tfprof (printed by run())
+#ifdef STARCH_TF_PROF
+__device__ unsigned long long g_tfprof[8];
+#define TPROF(v) const uint64_t v = __builtin_readcyclecounter()
+#else
+#define TPROF(v)
+#endif
 __global__ void __launch_bounds__(kThreads) __attribute__((amdgpu_waves_per_eu(STARCH_TF_WPE)))
 k_tf_fused(const uint8_t* __restrict__ bed, uint64_t n, uint32_t* __restrict__ tile_ctr,
            uint64_t* __restrict__ aw, uint64_t* __restrict__ iw,
@@ -1141,6 +1149,7 @@ k_tf_fused(const uint8_t* __restrict__ bed, uint64_t n, uint32_t* __restrict__ t
 {
     __shared__ FusedShared S;
     const uint32_t tid = threadIdx.x, lane = tid & 63;
+    TPROF(p0);
     if (tid == 0) {
         S.tile = atomicAdd(tile_ctr, 1u);
         S.ffpos = 0xFFFFFFFFu;
@@ -1162,6 +1171,7 @@ k_tf_fused(const uint8_t* __restrict__ bed, uint64_t n, uint32_t* __restrict__ t
         for (uint32_t w = tid; w < nw; w += kThreads) S.tb4[w] = src[w];
     }
     __syncthreads();
+    TPROF(p1);
     const uint8_t* tb = reinterpret_cast<const uint8_t*>(S.tb4);
     const uint32_t Lt0 = (uint32_t)(t0 - a0), Lend = (uint32_t)(tend - a0), Ls0 = (uint32_t)(s0 - a0);
     // newline / 0xFF masks of 32-byte LDS chunks covering [Lt0, Lend); a thread
@@ -1284,10 +1294,12 @@ k_tf_fused(const uint8_t* __restrict__ bed, uint64_t n, uint32_t* __restrict__ t
         S.wlast[0] = pk;
     }
     __syncthreads();
+    TPROF(p2);
     uint64_t bytes = 0;
     uint32_t segs = 0;
     if (!fallback && nl_tile > 0)
         fused_lines(S, tb, a0, nl_tile, first_ls, input_start, xflags, bytes, segs, prev_ls, prev_in_lines);
+    TPROF(p3);
     fallback = fallback || S.over;
     if (fallback && tid == 0) atomicOr(xflags, FX_FALLBACK);
     const TileAgg local{bytes, fallback ? 0ull : nl_tile, segs, ffpos != 0xFFFFFFFFu ? 1ull : 0ull};
@@ -1363,6 +1375,15 @@ k_tf_fused(const uint8_t* __restrict__ bed, uint64_t n, uint32_t* __restrict__ t
         }
     }
     __syncthreads();
+    TPROF(p4);
+#ifdef STARCH_TF_PROF
+    if (lane == 0) {
+        atomicAdd(&g_tfprof[0], (unsigned long long)(p1 - p0));
+        atomicAdd(&g_tfprof[1], (unsigned long long)(p2 - p1));
+        atomicAdd(&g_tfprof[2], (unsigned long long)(p3 - p2));
+        atomicAdd(&g_tfprof[3], (unsigned long long)(p4 - p3));
+    }
+#endif
     const TileAgg excl = S.excl;
     if (excl.ff || fallback || nl_tile == 0) return;   // dropped after an earlier 0xFF, or nothing here
     const uint64_t o0 = excl.bytes;
@@ -1390,6 +1411,13 @@ k_tf_fused(const uint8_t* __restrict__ bed, uint64_t n, uint32_t* __restrict__ t
         dst[w] = (uint32_t)ob[q] | ((uint32_t)ob[q + 1] << 8) | ((uint32_t)ob[q + 2] << 16) | ((uint32_t)ob[q + 3] << 24);
     }
     for (uint32_t k = head + 4u * nw4 + tid; k < wl; k += kThreads) text[o0 + k] = ob[k];
+#ifdef STARCH_TF_PROF
+    TPROF(p5);
+    if (lane == 0) {
+        atomicAdd(&g_tfprof[4], (unsigned long long)(p5 - p4));
+        atomicAdd(&g_tfprof[5], 1ull);
+    }
+#endif
 }
 
 // line_count / text_len of each segment from its successor; totals on the device
@@ -1590,6 +1618,19 @@ void TransformWorkspace::run(const uint8_t* d_bed, uint64_t n, hipStream_t st, T
             scap = std::max(scap, h[1] + 1);
             continue;
         }
+#ifdef STARCH_TF_PROF
+        {
+            unsigned long long g[8];
+            HIP_CHECK(hipMemcpyFromSymbol(g, HIP_SYMBOL(g_tfprof), sizeof(g)));
+            static const unsigned long long zero[8] = {};
+            HIP_CHECK(hipMemcpyToSymbol(HIP_SYMBOL(g_tfprof), zero, sizeof(zero)));
+            const char* nm[5] = {"ticket+stage", "masks+nl-scan+halo", "fused_lines", "look-back", "write-out"};
+            const double tot = (double)(g[0] + g[1] + g[2] + g[3] + g[4]);
+            for (int q = 0; q < 5; ++q)
+                fprintf(stderr, "[tfprof] %-20s %14llu (%.1f%%)\n", nm[q], g[q], 100.0 * (double)g[q] / (tot ? tot : 1));
+            fprintf(stderr, "[tfprof] waves %llu, cycles per wave-tile %.0f\n", g[5], tot / (double)(g[5] ? g[5] : 1));
+        }
+#endif
         res.n_lines = h[0];
         res.n_segments = h[1];
         res.text_bytes = h[2];

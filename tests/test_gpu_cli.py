@@ -57,3 +57,21 @@ def test_hpp_main_matches_cli(hook):
     want = _run("starch3", [], data)
     got = _run("starch3_hpp_example", ["--hook"] if hook else [], data)
     assert got == want
+
+
+@pytest.mark.parametrize("args", [["--hook"], ["--vdev", "2"], ["--vdev", "3"]])
+def test_hpp_batches_of_chromosome_runs(args, monkeypatch):
+    """transform_and_flush_in_stream and the multi-device compress_in_stream
+    read the input in batches of whole chromosome runs (bounded memory): with
+    64 KiB batches (many batches; runs longer than a batch held whole; stale
+    sscanf values and revisited chromosomes across batch cuts; a 0xFF that
+    ends the input) the archive is the CLI's byte for byte."""
+    import starch_amd
+    monkeypatch.setenv("STARCH_HPP_BATCH", str(64 << 10))
+    runs = corpus.multi_chrom_bed(9, 900, seed=31, kind="bed6")
+    stale = b"chrQ\t10\t20\nchrQ\t30\t45\n" + b"chrR\tq\tz\nchrR\t7\tw\n" * 40 + b"chrS\t5\t9\n"
+    for data in (runs + stale + corpus.fuzz_bed(4, 400) + runs[:30000],
+                 starch_amd.gen_bed(0, 60_000, chroms=[13, 14]) + b"chrZ\t1\t2\n\xffchrZ\t3\t4\n"):
+        want = _run("starch3", [], data)
+        got = _run("starch3_hpp_example", args, data)
+        assert got == want

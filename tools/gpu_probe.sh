@@ -15,6 +15,7 @@ env $ENVS timeout -k 10 ${TB:-300} python3 $ROOT/bench.py $BA --no-cpu-baseline 
     || { tail -20 $O/$TAG.err; exit 1; }
 cat $O/$TAG.json
 if [ -z "${NOPROF:-}" ]; then
+  [ -n "$ENVS" ] && export $ENVS
   rm -rf $O/prof_$TAG
   timeout -k 10 ${TP:-300} rocprofv3 --kernel-trace --stats -d $O/prof_$TAG -o run --output-format csv -- \
       python3 $ROOT/bench.py $BA --no-cpu-baseline --no-verify --no-e2e > $O/$TAG.prof.log 2>&1 \

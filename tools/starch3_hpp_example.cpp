@@ -18,8 +18,15 @@ int main(int argc, char** argv)
 {
     starch3::Starch starch;
     starch3::self = &starch;
-    bool hook = argc > 1 && std::strcmp(argv[1], "--hook") == 0;
-    if (argc > 1 + (hook ? 1 : 0)) starch.set_input_fn(argv[1 + (hook ? 1 : 0)]);
+    // --hook: the per-chromosome hand-off; --vdev N: N virtual devices (all on
+    // GPU 0: the multi-device batch path of compress_in_stream)
+    bool hook = false;
+    int a = 1;
+    for (; a < argc && argv[a][0] == '-' && argv[a][1] == '-'; ++a) {
+        if (std::strcmp(argv[a], "--hook") == 0) hook = true;
+        else if (std::strcmp(argv[a], "--vdev") == 0 && a + 1 < argc) starch.set_devices(std::vector<int>(std::atoi(argv[++a]), 0));
+    }
+    if (a < argc) starch.set_input_fn(argv[a]);
     starch.set_compression_method(starch3::Starch::k_bzip2);
     starch.test_stdin_availability();
     starch.initialize_in_stream();
