@@ -473,7 +473,7 @@ public:
                 const std::vector<unsigned char>& sv = streams[dev_of[k]];
                 if (segs[k].stream_bytes) std::fwrite(&sv[segs[k].stream_offset], 1, segs[k].stream_bytes, _out_stream);
                 starch_segment g = segs[k];
-                g.stream_offset = off[j];
+                g.stream_offset = off[k];          // (the layout's offsets are by segment)
                 all.push_back(g);
                 all_names.push_back(names[k]);
             }

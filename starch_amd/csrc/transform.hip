@@ -943,20 +943,21 @@ __global__ void k_seg_info(const uint64_t* __restrict__ seg_first, uint64_t nseg
 
 
 // --- single-pass transform (default) -----------------------------------------
-// One workgroup per 8 KiB byte tile, taken in order from an atomic counter.  A
-// line belongs to the tile holding its '\n'; the tile is staged in LDS with a
-// 1 KiB halo before it (the start of its first line and the whole previous
-// line, whose chromosome and start/stop the first line depends on).  The
-// workgroup finds its newlines, parses its lines 256 at a time (parse_fast /
-// the byte-serial parser), builds their output in LDS, and learns where it
-// goes from a decoupled look-back over the tiles before it: a tile publishes
-// its (bytes, lines, segments, saw 0xFF) aggregate, then its inclusive prefix;
-// the combine operator stops at the first tile holding a 0xFF (hpp:181: 0xFF
-// reads as EOF), so lines after it vanish.  Input is read once; no per-line
-// array exists in HBM.  Anything outside this shape sets a flag and the host
-// takes the two-pass path: a stale sscanf value (FX_FAIL: general path), a
-// line longer than the halo or a tile of > 2048 lines (FX_FALLBACK), or text /
-// segment capacity (FX_TEXT_CAP / FX_SEG_CAP: grow, rerun).
+// One workgroup per 8 KiB byte tile.  A line belongs to the tile holding its
+// '\n'; the tile is staged in LDS with a 1 KiB halo before it (the start of
+// its first line and the whole previous line, whose chromosome and
+// start/stop the first line depends on).  The workgroup finds its newlines,
+// parses its lines 256 at a time (parse_fast / the byte-serial parser) and
+// builds their output in LDS, then writes it to a bump-allocated piece of an
+// arena with the tile's (bytes, lines, segments) counts and segment records;
+// a 0xFF (hpp:181: EOF) is recorded as the first tile holding one.  Three
+// scans over the tiles give every tile's output offset, k_tf_place moves the
+// arena pieces there and k_tf_segs writes the segment records; tiles after
+// the first 0xFF are dropped.  Input is read once; no per-line array exists
+// in HBM.  Anything outside this shape sets a flag and the host takes the
+// two-pass path: a stale sscanf value (FX_FAIL: general path), a line longer
+// than the halo or a tile of > 2048 lines (FX_FALLBACK), or text / segment
+// capacity (FX_TEXT_CAP / FX_SEG_CAP: grow, rerun).
 #ifndef STARCH_FT
 #define STARCH_FT 8192
 #endif
@@ -967,24 +968,6 @@ constexpr uint32_t kFOut = kFT + kFT / 4;      // LDS output bytes per tile
 static_assert(kFT <= 16384, "tested tile sizes: 4, 8, 16 KiB (8 KiB measured fastest)");
 constexpr uint32_t kFSeg = 64;                 // segment records per tile in LDS
 enum : uint32_t { FX_FAIL = 1, FX_FALLBACK = 2, FX_TEXT_CAP = 4, FX_SEG_CAP = 8 };
-
-struct TileAgg { uint64_t bytes, lines, segs, ff; };
-
-__device__ __forceinline__ TileAgg agg_combine(const TileAgg& x, const TileAgg& y)   // x precedes y
-{
-    if (x.ff) return x;
-    return TileAgg{x.bytes + y.bytes, x.lines + y.lines, x.segs + y.segs, y.ff};
-}
-
-__device__ __forceinline__ TileAgg agg_shfl_up(const TileAgg& v, int d)
-{
-    TileAgg r;
-    r.bytes = __shfl_up(v.bytes, d, 64);
-    r.lines = __shfl_up(v.lines, d, 64);
-    r.segs = __shfl_up(v.segs, d, 64);
-    r.ff = __shfl_up(v.ff, d, 64);
-    return r;
-}
 
 template <class S>
 __device__ __forceinline__ LineVals parse_line_at(const S& bed, uint64_t ls, uint64_t le)
@@ -1006,6 +989,19 @@ __device__ __forceinline__ LineVals parse_line_at(const S& bed, uint64_t ls, uin
 }
 
 struct FusedSeg { uint32_t line, name_ls, name_len, text; };
+struct ArenaSeg { uint32_t tile, q, line, name_len; uint64_t name_off; uint32_t text, pad; };
+struct FusedOut {                  // k_tf_fused's outputs (arena form) and the scans over them
+    uint8_t* arena;                // tiles' texts, bump-allocated (4-byte aligned pieces)
+    uint64_t arena_cap;
+    unsigned long long* arena_ctr;
+    uint32_t *tile_bytes, *tile_lines, *tile_segs;
+    uint64_t* tile_arena;
+    uint32_t* first_ff;            // first tile holding a 0xFF (ntiles: none)
+    ArenaSeg* seg_arena;
+    uint64_t seg_cap;
+    unsigned long long* seg_ctr;
+    uint64_t *bytes_pre, *lines_pre, *segs_pre;   // ntiles + 1 exclusive prefixes
+};
 struct LineKey { int64_t a, b; uint32_t cls, clen; };   // what the next line needs of its predecessor
 
 struct FusedShared {
@@ -1017,7 +1013,7 @@ struct FusedShared {
     FusedSeg seg[kFSeg];
     LineKey wlast[kThreads / 64 + 1];          // [0]: carry into the chunk; [w+1]: wave w's last line
     uint32_t tile, ffpos, p1, p2, over, nul;
-    TileAgg excl;
+    struct { uint64_t bytes, segs; } excl;   // the tile's arena offsets
 };
 
 __device__ __forceinline__ LineKey shfl_up_key(const LineKey& k)
@@ -1142,16 +1138,14 @@ __device__ unsigned long long g_tfprof[8];
 #define TPROF(v)
 #endif
 __global__ void __launch_bounds__(kThreads) __attribute__((amdgpu_waves_per_eu(STARCH_TF_WPE)))
-k_tf_fused(const uint8_t* __restrict__ bed, uint64_t n, uint32_t* __restrict__ tile_ctr,
-           uint64_t* __restrict__ aw, uint64_t* __restrict__ iw,
-           uint8_t* __restrict__ text, uint64_t text_cap, SegInfo* __restrict__ info, uint64_t seg_cap,
-           uint32_t* __restrict__ xflags, uint64_t* __restrict__ totals, uint32_t ntiles, uint32_t dbg_mode)
+k_tf_fused(const uint8_t* __restrict__ bed, uint64_t n, const FusedOut fo, uint32_t* __restrict__ xflags,
+           uint32_t dbg_mode)
 {
     __shared__ FusedShared S;
     const uint32_t tid = threadIdx.x, lane = tid & 63;
     TPROF(p0);
     if (tid == 0) {
-        S.tile = atomicAdd(tile_ctr, 1u);
+        S.tile = blockIdx.x;
         S.ffpos = 0xFFFFFFFFu;
         S.p1 = 0;
         S.p2 = 0;
@@ -1302,122 +1296,102 @@ k_tf_fused(const uint8_t* __restrict__ bed, uint64_t n, uint32_t* __restrict__ t
     TPROF(p3);
     fallback = fallback || S.over;
     if (fallback && tid == 0) atomicOr(xflags, FX_FALLBACK);
-    const TileAgg local{bytes, fallback ? 0ull : nl_tile, segs, ffpos != 0xFFFFFFFFu ? 1ull : 0ull};
     if (dbg_mode == 1) return;                      // timing experiment: parse only
-    // decoupled look-back (wave 0).  Every published word carries its own
-    // valid bit (bit 63), so no fence orders separate stores: aggregates go to
-    // aw[3*tile..], inclusive prefixes to iw[3*tile..], each read and written
-    // with relaxed agent-scope atomics (no cache-wide invalidate per poll).
-    if (tid < 64) {
-        constexpr uint64_t V = 1ull << 63;
-        if (lane < 3) {
-            const uint64_t w = lane == 0 ? local.bytes : lane == 1 ? local.lines : (local.segs | (local.ff << 62));
-            __hip_atomic_store(aw + 3ull * tile + lane, w | V, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        }
-        TileAgg excl{0, 0, 0, 0};
-        int64_t j = (int64_t)tile - 1;
-        while (j >= 0) {
-            const int64_t idx = j - (63 - (int64_t)lane);
-            bool incl_here = true;
-            TileAgg v{0, 0, 0, 0};
-            if (idx >= 0) {
-                for (;;) {
-                    const uint64_t* ip = iw + 3ull * (uint64_t)idx;
-                    const uint64_t x0 = __hip_atomic_load(ip, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-                    const uint64_t x1 = __hip_atomic_load(ip + 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-                    const uint64_t x2 = __hip_atomic_load(ip + 2, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-                    if (x0 & x1 & x2 & V) {
-                        v = TileAgg{x0 & ~V, x1 & ~V, x2 & ((1ull << 62) - 1), (x2 >> 62) & 1ull};
-                        break;
-                    }
-                    const uint64_t* ap = aw + 3ull * (uint64_t)idx;
-                    const uint64_t y0 = __hip_atomic_load(ap, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-                    const uint64_t y1 = __hip_atomic_load(ap + 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-                    const uint64_t y2 = __hip_atomic_load(ap + 2, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-                    if (y0 & y1 & y2 & V) {
-                        v = TileAgg{y0 & ~V, y1 & ~V, y2 & ((1ull << 62) - 1), (y2 >> 62) & 1ull};
-                        incl_here = false;
-                        break;
-                    }
-                    __builtin_amdgcn_s_sleep(1);
-                }
-            }
-            const uint64_t pm = __ballot(incl_here);
-            const int hp = pm ? 63 - __clzll((long long)pm) : -1;   // nearest tile with its inclusive prefix
-            if ((int)lane < hp) v = TileAgg{0, 0, 0, 0};
-#pragma unroll
-            for (int d = 1; d < 64; d <<= 1) {
-                const TileAgg u = agg_shfl_up(v, d);
-                if ((int)lane >= d) v = agg_combine(u, v);
-            }
-            TileAgg w;
-            w.bytes = __shfl(v.bytes, 63, 64);
-            w.lines = __shfl(v.lines, 63, 64);
-            w.segs = __shfl(v.segs, 63, 64);
-            w.ff = __shfl(v.ff, 63, 64);
-            excl = agg_combine(w, excl);
-            if (pm) break;
-            j -= 64;
-        }
-        const TileAgg inc = agg_combine(excl, local);
-        if (lane < 3) {
-            const uint64_t w = lane == 0 ? inc.bytes : lane == 1 ? inc.lines : (inc.segs | (inc.ff << 62));
-            __hip_atomic_store(iw + 3ull * tile + lane, w | V, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        }
-        if (lane == 0) {
-            S.excl = excl;
-            if (tile == ntiles - 1) {
-                totals[0] = inc.lines;
-                totals[1] = inc.segs;
-                totals[2] = inc.bytes;
-                totals[3] = inc.ff;
-            }
-        }
+    TPROF(p4);
+    // No look-back: the tile's text goes to a bump-allocated place in the arena
+    // and its counts to per-tile arrays; k_tf_place moves it to its final
+    // offset after a scan over the tiles.  (Waiting here for the previous
+    // tiles' prefix, with the workgroup's LDS held, took ~65% of the
+    // workgroups' time: STARCH_TF_PROF.)
+    if (tid == 0) {
+        const bool ff = ffpos != 0xFFFFFFFFu;
+        fo.tile_bytes[tile] = fallback ? 0u : (uint32_t)bytes;
+        fo.tile_lines[tile] = fallback ? 0u : nl_tile;
+        fo.tile_segs[tile] = fallback ? 0u : segs;
+        if (ff) atomicMin(fo.first_ff, tile);
+        uint64_t ab = 0, sb = 0;
+        if (!fallback && bytes) ab = atomicAdd(fo.arena_ctr, (bytes + 3) & ~3ull);
+        if (!fallback && segs) sb = atomicAdd(fo.seg_ctr, (uint64_t)segs);
+        S.excl.bytes = ab;
+        S.excl.segs = sb;
+        fo.tile_arena[tile] = ab;
+        if (ab + bytes > fo.arena_cap) atomicOr(xflags, FX_TEXT_CAP);
+        if (sb + segs > fo.seg_cap) atomicOr(xflags, FX_SEG_CAP);
     }
     __syncthreads();
-    TPROF(p4);
-#ifdef STARCH_TF_PROF
-    if (lane == 0) {
-        atomicAdd(&g_tfprof[0], (unsigned long long)(p1 - p0));
-        atomicAdd(&g_tfprof[1], (unsigned long long)(p2 - p1));
-        atomicAdd(&g_tfprof[2], (unsigned long long)(p3 - p2));
-        atomicAdd(&g_tfprof[3], (unsigned long long)(p4 - p3));
-    }
-#endif
-    const TileAgg excl = S.excl;
-    if (excl.ff || fallback || nl_tile == 0) return;   // dropped after an earlier 0xFF, or nothing here
-    const uint64_t o0 = excl.bytes;
-    if (o0 + bytes > text_cap || excl.segs + segs > seg_cap) {
-        if (tid == 0) atomicOr(xflags, o0 + bytes > text_cap ? FX_TEXT_CAP : FX_SEG_CAP);
-        return;
-    }
+    if (fallback || nl_tile == 0) return;
+    const uint64_t ab = S.excl.bytes, sb = S.excl.segs;
+    if (ab + bytes > fo.arena_cap || sb + segs > fo.seg_cap) return;
     for (uint32_t q = tid; q < segs; q += kThreads) {
         const FusedSeg f = S.seg[q];
-        SegInfo& g = info[excl.segs + q];
-        g.first_line = excl.lines + f.line;
-        g.name_off = a0 + f.name_ls;
-        g.name_len = f.name_len;
-        g.text_off = o0 + f.text;
+        fo.seg_arena[sb + q] = ArenaSeg{tile, q, f.line, (uint32_t)f.name_len, a0 + f.name_ls, f.text};
     }
-    const uint8_t* ob = reinterpret_cast<const uint8_t*>(S.ob4);
-    const uint32_t wl = (uint32_t)bytes;
-    uint32_t head = (uint32_t)((4u - (o0 & 3u)) & 3u);
-    head = head < wl ? head : wl;
-    if (tid < head) text[o0 + tid] = ob[tid];
-    const uint32_t nw4 = (wl - head) / 4u;
-    uint32_t* dst = reinterpret_cast<uint32_t*>(text + o0 + head);
-    for (uint32_t w = tid; w < nw4; w += kThreads) {
-        const uint32_t q = head + 4u * w;
-        dst[w] = (uint32_t)ob[q] | ((uint32_t)ob[q + 1] << 8) | ((uint32_t)ob[q + 2] << 16) | ((uint32_t)ob[q + 3] << 24);
-    }
-    for (uint32_t k = head + 4u * nw4 + tid; k < wl; k += kThreads) text[o0 + k] = ob[k];
+    const uint32_t* ob4 = S.ob4;
+    uint32_t* dst = reinterpret_cast<uint32_t*>(fo.arena + ab);   // 4-byte aligned
+    const uint32_t nw4 = ((uint32_t)bytes + 3u) / 4u;
+    for (uint32_t w = tid; w < nw4; w += kThreads) dst[w] = ob4[w];
 #ifdef STARCH_TF_PROF
     TPROF(p5);
     if (lane == 0) {
+        atomicAdd(&g_tfprof[3], (unsigned long long)(p4 - p3));
         atomicAdd(&g_tfprof[4], (unsigned long long)(p5 - p4));
         atomicAdd(&g_tfprof[5], 1ull);
     }
 #endif
+}
+
+// after the scans over the tiles (exclusive prefixes of bytes, lines and
+// segments in fo.*_pre): every tile's text from the arena to its final
+// offset (4-byte stores, the head bytes up to an aligned destination and the
+// tail bytewise), tiles after the first one holding a 0xFF dropped
+__global__ void __launch_bounds__(256) k_tf_place(const FusedOut fo, uint8_t* __restrict__ text, uint32_t ntiles)
+{
+    __shared__ uint32_t buf[kFOut / 4 + 4];
+    const uint32_t t = blockIdx.x, tid = threadIdx.x;
+    if (t > *fo.first_ff || t >= ntiles) return;
+    const uint32_t bytes = fo.tile_bytes[t];
+    if (!bytes || fo.tile_arena[t] + bytes > fo.arena_cap) return;   // (overflow: the host reruns)
+    const uint32_t* src = reinterpret_cast<const uint32_t*>(fo.arena + fo.tile_arena[t]);
+    const uint32_t nw4 = (bytes + 3u) / 4u;
+    for (uint32_t w = tid; w < nw4; w += 256) buf[w] = src[w];
+    __syncthreads();
+    const uint8_t* ob = reinterpret_cast<const uint8_t*>(buf);
+    const uint64_t o0 = fo.bytes_pre[t];
+    uint32_t head = (uint32_t)((4u - (o0 & 3u)) & 3u);
+    head = head < bytes ? head : bytes;
+    if (tid < head) text[o0 + tid] = ob[tid];
+    const uint32_t nw = (bytes - head) / 4u;
+    uint32_t* dst = reinterpret_cast<uint32_t*>(text + o0 + head);
+    for (uint32_t w = tid; w < nw; w += 256) {
+        const uint32_t q = head + 4u * w;
+        dst[w] = (uint32_t)ob[q] | ((uint32_t)ob[q + 1] << 8) | ((uint32_t)ob[q + 2] << 16) | ((uint32_t)ob[q + 3] << 24);
+    }
+    for (uint32_t k = head + 4u * nw + tid; k < bytes; k += 256) text[o0 + k] = ob[k];
+}
+
+// segment records of the kept tiles at their final index; totals (lines,
+// segments, bytes, saw 0xFF) as k_seg_close_dev expects them
+__global__ void k_tf_segs(const FusedOut fo, SegInfo* __restrict__ info, uint64_t* __restrict__ totals, uint32_t ntiles)
+{
+    const uint32_t ff = *fo.first_ff;
+    const uint64_t nseg = *fo.seg_ctr < fo.seg_cap ? *fo.seg_ctr : fo.seg_cap;
+    const uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (i == 0) {
+        const uint32_t last = ff < ntiles ? ff + 1 : ntiles;      // tiles kept: [0, last)
+        totals[0] = fo.lines_pre[last];
+        totals[1] = fo.segs_pre[last];
+        totals[2] = fo.bytes_pre[last];
+        totals[3] = ff < ntiles ? 1 : 0;
+    }
+    for (uint64_t j = i; j < nseg; j += (uint64_t)gridDim.x * blockDim.x) {
+    const ArenaSeg e = fo.seg_arena[j];
+    if (e.tile > ff || fo.segs_pre[e.tile] + e.q >= fo.seg_cap) continue;
+    SegInfo& g = info[fo.segs_pre[e.tile] + e.q];
+    g.first_line = fo.lines_pre[e.tile] + e.line;
+    g.name_off = e.name_off;
+    g.name_len = e.name_len;
+    g.text_off = fo.bytes_pre[e.tile] + e.text;
+    }
 }
 
 // line_count / text_len of each segment from its successor; totals on the device
@@ -1581,27 +1555,40 @@ void TransformWorkspace::run(const uint8_t* d_bed, uint64_t n, hipStream_t st, T
     if (n == 0 || force == 2 || (force == 0 && ratio_seen && text_ratio > 0.6))
         return run_two_pass(d_bed, n, st, res, init_start, init_stop);
     const uint32_t ntiles = (uint32_t)ceil_div(n, kFT);
-    uint64_t* aw = b_faggs.as<uint64_t>(6ull * ntiles + 8);   // tagged look-back words: aggregates, prefixes
-    uint64_t* iw = aw + 3ull * ntiles + 4;
-    uint64_t* fx = b_fx.as<uint64_t>(16);     // [0..3] totals (lines, segments, bytes, saw 0xFF), [4] flags, [5] tile counter
+    // per-tile counts (u32 x 3) and arena offsets (u64), their exclusive
+    // prefixes (u64 x 3, ntiles + 1 each), the scan scratch
+    uint64_t* fw = b_faggs.as<uint64_t>(8ull * ntiles + 64);
+    FusedOut fo;
+    fo.tile_bytes = reinterpret_cast<uint32_t*>(fw);
+    fo.tile_lines = fo.tile_bytes + ntiles;
+    fo.tile_segs = fo.tile_lines + ntiles;
+    fo.tile_arena = fw + (3ull * ntiles + 2) / 2 + 1;
+    fo.bytes_pre = fo.tile_arena + ntiles;
+    fo.lines_pre = fo.bytes_pre + ntiles + 1;
+    fo.segs_pre = fo.lines_pre + ntiles + 1;
+    uint64_t* fx = b_fx.as<uint64_t>(16);   // [0..3] totals (lines, segments, bytes, saw 0xFF), [4] flags, [5] first 0xFF tile, [6] arena, [7] segs
+    fo.first_ff = reinterpret_cast<uint32_t*>(fx + 5);
+    fo.arena_ctr = reinterpret_cast<unsigned long long*>(fx + 6);
+    fo.seg_ctr = reinterpret_cast<unsigned long long*>(fx + 7);
     uint64_t tcap = std::max<uint64_t>(1u << 20, (uint64_t)(text_ratio * 1.05 * (double)n) + 4096);
     uint64_t scap = std::max<uint64_t>(4096, 2 * seg_hint);
-    static const uint32_t dbg_mode = [] { const char* e = getenv("STARCH_TF_MODE"); return e ? (uint32_t)atoi(e) : 0u; }();
-    if (dbg_mode == 1) {   // timing experiment: the parse phase alone, then the normal path
-        HIP_CHECK(hipMemsetAsync(fx, 0, 8 * sizeof(uint64_t), st));
-        hipLaunchKernelGGL(k_tf_fused, dim3(ntiles), dim3(kThreads), 0, st, d_bed, n,
-                           reinterpret_cast<uint32_t*>(fx + 5), aw, iw, b_text.as<uint8_t>(tcap + 64),
-                           tcap, b_seg_info.as<SegInfo>(scap + 1), scap, reinterpret_cast<uint32_t*>(fx + 4), fx,
-                           ntiles, 1u);
-    }
     for (int attempt = 0; attempt < 3; ++attempt) {
         uint8_t* txt = b_text.as<uint8_t>(tcap + 64);
         SegInfo* info = b_seg_info.as<SegInfo>(scap + 1);
-        HIP_CHECK(hipMemsetAsync(aw, 0, (6ull * ntiles + 8) * sizeof(uint64_t), st));
+        fo.arena = b_arena.as<uint8_t>(tcap + 4 * (uint64_t)ntiles + 64);
+        fo.arena_cap = tcap + 4 * (uint64_t)ntiles;   // pieces are padded to 4 bytes
+        fo.seg_arena = b_seg_arena.as<ArenaSeg>(scap + 1);
+        fo.seg_cap = scap;
         HIP_CHECK(hipMemsetAsync(fx, 0, 8 * sizeof(uint64_t), st));
-        hipLaunchKernelGGL(k_tf_fused, dim3(ntiles), dim3(kThreads), 0, st, d_bed, n,
-                           reinterpret_cast<uint32_t*>(fx + 5), aw, iw, txt, tcap, info, scap,
-                           reinterpret_cast<uint32_t*>(fx + 4), fx, ntiles, 0u);
+        HIP_CHECK(hipMemsetAsync(fo.first_ff, 0xFF, sizeof(uint32_t), st));
+        hipLaunchKernelGGL(k_tf_fused, dim3(ntiles), dim3(kThreads), 0, st, d_bed, n, fo,
+                           reinterpret_cast<uint32_t*>(fx + 4), 0u);
+        scan::excl_sum_u32_to_u64(fo.tile_bytes, fo.bytes_pre, ntiles, fo.bytes_pre + ntiles, b_tmp, st);
+        scan::excl_sum_u32_to_u64(fo.tile_lines, fo.lines_pre, ntiles, fo.lines_pre + ntiles, b_tmp, st);
+        scan::excl_sum_u32_to_u64(fo.tile_segs, fo.segs_pre, ntiles, fo.segs_pre + ntiles, b_tmp, st);
+        hipLaunchKernelGGL(k_tf_place, dim3(ntiles), dim3(256), 0, st, fo, txt, ntiles);
+        const uint32_t sg = (uint32_t)std::min<uint64_t>(65535, ceil_div(scap, 256));
+        hipLaunchKernelGGL(k_tf_segs, dim3(sg), dim3(256), 0, st, fo, info, fx, ntiles);
         const uint32_t cg = (uint32_t)std::min<uint64_t>(1024, ceil_div(scap, 256));
         hipLaunchKernelGGL(k_seg_close_dev, dim3(cg), dim3(256), 0, st, info, fx, scap);
         HIP_CHECK(hipGetLastError());
@@ -1624,7 +1611,7 @@ void TransformWorkspace::run(const uint8_t* d_bed, uint64_t n, hipStream_t st, T
             HIP_CHECK(hipMemcpyFromSymbol(g, HIP_SYMBOL(g_tfprof), sizeof(g)));
             static const unsigned long long zero[8] = {};
             HIP_CHECK(hipMemcpyToSymbol(HIP_SYMBOL(g_tfprof), zero, sizeof(zero)));
-            const char* nm[5] = {"ticket+stage", "masks+nl-scan+halo", "fused_lines", "look-back", "write-out"};
+            const char* nm[5] = {"stage", "masks+nl-scan+halo", "fused_lines", "counts+arena alloc", "arena write"};
             const double tot = (double)(g[0] + g[1] + g[2] + g[3] + g[4]);
             for (int q = 0; q < 5; ++q)
                 fprintf(stderr, "[tfprof] %-20s %14llu (%.1f%%)\n", nm[q], g[q], 100.0 * (double)g[q] / (tot ? tot : 1));

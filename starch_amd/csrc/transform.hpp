@@ -21,7 +21,7 @@ struct TransformResult {
 struct TransformWorkspace {
     DevBuf b_tile_cnt, b_tile_off, b_scal, b_tmp, b_line_end, b_start, b_stop, b_flags, b_rem_beg, b_rem_len,
         b_chr_len, b_idx, b_vcopy, b_out_len, b_seg_flag, b_out_off, b_seg_ord, b_seg_first, b_seg_info, b_text,
-        b_fstatus, b_faggs, b_fx;
+        b_fstatus, b_faggs, b_fx, b_arena, b_seg_arena;
     double text_ratio = 1.0;          // text bytes per input byte of the last run (single-pass capacity, path choice)
     bool ratio_seen = false;
     uint64_t seg_hint = 0;
