@@ -80,8 +80,8 @@ def test_cfg5_all_24_fullsize():
     cap = max(starch_amd.gen_perpos_device(c) for c in range(24))
     dev = torch.empty(cap + 64, dtype=torch.uint8, device="cuda")
     c = starch_amd.Starch(0)
-    stream = torch.cuda.current_stream()
-    c.set_stream(stream.cuda_stream)
+    stream = torch.cuda.Stream()          # a real stream: set_stream(0) selects the context's own stream
+    c.set_stream(stream.cuda_stream)      # generator and encoder ordered on it
     done = 0
     for ci, name in enumerate(starch_amd.HG38):
         n = starch_amd.gen_perpos_device(ci, dev.data_ptr(), cap + 64, stream=stream.cuda_stream)

@@ -5,9 +5,15 @@ Reads gpurun_out/pmc/{fetch,write}/**/run_counter_collection.csv of ONE bench
 step (tools/gpu_pmc.sh, PASSES="fetch write", LINES=100000000), sums the
 FETCH_SIZE and WRITE_SIZE (KB) of the block-sort kernels (k3_*, k_fallback*,
 k_last_col, scan helpers launched by the sort are not separable and are
-excluded), applies MI355X_MICROARCH.md's gfx950 correction (FETCH_SIZE counts
-half of wide streaming reads: doubled) and writes profiles/pmc_k_bwt.json,
-which bench.py reports as roofline.traffic.
+excluded), applies the gfx950 correction FETCH_SIZE x 2 and writes profiles/pmc_k_bwt.json,
+which bench.py reports as roofline.traffic.  The factor 2 is calibrated for
+the block sort's own access widths (tools/probes/fetch_calib.hip,
+profiles/r04/fetch_calib.json): a 16-B/lane stream reads 0.500 of its bytes in
+FETCH_SIZE, and an 8-B or 16-B gather to its own 128-B line reads 64 units --
+the whole line fetched, counted at half -- while two gathers to the halves of
+one line read 64 per line, so fetched bytes = 2 x FETCH_SIZE for streams and
+gathers alike; WRITE_SIZE is exact for streams (1.000) and counts a partial
+line write as one 32-B sector.
 usage: pmc_bwt_traffic.py [PMC_DIR] [OUT_JSON]
 """
 import collections
@@ -50,7 +56,7 @@ def main():
         "fetch_bytes": fetch_b,
         "write_bytes": write_b,
         "method": "rocprofv3 --pmc FETCH_SIZE and WRITE_SIZE in separate passes over one bench step (kind/lines above); "
-                  "FETCH_SIZE doubled (gfx950 wide-read correction, MI355X_MICROARCH.md HBM section); "
+                  "FETCH_SIZE doubled (calibrated for 8/16-B gathers and 16-B streams: profiles/r04/fetch_calib.json); "
                   "block-sort kernels k3_*, k_fallback*, k_last_col summed; Infinity-Cache hits are counted",
         "per_kernel_fetch_bytes": {k: 2.0 * v * 1024.0 for k, v in f.most_common()},
         "per_kernel_write_bytes": {k: v * 1024.0 for k, v in w.most_common()},
