@@ -991,11 +991,10 @@ __device__ __forceinline__ LineVals parse_line_at(const S& bed, uint64_t ls, uin
 struct FusedSeg { uint32_t line, name_ls, name_len, text; };
 struct ArenaSeg { uint32_t tile, q, line, name_len; uint64_t name_off; uint32_t text, pad; };
 struct FusedOut {                  // k_tf_fused's outputs (arena form) and the scans over them
-    uint8_t* arena;                // tiles' texts, bump-allocated (4-byte aligned pieces)
-    uint64_t arena_cap;
-    unsigned long long* arena_ctr;
+    uint8_t* arena;                // tile t's text at arena + t * kFOut (a fixed slot: no allocator)
+    uint64_t text_cap;             // capacity of the final text buffer (k_tf_place)
+    uint32_t* xflags;
     uint32_t *tile_bytes, *tile_lines, *tile_segs;
-    uint64_t* tile_arena;
     uint32_t* first_ff;            // first tile holding a 0xFF (ntiles: none)
     ArenaSeg* seg_arena;
     uint64_t seg_cap;
@@ -1013,7 +1012,7 @@ struct FusedShared {
     FusedSeg seg[kFSeg];
     LineKey wlast[kThreads / 64 + 1];          // [0]: carry into the chunk; [w+1]: wave w's last line
     uint32_t tile, ffpos, p1, p2, over, nul;
-    struct { uint64_t bytes, segs; } excl;   // the tile's arena offsets
+    struct { uint64_t segs; } excl;          // the tile's first record in the segment arena
 };
 
 __device__ __forceinline__ LineKey shfl_up_key(const LineKey& k)
@@ -1036,7 +1035,7 @@ __device__ __forceinline__ LineKey shfl_up_key(const LineKey& k)
 __device__ __forceinline__ void fused_lines(FusedShared& S, const uint8_t* tb, uint64_t a0, uint32_t nl,
                                             uint32_t first_ls, bool input_start, uint32_t* __restrict__ xflags,
                                             uint64_t& bytes_out, uint32_t& segs_out, uint32_t prev_ls = 0,
-                                            bool parse_prev = false)
+                                            bool parse_prev = false, bool no_write = false)
 {
     const uint32_t tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
     if (parse_prev && tid == kThreads - 1) {      // its slots 2*tid, 2*tid+1 are past nl
@@ -1103,7 +1102,8 @@ __device__ __forceinline__ void fused_lines(FusedShared& S, const uint8_t* tb, u
 #pragma unroll
         for (int u = 0; u < 2; ++u) {
             if (!have[u]) continue;
-            if (off + len[u] <= kFOut) tf_write(lsrc, t[u], ob + off);
+            if (no_write) { /* timing experiment */ }
+            else if (off + len[u] <= kFOut) tf_write(lsrc, t[u], ob + off);
             else S.over = 1;
             if (ns[u]) {
                 if (sl < kFSeg) S.seg[sl] = FusedSeg{c0 + 2 * tid + u, ls[u], t[u].r.chr_len, (uint32_t)off};
@@ -1291,37 +1291,43 @@ k_tf_fused(const uint8_t* __restrict__ bed, uint64_t n, const FusedOut fo, uint3
     TPROF(p2);
     uint64_t bytes = 0;
     uint32_t segs = 0;
+    if (dbg_mode == 1 || dbg_mode == 2) {           // timing experiments: no output (empty tiles)
+        if (tid == 0) {
+            fo.tile_bytes[tile] = 0u;
+            fo.tile_lines[tile] = 0u;
+            fo.tile_segs[tile] = 0u;
+        }
+        if (dbg_mode == 2) return;                  // staging + masks only
+    }
     if (!fallback && nl_tile > 0)
-        fused_lines(S, tb, a0, nl_tile, first_ls, input_start, xflags, bytes, segs, prev_ls, prev_in_lines);
+        fused_lines(S, tb, a0, nl_tile, first_ls, input_start, xflags, bytes, segs, prev_ls, prev_in_lines,
+                    dbg_mode == 3);
     TPROF(p3);
     fallback = fallback || S.over;
     if (fallback && tid == 0) atomicOr(xflags, FX_FALLBACK);
-    if (dbg_mode == 1) return;                      // timing experiment: parse only
+    if (dbg_mode == 1) return;                      // timing experiment: parse only (tile counts zeroed above)
     TPROF(p4);
-    // No look-back: the tile's text goes to a bump-allocated place in the arena
-    // and its counts to per-tile arrays; k_tf_place moves it to its final
-    // offset after a scan over the tiles.  (Waiting here for the previous
-    // tiles' prefix, with the workgroup's LDS held, took ~65% of the
-    // workgroups' time: STARCH_TF_PROF.)
+    // No look-back: the tile's text goes to its fixed slot of the arena and its
+    // counts to per-tile arrays; k_tf_place moves it to its final offset after
+    // a scan over the tiles.  (Waiting here for the previous tiles' prefix,
+    // with the workgroup's LDS held, took ~65% of the workgroups' time
+    // (STARCH_TF_PROF); a bump allocator -- one atomic per tile on one counter
+    // -- serialised the tiles' tails: 1.7 of 4.4 ms, STARCH_TF_DBG=1.)
     if (tid == 0) {
         const bool ff = ffpos != 0xFFFFFFFFu;
         fo.tile_bytes[tile] = fallback ? 0u : (uint32_t)bytes;
         fo.tile_lines[tile] = fallback ? 0u : nl_tile;
         fo.tile_segs[tile] = fallback ? 0u : segs;
         if (ff) atomicMin(fo.first_ff, tile);
-        uint64_t ab = 0, sb = 0;
-        if (!fallback && bytes) ab = atomicAdd(fo.arena_ctr, (bytes + 3) & ~3ull);
-        if (!fallback && segs) sb = atomicAdd(fo.seg_ctr, (uint64_t)segs);
-        S.excl.bytes = ab;
+        uint64_t sb = 0;
+        if (!fallback && segs) sb = atomicAdd(fo.seg_ctr, (uint64_t)segs);   // tiles with a segment start only
         S.excl.segs = sb;
-        fo.tile_arena[tile] = ab;
-        if (ab + bytes > fo.arena_cap) atomicOr(xflags, FX_TEXT_CAP);
         if (sb + segs > fo.seg_cap) atomicOr(xflags, FX_SEG_CAP);
     }
     __syncthreads();
     if (fallback || nl_tile == 0) return;
-    const uint64_t ab = S.excl.bytes, sb = S.excl.segs;
-    if (ab + bytes > fo.arena_cap || sb + segs > fo.seg_cap) return;
+    const uint64_t ab = (uint64_t)tile * kFOut, sb = S.excl.segs;
+    if (sb + segs > fo.seg_cap) return;
     for (uint32_t q = tid; q < segs; q += kThreads) {
         const FusedSeg f = S.seg[q];
         fo.seg_arena[sb + q] = ArenaSeg{tile, q, f.line, (uint32_t)f.name_len, a0 + f.name_ls, f.text};
@@ -1341,32 +1347,43 @@ k_tf_fused(const uint8_t* __restrict__ bed, uint64_t n, const FusedOut fo, uint3
 }
 
 // after the scans over the tiles (exclusive prefixes of bytes, lines and
-// segments in fo.*_pre): every tile's text from the arena to its final
-// offset (4-byte stores, the head bytes up to an aligned destination and the
-// tail bytewise), tiles after the first one holding a 0xFF dropped
+// segments in fo.*_pre): every tile's text from its arena slot to its final
+// offset, tiles after the first one holding a 0xFF dropped.  The slot is
+// staged in LDS with 16-byte loads; the destination is written with 16-byte
+// stores from its first 16-aligned byte (each built from five aligned LDS
+// words by byte funnel shifts), the bytes before and after bytewise.
 __global__ void __launch_bounds__(256) k_tf_place(const FusedOut fo, uint8_t* __restrict__ text, uint32_t ntiles)
 {
-    __shared__ uint32_t buf[kFOut / 4 + 4];
+    __shared__ uint4 buf[kFOut / 16 + 2];
     const uint32_t t = blockIdx.x, tid = threadIdx.x;
     if (t > *fo.first_ff || t >= ntiles) return;
     const uint32_t bytes = fo.tile_bytes[t];
-    if (!bytes || fo.tile_arena[t] + bytes > fo.arena_cap) return;   // (overflow: the host reruns)
-    const uint32_t* src = reinterpret_cast<const uint32_t*>(fo.arena + fo.tile_arena[t]);
-    const uint32_t nw4 = (bytes + 3u) / 4u;
-    for (uint32_t w = tid; w < nw4; w += 256) buf[w] = src[w];
+    if (!bytes) return;
+    const uint64_t o0 = fo.bytes_pre[t];
+    if (o0 + bytes > fo.text_cap) {                 // the host grows the text buffer and reruns
+        if (tid == 0) atomicOr(fo.xflags, FX_TEXT_CAP);
+        return;
+    }
+    const uint4* src = reinterpret_cast<const uint4*>(fo.arena + (uint64_t)t * kFOut);
+    const uint32_t n16 = (bytes + 15u) / 16u;
+    for (uint32_t w = tid; w < n16; w += 256) buf[w] = src[w];
+    if (tid == 0) buf[n16] = make_uint4(0, 0, 0, 0);   // the funnel shifts read one word past the end
     __syncthreads();
     const uint8_t* ob = reinterpret_cast<const uint8_t*>(buf);
-    const uint64_t o0 = fo.bytes_pre[t];
-    uint32_t head = (uint32_t)((4u - (o0 & 3u)) & 3u);
+    const uint32_t* ow = reinterpret_cast<const uint32_t*>(buf);
+    uint32_t head = (uint32_t)((16u - (o0 & 15u)) & 15u);
     head = head < bytes ? head : bytes;
     if (tid < head) text[o0 + tid] = ob[tid];
-    const uint32_t nw = (bytes - head) / 4u;
-    uint32_t* dst = reinterpret_cast<uint32_t*>(text + o0 + head);
+    const uint32_t nw = (bytes - head) / 16u;
+    uint4* dst = reinterpret_cast<uint4*>(text + o0 + head);
+    const uint32_t sh = head & 3u, wb = head >> 2;
     for (uint32_t w = tid; w < nw; w += 256) {
-        const uint32_t q = head + 4u * w;
-        dst[w] = (uint32_t)ob[q] | ((uint32_t)ob[q + 1] << 8) | ((uint32_t)ob[q + 2] << 16) | ((uint32_t)ob[q + 3] << 24);
+        const uint32_t* q = ow + wb + 4u * w;
+        const uint32_t a0 = q[0], a1 = q[1], a2 = q[2], a3 = q[3], a4 = q[4];
+        dst[w] = make_uint4(__builtin_amdgcn_alignbyte(a1, a0, sh), __builtin_amdgcn_alignbyte(a2, a1, sh),
+                            __builtin_amdgcn_alignbyte(a3, a2, sh), __builtin_amdgcn_alignbyte(a4, a3, sh));
     }
-    for (uint32_t k = head + 4u * nw + tid; k < bytes; k += 256) text[o0 + k] = ob[k];
+    for (uint32_t k = head + 16u * nw + tid; k < bytes; k += 256) text[o0 + k] = ob[k];
 }
 
 // segment records of the kept tiles at their final index; totals (lines,
@@ -1555,34 +1572,36 @@ void TransformWorkspace::run(const uint8_t* d_bed, uint64_t n, hipStream_t st, T
     if (n == 0 || force == 2 || (force == 0 && ratio_seen && text_ratio > 0.6))
         return run_two_pass(d_bed, n, st, res, init_start, init_stop);
     const uint32_t ntiles = (uint32_t)ceil_div(n, kFT);
-    // per-tile counts (u32 x 3) and arena offsets (u64), their exclusive
-    // prefixes (u64 x 3, ntiles + 1 each), the scan scratch
+    // per-tile counts (u32 x 3), their exclusive prefixes (u64 x 3, ntiles + 1
+    // each)
     uint64_t* fw = b_faggs.as<uint64_t>(8ull * ntiles + 64);
     FusedOut fo;
     fo.tile_bytes = reinterpret_cast<uint32_t*>(fw);
     fo.tile_lines = fo.tile_bytes + ntiles;
     fo.tile_segs = fo.tile_lines + ntiles;
-    fo.tile_arena = fw + (3ull * ntiles + 2) / 2 + 1;
-    fo.bytes_pre = fo.tile_arena + ntiles;
+    fo.bytes_pre = fw + (3ull * ntiles + 2) / 2 + 1;
     fo.lines_pre = fo.bytes_pre + ntiles + 1;
     fo.segs_pre = fo.lines_pre + ntiles + 1;
-    uint64_t* fx = b_fx.as<uint64_t>(16);   // [0..3] totals (lines, segments, bytes, saw 0xFF), [4] flags, [5] first 0xFF tile, [6] arena, [7] segs
+    uint64_t* fx = b_fx.as<uint64_t>(16);   // [0..3] totals (lines, segments, bytes, saw 0xFF), [4] flags, [5] first 0xFF tile, [7] segs
     fo.first_ff = reinterpret_cast<uint32_t*>(fx + 5);
-    fo.arena_ctr = reinterpret_cast<unsigned long long*>(fx + 6);
+    fo.xflags = reinterpret_cast<uint32_t*>(fx + 4);
     fo.seg_ctr = reinterpret_cast<unsigned long long*>(fx + 7);
     uint64_t tcap = std::max<uint64_t>(1u << 20, (uint64_t)(text_ratio * 1.05 * (double)n) + 4096);
     uint64_t scap = std::max<uint64_t>(4096, 2 * seg_hint);
     for (int attempt = 0; attempt < 3; ++attempt) {
         uint8_t* txt = b_text.as<uint8_t>(tcap + 64);
         SegInfo* info = b_seg_info.as<SegInfo>(scap + 1);
-        fo.arena = b_arena.as<uint8_t>(tcap + 4 * (uint64_t)ntiles + 64);
-        fo.arena_cap = tcap + 4 * (uint64_t)ntiles;   // pieces are padded to 4 bytes
+        fo.arena = b_arena.as<uint8_t>((uint64_t)ntiles * kFOut + 64);   // one kFOut slot per tile
+        fo.text_cap = tcap;
         fo.seg_arena = b_seg_arena.as<ArenaSeg>(scap + 1);
         fo.seg_cap = scap;
         HIP_CHECK(hipMemsetAsync(fx, 0, 8 * sizeof(uint64_t), st));
         HIP_CHECK(hipMemsetAsync(fo.first_ff, 0xFF, sizeof(uint32_t), st));
+        // STARCH_TF_DBG (timing experiments only, wrong output): 1 parse without
+        // the arena write, 2 staging + masks only, 3 parse + lengths without text
+        static const uint32_t dbg_mode = getenv("STARCH_TF_DBG") ? (uint32_t)atoi(getenv("STARCH_TF_DBG")) : 0u;
         hipLaunchKernelGGL(k_tf_fused, dim3(ntiles), dim3(kThreads), 0, st, d_bed, n, fo,
-                           reinterpret_cast<uint32_t*>(fx + 4), 0u);
+                           reinterpret_cast<uint32_t*>(fx + 4), dbg_mode);
         scan::excl_sum_u32_to_u64(fo.tile_bytes, fo.bytes_pre, ntiles, fo.bytes_pre + ntiles, b_tmp, st);
         scan::excl_sum_u32_to_u64(fo.tile_lines, fo.lines_pre, ntiles, fo.lines_pre + ntiles, b_tmp, st);
         scan::excl_sum_u32_to_u64(fo.tile_segs, fo.segs_pre, ntiles, fo.segs_pre + ntiles, b_tmp, st);
