@@ -1040,8 +1040,11 @@ __device__ __forceinline__ void fused_lines(FusedShared& S, const uint8_t* tb, u
     const uint32_t tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
     if (parse_prev && tid == kThreads - 1) {      // its slots 2*tid, 2*tid+1 are past nl
         LineVals pr;
-        if (!parse_fast(tb, prev_ls, first_ls - prev_ls, a0 + prev_ls, pr))
-            pr = parse_line_at(LSrc{tb, a0}, a0 + prev_ls, a0 + first_ls);
+        if (!parse_mask(tb, S.tabm, prev_ls, first_ls - prev_ls, a0 + prev_ls, pr)) {
+            S.over = 1;                           // not the fast shape: the two-pass path takes the input
+            pr.a = pr.b = 0;
+            pr.chr_len = 0;
+        }
         S.wlast[0] = LineKey{pr.a, pr.b, prev_ls, pr.chr_len};   // read after the chunk's first barrier
     }
     const LSrc lsrc{tb, a0};
@@ -1062,9 +1065,13 @@ __device__ __forceinline__ void fused_lines(FusedShared& S, const uint8_t* tb, u
                 ls[u] = k ? (uint32_t)S.nlp[k - 1] + 1u : first_ls;
                 const uint32_t le = (uint32_t)S.nlp[k] + 1u;
                 t[u].ls = a0 + ls[u];
-                const bool fast = S.nul ? parse_fast(tb, ls[u], le - ls[u], t[u].ls, t[u].r)
-                                        : parse_mask(tb, S.tabm, ls[u], le - ls[u], t[u].ls, t[u].r);
-                if (!fast) t[u].r = parse_line_at(lsrc, a0 + ls[u], a0 + le);
+                // only the fast shape here (no NUL in the tile, line <= 128 bytes,
+                // plain digit fields): anything else hands the input to the
+                // two-pass path, whose byte-serial parser is the definition
+                if (!parse_mask(tb, S.tabm, ls[u], le - ls[u], t[u].ls, t[u].r)) {
+                    S.over = 1;
+                    t[u].r = LineVals{0, 0, t[u].ls, 0u, 0u, true, true, false};
+                }
                 if (!t[u].r.aok || !t[u].r.bok) atomicOr(xflags, FX_FAIL);
                 key[u] = LineKey{t[u].r.a, t[u].r.b, ls[u], t[u].r.chr_len};
             }
@@ -1179,19 +1186,21 @@ k_tf_fused(const uint8_t* __restrict__ bed, uint64_t n, const FusedOut fo, uint3
         const uint4* q = reinterpret_cast<const uint4*>(tb + ch * 32);
         const uint4 x = q[0], y = q[1];
         const uint32_t w[8] = {x.x, x.y, x.z, x.w, y.x, y.y, y.z, y.w};
-        uint32_t nm = 0, fm = 0, tm = 0, zf = 0;
+        uint32_t nm = 0, fm = 0, tm = 0, zm = 0;
 #pragma unroll
         for (int j = 0; j < 8; ++j) {
             nm |= eq4(w[j], 0x0a0a0a0au) << (4 * j);
             tm |= eq4(w[j], 0x09090909u) << (4 * j);
-            zf |= (w[j] - 0x01010101u) & ~w[j] & 0x80808080u;   // some byte is NUL
+            zm |= eq4(w[j], 0u) << (4 * j);
             fm |= eq4(w[j], 0xffffffffu) << (4 * j);
         }
         S.tabm[ch] = tm;
-        if (zf) S.nul = 1;
         const uint32_t lo = ch * 32 < Lt0 ? Lt0 - ch * 32 : 0u;
         const uint32_t hi = Lend - ch * 32 < 32u ? Lend - ch * 32 : 32u;
         const uint32_t keep = (hi >= 32u ? 0xFFFFFFFFu : ((1u << hi) - 1u)) & ~((1u << lo) - 1u);
+        // a NUL among the staged bytes (everything from a0 up to the tile's end;
+        // the bytes after it are not staged)
+        if (zm & (hi >= 32u ? 0xFFFFFFFFu : ((1u << hi) - 1u))) S.nul = 1;
         nlm[it] = nm & keep;
         fm &= keep;
         if (fm) atomicMin(&S.ffpos, ch * 32 + (uint32_t)__builtin_ctz(fm));
@@ -1243,7 +1252,7 @@ k_tf_fused(const uint8_t* __restrict__ bed, uint64_t n, const FusedOut fo, uint3
     }
     uint32_t nl_tile = 0;
     const uint32_t pre = block_excl_scan_add<uint32_t>(cnt, reinterpret_cast<uint32_t*>(S.scan), &nl_tile);
-    bool fallback = nl_tile > kFMaxLines;
+    bool fallback = nl_tile > kFMaxLines || S.nul;   // (a NUL: C-string rules apply, the two-pass path)
     if (!fallback) {
         uint32_t o = pre;
 #pragma unroll
@@ -1281,9 +1290,10 @@ k_tf_fused(const uint8_t* __restrict__ bed, uint64_t n, const FusedOut fo, uint3
         if (need_prev && !prev_in_lines) {
             LineVals pr;
             const uint32_t ple = first_ls;         // one past the previous line's '\n'
-            if (!parse_fast(tb, prev_ls, ple - prev_ls, a0 + prev_ls, pr))
-                pr = parse_line_at(LSrc{tb, a0}, a0 + prev_ls, a0 + ple);
-            pk = LineKey{pr.a, pr.b, prev_ls, pr.chr_len};
+            if (!fallback && parse_mask(tb, S.tabm, prev_ls, ple - prev_ls, a0 + prev_ls, pr))
+                pk = LineKey{pr.a, pr.b, prev_ls, pr.chr_len};
+            else
+                S.over = 1;
         }
         S.wlast[0] = pk;
     }
