@@ -10,6 +10,7 @@
 #include <atomic>
 #include <condition_variable>
 #include <memory>
+#include <map>
 #include <mutex>
 #include <string>
 #include <thread>
@@ -171,16 +172,19 @@ struct starch_ctx {
         bool active = false, eof = false;
         starch_options opt{};
         std::string note;
-        // two pinned buffers: the caller's bytes go into buf[cur] (from a
-        // segment boundary on); a finished prefix is handed to the encoder
-        // thread while the tail moves to the other buffer (double buffering)
-        uint8_t* buf[2] = {nullptr, nullptr};
-        uint64_t cap[2] = {0, 0};
+        // three pinned buffers: the caller's bytes go into buf[cur] (from a
+        // segment boundary on); a finished prefix is handed to one of two
+        // encoder lanes while the tail moves to a free buffer, so two batches
+        // encode while the third fills
+        static constexpr int NBUF = 3, NLANE = 2;
+        uint8_t* buf[NBUF] = {nullptr, nullptr, nullptr};
+        uint64_t cap[NBUF] = {0, 0, 0};
         // device mirrors: every committed piece is copied to dbuf[cur] at once
         // (copy stream), so a batch is in HBM when it is handed over and the
-        // encoder thread only encodes
-        DevBuf dbuf[2];
-        hipEvent_t job_ev = nullptr;  // the handed-over batch's bytes are in HBM
+        // lane only encodes
+        DevBuf dbuf[NBUF];
+        hipEvent_t buf_ev[NBUF] = {nullptr, nullptr, nullptr};   // the handed-over bytes are in HBM
+        bool buf_busy[NBUF] = {false, false, false};            // handed to a lane, not finished
         CopyPool pool;
         int cur = 0;
         uint64_t held_n = 0, try_at = 0, batch = 0, batches = 0;
@@ -191,15 +195,32 @@ struct starch_ctx {
         // batch cut inside a chromosome, re-parsed for the transform state of
         // the lines after it (its own output is dropped)
         uint64_t ctx_len = 0;
-        // encoder thread and its one job slot
-        std::thread worker;
-        std::mutex mu;                // guards the job slot, ready, segs/names/stats, err
+        // encoder lanes (lane 0: the context itself, lane 1: an extra context
+        // on the same device), one job slot each
+        struct Job {
+            bool pending = false, busy = false;
+            int bufi = 0;
+            uint64_t n = 0, ctx = 0, seq = 0;
+            bool open = false;          // the batch ends inside a chromosome
+            bool cont = false;          // ... the batch before it did
+            int64_t is = 0, ip = 0;
+        } lj[NLANE];
+        std::thread workers[NLANE];
+        std::mutex mu;                // guards the job slots, buffers' busy flags, ready, segs/names/stats, err
         std::condition_variable cv;
-        bool job = false, busy = false, stop = false;
-        const uint8_t* job_buf = nullptr;   // device (dbuf)
-        uint64_t job_n = 0, job_ctx = 0;
-        bool job_open = false;          // the batch ends inside a chromosome
-        int64_t job_is = 0, job_ip = 0;
+        bool stop = false;
+        bool last_open = false;       // the last batch handed over ends inside a chromosome
+        // batches are appended to `ready` in hand-over order: seq_commit is the
+        // next one; a lane that finishes out of order parks its result
+        uint64_t seq_next = 0, seq_commit = 0;
+        struct Done {
+            std::vector<uint8_t> bytes;
+            std::vector<starch_segment> segs;
+            std::vector<std::string> names;
+            starch_stats stats{};
+        };
+        std::map<uint64_t, Done> done;
+        PinnedBuf back[NLANE];        // a lane's streams come back here (pinned D2H)
         struct OpenStream {             // a chromosome's bzip2 stream encoded batch by batch (encoder thread)
             bool active = false;
             std::string name;
@@ -227,14 +248,13 @@ struct starch_ctx {
     } sm;
     void stream_shutdown()
     {
-        if (sm.worker.joinable()) {
-            {
-                std::lock_guard<std::mutex> lk(sm.mu);
-                sm.stop = true;
-            }
-            sm.cv.notify_all();
-            sm.worker.join();
+        {
+            std::lock_guard<std::mutex> lk(sm.mu);
+            sm.stop = true;
         }
+        sm.cv.notify_all();
+        for (auto& w : sm.workers)
+            if (w.joinable()) w.join();
         sm.stop = false;
         sm.active = false;
     }
@@ -249,9 +269,10 @@ struct starch_ctx {
             if (cst) (void)hipStreamDestroy(cst);
             if (own) (void)hipStreamDestroy(own);
         }
-        for (int i = 0; i < 2; ++i)
+        for (int i = 0; i < Streaming::NBUF; ++i) {
             if (sm.buf[i]) (void)hipHostFree(sm.buf[i]);
-        if (sm.job_ev) (void)hipEventDestroy(sm.job_ev);
+            if (sm.buf_ev[i]) (void)hipEventDestroy(sm.buf_ev[i]);
+        }
         for (auto& e : tev)
             if (e) (void)hipEventDestroy(e);
     }

@@ -945,6 +945,8 @@ void stream_reserve(starch_ctx* c, int i, uint64_t need)
 // header goes with the first piece, the trailer with the last one.  The
 // context line is transformed on its own as well, and that output (the line
 // as a segment's first) is dropped from the batch's first segment.
+void stream_flush(starch_ctx::Streaming& m);
+
 void stream_encode_pieces(starch_ctx* c, const uint8_t* d, uint64_t n, int64_t is, int64_t ip, uint64_t ctx,
                           bool open)
 {
@@ -1022,8 +1024,8 @@ void stream_encode_pieces(starch_ctx* c, const uint8_t* d, uint64_t n, int64_t i
     const uint64_t cap = align_up(total + 64, 256);
     uint8_t* out = c->part.as<uint8_t>(cap);
     c->enc.emit(out, cap, 0, outs, c->st, &bst);
-    std::vector<uint8_t> part(total);
-    if (total) HIP_CHECK(hipMemcpyAsync(part.data(), out, total, hipMemcpyDeviceToHost, c->st));
+    uint8_t* part = static_cast<uint8_t*>(m.back[0].get(total + 64));   // pinned: D2H at full PCIe rate
+    if (total) HIP_CHECK(hipMemcpyAsync(part, out, total, hipMemcpyDeviceToHost, c->st));
     if (open) {   // the text after the last complete block waits for the next batch
         const uint64_t r0 = c->enc.open_rest(), r1 = sin[nseg - 1].text_off + sin[nseg - 1].text_len;
         os.rest_len = r1 - r0;
@@ -1044,7 +1046,7 @@ void stream_encode_pieces(starch_ctx* c, const uint8_t* d, uint64_t n, int64_t i
     for (uint64_t s = 0; s < nseg; ++s) {
         const bz::StreamOut& o = outs[s];
         const bool is_cont = s == 0 && cont, is_open = s + 1 == nseg && open;
-        const uint8_t* b = part.data() + o.out_off;
+        const uint8_t* b = part + o.out_off;
         const uint64_t bits = ((o.frame >> 8) & 7u) + ((o.frame & 1u) ? 32u : 0u) + o.block_bits +
                               ((o.frame & 2u) ? 80u : 0u);
         const uint64_t full = is_open ? bits / 8 : o.bytes;   // an open piece keeps its last partial byte
@@ -1090,6 +1092,7 @@ void stream_encode_pieces(starch_ctx* c, const uint8_t* d, uint64_t n, int64_t i
     }
     if (!open) os.rest_len = 0;
     ++m.batches;
+    ++m.seq_commit;                   // (pieces start with every earlier batch appended)
     starch_stats& t = m.stats;
     t.n_lines += tr.n_lines - (ctx ? 1 : 0);
     t.text_bytes += tr.text_bytes - o_ctx;
@@ -1106,43 +1109,11 @@ void stream_encode_pieces(starch_ctx* c, const uint8_t* d, uint64_t n, int64_t i
     t.ms_tables += bst.tables;
     t.ms_emit += bst.emit;
     t.ms_total += ms_all;
+    stream_flush(m);                  // batches after it that finished first
 }
 
-// encoder thread: encode b[0, n) (segment boundary to segment boundary, or to
-// the end) with the given initial values and append its streams
-void stream_encode(starch_ctx* c, const uint8_t* d, uint64_t n, int64_t is, int64_t ip, uint64_t ctx, bool open)
+void add_stats(starch_stats& t, const starch_stats& x)
 {
-    auto& m = c->sm;
-    if (m.opt.reference_compat) return;   // the reference writes only the magic (hpp:765-769)
-    // the batch's H2D (copy stream) must be done before any kernel on c->st
-    // reads it -- the piece path (context line + open stream) included
-    HIP_CHECK(hipStreamWaitEvent(c->st, m.job_ev, 0));
-    if (ctx || open || m.os.active) {
-        stream_encode_pieces(c, d, n, is, ip, ctx, open);
-        return;
-    }
-    STRACE("stream batch %llu: %llu bytes, encode", (unsigned long long)m.batches, (unsigned long long)n);
-    std::vector<UnitIn> u(1, UnitIn{0, n, is, ip, 0});
-    encode_units(c, d, u, m.opt, L_STREAMS);
-    STRACE("stream batch %llu: encoded, device %.3f ms", (unsigned long long)m.batches, c->stats.ms_total);
-    std::vector<uint8_t> part(c->part_bytes);
-    if (c->part_bytes)
-        HIP_CHECK(hipMemcpyAsync(part.data(), c->part.p, c->part_bytes, hipMemcpyDeviceToHost, c->st));
-    HIP_CHECK(hipStreamSynchronize(c->st));
-    STRACE("stream batch %llu: streams read back", (unsigned long long)m.batches);
-    std::lock_guard<std::mutex> lk(m.mu);
-    m.ready.insert(m.ready.end(), part.begin(), part.end());
-    for (size_t s = 0; s < c->segs.size(); ++s) {
-        starch_segment g = c->segs[s];
-        g.stream_offset += m.stream_end;
-        g.unit = m.batches;
-        m.segs.push_back(g);
-        m.names.push_back(c->names[s]);
-    }
-    m.stream_end += c->part_bytes;
-    ++m.batches;
-    const starch_stats& x = c->stats;
-    starch_stats& t = m.stats;
     t.n_lines += x.n_lines;
     t.text_bytes += x.text_bytes;
     t.n_blocks += x.n_blocks;
@@ -1160,32 +1131,98 @@ void stream_encode(starch_ctx* c, const uint8_t* d, uint64_t n, int64_t is, int6
     t.ms_total += x.ms_total;
 }
 
-void stream_worker(starch_ctx* c)
+// append the next batch in hand-over order to the ready bytes (m.mu held)
+void stream_append(starch_ctx::Streaming& m, const uint8_t* b, uint64_t nb, const std::vector<starch_segment>& segs,
+                   const std::vector<std::string>& names, const starch_stats& x)
+{
+    m.ready.insert(m.ready.end(), b, b + nb);
+    for (size_t s = 0; s < segs.size(); ++s) {
+        starch_segment g = segs[s];
+        g.stream_offset += m.stream_end;
+        g.unit = m.batches;
+        m.segs.push_back(g);
+        m.names.push_back(names[s]);
+    }
+    m.stream_end += nb;
+    ++m.batches;
+    ++m.seq_commit;
+    add_stats(m.stats, x);
+    stream_flush(m);
+}
+
+// the parked batches that are next in hand-over order (m.mu held)
+void stream_flush(starch_ctx::Streaming& m)
+{
+    for (auto it = m.done.find(m.seq_commit); it != m.done.end(); it = m.done.find(m.seq_commit)) {
+        starch_ctx::Streaming::Done d = std::move(it->second);
+        m.done.erase(it);
+        stream_append(m, d.bytes.data(), d.bytes.size(), d.segs, d.names, d.stats);
+    }
+}
+
+// lane `lane`: encode the job's batch (segment boundary to segment boundary,
+// or to the end) and append its streams in hand-over order
+void stream_encode(starch_ctx* c, int lane, const starch_ctx::Streaming::Job& j)
+{
+    auto& m = c->sm;
+    starch_ctx* L = lane ? c->lanes[lane - 1].get() : c;
+    if (m.opt.reference_compat) {     // the reference writes only the magic (hpp:765-769)
+        std::lock_guard<std::mutex> lk(m.mu);
+        if (j.seq == m.seq_commit) stream_append(m, nullptr, 0, {}, {}, starch_stats{});
+        else m.done[j.seq] = starch_ctx::Streaming::Done{};
+        return;
+    }
+    const uint8_t* d = static_cast<const uint8_t*>(m.dbuf[j.bufi].p);
+    // the batch's H2D (copy stream) must be done before any kernel of the
+    // lane reads it -- the piece path (context line + open stream) included
+    HIP_CHECK(hipStreamWaitEvent(L->st, m.buf_ev[j.bufi], 0));
+    if (j.ctx || j.open || j.cont) {   // handed over with no other batch in flight, to lane 0
+        if (lane) throw StarchError(STARCH_ERR_INTERNAL, "stream: piece batch on an extra lane");
+        stream_encode_pieces(c, d, j.n, j.is, j.ip, j.ctx, j.open);
+        return;
+    }
+    STRACE("stream batch %llu (lane %d): %llu bytes, encode", (unsigned long long)j.seq, lane, (unsigned long long)j.n);
+    std::vector<UnitIn> u(1, UnitIn{0, j.n, j.is, j.ip, 0});
+    encode_units(L, d, u, m.opt, L_STREAMS);
+    STRACE("stream batch %llu: encoded, device %.3f ms", (unsigned long long)j.seq, L->stats.ms_total);
+    uint8_t* part = static_cast<uint8_t*>(m.back[lane].get(L->part_bytes + 64));   // pinned: D2H at full PCIe rate
+    if (L->part_bytes) HIP_CHECK(hipMemcpyAsync(part, L->part.p, L->part_bytes, hipMemcpyDeviceToHost, L->st));
+    HIP_CHECK(hipStreamSynchronize(L->st));
+    STRACE("stream batch %llu: streams read back", (unsigned long long)j.seq);
+    std::unique_lock<std::mutex> lk(m.mu);
+    if (j.seq == m.seq_commit) {
+        stream_append(m, part, L->part_bytes, L->segs, L->names, L->stats);
+    } else {                          // an earlier batch is still encoding on the other lane
+        lk.unlock();
+        starch_ctx::Streaming::Done dn;
+        dn.bytes.assign(part, part + L->part_bytes);
+        dn.segs = L->segs;
+        dn.names = L->names;
+        dn.stats = L->stats;
+        lk.lock();
+        if (j.seq == m.seq_commit) stream_append(m, dn.bytes.data(), dn.bytes.size(), dn.segs, dn.names, dn.stats);
+        else m.done[j.seq] = std::move(dn);
+    }
+}
+
+void stream_worker(starch_ctx* c, int lane)
 {
     auto& m = c->sm;
     (void)hipSetDevice(c->device);
     for (;;) {
-        const uint8_t* b;
-        uint64_t n, ctx;
-        bool open;
-        int64_t is, ip;
+        starch_ctx::Streaming::Job j;
         {
             std::unique_lock<std::mutex> lk(m.mu);
-            m.cv.wait(lk, [&] { return m.job || m.stop; });
-            if (!m.job) return;
-            b = m.job_buf;
-            n = m.job_n;
-            ctx = m.job_ctx;
-            open = m.job_open;
-            is = m.job_is;
-            ip = m.job_ip;
-            m.job = false;
-            m.busy = true;
+            m.cv.wait(lk, [&] { return m.lj[lane].pending || m.stop; });
+            if (!m.lj[lane].pending) return;
+            j = m.lj[lane];
+            m.lj[lane].pending = false;
+            m.lj[lane].busy = true;
         }
         int code = 0;
         std::string msg;
         try {
-            stream_encode(c, b, n, is, ip, ctx, open);
+            stream_encode(c, lane, j);
         } catch (const StarchError& e) {
             code = e.code;
             msg = e.what();
@@ -1195,39 +1232,84 @@ void stream_worker(starch_ctx* c)
         }
         {
             std::lock_guard<std::mutex> lk(m.mu);
-            m.busy = false;
+            m.lj[lane].busy = false;
+            m.buf_busy[j.bufi] = false;
             if (code && !m.err) { m.err = code; m.err_msg = msg; }
         }
         m.cv.notify_all();
     }
 }
 
-// wait until the encoder thread is idle; rethrow its error
+bool lane_idle(const starch_ctx::Streaming& m, int i) { return !m.lj[i].pending && !m.lj[i].busy; }
+
+// wait until every lane is idle; rethrow a lane's error
 void stream_wait(starch_ctx* c)
 {
     auto& m = c->sm;
     std::unique_lock<std::mutex> lk(m.mu);
-    m.cv.wait(lk, [&] { return !m.job && !m.busy; });
+    m.cv.wait(lk, [&] {
+        for (int i = 0; i < starch_ctx::Streaming::NLANE; ++i)
+            if (!lane_idle(m, i)) return false;
+        return true;
+    });
     if (m.err) throw StarchError(m.err, m.err_msg);
 }
 
-// hand buf[cur][0, n) to the encoder thread (the caller has waited for idle);
-// its first m.ctx_len bytes are context (already counted), open: it ends
-// inside a chromosome
+// a buffer other than buf[cur] that no lane holds (waits for one)
+int stream_free_buf(starch_ctx* c)
+{
+    auto& m = c->sm;
+    std::unique_lock<std::mutex> lk(m.mu);
+    int o = -1;
+    m.cv.wait(lk, [&] {
+        if (m.err) return true;
+        for (int i = 0; i < starch_ctx::Streaming::NBUF; ++i)
+            if (i != m.cur && !m.buf_busy[i]) { o = i; return true; }
+        return false;
+    });
+    if (m.err) throw StarchError(m.err, m.err_msg);
+    return o;
+}
+
+// hand buf[cur][0, n) to a lane: its first m.ctx_len bytes are context
+// (already counted), open: it ends inside a chromosome.  A batch cut inside a
+// chromosome, and the one after it, depend on each other's state (the open
+// bzip2 stream): they go to lane 0 with no other batch in flight; any other
+// batch to the first idle lane
 void stream_submit(starch_ctx* c, uint64_t n, bool open = false)
 {
     auto& m = c->sm;
-    m.stats.input_bytes += n - m.ctx_len;
-    HIP_CHECK(hipEventRecord(m.job_ev, c->cst));
+    const bool serial = m.ctx_len > 0 || open || m.last_open;
+    HIP_CHECK(hipEventRecord(m.buf_ev[m.cur], c->cst));
     {
-        std::lock_guard<std::mutex> lk(m.mu);
-        m.job = true;
-        m.job_buf = static_cast<const uint8_t*>(m.dbuf[m.cur].p);
-        m.job_n = n;
-        m.job_ctx = m.ctx_len;
-        m.job_open = open;
-        m.job_is = m.init_start;
-        m.job_ip = m.init_stop;
+        std::unique_lock<std::mutex> lk(m.mu);
+        int lane = -1;
+        m.cv.wait(lk, [&] {
+            if (m.err) return true;
+            if (serial) {
+                for (int i = 0; i < starch_ctx::Streaming::NLANE; ++i)
+                    if (!lane_idle(m, i)) return false;
+                lane = 0;
+                return true;
+            }
+            for (int i = 0; i < starch_ctx::Streaming::NLANE; ++i)
+                if (lane_idle(m, i)) { lane = i; return true; }
+            return false;
+        });
+        if (m.err) throw StarchError(m.err, m.err_msg);
+        auto& j = m.lj[lane];
+        j.pending = true;
+        j.bufi = m.cur;
+        j.n = n;
+        j.ctx = m.ctx_len;
+        j.open = open;
+        j.cont = m.last_open;
+        j.is = m.init_start;
+        j.ip = m.init_stop;
+        j.seq = m.seq_next++;
+        m.buf_busy[m.cur] = true;
+        m.last_open = open;
+        m.stats.input_bytes += n - m.ctx_len;
     }
     m.cv.notify_all();
 }
@@ -1265,8 +1347,7 @@ void stream_cut(starch_ctx* c)
         const uint64_t tail = m.held_n - ls;
         STRACE("stream cut inside a chromosome at %llu of %llu held", (unsigned long long)cut,
                (unsigned long long)m.held_n);
-        stream_wait(c);
-        const int o = 1 - m.cur;
+        const int o = stream_free_buf(c);
         stream_reserve(c, o, std::max<uint64_t>(tail + m.batch + (m.batch >> 2), 1ull << 20));
         m.pool.copy(m.buf[o], h + ls, tail);
         HIP_CHECK(hipMemcpyAsync(m.dbuf[o].p, static_cast<uint8_t*>(m.dbuf[m.cur].p) + ls, tail,
@@ -1281,10 +1362,9 @@ void stream_cut(starch_ctx* c)
         return;
     }
     const uint64_t cut = u.back().offset, tail = m.held_n - cut;
-    STRACE("stream cut at %llu of %llu held: wait for the encoder", (unsigned long long)cut, (unsigned long long)m.held_n);
-    stream_wait(c);                                   // the other buffer is free again
-    STRACE("stream cut: encoder idle");
-    const int o = 1 - m.cur;
+    STRACE("stream cut at %llu of %llu held: wait for a free buffer", (unsigned long long)cut, (unsigned long long)m.held_n);
+    const int o = stream_free_buf(c);
+    STRACE("stream cut: buffer %d free", o);
     stream_reserve(c, o, std::max<uint64_t>(tail + m.batch + (m.batch >> 2), 1ull << 20));
     m.pool.copy(m.buf[o], h + cut, tail);
     if (tail)   // the tail's device bytes move with it (ordered after their H2D on cst)
@@ -1806,7 +1886,9 @@ int starch_stream_begin(starch_ctx* c, const starch_options* opt, uint64_t batch
     c->stream_shutdown();                       // a session left open is abandoned
     auto& m = c->sm;
     if (!c->cst) HIP_CHECK(hipStreamCreateWithFlags(&c->cst, hipStreamNonBlocking));
-    if (!m.job_ev) HIP_CHECK(hipEventCreateWithFlags(&m.job_ev, hipEventDisableTiming));
+    for (auto& e : m.buf_ev)
+        if (!e) HIP_CHECK(hipEventCreateWithFlags(&e, hipEventDisableTiming));
+    for (int i = 1; i < starch_ctx::Streaming::NLANE; ++i) lane_ctx(c, i);   // (created here, not in a worker)
     HIP_CHECK(hipStreamSynchronize(c->cst));
     m.active = true;
     m.eof = false;
@@ -1822,7 +1904,11 @@ int starch_stream_begin(starch_ctx* c, const starch_options* opt, uint64_t batch
     m.try_at = m.batch;
     m.batches = 0;
     m.init_start = m.init_stop = 0;
-    m.job = m.busy = false;
+    for (auto& j : m.lj) j = starch_ctx::Streaming::Job{};
+    for (auto& b : m.buf_busy) b = false;
+    m.last_open = false;
+    m.seq_next = m.seq_commit = 0;
+    m.done.clear();
     m.err = 0;
     m.err_msg.clear();
     m.ready.assign(kMagic, kMagic + 4);
@@ -1833,11 +1919,10 @@ int starch_stream_begin(starch_ctx* c, const starch_options* opt, uint64_t batch
     m.stats = starch_stats{};
     c->have = false;
     c->streamed = false;
-    // both pinned buffers sized once for a batch plus a long held run (kept
+    // the pinned buffers sized once for a batch plus a long held run (kept
     // across sessions: pinning is paid on the context's first session only)
-    stream_reserve(c, 0, 2 * m.batch);
-    stream_reserve(c, 1, 2 * m.batch);
-    m.worker = std::thread(stream_worker, c);
+    for (int i = 0; i < starch_ctx::Streaming::NBUF; ++i) stream_reserve(c, i, 2 * m.batch);
+    for (int i = 0; i < starch_ctx::Streaming::NLANE; ++i) m.workers[i] = std::thread(stream_worker, c, i);
     return STARCH_OK;
     END_GUARD(c)
 }
@@ -1908,11 +1993,10 @@ int starch_stream_end(starch_ctx* c)
     auto& m = c->sm;
     if (!m.active) return STARCH_ERR_STATE;
     try {
+        // the rest goes to a lane as soon as one is free (the other may still
+        // be encoding); an open stream's last piece waits for its predecessor
+        if (m.held_n > m.ctx_len || m.last_open) stream_submit(c, m.held_n);
         stream_wait(c);
-        if (m.held_n > m.ctx_len || m.os.active) {
-            stream_submit(c, m.held_n);
-            stream_wait(c);
-        }
     } catch (...) {
         c->stream_shutdown();
         throw;
