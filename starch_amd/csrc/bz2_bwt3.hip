@@ -842,9 +842,19 @@ __global__ void __launch_bounds__(1024) k3_bin_scan(uint32_t* __restrict__ hist,
     __shared__ uint32_t tot[4096];
     __shared__ uint32_t scan_sh[1024 / 64 + 1];
     const int tid = threadIdx.x;
+    // the row loads of a bin are independent: 16 in flight at a time (a
+    // dependent walk over up to 128 rows cost ~70 us per call)
     for (uint32_t s = tid; s < nb; s += 1024) {
         uint32_t t = 0;
-        for (uint32_t w = 0; w < nwg; ++w) t += hist[(uint64_t)w * nb + s];
+        uint32_t w = 0;
+        for (; w + 16 <= nwg; w += 16) {
+            uint32_t x[16];
+#pragma unroll
+            for (int q = 0; q < 16; ++q) x[q] = hist[(uint64_t)(w + q) * nb + s];
+#pragma unroll
+            for (int q = 0; q < 16; ++q) t += x[q];
+        }
+        for (; w < nwg; ++w) t += hist[(uint64_t)w * nb + s];
         tot[s] = t;
     }
     __syncthreads();
@@ -867,7 +877,18 @@ __global__ void __launch_bounds__(1024) k3_bin_scan(uint32_t* __restrict__ hist,
         if (j < 8 * NS && (j % NS) == 0) seg[j / NS] = run;
         if (j < 8 * NS && s < nb) {
             uint32_t r = run;
-            for (uint32_t w = 0; w < nwg; ++w) {
+            uint32_t w = 0;
+            for (; w + 16 <= nwg; w += 16) {
+                uint32_t x[16];
+#pragma unroll
+                for (int q = 0; q < 16; ++q) x[q] = hist[(uint64_t)(w + q) * nb + s];
+#pragma unroll
+                for (int q = 0; q < 16; ++q) {
+                    hist[(uint64_t)(w + q) * nb + s] = r;
+                    r += x[q];
+                }
+            }
+            for (; w < nwg; ++w) {
                 uint32_t& hv = hist[(uint64_t)w * nb + s];
                 const uint32_t t = hv;
                 hv = r;
@@ -2755,15 +2776,28 @@ __global__ void __launch_bounds__(256) k3_period(Ctx c)
 {
     __shared__ uint32_t q_sh[16];
     __shared__ uint32_t nq_sh;
+    __shared__ uint32_t dv[32];                    // divisors d <= sqrt(n) < 1024, as bits
     const uint32_t slot = blockIdx.x, b = c.b0 + slot;
     const uint32_t n = c.blocks[b].n;
     if (n < 2) return;
+    // prime factors of n: the workgroup marks every divisor <= sqrt(n) (a few
+    // trial divisions per thread: there is no integer divide, and one thread
+    // walking all ~950 candidates took ~70 us), then one thread divides out the
+    // marked ones in increasing order (composites no longer divide by then)
+    if (threadIdx.x < 32) dv[threadIdx.x] = 0;
+    __syncthreads();
+    for (uint32_t d = 2 + threadIdx.x; d * d <= n; d += 256)
+        if (n % d == 0) atomicOr(&dv[d >> 5], 1u << (d & 31));
+    __syncthreads();
     if (threadIdx.x == 0) {
         uint32_t m = n, k = 0;
-        for (uint32_t d = 2; d * d <= m; ++d)
-            if (m % d == 0) {
-                q_sh[k++] = d;
-                while (m % d == 0) m /= d;
+        for (uint32_t w = 0; w < 32; ++w)
+            for (uint32_t bits = dv[w]; bits; bits &= bits - 1) {
+                const uint32_t d = 32 * w + (uint32_t)__builtin_ctz(bits);
+                if (m % d == 0) {
+                    q_sh[k++] = d;
+                    while (m % d == 0) m /= d;
+                }
             }
         if (m > 1) q_sh[k++] = m;
         nq_sh = k;
