@@ -193,6 +193,9 @@ __device__ __forceinline__ uint64_t lanemask_lt()
 #ifndef STARCH_NT
 #define STARCH_NT 0   // 1: non-temporal SA/LL/value streams (measured: cfg2 sort 23.5 -> 34.3 ms, cfg4 110 -> 130 ms)
 #endif
+#ifndef STARCH_W_UNROLL
+#define STARCH_W_UNROLL 0   // k3_sort_w's rank loops unrolled by 4 (experiment)
+#endif
 template <class T>
 __device__ __forceinline__ T ld_nt(const T* p)
 {
@@ -1482,6 +1485,9 @@ __global__ void __launch_bounds__(256) k3_sort_w(Ctx c, const uint64_t* __restri
             // scalar broadcasts when the pass holds one group, lane shuffles otherwise
             uint32_t r = 0;
             if (ng == 1) {
+#if STARCH_W_UNROLL
+#pragma unroll 4
+#endif
                 for (uint32_t q = 0; q < total; ++q) {
                     const uint64_t kq = ((uint64_t)(uint32_t)__builtin_amdgcn_readlane((int)(k >> 32), (int)q) << 32) |
                                         (uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)k, (int)q);
@@ -1489,6 +1495,9 @@ __global__ void __launch_bounds__(256) k3_sort_w(Ctx c, const uint64_t* __restri
                 }
             } else {
                 const uint32_t maxm = wave_reduce_max(valid ? m : 0u);
+#if STARCH_W_UNROLL
+#pragma unroll 4
+#endif
                 for (uint32_t q = 0; q < maxm; ++q) {
                     const bool in = valid && q < m;
                     const uint64_t kq = shfl64(k, in ? gstart + q : lane);
@@ -1535,10 +1544,29 @@ __global__ void __launch_bounds__(256) k3_sort_w(Ctx c, const uint64_t* __restri
 // rank of key kj among positions [rs, re) of xk.  Keys are (key << IDXB) |
 // group index: unique, so one 64-bit compare orders them (ties of the key
 // broken by index)
+#ifndef STARCH_RANK_UNROLL
+#define STARCH_RANK_UNROLL 4   // keys in flight per step: 4 (cfg2 sort 22.8 -> 21.5-21.9 ms, cfg4 107.6 -> 104.1-104.4); 8 no better; 0 one at a time
+#endif
 __device__ __forceinline__ uint32_t rank_in(const uint64_t* xk, uint32_t rs, uint32_t re, uint64_t kj)
 {
     uint32_t r = 0;
-    for (uint32_t q = rs; q < re; ++q) r += xk[q] < kj ? 1u : 0u;
+    uint32_t q = rs;
+    if constexpr (STARCH_RANK_UNROLL >= 8) {
+        for (; q + 8 <= re; q += 8) {
+            uint64_t x[8];
+#pragma unroll
+            for (int i = 0; i < 8; ++i) x[i] = xk[q + i];
+#pragma unroll
+            for (int i = 0; i < 8; ++i) r += x[i] < kj ? 1u : 0u;
+        }
+    }
+    if constexpr (STARCH_RANK_UNROLL != 0) {
+        for (; q + 4 <= re; q += 4) {
+            const uint64_t a = xk[q], b = xk[q + 1], c2 = xk[q + 2], d = xk[q + 3];
+            r += (a < kj ? 1u : 0u) + (b < kj ? 1u : 0u) + (c2 < kj ? 1u : 0u) + (d < kj ? 1u : 0u);
+        }
+    }
+    for (; q < re; ++q) r += xk[q] < kj ? 1u : 0u;
     return r;
 }
 
