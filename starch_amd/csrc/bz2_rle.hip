@@ -584,7 +584,9 @@ __global__ void __launch_bounds__(256) k_rle_emit(const uint8_t* __restrict__ te
         const int slot = (Wt + o >= wnext) ? 1 : 0;
         if (t < 3) {
             ob[o] = c;
-            if (t == 0) ul[slot][c >> 5][threadIdx.x] |= 1u << (c & 31);
+            // an LDS OR with no return (ds_or_b32): no read-modify-write chain
+            // through the byte loop
+            if (t == 0) atomicOr(&ul[slot][c >> 5][threadIdx.x], 1u << (c & 31));
         } else if (t == 3) {
             const uint64_t i = d.beg + off + k;
             uint64_t j = i + 1;
@@ -593,7 +595,7 @@ __global__ void __launch_bounds__(256) k_rle_emit(const uint8_t* __restrict__ te
             const uint8_t cnt_byte = (uint8_t)(L - 4);
             ob[o] = c;
             ob[o + 1] = cnt_byte;
-            ul[slot][cnt_byte >> 5][threadIdx.x] |= 1u << (cnt_byte & 31);
+            atomicOr(&ul[slot][cnt_byte >> 5][threadIdx.x], 1u << (cnt_byte & 31));
         }
         o += rle_w(t);
     }

@@ -1186,18 +1186,28 @@ k_tf_fused(const uint8_t* __restrict__ bed, uint64_t n, const FusedOut fo, uint3
         const uint4* q = reinterpret_cast<const uint4*>(tb + ch * 32);
         const uint4 x = q[0], y = q[1];
         const uint32_t w[8] = {x.x, x.y, x.z, x.w, y.x, y.y, y.z, y.w};
-        uint32_t nm = 0, fm = 0, tm = 0, zm = 0;
+        uint32_t nm = 0, tm = 0, anyz = 0, anyf = 0;
 #pragma unroll
         for (int j = 0; j < 8; ++j) {
             nm |= eq4(w[j], 0x0a0a0a0au) << (4 * j);
             tm |= eq4(w[j], 0x09090909u) << (4 * j);
-            zm |= eq4(w[j], 0u) << (4 * j);
-            fm |= eq4(w[j], 0xffffffffu) << (4 * j);
+            anyz |= (w[j] - 0x01010101u) & ~w[j] & 0x80808080u;    // some byte is NUL
+            anyf |= (~w[j] - 0x01010101u) & w[j] & 0x80808080u;    // some byte is 0xFF
         }
         S.tabm[ch] = tm;
         const uint32_t lo = ch * 32 < Lt0 ? Lt0 - ch * 32 : 0u;
         const uint32_t hi = Lend - ch * 32 < 32u ? Lend - ch * 32 : 32u;
         const uint32_t keep = (hi >= 32u ? 0xFFFFFFFFu : ((1u << hi) - 1u)) & ~((1u << lo) - 1u);
+        // exact per-byte NUL / 0xFF masks only where a word holds one, or in the
+        // chunk that runs past the tile's end (its last bytes are not staged)
+        uint32_t zm = 0, fm = 0;
+        if (anyz | anyf | (hi < 32u)) {
+#pragma unroll
+            for (int j = 0; j < 8; ++j) {
+                zm |= eq4(w[j], 0u) << (4 * j);
+                fm |= eq4(w[j], 0xffffffffu) << (4 * j);
+            }
+        }
         // a NUL among the staged bytes (everything from a0 up to the tile's end;
         // the bytes after it are not staged)
         if (zm & (hi >= 32u ? 0xFFFFFFFFu : ((1u << hi) - 1u))) S.nul = 1;
