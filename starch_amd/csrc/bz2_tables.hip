@@ -517,26 +517,51 @@ __global__ void __launch_bounds__(T32) __attribute__((amdgpu_waves_per_eu(STARCH
             }
             if (valid) sel_l[g] = (uint8_t)bt;
             // rfreq: once per distinct table chosen in this wave, sum the lanes'
-            // byte histograms as u16 pairs (<= 64 x 50 per field) and let one
-            // lane add them to the wave's private rows -- no same-address LDS
-            // atomics (a wave's 64 groups mostly pick one or two tables)
+            // byte histograms as u16 pairs (<= 64 x 50 per field) into the
+            // wave's private rows -- no same-address LDS atomics (a wave's 64
+            // groups mostly pick one or two tables).  The counts are summed
+            // over the wave by recursive halving, all on the VALU: at lane
+            // bits 5 and 4 (gfx950 v_permlane32_swap / v_permlane16_swap) a
+            // lane keeps half of its packed u8 words (<= 4 x 50 per byte)
+            // plus its partner's copy of that half; the two words left become
+            // u16 pairs, bit 3 halves again (DPP row_ror:8) and three DPP row
+            // shifts sum each 8-lane run.  Lanes 7 and 15 of every row then
+            // hold symbols 4q..4q+3, q = 4 * bit5 + 2 * bit4 + bit3, summed
+            // over the wave, and add them to the wave's rows.
             uint32_t rem = valid ? (uint32_t)bt : 7u;
             for (;;) {
                 const uint64_t act = __ballot(rem != 7u);
                 if (!act) break;
                 const uint32_t t = (uint32_t)__builtin_amdgcn_readlane((int)rem, (int)(__ffsll((long long)act) - 1));
                 const bool mine = rem == t;
+                uint32_t a[8];
 #pragma unroll
-                for (int q = 0; q < 8; ++q) {
-                    if (4 * q >= alpha) break;
-                    const uint32_t x = mine ? h[q] : 0u;
-                    const uint32_t ev = wave_reduce_add(x & 0x00ff00ffu), od = wave_reduce_add((x >> 8) & 0x00ff00ffu);
-                    if (lane == 0) {
-                        rf[wid][t][4 * q] += ev & 0xffffu;
-                        rf[wid][t][4 * q + 1] += od & 0xffffu;
-                        rf[wid][t][4 * q + 2] += ev >> 16;
-                        rf[wid][t][4 * q + 3] += od >> 16;
-                    }
+                for (int q = 0; q < 8; ++q) a[q] = mine ? h[q] : 0u;
+#pragma unroll
+                for (int i = 0; i < 4; ++i) {                  // bit 5: words q (lo half) | q + 4 (hi half)
+                    const auto r = __builtin_amdgcn_permlane32_swap(a[i], a[4 + i], false, false);
+                    a[i] = r[0] + r[1];
+                }
+#pragma unroll
+                for (int i = 0; i < 2; ++i) {                  // bit 4: words q | q + 2
+                    const auto r = __builtin_amdgcn_permlane16_swap(a[i], a[2 + i], false, false);
+                    a[i] = r[0] + r[1];
+                }
+                // words q0, q0 + 1 -> u16 pairs (ev: symbols 4q, 4q+2; od: 4q+1, 4q+3)
+                const bool b3 = (lane & 8) != 0;
+                const uint32_t src = b3 ? a[0] : a[1], own = b3 ? a[1] : a[0];   // bit 3: q0 | q0 + 1
+                uint32_t ev = own & 0x00ff00ffu, od = (own >> 8) & 0x00ff00ffu;
+                ev += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)(src & 0x00ff00ffu), 0x128, 0xf, 0xf, false);
+                od += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)((src >> 8) & 0x00ff00ffu), 0x128, 0xf, 0xf, false);
+                ev += dpp_up(ev, 1); od += dpp_up(od, 1);      // 8-lane runs: lanes 7, 15 of a row
+                ev += dpp_up(ev, 2); od += dpp_up(od, 2);
+                ev += dpp_up(ev, 4); od += dpp_up(od, 4);
+                if ((lane & 7) == 7) {
+                    const uint32_t q = ((uint32_t)lane >> 5) * 4u + (((uint32_t)lane >> 4) & 1u) * 2u + (b3 ? 1u : 0u);
+                    rf[wid][t][4 * q] += ev & 0xffffu;
+                    rf[wid][t][4 * q + 1] += od & 0xffffu;
+                    rf[wid][t][4 * q + 2] += ev >> 16;
+                    rf[wid][t][4 * q + 3] += od >> 16;
                 }
                 if (mine) rem = 7u;
             }

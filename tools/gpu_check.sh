@@ -1,19 +1,18 @@
 #!/usr/bin/env bash
-# GPU box: selected test files (FILES), then the whole -m gpu suite, then one
-# bench line.  Each GPU step has its own time limit; a failure ends the run.
+# GPU box (dev): optional GPU tests (TESTS=1 all, TESTS=<-k expr>), then the cfg2
+# bench line (verified 24/24 against the goldens) and the 1/8-of-cfg2 line
 set -o pipefail
-mkdir -p gpurun_out
+mkdir -p gpurun_out/chk
+O=gpurun_out/chk
 export PYTHONUNBUFFERED=1
-PT="python -u -m pytest -x --timeout ${TT:-200} --timeout-method thread"
-if [ -n "${FILES:-}" ]; then
-  timeout -k 10 ${T0:-600} $PT -v $FILES > gpurun_out/t_new.log 2>&1 || { tail -30 gpurun_out/t_new.log; exit 1; }
-  tail -3 gpurun_out/t_new.log
+if [ "${TESTS:-}" = 1 ]; then
+  timeout -k 10 600 python -u -m pytest tests -m gpu -x -q --timeout 300 --timeout-method thread > $O/tests.log 2>&1 || { tail -30 $O/tests.log; exit 1; }
+  tail -1 $O/tests.log
+elif [ -n "${TESTS:-}" ]; then
+  timeout -k 10 600 python -u -m pytest tests -m gpu -x -q --timeout 300 --timeout-method thread -k "$TESTS" > $O/tests.log 2>&1 || { tail -30 $O/tests.log; exit 1; }
+  tail -1 $O/tests.log
 fi
-if [ -z "${NOALL:-}" ]; then
-  timeout -k 10 ${T1:-900} $PT -q -m gpu tests > gpurun_out/t_all.log 2>&1 || { tail -30 gpurun_out/t_all.log; exit 1; }
-  tail -3 gpurun_out/t_all.log
-fi
-if [ -z "${NOBENCH:-}" ]; then
-  timeout -k 10 ${TB:-600} python bench.py ${BENCH_ARGS:---steps 10 --warmup 3} > gpurun_out/bench.json 2> gpurun_out/bench.err || { tail -30 gpurun_out/bench.err; exit 1; }
-  cat gpurun_out/bench.json
-fi
+timeout -k 10 300 python bench.py --no-cpu-baseline --no-e2e ${BENCH_EXTRA:-} > $O/cfg2.json 2> $O/cfg2.err || { tail -20 $O/cfg2.err; exit 1; }
+python3 -c "import json;d=json.load(open('$O/cfg2.json'));print('cfg2', d['ms_per_step'], d['value'], d['verify']['match'], d['stage_ms'])"
+timeout -k 10 300 python bench.py --lines 12500000 --steps 10 --warmup 3 --no-cpu-baseline --no-e2e ${BENCH_EXTRA:-} > $O/eighth.json 2> $O/eighth.err || { tail -20 $O/eighth.err; exit 1; }
+python3 -c "import json;d=json.load(open('$O/eighth.json'));print('eighth', d['ms_per_step'], d['stage_ms'])"
