@@ -373,6 +373,43 @@ __device__ __forceinline__ uint32_t byte_of(const uint32_t (&h)[8], int v)
     return (h[v >> 2] >> (8 * (v & 3))) & 0xffu;
 }
 
+// Sum over the wave of 32 u8 counts per lane (each <= 50; a lane adds only
+// when `mine`), by recursive halving, all on the VALU: at lane bits 5 and 4
+// (gfx950 v_permlane32_swap / v_permlane16_swap) a lane keeps half of its
+// packed u8 words (<= 4 x 50 per byte) plus its partner's copy of that half;
+// the two words left become u16 pairs, bit 3 halves again (DPP row_ror:8) and
+// three DPP row shifts sum each 8-lane run.  Lanes 7 and 15 of every row then
+// hold symbols 4q..4q+3, q = 4 * bit5 + 2 * bit4 + bit3, summed over the wave:
+// ev = counts of 4q | 4q+2 << 16, od = 4q+1 | 4q+3 << 16.  ~30 VALU ops
+// where 16 wave reductions took ~110.
+__device__ __forceinline__ void wave_sum_u8x32(const uint32_t (&h)[8], bool mine, int lane, uint32_t& ev,
+                                               uint32_t& od, uint32_t& q)
+{
+    uint32_t a[8];
+#pragma unroll
+    for (int k = 0; k < 8; ++k) a[k] = mine ? h[k] : 0u;
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {                  // bit 5: words k (lo half) | k + 4 (hi half)
+        const auto r = __builtin_amdgcn_permlane32_swap(a[i], a[4 + i], false, false);
+        a[i] = r[0] + r[1];
+    }
+#pragma unroll
+    for (int i = 0; i < 2; ++i) {                  // bit 4: words k | k + 2
+        const auto r = __builtin_amdgcn_permlane16_swap(a[i], a[2 + i], false, false);
+        a[i] = r[0] + r[1];
+    }
+    const bool b3 = (lane & 8) != 0;               // bit 3: words q0 | q0 + 1, as u16 pairs
+    const uint32_t src = b3 ? a[0] : a[1], own = b3 ? a[1] : a[0];
+    ev = own & 0x00ff00ffu;
+    od = (own >> 8) & 0x00ff00ffu;
+    ev += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)(src & 0x00ff00ffu), 0x128, 0xf, 0xf, false);
+    od += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)((src >> 8) & 0x00ff00ffu), 0x128, 0xf, 0xf, false);
+    ev += dpp_up(ev, 1); od += dpp_up(od, 1);      // 8-lane runs: lanes 7, 15 of a row
+    ev += dpp_up(ev, 2); od += dpp_up(od, 2);
+    ev += dpp_up(ev, 4); od += dpp_up(od, 4);
+    q = ((uint32_t)lane >> 5) * 4u + (((uint32_t)lane >> 4) & 1u) * 2u + (b3 ? 1u : 0u);
+}
+
 // T32 threads per block: 256 when the batch fills the GPU with blocks (their
 // serial phases overlap other blocks'), 1024 for a batch of few blocks (each
 // block's group loops and its six heaps spread over 16 waves: per-block latency)
@@ -433,29 +470,36 @@ __global__ void __launch_bounds__(T32) __attribute__((amdgpu_waves_per_eu(STARCH
             for (int q = 0; q < 8; ++q) hl[q][tid] = 0;
             const uint32_t gs = g * 50;
             const uint32_t cnt = gs + 50 < n_mtf ? 50u : n_mtf - gs;
-            const uint32_t* m32 = reinterpret_cast<const uint32_t*>(mtfv + gs);   // gs even: 4-B aligned
-            uint32_t wv[25];
+            // the group's 100 bytes (4-B aligned: gs even) by seven aligned
+            // 16-B loads over its 112-byte window -- a lane per group strides
+            // 100 B, so 16-B loads touch the same lines in a quarter of the
+            // instructions 4-B loads took; o = the group's first word in it
+            const uintptr_t ga = reinterpret_cast<uintptr_t>(mtfv + gs);
+            const uint4* w4 = reinterpret_cast<const uint4*>(ga & ~(uintptr_t)15);
+            const uint32_t o = (uint32_t)(ga & 15u) >> 2, wend = o + (cnt + 1) / 2;   // words [o, wend)
+            uint32_t wv[28];
 #pragma unroll
-            for (int q = 0; q < 25; ++q) wv[q] = (2u * q < cnt) ? m32[q] : 0u;   // all loads in flight
+            for (int k = 0; k < 7; ++k) {
+                const uint4 x = 4u * k < wend ? w4[k] : make_uint4(0, 0, 0, 0);   // all loads in flight
+                wv[4 * k] = x.x; wv[4 * k + 1] = x.y; wv[4 * k + 2] = x.z; wv[4 * k + 3] = x.w;
+            }
 #pragma unroll
-            for (int q = 0; q < 25; ++q) {
-                const uint32_t v0 = wv[q] & 0xffffu, v1 = wv[q] >> 16;
-                if (2u * q < cnt) atomicAdd(&hl[v0 >> 2][tid], 1u << (8 * (v0 & 3)));
-                if (2u * q + 1 < cnt) atomicAdd(&hl[v1 >> 2][tid], 1u << (8 * (v1 & 3)));
+            for (int k = 0; k < 28; ++k) {
+                const uint32_t j = (uint32_t)k - o;                          // word of the group (wraps if k < o)
+                const uint32_t v0 = wv[k] & 0xffffu, v1 = wv[k] >> 16;
+                if (j < 25u && 2u * j < cnt) atomicAdd(&hl[v0 >> 2][tid], 1u << (8 * (v0 & 3)));
+                if (j < 25u && 2u * j + 1 < cnt) atomicAdd(&hl[v1 >> 2][tid], 1u << (8 * (v1 & 3)));
             }
 #pragma unroll
             for (int q = 0; q < 8; ++q) h[q] = hl[q][tid];
             hist[2 * g] = make_uint4(h[0], h[1], h[2], h[3]);
             hist[2 * g + 1] = make_uint4(h[4], h[5], h[6], h[7]);
         }
-        // mtfFreq: wave sums of u16 pairs, one lane adds
-#pragma unroll
-        for (int q = 0; q < 8; ++q) {
-            if (4 * q >= alpha) break;
-            uint32_t ev = h[q] & 0x00ff00ffu, od = (h[q] >> 8) & 0x00ff00ffu;
-            ev = wave_reduce_add(ev);
-            od = wave_reduce_add(od);
-            if (lane == 0) {
+        // mtfFreq: wave sums (wave_sum_u8x32), its 8 result lanes add
+        {
+            uint32_t ev, od, q;
+            wave_sum_u8x32(h, true, lane, ev, od, q);
+            if ((lane & 7) == 7) {
                 if (ev & 0xffffu) atomicAdd(&freq[4 * q], ev & 0xffffu);
                 if (od & 0xffffu) atomicAdd(&freq[4 * q + 1], od & 0xffffu);
                 if (ev >> 16) atomicAdd(&freq[4 * q + 2], ev >> 16);
@@ -519,45 +563,17 @@ __global__ void __launch_bounds__(T32) __attribute__((amdgpu_waves_per_eu(STARCH
             // rfreq: once per distinct table chosen in this wave, sum the lanes'
             // byte histograms as u16 pairs (<= 64 x 50 per field) into the
             // wave's private rows -- no same-address LDS atomics (a wave's 64
-            // groups mostly pick one or two tables).  The counts are summed
-            // over the wave by recursive halving, all on the VALU: at lane
-            // bits 5 and 4 (gfx950 v_permlane32_swap / v_permlane16_swap) a
-            // lane keeps half of its packed u8 words (<= 4 x 50 per byte)
-            // plus its partner's copy of that half; the two words left become
-            // u16 pairs, bit 3 halves again (DPP row_ror:8) and three DPP row
-            // shifts sum each 8-lane run.  Lanes 7 and 15 of every row then
-            // hold symbols 4q..4q+3, q = 4 * bit5 + 2 * bit4 + bit3, summed
-            // over the wave, and add them to the wave's rows.
+            // groups mostly pick one or two tables), summed over the wave by
+            // wave_sum_u8x32; its 8 result lanes add them to the wave's rows
             uint32_t rem = valid ? (uint32_t)bt : 7u;
             for (;;) {
                 const uint64_t act = __ballot(rem != 7u);
                 if (!act) break;
                 const uint32_t t = (uint32_t)__builtin_amdgcn_readlane((int)rem, (int)(__ffsll((long long)act) - 1));
                 const bool mine = rem == t;
-                uint32_t a[8];
-#pragma unroll
-                for (int q = 0; q < 8; ++q) a[q] = mine ? h[q] : 0u;
-#pragma unroll
-                for (int i = 0; i < 4; ++i) {                  // bit 5: words q (lo half) | q + 4 (hi half)
-                    const auto r = __builtin_amdgcn_permlane32_swap(a[i], a[4 + i], false, false);
-                    a[i] = r[0] + r[1];
-                }
-#pragma unroll
-                for (int i = 0; i < 2; ++i) {                  // bit 4: words q | q + 2
-                    const auto r = __builtin_amdgcn_permlane16_swap(a[i], a[2 + i], false, false);
-                    a[i] = r[0] + r[1];
-                }
-                // words q0, q0 + 1 -> u16 pairs (ev: symbols 4q, 4q+2; od: 4q+1, 4q+3)
-                const bool b3 = (lane & 8) != 0;
-                const uint32_t src = b3 ? a[0] : a[1], own = b3 ? a[1] : a[0];   // bit 3: q0 | q0 + 1
-                uint32_t ev = own & 0x00ff00ffu, od = (own >> 8) & 0x00ff00ffu;
-                ev += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)(src & 0x00ff00ffu), 0x128, 0xf, 0xf, false);
-                od += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)((src >> 8) & 0x00ff00ffu), 0x128, 0xf, 0xf, false);
-                ev += dpp_up(ev, 1); od += dpp_up(od, 1);      // 8-lane runs: lanes 7, 15 of a row
-                ev += dpp_up(ev, 2); od += dpp_up(od, 2);
-                ev += dpp_up(ev, 4); od += dpp_up(od, 4);
+                uint32_t ev, od, q;
+                wave_sum_u8x32(h, mine, lane, ev, od, q);
                 if ((lane & 7) == 7) {
-                    const uint32_t q = ((uint32_t)lane >> 5) * 4u + (((uint32_t)lane >> 4) & 1u) * 2u + (b3 ? 1u : 0u);
                     rf[wid][t][4 * q] += ev & 0xffffu;
                     rf[wid][t][4 * q + 1] += od & 0xffffu;
                     rf[wid][t][4 * q + 2] += ev >> 16;
