@@ -813,7 +813,8 @@ __device__ __forceinline__ uint32_t bin_of(uint64_t it, uint32_t i, uint32_t vs)
 
 // chunks are multiples of 64 items, so every wave's 64 items share i >> 6
 __global__ void __launch_bounds__(256) k3_bin_hist(const uint64_t* __restrict__ in, uint32_t n, uint32_t nb,
-                                                    uint32_t ch, uint32_t* __restrict__ hist, uint32_t vs)
+                                                    uint32_t ch, uint32_t* __restrict__ hist,
+                                                    uint32_t* __restrict__ colsum, uint32_t vs)
 {
     __shared__ uint32_t h[4096];
     for (uint32_t i = threadIdx.x; i < nb; i += 256) h[i] = 0;
@@ -834,33 +835,23 @@ __global__ void __launch_bounds__(256) k3_bin_hist(const uint64_t* __restrict__ 
         }
     }
     __syncthreads();
-    for (uint32_t i = threadIdx.x; i < nb; i += 256) hist[(uint64_t)blockIdx.x * nb + i] = h[i];
+    // this chunk's place inside each bin: one global atomic per non-empty bin
+    // (chunks take their places in any order; a bin's items are independent)
+    for (uint32_t i = threadIdx.x; i < nb; i += 256) {
+        const uint32_t x = h[i];
+        hist[(uint64_t)blockIdx.x * nb + i] = x ? atomicAdd(&colsum[i], x) : 0u;
+    }
 }
 
-// one workgroup: per-block totals, XCD-ordered exclusive scan, per-(chunk,
-// block) write offsets in place; seg[x] = start of XCD x's segment
-__global__ void __launch_bounds__(1024) k3_bin_scan(uint32_t* __restrict__ hist, uint32_t nwg, uint32_t nb,
-                                                     uint32_t* __restrict__ seg)
+// one workgroup: the bins' totals (k3_bin_hist's atomics), reset for the
+// next binning, and their XCD-ordered exclusive scan -> each bin's start;
+// seg[x] = start of XCD x's segment.  (Per-(chunk, bin) offsets used to be
+// scanned here row by row: a dependent walk over up to 128 rows per bin.)
+__global__ void __launch_bounds__(1024) k3_bin_scan(uint32_t* __restrict__ colsum, uint32_t* __restrict__ bstart,
+                                                     uint32_t nb, uint32_t* __restrict__ seg)
 {
-    __shared__ uint32_t tot[4096];
     __shared__ uint32_t scan_sh[1024 / 64 + 1];
     const int tid = threadIdx.x;
-    // the row loads of a bin are independent: 16 in flight at a time (a
-    // dependent walk over up to 128 rows cost ~70 us per call)
-    for (uint32_t s = tid; s < nb; s += 1024) {
-        uint32_t t = 0;
-        uint32_t w = 0;
-        for (; w + 16 <= nwg; w += 16) {
-            uint32_t x[16];
-#pragma unroll
-            for (int q = 0; q < 16; ++q) x[q] = hist[(uint64_t)(w + q) * nb + s];
-#pragma unroll
-            for (int q = 0; q < 16; ++q) t += x[q];
-        }
-        for (; w < nwg; ++w) t += hist[(uint64_t)w * nb + s];
-        tot[s] = t;
-    }
-    __syncthreads();
     const uint32_t NS = (nb + 7) / 8;               // blocks per XCD segment (upper bound)
     // XCD-ordered sequence j -> block s = (j / NS) + 8 * (j % NS); 4 entries per thread
     uint32_t v[4], sum = 0;
@@ -868,7 +859,11 @@ __global__ void __launch_bounds__(1024) k3_bin_scan(uint32_t* __restrict__ hist,
     for (int q = 0; q < 4; ++q) {
         const uint32_t j = tid * 4 + q;
         const uint32_t s = (j / NS) + 8u * (j % NS);
-        v[q] = (j < 8 * NS && s < nb) ? tot[s] : 0u;
+        v[q] = 0u;
+        if (j < 8 * NS && s < nb) {
+            v[q] = colsum[s];
+            colsum[s] = 0u;
+        }
         sum += v[q];
     }
     uint32_t total = 0;
@@ -878,26 +873,7 @@ __global__ void __launch_bounds__(1024) k3_bin_scan(uint32_t* __restrict__ hist,
         const uint32_t j = tid * 4 + q;
         const uint32_t s = (j / NS) + 8u * (j % NS);
         if (j < 8 * NS && (j % NS) == 0) seg[j / NS] = run;
-        if (j < 8 * NS && s < nb) {
-            uint32_t r = run;
-            uint32_t w = 0;
-            for (; w + 16 <= nwg; w += 16) {
-                uint32_t x[16];
-#pragma unroll
-                for (int q = 0; q < 16; ++q) x[q] = hist[(uint64_t)(w + q) * nb + s];
-#pragma unroll
-                for (int q = 0; q < 16; ++q) {
-                    hist[(uint64_t)(w + q) * nb + s] = r;
-                    r += x[q];
-                }
-            }
-            for (; w < nwg; ++w) {
-                uint32_t& hv = hist[(uint64_t)w * nb + s];
-                const uint32_t t = hv;
-                hv = r;
-                r += t;
-            }
-        }
+        if (j < 8 * NS && s < nb) bstart[s] = run;
         run += v[q];
     }
     if (tid == 0) seg[8] = total;
@@ -905,10 +881,11 @@ __global__ void __launch_bounds__(1024) k3_bin_scan(uint32_t* __restrict__ hist,
 
 __global__ void __launch_bounds__(256) k3_bin_scatter(const uint64_t* __restrict__ in, uint32_t n, uint32_t nb,
                                                        uint32_t ch, const uint32_t* __restrict__ hist,
+                                                       const uint32_t* __restrict__ bstart,
                                                        uint64_t* __restrict__ out, uint32_t vs)
 {
     __shared__ uint32_t cur[4096];
-    for (uint32_t i = threadIdx.x; i < nb; i += 256) cur[i] = hist[(uint64_t)blockIdx.x * nb + i];
+    for (uint32_t i = threadIdx.x; i < nb; i += 256) cur[i] = bstart[i] + hist[(uint64_t)blockIdx.x * nb + i];
     __syncthreads();
     const uint32_t a = blockIdx.x * ch, e = a + ch < n ? a + ch : n;
     for (uint32_t i0 = a; i0 < e; i0 += 256) {     // wave-uniform trip count
@@ -2885,7 +2862,7 @@ bool launch_bwt3(BlockDesc* blocks, uint32_t b0, uint32_t nb, const uint8_t* blk
     const uint64_t nb_bins = nb < 64 ? 8ull * nb : nb;     // bins of k3_bin_* (see bin_of)
     constexpr uint32_t QSETS = 64, QSET = 8 * XQ_STRIDE + 32;   // queue heads (a line each) + segments per launch
     const uint64_t hg_words = 2ull * HG_MAXN + (uint64_t)HG_MAXN * 512 + 3ull * GB_MAXN + 64;
-    const uint64_t words = 2 * C_N + 14ull * nb + QSETS * QSET + nwg_bin * nb_bins +
+    const uint64_t words = 2 * C_N + 14ull * nb + QSETS * QSET + (nwg_bin + 2) * nb_bins +
                            2 * (cap_s + cap_s2 + cap_m0 + cap_m1 + cap_m2 + cap_m3 + 2 * cap_l) + 64 + hg_words;
     uint32_t* mw = meta.as<uint32_t>(words);
     Ctx c;
@@ -2903,7 +2880,9 @@ bool launch_bwt3(BlockDesc* blocks, uint32_t b0, uint32_t nb, const uint8_t* blk
     c.L.tied = c.L.rounds + nb;
     c.L.geo = reinterpret_cast<Geo*>(c.L.tied + nb);            // 8 words per slot
     uint32_t* qpool = reinterpret_cast<uint32_t*>(c.L.geo + nb);
-    uint32_t* binh = qpool + QSETS * QSET;
+    uint32_t* bincol = qpool + QSETS * QSET;       // per-bin running totals (zeroed below, reset by k3_bin_scan)
+    uint32_t* binst = bincol + nb_bins;            // per-bin starts
+    uint32_t* binh = binst + nb_bins;
     uintptr_t p = reinterpret_cast<uintptr_t>(binh + nwg_bin * nb_bins);
     p = (p + 7) & ~(uintptr_t)7;
     c.L.s = reinterpret_cast<uint64_t*>(p);
@@ -2938,7 +2917,7 @@ bool launch_bwt3(BlockDesc* blocks, uint32_t b0, uint32_t nb, const uint8_t* blk
     c.qhead = nullptr;
     c.qseg = nullptr;
     c.nbins = wide ? PNB_WIDE : PNB;
-    HIP_CHECK(hipMemsetAsync(mw, 0, (2 * C_N + 14ull * nb + QSETS * QSET) * sizeof(uint32_t), st));
+    HIP_CHECK(hipMemsetAsync(mw, 0, (2 * C_N + 14ull * nb + QSETS * QSET + nb_bins) * sizeof(uint32_t), st));
     static const bool period_off = [] { const char* e = getenv("STARCH_PERIOD_CHECK"); return e && !strcmp(e, "0"); }();
     if (!period_off) hipLaunchKernelGGL(k3_period, dim3(nb), dim3(256), 0, st, c);
 
@@ -2979,9 +2958,9 @@ bool launch_bwt3(BlockDesc* blocks, uint32_t b0, uint32_t nb, const uint8_t* blk
         if (nwg > BIN_MAXWG) nwg = BIN_MAXWG;
         const uint32_t ch = ((n + nwg - 1) / nwg + 63) & ~63u;   // whole waves of items
         const uint32_t vs = nb_bins > nb ? 3u : 0u, nbv = nb << vs;
-        hipLaunchKernelGGL(k3_bin_hist, dim3(nwg), dim3(256), 0, st, list, n, nbv, ch, binh, vs);
-        hipLaunchKernelGGL(k3_bin_scan, dim3(1), dim3(1024), 0, st, binh, nwg, nbv, seg);
-        hipLaunchKernelGGL(k3_bin_scatter, dim3(nwg), dim3(256), 0, st, list, n, nbv, ch, binh, out, vs);
+        hipLaunchKernelGGL(k3_bin_hist, dim3(nwg), dim3(256), 0, st, list, n, nbv, ch, binh, bincol, vs);
+        hipLaunchKernelGGL(k3_bin_scan, dim3(1), dim3(1024), 0, st, bincol, binst, nbv, seg);
+        hipLaunchKernelGGL(k3_bin_scatter, dim3(nwg), dim3(256), 0, st, list, n, nbv, ch, binh, binst, out, vs);
         HIP_CHECK(hipGetLastError());
         c.qhead = head;
         c.qseg = seg;
