@@ -137,102 +137,79 @@ __device__ __forceinline__ uint32_t byte16(const uint4& v, int k)
     return (w >> (8 * (k & 3))) & 0xffu;
 }
 
-struct RunSum {
-    uint32_t len, trail;
-    int first, last;
-    bool uni;
-};
-__device__ __forceinline__ RunSum rs_combine(const RunSum& A, const RunSum& B)
+// Runs inside a tile are located by their change positions: byte y > 0 of a
+// tile starts a new run iff it differs from byte y - 1.  A lane holds one
+// 16-byte strip; chg_mask marks its changed bytes (the byte before the strip
+// comes from the previous strip's last byte; the tile's first byte is never a
+// change) and the last change at or before a byte, a prefix maximum, gives
+// every run length -- one integer max-scan instead of a scan of run summaries.
+__device__ __forceinline__ uint32_t nonzero_bytes(uint32_t x)   // 0x80 in each nonzero byte (exact)
 {
-    if (A.len == 0) return B;
-    if (B.len == 0) return A;
-    RunSum R;
-    R.first = A.first;
-    R.last = B.last;
-    R.len = A.len + B.len;
-    R.uni = A.uni && B.uni && A.last == B.first;
-    R.trail = (B.uni && B.first == A.last) ? B.len + A.trail : B.trail;
-    return R;
+    return (((x & 0x7f7f7f7fu) + 0x7f7f7f7fu) | x) & 0x80808080u;
 }
 
-__device__ __forceinline__ RunSum strip_summary(const uint4& v, int cnt)
+// per-word masks of changed bytes among the strip's first cnt bytes
+__device__ __forceinline__ void chg_mask(const uint4& v, uint32_t pb, int cnt, uint32_t (&m)[4])
 {
-    RunSum r;
-    r.len = 0; r.trail = 0; r.first = -1; r.last = -1; r.uni = true;
-    if (cnt <= 0) return r;
-    r.len = cnt;
-    r.first = (int)byte16(v, 0);
-    int last = r.first;
-    uint32_t tr = 1;
+    const uint32_t w[4] = {v.x, v.y, v.z, v.w};
+    uint32_t carry = pb;
 #pragma unroll
-    for (int k = 1; k < 16; ++k) {
-        if (k < cnt) {
-            const int c = (int)byte16(v, k);
-            if (c == last) ++tr; else { tr = 1; r.uni = false; }
-            last = c;
-        }
+    for (int i = 0; i < 4; ++i) {
+        const uint32_t sh = (w[i] << 8) | carry;          // byte k of sh = byte k - 1 of the strip
+        carry = w[i] >> 24;
+        const int lim = cnt - 4 * i;                      // valid bytes of this word
+        const uint32_t keep = lim >= 4 ? 0x80808080u : (lim <= 0 ? 0u : (0x80808080u >> (8 * (4 - lim))));
+        m[i] = nonzero_bytes(w[i] ^ sh) & keep;
     }
-    r.last = last;
-    r.trail = tr;
-    return r;
 }
 
-__device__ __forceinline__ RunSum rs_shfl_up(const RunSum& v, int d)
+// index (0..15) of the strip's last changed byte, or -1
+__device__ __forceinline__ int last_change(const uint32_t (&m)[4])
 {
-    RunSum r;
-    r.len = __shfl_up(v.len, d, 64);
-    r.trail = __shfl_up(v.trail, d, 64);
-    r.first = __shfl_up(v.first, d, 64);
-    r.last = __shfl_up(v.last, d, 64);
-    r.uni = __shfl_up((int)v.uni, d, 64) != 0;
-    return r;
+    return m[3] ? 12 + ((31 - __clz((int)m[3])) >> 3)
+         : m[2] ? 8 + ((31 - __clz((int)m[2])) >> 3)
+         : m[1] ? 4 + ((31 - __clz((int)m[1])) >> 3)
+         : m[0] ? ((31 - __clz((int)m[0])) >> 3) : -1;
 }
 
-// inclusive scan of strip summaries over a 256-thread workgroup; returns this
-// thread's exclusive prefix combined after `init`, and the tile total
-__device__ __forceinline__ RunSum rs_block_scan(const RunSum& mine, const RunSum& init, RunSum* wsh, RunSum* total)
+// the strip of this lane and the byte before it (the strip's own first byte
+// at the tile start, so that position 0 is never a change)
+__device__ __forceinline__ void load_strip(const uint8_t* text, const TileDesc& d, int off, int cnt, uint4& v,
+                                           uint32_t& pb)
 {
-    const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
-    RunSum inc = mine;
-#pragma unroll
-    for (int d = 1; d < 64; d <<= 1) {
-        const RunSum o = rs_shfl_up(inc, d);
-        if (lane >= d) inc = rs_combine(o, inc);
-    }
-    if (lane == 63) wsh[wid] = inc;
-    __syncthreads();
-    RunSum pre = init;
-    for (int w = 0; w < wid; ++w) pre = rs_combine(pre, wsh[w]);
-    RunSum ex = rs_shfl_up(inc, 1);
-    if (lane == 0) { ex.len = 0; ex.trail = 0; ex.first = -1; ex.last = -1; ex.uni = true; }
-    if (total) {
-        RunSum t = init;
-        for (int w = 0; w < 4; ++w) t = rs_combine(t, wsh[w]);
-        *total = t;
-    }
-    return rs_combine(pre, ex);
+    v = cnt > 0 ? load16u(text + d.beg + off, text + d.beg + d.len) : make_uint4(0, 0, 0, 0);
+    pb = off > 0 && cnt > 0 ? (uint32_t)text[d.beg + off - 1] : (v.x & 0xffu);
 }
 
 __global__ void __launch_bounds__(256) k_rle_sum(const uint8_t* __restrict__ text, const TileDesc* __restrict__ tiles,
                                                   TileSum* __restrict__ sums)
 {
-    __shared__ RunSum wsh[4];
-    TileDesc d = tiles[blockIdx.x];
-    int off = threadIdx.x * 16;
+    __shared__ int wsh[4];
+    const TileDesc d = tiles[blockIdx.x];
+    const int off = threadIdx.x * 16;
     int cnt = (int)d.len - off;
     cnt = cnt < 0 ? 0 : (cnt > 16 ? 16 : cnt);
-    const uint4 v = cnt > 0 ? load16u(text + d.beg + off, text + d.beg + d.len) : make_uint4(0, 0, 0, 0);
-    RunSum none;
-    none.len = 0; none.trail = 0; none.first = -1; none.last = -1; none.uni = true;
-    RunSum acc;
-    (void)rs_block_scan(strip_summary(v, cnt), none, wsh, &acc);
+    uint4 v;
+    uint32_t pb;
+    load_strip(text, d, off, cnt, v, pb);
+    uint32_t m[4];
+    chg_mask(v, pb, cnt, m);
+    const int lc = last_change(m);
+    // tile's last change: max over the workgroup (+1 so "none" is 0)
+    uint32_t x = lc >= 0 ? (uint32_t)(off + lc + 1) : 0u;
+    x = (uint32_t)__builtin_amdgcn_readlane((int)wave_incl_scan_max<uint32_t>(x), 63);
+    if ((threadIdx.x & 63) == 0) wsh[threadIdx.x >> 6] = (int)x;
+    __syncthreads();
     if (threadIdx.x == 0) {
+        uint32_t p = 0;
+        for (int w = 0; w < 4; ++w) p = (uint32_t)wsh[w] > p ? (uint32_t)wsh[w] : p;
         TileSum o;
-        o.first = (uint8_t)acc.first;
-        o.last = (uint8_t)acc.last;
-        o.uni = acc.uni ? 1 : 0;
-        o.len = acc.len;
-        o.trail = acc.trail;
+        o.len = d.len;
+        o.first = d.len ? text[d.beg] : (uint8_t)0xff;
+        o.last = d.len ? text[d.beg + d.len - 1] : (uint8_t)0xff;
+        o.uni = p == 0 ? 1 : 0;
+        o.trail = p == 0 ? d.len : d.len - (p - 1);
+        o.pad = 0;
         sums[blockIdx.x] = o;
     }
 }
@@ -304,29 +281,40 @@ __global__ void __launch_bounds__(256) k_rle_pos(const uint8_t* __restrict__ tex
                                                   const uint32_t* __restrict__ carry, uint8_t* __restrict__ tpos,
                                                   uint32_t* __restrict__ tile_w)
 {
-    __shared__ RunSum rsh[4];
+    __shared__ uint32_t msh[4];
     __shared__ uint32_t wsh[5];
-    TileDesc d = tiles[blockIdx.x];
-    int off = threadIdx.x * 16;
+    const TileDesc d = tiles[blockIdx.x];
+    const int off = threadIdx.x * 16;
+    const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
     int cnt = (int)d.len - off;
     cnt = cnt < 0 ? 0 : (cnt > 16 ? 16 : cnt);
-    const uint4 v = cnt > 0 ? load16u(text + d.beg + off, text + d.beg + d.len) : make_uint4(0, 0, 0, 0);
-    const RunSum S = strip_summary(v, cnt);
-    RunSum init;
+    uint4 v;
+    uint32_t pb;
+    load_strip(text, d, off, cnt, v, pb);
+    uint32_t m[4];
+    chg_mask(v, pb, cnt, m);
+    const int lc = last_change(m);
+    // last change before this strip: exclusive prefix max over the workgroup
+    // (positions + 1, 0 = none)
+    const uint32_t x = lc >= 0 ? (uint32_t)(off + lc + 1) : 0u;
+    const uint32_t incl = wave_incl_scan_max<uint32_t>(x);
+    uint32_t ex = (uint32_t)__shfl_up((int)incl, 1, 64);
+    if (lane == 0) ex = 0;
+    if (lane == 63) msh[wid] = incl;
+    __syncthreads();
+    for (int w = 0; w < wid; ++w) ex = msh[w] > ex ? msh[w] : ex;
+    // run position of each byte: since the last change, or from the run
+    // carried into the tile when there is none
     const uint32_t c = carry[blockIdx.x];
-    init.len = c; init.trail = c; init.uni = true;
-    init.first = init.last = (d.len ? (int)text[d.beg] : -1);
-    const RunSum P = rs_block_scan(S, init, rsh, (RunSum*)nullptr);
-    uint32_t run = (P.len > 0 && S.len > 0 && P.last == S.first) ? P.trail : 0;
     uint32_t w = 0;
-    int prev = -1;
     uint32_t tw[4] = {0, 0, 0, 0};
+    uint32_t last = ex;                                   // last change + 1 (0 = none)
 #pragma unroll
     for (int k = 0; k < 16; ++k) {
         if (k < cnt) {
-            const int ch = (int)byte16(v, k);
-            if (k > 0) run = (ch == prev) ? run + 1 : 0;
-            prev = ch;
+            if ((m[k >> 2] >> (8 * (k & 3) + 7)) & 1u) last = (uint32_t)(off + k + 1);
+            const uint32_t y = (uint32_t)(off + k);
+            const uint32_t run = last ? y + 1 - last : c + y;
             const uint32_t t = run % 255u;
             tw[k >> 2] |= t << (8 * (k & 3));
             w += rle_w(t);

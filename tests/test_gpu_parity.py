@@ -104,6 +104,23 @@ def test_bz2_fuzz_vs_oracle(ctx):
         assert ctx.bz2_compress(data, bs) == oracle_lib.bz2(data, bs), (i, kind, n, bs)
 
 
+def test_bz2_runs_across_tiles_vs_oracle(ctx):
+    """RLE1 run positions carried across 4 KiB tiles (k_rle_sum/k_rle_carry/
+    k_rle_pos): runs longer than a tile, runs ending exactly at a tile edge,
+    runs of 255k +- 1 bytes straddling edges, single-byte alternations."""
+    r = random.Random(4321)
+    cases = [b"a" * 4096, b"a" * 4097, b"a" * 12289 + b"b", b"x" * 4095 + b"yy" + b"x" * 4095,
+             b"ab" * 5000, b"a" * (255 * 17 + 1) + b"b" * (255 * 3 - 1) + b"a" * 4]
+    for _ in range(12):
+        parts = []
+        for _ in range(r.randint(1, 12)):
+            parts.append(bytes([97 + r.randrange(3)]) * r.choice([1, 4, 254, 255, 256, 509, 510, 511, 4093, 4096, 9000]))
+        cases.append(b"".join(parts))
+    for data in cases:
+        for bs in (1, 9):
+            assert ctx.bz2_compress(data, bs) == oracle_lib.bz2(data, bs), (len(data), bs)
+
+
 def test_bz2_many_streams_one_launch(ctx):
     import torch
     r = random.Random(99)
