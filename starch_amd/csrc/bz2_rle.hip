@@ -422,14 +422,36 @@ __global__ void __launch_bounds__(64) k_cut(const StreamIn* __restrict__ streams
                 if (ball) {
                     const int L = __ffsll((unsigned long long)ball) - 1;
                     uint64_t x = a < y0 ? y0 : a, Wx = W0 + incl - ssum;
-                    if (lane == L) {               // the crossing byte, from the registers
+                    {   // the crossing byte, from the registers: per-word weights
+                        // by SWAR (rle_w = [t <= 3] + [t == 3]), then a walk over
+                        // 16 words and 4 bytes instead of 64 bytes
+                        const int kq = y0 > a ? (y0 - a < 64 ? (int)(y0 - a) : 64) : 0;
+                        const int kt = tend > a ? (tend - a < 64 ? (int)(tend - a) : 64) : 0;
+                        auto upto = [](int n) { return n >= 4 ? 0x80808080u : (n <= 0 ? 0u : (0x80808080u >> (8 * (4 - n)))); };
+                        uint32_t need = (uint32_t)(target - Wx);   // > 0 in lane L
+                        uint32_t le = 0, eq = 0;
+                        int wsel = -1;
 #pragma unroll
-                        for (int k = 0; k < 64; ++k) {
-                            const uint64_t y = a + (uint64_t)k;
-                            if (Wx < target) {
-                                if (y >= y0 && y < tend) Wx += rle_w((tw[k >> 2] >> (8 * (k & 3))) & 0xffu);
-                                x = y + 1;
+                        for (int i = 0; i < 16; ++i) {
+                            const uint32_t vm = upto(kt - 4 * i) & ~upto(kq - 4 * i);
+                            const uint32_t l3 = ~nonzero_bytes(tw[i] & 0xFCFCFCFCu) & vm;
+                            const uint32_t e3 = ~nonzero_bytes(tw[i] ^ 0x03030303u) & vm;
+                            const uint32_t wi = (uint32_t)(__popc(l3) + __popc(e3));
+                            if (wsel < 0) {
+                                if (wi < need) need -= wi;
+                                else { wsel = i; le = l3; eq = e3; }
                             }
+                        }
+                        if (wsel >= 0) {
+                            int jsel = 3;
+#pragma unroll
+                            for (int j = 3; j >= 0; --j) {   // first byte j whose prefix weight reaches need
+                                const uint32_t c = (uint32_t)(__popc(le & upto(j + 1)) + __popc(eq & upto(j + 1)));
+                                if (c >= need) jsel = j;
+                            }
+                            const uint32_t cj = (uint32_t)(__popc(le & upto(jsel + 1)) + __popc(eq & upto(jsel + 1)));
+                            x = a + (uint64_t)(4 * wsel + jsel) + 1;
+                            Wx = target - need + cj;
                         }
                     }
                     q = __shfl(x, L, 64);
@@ -439,17 +461,25 @@ __global__ void __launch_bounds__(64) k_cut(const StreamIn* __restrict__ streams
                 ++lo;   // cannot happen when the tile search is exact; stay safe
                 if (lo >= t1) { q = end; Wq = wend; break; }
             }
-            uint64_t p = end;
+            // the first chunk start p >= q (within 255 bytes) and the weight of
+            // [q, p): the 256 bytes after q in one round of loads
+            uint32_t tv[4];
+#pragma unroll
             for (int r = 0; r < 4; ++r) {
                 const uint64_t pos = q + (uint64_t)r * 64 + lane;
-                const uint64_t hit = __ballot(pos < end && tpos[pos] == 0);
+                tv[r] = pos < end ? tpos[pos] : 1u;
+            }
+            uint64_t p = end;
+#pragma unroll
+            for (int r = 0; r < 4; ++r) {
+                const uint64_t hit = __ballot(tv[r] == 0);
                 if (hit) { p = q + (uint64_t)r * 64 + (__ffsll((unsigned long long)hit) - 1); break; }
-                if (q + (uint64_t)(r + 1) * 64 >= end) break;
             }
             uint32_t part = 0;
+#pragma unroll
             for (int r = 0; r < 4; ++r) {
                 const uint64_t pos = q + (uint64_t)r * 64 + lane;
-                if (pos < p) part += rle_w(tpos[pos]);
+                if (pos < p) part += rle_w(tv[r]);
             }
             const uint64_t Wp = Wq + wave_reduce_add(part);
             if (p < end && !(frj && p == end - 1)) { block_end = p; wblock_end = Wp; }
