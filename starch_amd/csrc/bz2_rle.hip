@@ -561,7 +561,6 @@ __global__ void __launch_bounds__(256) k_rle_emit(const uint8_t* __restrict__ te
                                                    BlockDesc* __restrict__ blocks, uint8_t* __restrict__ blk,
                                                    uint64_t stride)
 {
-    __shared__ uint32_t used[2][8];
     __shared__ uint32_t wsh[5];
     __shared__ uint8_t ob[kTB + kTB / 4 + 16];      // the tile's RLE1 output (<= 5/4 of its bytes)
     // inUse bits per lane ([slot][word][lane]: no two lanes share a word, so no
@@ -570,7 +569,6 @@ __global__ void __launch_bounds__(256) k_rle_emit(const uint8_t* __restrict__ te
     TileDesc d = tiles[blockIdx.x];
     const uint32_t s = d.stream;
     const uint64_t send = streams[s].text_off + streams[s].text_len;
-    if (threadIdx.x < 16) used[threadIdx.x >> 3][threadIdx.x & 7] = 0;
 #pragma unroll
     for (int q = 0; q < 16; ++q) ul[q >> 3][q & 7][threadIdx.x] = 0;
     const uint32_t bsel = tile_block[blockIdx.x];   // block holding the tile's first byte
@@ -621,17 +619,20 @@ __global__ void __launch_bounds__(256) k_rle_emit(const uint8_t* __restrict__ te
     const uint32_t split = wnext > Wt ? (wnext - Wt < tot ? (uint32_t)(wnext - Wt) : tot) : 0u;
     copy_out(blk + (uint64_t)b0 * stride + (Wt - wb0), ob, split);
     if (split < tot) copy_out(blk + (uint64_t)(b0 + 1) * stride, ob + split, tot - split);
+    {   // OR of the 256 lanes' words: 16 threads per (slot, word), each ORs 16
+        // lanes' words (four 16-B LDS reads), then DPP row shifts OR the 16
+        // threads into the row's last lane, which publishes the word
+        const int pr = threadIdx.x >> 4, r = threadIdx.x & 15;
+        const uint4* row = reinterpret_cast<const uint4*>(&ul[pr >> 3][pr & 7][r * 16]);
+        uint32_t v = 0;
 #pragma unroll
-    for (int q = 0; q < 16; ++q) {                  // OR over the wave, one LDS atomic per wave and word
-        const uint32_t v = (uint32_t)__builtin_amdgcn_readlane(
-            (int)wave_incl_scan_or(ul[q >> 3][q & 7][threadIdx.x]), 63);
-        if ((threadIdx.x & 63) == 0 && v) atomicOr(&used[q >> 3][q & 7], v);
-    }
-    __syncthreads();
-    if (threadIdx.x < 16) {
-        int slot = threadIdx.x >> 3, j = threadIdx.x & 7;
-        uint32_t bb = b0 + slot;
-        if (used[slot][j] && bb < bl) atomicOr(&blocks[bb].in_use[j], used[slot][j]);
+        for (int i = 0; i < 4; ++i) { const uint4 x = row[i]; v |= x.x | x.y | x.z | x.w; }
+        v |= dpp_up(v, 1);
+        v |= dpp_up(v, 2);
+        v |= dpp_up(v, 4);
+        v |= dpp_up(v, 8);
+        const uint32_t bb = b0 + (uint32_t)(pr >> 3);
+        if (r == 15 && v && bb < bl) atomicOr(&blocks[bb].in_use[pr & 7], v);
     }
 }
 
