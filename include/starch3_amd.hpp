@@ -414,6 +414,12 @@ public:
     int compress_in_stream_multi(void)
     {
         const starch_options o = options();
+        if (o.reference_compat) {      // the reference's stdout is the magic alone: read, write nothing
+            std::vector<unsigned char> sink(1u << 24);
+            while (std::fread(&sink[0], 1, sink.size(), _in_stream) > 0) {}
+            std::fflush(_out_stream);
+            return STARCH_OK;
+        }
         const int nd = (int)_ctx.size();
         std::vector<starch_segment> all;
         std::vector<std::string> all_names;

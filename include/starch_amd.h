@@ -109,9 +109,16 @@ const char* starch_last_error(starch_ctx* ctx);   /* detail text of the last fai
 
 int starch_create(int device, starch_ctx** out);
 void starch_destroy(starch_ctx* ctx);
-/* Use an external hipStream_t (e.g. torch.cuda.current_stream().cuda_stream);
- * NULL restores the context's own stream. */
+/* Run the context's work on an external hipStream_t, e.g.
+ * torch.cuda.current_stream().cuda_stream.  NULL (0) is the HIP null stream
+ * itself: work the caller queued there (an H2D copy, a generator kernel) is
+ * ordered before the encode with no host synchronisation.  The context still
+ * uses private streams inside a call; they wait for the selected stream on
+ * entry and the selected stream waits for them before the call returns. */
 int starch_set_stream(starch_ctx* ctx, void* hip_stream);
+/* Back to the context's own non-blocking stream (the default after
+ * starch_create; not ordered with the null stream). */
+int starch_use_own_stream(starch_ctx* ctx);
 void starch_options_init(starch_options* opt);
 
 /* Whole pipeline.  Input BED bytes already in HBM (d_bed, n bytes).  The

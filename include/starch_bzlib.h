@@ -12,13 +12,18 @@
  * Differences from the patched library (documented in INTEGRATION.md):
  *  - a NULL block_close_functor is allowed (the patched library calls it
  *    unconditionally at BZ_STREAM_END, bz:bzlib.c:470, and crashes);
- *  - the compressed bytes are produced on the GPU, one flush-delimited piece
- *    at a time: BZ_FLUSH encodes the input since the previous FLUSH and makes
+ *  - the compressed bytes are produced on the GPU.  The state machine is the
+ *    library's step for step (bz:bzlib.c:369-471): BZ_RUN buffers input with
+ *    libbz2's RLE1 bookkeeping and emits a block as soon as nblockMAX bytes
+ *    are held (the pending run carried into the next block), BZ_FLUSH makes
  *    every whole byte so far readable (BZ_FLUSH_OK while it does not fit
- *    avail_out, then BZ_RUN_OK, bz:bzlib.c:437-459), exactly as the library
- *    does; BZ_RUN only consumes input (the library also emits a block once
- *    900 k are buffered).  The bytes, and total_out after every FLUSH and
- *    FINISH, are identical to the patched library for the same call sequence.
+ *    avail_out, then BZ_RUN_OK), BZ_FINISH ends the stream.  The bytes, the
+ *    return codes and total_in / total_out after EVERY call (BZ_RUN included)
+ *    are identical to the patched library for the same call sequence;
+ *  - a GPU failure inside BZ2_bzCompress returns BZ_CONFIG_ERROR and ENDS the
+ *    stream: the input of that call may already be consumed (next_in /
+ *    avail_in / total_in advanced), every later BZ2_bzCompress returns
+ *    BZ_SEQUENCE_ERROR, and BZ2_bzCompressEnd is the only valid call left.
  */
 #ifndef STARCH_BZLIB_H_
 #define STARCH_BZLIB_H_

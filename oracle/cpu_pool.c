@@ -138,10 +138,18 @@ int cpu_pool_run(const uint8_t* data, const uint64_t* offs, const uint64_t* lens
     qsort(P.order, (size_t)n, sizeof(int), by_len_desc);
     if (threads < 1) threads = 1;
     pthread_t* th = (pthread_t*)malloc((size_t)threads * sizeof(pthread_t));
+    if (!th) {
+        free(P.order);
+        pthread_mutex_destroy(&P.mu);
+        return -1;
+    }
     double t0 = now_s();
     int started = 0;
-    for (int k = 0; k < threads; ++k)
-        if (pthread_create(&th[k], NULL, worker, &P) == 0) ++started;
+    for (int k = 0; k < threads; ++k) {   /* only created handles are kept (and joined) */
+        pthread_t t;
+        if (pthread_create(&t, NULL, worker, &P) != 0) break;
+        th[started++] = t;
+    }
     for (int k = 0; k < started; ++k) pthread_join(th[k], NULL);
     *seconds = now_s() - t0;
     free(th);

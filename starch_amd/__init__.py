@@ -117,6 +117,7 @@ def load():
         "starch_create": ([ctypes.c_int, ctypes.POINTER(vp)], ctypes.c_int),
         "starch_destroy": ([vp], None),
         "starch_set_stream": ([vp, vp], ctypes.c_int),
+        "starch_use_own_stream": ([vp], ctypes.c_int),
         "starch_options_init": ([ctypes.POINTER(Options)], None),
         "starch_encode_device": ([vp, vp, u64, ctypes.POINTER(Options)], ctypes.c_int),
         "starch_encode_host": ([vp, ctypes.c_char_p, u64, ctypes.POINTER(Options)], ctypes.c_int),
@@ -249,7 +250,12 @@ class Starch:
         return self._magic
 
     def set_stream(self, hip_stream_ptr):
+        """Run on an external HIP stream; 0 is the HIP null stream (torch's default stream)."""
         _check(self._L.starch_set_stream(self._h, ctypes.c_void_p(hip_stream_ptr)), self._h)
+
+    def use_own_stream(self):
+        """Back to the context's own non-blocking stream (the default)."""
+        _check(self._L.starch_use_own_stream(self._h), self._h)
 
     # -- the hot path ----------------------------------------------------------
     def _opts(self, emit_index=True, reference_compat=False):

@@ -370,10 +370,18 @@ void compress_block(GpuStreamState* g, bool flush, bool last)
 
 // code the blocks of input that is certain to be consumed in one GPU plan
 // (see the header comment); at most kAhead bytes of new input at a time
-constexpr uint64_t kAhead = 64ull << 20;
+// (STARCH_BZ_AHEAD overrides it, for tests: a small limit exercises the open,
+// non-final plans that larger FLUSH / FINISH / BZ_RUN commitments take)
+uint64_t ahead_limit()
+{
+    const char* e = getenv("STARCH_BZ_AHEAD");
+    const long long v = e ? atoll(e) : 0;
+    return v > 0 ? (uint64_t)v : 64ull << 20;
+}
 void code_ahead(GpuStreamState* g)
 {
     if (!g->ahead.empty()) return;
+    const uint64_t kAhead = ahead_limit();
     bz_stream* s = g->strm;
     uint64_t avail = s->avail_in;
     bool closed = false;

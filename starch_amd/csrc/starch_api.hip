@@ -1446,7 +1446,14 @@ void starch_destroy(starch_ctx* c)
 int starch_set_stream(starch_ctx* c, void* s)
 {
     if (!c) return STARCH_ERR_ARG;
-    c->st = s ? static_cast<hipStream_t>(s) : c->own;
+    c->st = static_cast<hipStream_t>(s);   // NULL = the HIP null stream (include/starch_amd.h)
+    return STARCH_OK;
+}
+
+int starch_use_own_stream(starch_ctx* c)
+{
+    if (!c) return STARCH_ERR_ARG;
+    c->st = c->own;
     return STARCH_OK;
 }
 

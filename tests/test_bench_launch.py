@@ -51,6 +51,25 @@ def test_launcher_refuses_missing_gpus():
     assert b"refusing" in r.stderr
 
 
+def test_kfd_gpu_count_from_sysfs(tmp_path):
+    """The launcher counts GPUs from the KFD topology (no HIP call): nodes with
+    SIMDs whose render node is accessible; CPU nodes (simd_count 0) and GPUs
+    whose render node this process cannot open are not counted."""
+    sys.path.insert(0, ROOT)
+    import bench
+    nodes, dri = tmp_path / "nodes", tmp_path / "dri"
+    dri.mkdir()
+    for i, (simd, minor, present) in enumerate([(0, 0, False), (1024, 128, True), (1024, 129, True),
+                                                 (1024, 130, False)]):
+        d = nodes / str(i)
+        d.mkdir(parents=True)
+        (d / "properties").write_text("cpu_cores_count 0\nsimd_count %d\ndrm_render_minor %d\n" % (simd, minor))
+        if present:
+            (dri / ("renderD%d" % minor)).write_text("")
+    assert bench._kfd_gpus(str(nodes), str(dri)) == 2
+    assert bench._kfd_gpus(str(tmp_path / "absent"), str(dri)) is None
+
+
 def test_world_size_mismatch_fails():
     env = _env()
     env.update(WORLD_SIZE="2", RANK="0", LOCAL_RANK="0")
@@ -85,3 +104,19 @@ def test_launcher_one_gpu_bench():
     res = json.loads([ln for ln in r.stdout.decode().splitlines() if ln.startswith("{")][-1])
     assert res["n_gpus"] == 1
     assert res["dist"]["ms_encode_max"] > 0 and res["dist"]["ms_gather_max"] >= 0
+
+
+@pytest.mark.gpu
+def test_launcher_counts_gpus_without_hip():
+    """bench.visible_gpus() in a fresh process equals torch's device count
+    (taken in another process) and leaves no HIP runtime mapped: the launcher
+    must not initialise the GPU before it starts its rank processes."""
+    code = ("import sys; sys.path.insert(0, %r); import bench; n = bench.visible_gpus(); "
+            "maps = open('/proc/self/maps').read(); print(n, int('libamdhip64' in maps))" % ROOT)
+    r = subprocess.run([sys.executable, "-c", code], env=_env(), capture_output=True, timeout=120)
+    assert r.returncode == 0, r.stderr.decode()[-2000:]
+    n, hip = map(int, r.stdout.split())
+    r2 = subprocess.run([sys.executable, "-c", "import torch; print(torch.cuda.device_count())"], env=_env(),
+                        capture_output=True, timeout=300)
+    assert n == int(r2.stdout.split()[-1]) and n >= 1
+    assert hip == 0

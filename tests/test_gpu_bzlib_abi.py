@@ -216,6 +216,20 @@ def test_default_allocators_installed():
 @pytest.mark.skipif(oracle_lib.ref() is None, reason="oracle/_ref not built")
 @pytest.mark.parametrize("seed", range(6))
 def test_every_call_matches_reference_lib(seed):
+    _every_call(seed, (0, 4093, 65536))
+
+
+@pytest.mark.skipif(oracle_lib.ref() is None, reason="oracle/_ref not built")
+@pytest.mark.parametrize("seed", range(6))
+def test_every_call_matches_reference_lib_small_ahead(seed, monkeypatch):
+    """The same with the coded-ahead limit at 300 KB (STARCH_BZ_AHEAD): FLUSH /
+    FINISH commitments and BZ_RUN input larger than it are coded in open
+    plans whose last block is dropped and re-planned from the pending run."""
+    monkeypatch.setenv("STARCH_BZ_AHEAD", "300000")
+    _every_call(seed, (0, 65536))
+
+
+def _every_call(seed, chunks):
     """libbz2's state machine call for call (bz:bzlib.c:369-471): the reference
     library and the GPU ABI driven by the same Python loop give the same return
     code, total_in and total_out after EVERY BZ2_bzCompress call -- BZ_RUN
@@ -239,7 +253,7 @@ def test_every_call_matches_reference_lib(seed):
         ops.append((act, k))
         left -= k
     ops.append((BZ_FINISH, left))
-    for chunk in (0, 4093, 65536):
+    for chunk in chunks:
         want_calls, got_calls = [], []
         want, wrcs = run_script(data, ops, bs=bs, out_chunk=chunk, lib=_ref_lib(), calls=want_calls)
         got, rcs = run_script(data, ops, bs=bs, out_chunk=chunk, calls=got_calls)

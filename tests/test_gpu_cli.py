@@ -37,8 +37,28 @@ def test_cli_stdout_is_the_archive_cfg1(tmp_path):
     assert streams[0] == oracle_lib.bz2(segs[0][2], 9)
 
 
+def test_cli_file_whose_size_reads_zero():
+    """A regular file whose st_size is 0 but which has content (/proc) is read
+    to EOF, not taken as empty: same archive as its bytes piped in."""
+    path = "/proc/version"
+    data = open(path, "rb").read()
+    assert os.stat(path).st_size == 0 and data
+    got = _run("starch3", [path], b"")
+    assert got == _run("starch3", [], data)
+    assert len(got) > 4 + 32
+
+
 def test_cli_reference_compat_is_magic_only():
     assert _run("starch3", ["--reference-compat"], corpus.cfg1_bed(500)) == b"\xca\x5c\xad\x1a"
+
+
+@pytest.mark.parametrize("args", [[], ["--vdev", "2"], ["--vdev", "3"]])
+def test_hpp_reference_compat_is_magic_only(args):
+    """compress_in_stream under --reference-compat writes the magic alone on
+    one device and on the multi-device batch path alike (the reference's
+    stdout, hpp:765-769)."""
+    data = corpus.multi_chrom_bed(5, 700, seed=12, kind="bed6")
+    assert _run("starch3_hpp_example", ["--reference-compat"] + args, data) == b"\xca\x5c\xad\x1a"
 
 
 def test_cli_note_and_level():

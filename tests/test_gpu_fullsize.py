@@ -80,8 +80,8 @@ def test_cfg5_all_24_fullsize():
     cap = max(starch_amd.gen_perpos_device(c) for c in range(24))
     dev = torch.empty(cap + 64, dtype=torch.uint8, device="cuda")
     c = starch_amd.Starch(0)
-    stream = torch.cuda.Stream()          # a real stream: set_stream(0) selects the context's own stream
-    c.set_stream(stream.cuda_stream)      # generator and encoder ordered on it
+    stream = torch.cuda.Stream()          # a non-default stream: generator and encoder ordered on it
+    c.set_stream(stream.cuda_stream)
     done = 0
     for ci, name in enumerate(starch_amd.HG38):
         n = starch_amd.gen_perpos_device(ci, dev.data_ptr(), cap + 64, stream=stream.cuda_stream)
@@ -100,4 +100,41 @@ def test_cfg5_all_24_fullsize():
         assert st["n_blocks"] - st["dedup_blocks"] <= 4, (name, st["n_blocks"], st["dedup_blocks"])
         done += 1
     assert done == 24
+    c.close()
+
+
+def test_null_stream_orders_input_before_encode():
+    """set_stream(0) is the HIP null stream (include/starch_amd.h): input written
+    there -- the GPU generator, then torch's default stream (also the null
+    stream) overwriting a prefix -- is ordered before the encode with no host
+    synchronisation in between.  This is the race of a generator on the null
+    stream and an encoder on the context's own stream ("split chr11").  chrY's
+    1.29 GB per-position input must give the CPU path's stream."""
+    import torch
+    import starch_amd
+    g = json.load(open(os.path.join(GOLDEN, "fullsize_cfg5.json")))
+    w = {s["chromosome"]: s for s in g["streams"]}["chrY"]
+    ci = starch_amd.HG38.index("chrY")
+    n = starch_amd.gen_perpos_device(ci)
+    dev = torch.empty(n + 64, dtype=torch.uint8, device="cuda")
+    c = starch_amd.Starch(0)
+    c.set_stream(0)
+    for rep in range(2):
+        torch.cuda.synchronize()
+        dev.fill_(0x41)                    # garbage the encoder must never see
+        got = starch_amd.gen_perpos_device(ci, dev.data_ptr(), n + 64, stream=0)
+        assert got == n == w["input_bytes"]
+        if rep == 1:
+            # torch's default stream is the null stream: rewrite the first 64 MiB
+            # there (same bytes) right before the encode
+            assert torch.cuda.current_stream().cuda_stream == 0
+            head = dev[:64 << 20].clone()
+            dev[:64 << 20].fill_(0x42)
+            dev[:64 << 20].copy_(head)
+        c.compress_device(dev.data_ptr(), n)
+        idx, streams = starch_amd.parse_archive(c.archive())
+        assert [m["chromosome"] for m in idx["streams"]] == ["chrY"]
+        assert len(streams[0]) == w["stream_bytes"]
+        assert hashlib.sha256(streams[0]).hexdigest() == w["sha256"]
+    c.use_own_stream()
     c.close()

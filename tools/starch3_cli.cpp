@@ -305,15 +305,18 @@ int main(int argc, char** argv)
         };
         const int fd = fileno(in);
         // a regular file (a path, or stdin redirected from one) is read by
-        // several threads at once with pread(2): one read(2) stream from the
-        // page cache runs at a few GB/s, below what the encoder takes
+        // several threads at once with pread(2) up to the size it had at the
+        // start: one read(2) stream from the page cache runs at a few GB/s,
+        // below what the encoder takes.  Past that size (a growing file, or
+        // one whose st_size says 0, as in /proc) read(2) goes on to EOF.
         struct stat fs;
-        const bool regular = fstat(fd, &fs) == 0 && S_ISREG(fs.st_mode);
+        const bool regular = fstat(fd, &fs) == 0 && S_ISREG(fs.st_mode) && fs.st_size > 0;
         const off_t start = regular ? lseek(fd, 0, SEEK_CUR) : (off_t)-1;
-        const bool par = regular && start >= 0;
+        bool par = regular && start >= 0;
         uint64_t off = par ? (uint64_t)start : 0;
         const uint64_t fsize = par ? (uint64_t)fs.st_size : 0;
         const int nthr = std::max(1, std::min(16, (int)std::thread::hardware_concurrency()));
+        bool read_err = false;
         rc = starch_stream_begin(ctx, &opt, batch_mb << 20);
         drain();
         g_setup_s = std::chrono::duration<double>(std::chrono::steady_clock::now() - t0).count();
@@ -326,9 +329,14 @@ int main(int argc, char** argv)
             uint64_t got = 0;
             if (par) {
                 want = std::min<uint64_t>(want, fsize > off ? fsize - off : 0);
-                if (want == 0) break;
+                if (want == 0) {          // the size taken at the start is read: on with read(2)
+                    par = false;
+                    if (lseek(fd, (off_t)off, SEEK_SET) < 0) { read_err = true; break; }
+                    continue;
+                }
                 const uint64_t sub = (want + nthr - 1) / nthr;
                 std::vector<uint64_t> n_read(nthr, 0);
+                std::vector<int> failed(nthr, 0);
                 std::vector<std::thread> th;
                 for (int t = 0; t < nthr; ++t)
                     th.emplace_back([&, t]() {
@@ -337,26 +345,40 @@ int main(int argc, char** argv)
                         while (q < e) {
                             const ssize_t r = pread(fd, static_cast<char*>(w) + q, e - q, (off_t)(off + q));
                             if (r < 0 && errno == EINTR) continue;
+                            if (r < 0) failed[t] = 1;
                             if (r <= 0) break;
                             q += (uint64_t)r;
                         }
                         n_read[t] = q - b;
                     });
                 for (auto& x : th) x.join();
+                for (int t = 0; t < nthr; ++t) read_err |= failed[t] != 0;
+                if (read_err) break;
                 for (int t = 0; t < nthr; ++t) {   // the bytes read contiguously from the piece's start
                     got += n_read[t];
                     if (n_read[t] < std::min<uint64_t>(want, (uint64_t)(t + 1) * sub) - std::min<uint64_t>(want, (uint64_t)t * sub)) break;
                 }
-                if (got == 0) break;
                 off += got;
+                if (got < want) {         // shorter than its size said: read(2) decides where EOF is
+                    par = false;
+                    if (lseek(fd, (off_t)off, SEEK_SET) < 0) { read_err = true; break; }
+                    if (got == 0) continue;
+                }
             } else {
                 const ssize_t k = read(fd, w, want);
                 if (k < 0 && errno == EINTR) continue;
-                if (k <= 0) break;
+                if (k < 0) { read_err = true; break; }
+                if (k == 0) break;
                 got = (uint64_t)k;
             }
             rc = starch_stream_commit(ctx, got);
             drain();
+        }
+        if (read_err && rc == STARCH_OK) {
+            fprintf(stderr, "Error: reading the input failed (%s)\n", strerror(errno));
+            if (in != stdin) fclose(in);
+            for (auto* c2 : ctxs) starch_destroy(c2);
+            return EIO;
         }
         if (in != stdin) fclose(in);
         if (rc == STARCH_OK) rc = starch_stream_end(ctx);

@@ -19,11 +19,13 @@ int main(int argc, char** argv)
     starch3::Starch starch;
     starch3::self = &starch;
     // --hook: the per-chromosome hand-off; --vdev N: N virtual devices (all on
-    // GPU 0: the multi-device batch path of compress_in_stream)
+    // GPU 0: the multi-device batch path of compress_in_stream);
+    // --reference-compat: stdout is the reference's (the magic bytes only)
     bool hook = false;
     int a = 1;
     for (; a < argc && argv[a][0] == '-' && argv[a][1] == '-'; ++a) {
         if (std::strcmp(argv[a], "--hook") == 0) hook = true;
+        else if (std::strcmp(argv[a], "--reference-compat") == 0) starch.set_reference_compat(true);
         else if (std::strcmp(argv[a], "--vdev") == 0 && a + 1 < argc) starch.set_devices(std::vector<int>(std::atoi(argv[++a]), 0));
     }
     if (a < argc) starch.set_input_fn(argv[a]);
