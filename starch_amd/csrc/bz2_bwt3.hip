@@ -82,7 +82,7 @@ constexpr uint32_t W_MAX = 64, S1_MAX = 128, S_MAX = 256, M0_MAX = 512, M1_MAX =
 #endif
 constexpr uint32_t L_MIN = STARCH_L_MIN;
 constexpr uint32_t GB_MIN = 16384;      // doubling: tie groups above this are gathered by the whole grid
-constexpr uint32_t GB_MAXN = 4096;
+constexpr uint32_t GB_MAXN = 8192;      // (two per block of a 2,048-block batch of near-periodic blocks, and spare)
 constexpr uint32_t HG_MIN_PUSH = 32768;  // (= HG_MIN) L groups above it are partitioned by the whole grid
 constexpr uint32_t RBITS = 20;          // rank bits (n <= 899,985 < 2^20)
 constexpr uint32_t TEXT_ROUNDS = 4;     // max text-extension rounds before doubling
@@ -145,6 +145,12 @@ struct Lists {
     uint32_t* tied;         // per slot: still tied when doubling starts
     uint64_t* hg;           // huge groups of the current partition level (k3_hg_*), HG_MAXN
     uint32_t* hg_info;      // [HG_MAXN][512]: bin start | final flag; bin totals -> scatter cursors
+    uint32_t* hg_pre;       // [HG_MAXN + 1]: chunk prefix of the huge groups (k3_hg_prefix)
+    uint64_t* hg_vary;      // [HG_MAXN]: key bits that differ inside the group (OR of key ^ first key)
+    uint32_t* hg_flag;      // [HG_MAXN]: HG_SKIP_* / HG_THREE (k3_hg_scan)
+    uint32_t* hg_eqlt;      // [HG_MAXN][2]: elements equal to / below the group's first key
+    uint32_t* hg_mc;        // [HG_MAXN][6]: in-place three-way: movers to / holes in each part
+    uint32_t* hg_rank;      // [HG_MAXN]: in-place three-way: the equal part's rank (HG_KEEP: as it is)
     uint64_t* gb;           // doubling: tie groups gathered by the whole grid (k3_gather_big), GB_MAXN
     uint32_t* gb_h;         // ... their key offset h mod n
 };
@@ -1065,11 +1071,55 @@ __global__ void __launch_bounds__(LT) k3_part_l(Ctx c, const uint64_t* __restric
 // left) are written out by k3_hg_final -- after the scatter, so no chunk's
 // source reads race the final SA writes.
 // ---------------------------------------------------------------------------
+// the grid split over ng groups: several workgroups per group when there are
+// fewer groups than workgroups, else one (every workgroup looping over all
+// groups cost thousands of empty iterations per workgroup with 4k groups)
+struct GridSplit {
+    uint32_t per, gstride, q0, slice;
+    bool idle;
+};
+__device__ __forceinline__ GridSplit grid_split(uint32_t ng)
+{
+    GridSplit s;
+    const uint32_t G = gridDim.x;
+    s.per = ng >= G ? 1u : G / (ng ? ng : 1u);
+    s.gstride = G / s.per;
+    s.idle = blockIdx.x >= s.per * s.gstride;
+    s.q0 = blockIdx.x / s.per;
+    s.slice = blockIdx.x % s.per;
+    return s;
+}
+
 constexpr uint32_t HG_MIN = HG_MIN_PUSH;
 constexpr uint32_t HG_CH = 1024;        // elements per chunk: 4 per thread, every chunk in flight at once
-constexpr uint32_t HG_MAXCH = 16384;    // chunks per level (the pick's budget)
-constexpr uint32_t HG_MAXN = 256;
+constexpr uint32_t HG_MAXCH = 1u << 22; // chunks per level (the pick's budget: any batch)
+constexpr uint32_t HG_MAXN = 8192;      // huge groups per level (two per near-periodic block of a full batch)
 constexpr uint32_t HG_FINAL = 1u << 31;
+// k3_hg_scan's verdict on a group whose digit window holds no varying key bit
+// (hg_vary): HG_SKIP_ALL -- every remaining key bit is equal: the whole group
+// is one final tie group, written out from where it is; HG_SKIP_RELABEL -- it
+// goes back to the L list with its shift lowered to its highest varying bit.
+// Either way no element moves at this level.  (Near-periodic blocks -- a
+// per-position BED's "0\n" repeated -- send groups of ~450k rotations whose
+// 52-64 key bits are all equal through here: seven 8-bit levels each, per
+// round, before this.)
+constexpr uint32_t HG_SKIP_ALL = 1, HG_SKIP_RELABEL = 2;
+// ... and when more than half the group's keys equal its first element's key
+// over every remaining bit -- a doubling round's unresolved rotations, all
+// ranked at the same tie group -- the level is a three-way split instead of a
+// digit: below / equal / above that key.  The equal part is final at once (a
+// tie group for the next round); the other two keep the shift.  One pass per
+// round instead of a digit level per 8 key bits, each moving the whole group.
+constexpr uint32_t HG_THREE = 3;
+// The three-way split in place (par 0, no last-column stream): only the
+// elements outside their part's range move (each into a hole of its part,
+// through short lists), and the equal part -- most of the group -- stays where
+// it is.  Its rank (RK) is any position inside its range (ranks only have to
+// order the groups' disjoint ranges), so the previous round's rank is kept
+// when it still lies inside: a doubling round of a near-periodic block then
+// writes neither SA nor RK for its unresolved rotations.
+constexpr uint32_t HG_THREE_IP = 4;
+constexpr uint32_t HG_KEEP = 0xFFFFFFFFu;
 
 // L-list items above HG_MIN whose chunks fit go to the huge list; their
 // L-list entry gets size 0 (k3_part_l skips it)
@@ -1130,78 +1180,159 @@ __device__ __forceinline__ uint32_t wave_bin_add(uint32_t* cnt, bool act, uint32
 }
 
 // the chunks of every huge group as one flat index space: chunk j of the
-// launch -> (group q, chunk in group); groups' chunk counts prefix-summed in LDS
-struct HgMap {
-    uint32_t nh, total;
-    uint32_t pre[HG_MAXN + 1];
-};
-__device__ __forceinline__ void hg_map_load(const Ctx& c, HgMap& mp)
+// launch -> (group q, chunk in group), from the groups' chunk-count prefix
+// (k3_hg_prefix, global: thousands of groups per level)
+__device__ __forceinline__ uint32_t hg_count(const Ctx& c) { return min(c.L.ctr[C_HG], HG_MAXN); }
+__device__ __forceinline__ uint32_t hg_group_of(const uint32_t* __restrict__ pre, uint32_t nh, uint32_t j)
 {
-    if (threadIdx.x == 0) {
-        const uint32_t nh = min(c.L.ctr[C_HG], HG_MAXN);
-        uint32_t t = 0;
-        for (uint32_t q = 0; q < nh; ++q) {
-            mp.pre[q] = t;
-            t += hg_group(c.L.hg[q]).nch;   // 0 for a group left to k3_part_l
-        }
-        mp.pre[nh] = t;
-        mp.nh = nh;
-        mp.total = t;
-    }
-    __syncthreads();
-}
-__device__ __forceinline__ uint32_t hg_group_of(const HgMap& mp, uint32_t j)
-{
-    uint32_t lo = 0, hi = mp.nh - 1;
+    uint32_t lo = 0, hi = nh - 1;
     while (lo < hi) {                      // last q with pre[q] <= j (empty groups share a start)
         const uint32_t mid = (lo + hi + 1) >> 1;
-        if (mp.pre[mid] <= j) lo = mid; else hi = mid - 1;
+        if (pre[mid] <= j) lo = mid; else hi = mid - 1;
     }
     return lo;
 }
 
-// per-chunk digit counts, added into the group's 256 bin totals
+// one workgroup: the huge groups' chunk counts, prefix-summed (0 for a group
+// left to k3_part_l)
+__global__ void __launch_bounds__(1024) k3_hg_prefix(Ctx c)
+{
+    __shared__ uint32_t scan_sh[17];
+    const uint32_t nh = hg_count(c), tid = threadIdx.x;
+    uint32_t run = 0;
+    for (uint32_t q0 = 0; q0 < nh; q0 += 1024) {
+        const uint32_t q = q0 + tid;
+        const uint32_t k = q < nh ? hg_group(c.L.hg[q]).nch : 0u;
+        uint32_t tot = 0;
+        const uint32_t p = block_excl_scan_add<uint32_t>(k, scan_sh, &tot);
+        if (q < nh) c.L.hg_pre[q] = run + p;
+        run += tot;
+        __syncthreads();
+    }
+    if (tid == 0) c.L.hg_pre[nh] = run;
+}
+
+// per-chunk digit counts, added into the group's 256 bin totals; and the key
+// bits that vary inside the group (OR of key ^ the group's first key)
 template <bool DBL>
 __global__ void __launch_bounds__(256) k3_hg_hist(Ctx c)
 {
     __shared__ uint32_t h[256];
-    __shared__ HgMap mp;
+    __shared__ uint64_t vx[4];
+    __shared__ uint32_t ve[4], vl[4];
     const uint32_t tid = threadIdx.x;
-    hg_map_load(c, mp);
-    for (uint32_t j = blockIdx.x; j < mp.total; j += gridDim.x) {
-        const uint32_t q = hg_group_of(mp, j), ch = j - mp.pre[q];
+    const uint32_t nh = hg_count(c);
+    if (nh == 0) return;
+    const uint32_t total = c.L.hg_pre[nh];
+    for (uint32_t j = blockIdx.x; j < total; j += gridDim.x) {
+        const uint32_t q = hg_group_of(c.L.hg_pre, nh, j), ch = j - c.L.hg_pre[q];
         const HgGroup g = hg_group(c.L.hg[q]);
         const KeySrc ks = key_src(c, g.slot, g.par);
         const uint32_t* sv = (g.par ? c.scr.V : c.scr.SA) + (uint64_t)g.slot * c.scr.stride + g.s;
         h[tid] = 0;
         __syncthreads();
         const uint32_t a = ch * HG_CH, e = min(g.m, a + HG_CH);
+        const uint64_t ref = elem_key<DBL>(ks, g.s, sv[0]);
         uint32_t d[HG_CH / 256];
+        uint64_t vary = 0;
+        uint32_t neq = 0, nlt = 0;
 #pragma unroll
         for (uint32_t u = 0; u < HG_CH / 256; ++u) {   // all loads issued first
             const uint32_t i = a + u * 256 + tid, ic = i < e ? i : a;
-            d[u] = (uint32_t)((elem_key<DBL>(ks, g.s + ic, sv[ic]) >> g.sh2) & g.dmask);
+            const uint64_t k = elem_key<DBL>(ks, g.s + ic, sv[ic]);
+            d[u] = (uint32_t)((k >> g.sh2) & g.dmask);
+            vary |= k ^ ref;
+            neq += (i < e && k == ref) ? 1u : 0u;
+            nlt += (i < e && k < ref) ? 1u : 0u;
         }
 #pragma unroll
         for (uint32_t u = 0; u < HG_CH / 256; ++u) (void)wave_bin_add(h, a + u * 256 + tid < e, d[u]);
+        vary = wave_reduce_or64(vary);
+        neq = wave_reduce_add<uint32_t>(neq);
+        nlt = wave_reduce_add<uint32_t>(nlt);
+        if ((tid & 63) == 0) { vx[tid >> 6] = vary; ve[tid >> 6] = neq; vl[tid >> 6] = nlt; }
         __syncthreads();
         if (h[tid]) atomicAdd(&c.L.hg_info[(uint64_t)q * 512 + 256 + tid], h[tid]);   // bin totals
+        if (tid == 0) {
+            const uint64_t v = vx[0] | vx[1] | vx[2] | vx[3];
+            if (v) atomicOr(reinterpret_cast<unsigned long long*>(&c.L.hg_vary[q]), (unsigned long long)v);
+            const uint32_t te = ve[0] + ve[1] + ve[2] + ve[3], tl = vl[0] + vl[1] + vl[2] + vl[3];
+            if (te) atomicAdd(&c.L.hg_eqlt[2 * q], te);
+            if (tl) atomicAdd(&c.L.hg_eqlt[2 * q + 1], tl);
+        }
         __syncthreads();
     }
 }
 
 // one workgroup per huge group: bin starts -> the group's global cursors,
-// sub-bucket classes (k3_part_l's rules), final-bin flags
+// sub-bucket classes (k3_part_l's rules), final-bin flags; or, when the digit
+// window holds no varying key bit, one of the two skips (HG_SKIP_*)
 __global__ void __launch_bounds__(256) k3_hg_scan(Ctx c)
 {
     __shared__ uint32_t scan_sh[5];
     __shared__ uint32_t cls_sh[16];
     const uint32_t q = blockIdx.x, tid = threadIdx.x;
-    if (q >= min(c.L.ctr[C_HG], HG_MAXN)) return;
+    if (q >= hg_count(c)) return;
     const uint64_t item = c.L.hg[q];
     if (it_size(item) == 0) return;                   // uniform
     const HgGroup g = hg_group(item);
+    const uint64_t vary = c.L.hg_vary[q] & (g.shift >= 64 ? ~0ull : ((1ull << g.shift) - 1ull));
+    const int hb = vary ? 63 - __clzll((long long)vary) : -1;   // highest unsorted bit that varies
+    if (hb < (int)g.sh2) {                            // uniform: no element moves at this level
+        if (hb < 0) {                                 // every remaining key bit equal: one final tie group
+            if (tid == 0) {
+                c.L.hg_flag[q] = HG_SKIP_ALL;
+                const uint32_t o = atomicAdd(c.L.ctr + C_T0 + c.tsel, 1u);
+                c.L.t[c.tsel][o] = mk_item(g.slot, g.s, g.m, 0, 0);
+                atomicAdd(c.L.ctr + C_TS0 + c.tsel, g.m);
+                if (c.mode) atomicAdd(&c.L.runs[g.slot], 1u);
+            }
+            wg_classify(c, cls_sh, false, 0, 0, 0, 0, 0);
+        } else {                                      // back to the L list at its highest varying bit
+            if (tid == 0) c.L.hg_flag[q] = HG_SKIP_RELABEL;
+            wg_classify(c, cls_sh, tid == 0, g.slot, g.s, g.m, (uint32_t)hb + 1u, g.par);
+        }
+        return;
+    }
     uint32_t* info = c.L.hg_info + (uint64_t)q * 512;   // [0,256) start | flags, [256,512) totals -> cursors
+    const uint32_t neq = c.L.hg_eqlt[2 * q], nlt = c.L.hg_eqlt[2 * q + 1];
+    static_assert(L_MIN < HG_MIN, "three-way parts above L_MIN stay L items");
+    if (2 * neq > g.m) {                              // uniform: three-way split around the first key
+        const uint32_t ngt = g.m - neq - nlt;
+        const uint32_t st3[3] = {0u, nlt, nlt + neq}, n3[3] = {nlt, neq, ngt};
+        const KeySrc ks = key_src(c, g.slot, g.par);
+        const bool ip = g.par == 0 && ks.l == nullptr;
+        if (tid == 0) {
+            c.L.hg_flag[q] = ip ? HG_THREE_IP : HG_THREE;
+            if (ip) {
+                uint32_t rk = g.s + nlt + neq / 2;
+                if (c.mode) {                         // keep the previous rank if it lies in the equal part
+                    const uint64_t so = (uint64_t)g.slot * c.scr.stride;
+                    const uint32_t r0 = c.scr.RK[so + c.scr.SA[so + g.s]];
+                    if (r0 >= g.s + nlt && r0 < g.s + nlt + neq) rk = HG_KEEP;
+                }
+                c.L.hg_rank[q] = rk;
+            }
+        }
+        if (tid < 3) {
+            const bool f = tid == 1 || n3[tid] == 1;
+            info[tid] = st3[tid] | (f ? HG_FINAL : 0u);
+            info[256 + tid] = st3[tid];
+        } else {
+            info[tid] = g.m;                          // empty bins after the three
+            info[256 + tid] = g.m;
+        }
+        if (tid == 1 && neq >= 2) {                   // the equal part: a final tie group
+            const uint32_t o = atomicAdd(c.L.ctr + C_T0 + c.tsel, 1u);
+            c.L.t[c.tsel][o] = mk_item(g.slot, g.s + nlt, neq, 0, 0);
+            atomicAdd(c.L.ctr + C_TS0 + c.tsel, neq);
+        }
+        const uint32_t t3 = tid == 2 ? 2u : 0u;      // the two parts that are sorted further
+        const bool push = (tid == 0 || tid == 2) && n3[t3] >= 2;
+        wg_classify(c, cls_sh, push, g.slot, g.s + st3[t3], n3[t3], g.shift, ip ? g.par : g.par ^ 1u);   // in place: same buffer
+        if (tid == 0 && c.mode) atomicAdd(&c.L.runs[g.slot], 1u + (nlt == 1 ? 1u : 0u) + (ngt == 1 ? 1u : 0u));
+        return;
+    }
     const uint32_t cc = info[256 + tid];
     const uint32_t ss = block_excl_scan_add<uint32_t>(cc, scan_sh, (uint32_t*)nullptr);
     info[256 + tid] = ss;                             // scatter cursor
@@ -1218,18 +1349,116 @@ __global__ void __launch_bounds__(256) k3_hg_scan(Ctx c)
     if (c.mode && (tid & 63) == 0 && r) atomicAdd(&c.L.runs[g.slot], r);
 }
 
+// In-place three-way lists of a group (parts L = [0, nlt), E, G = [nlt + neq,
+// m) of its range): an element outside its part's range is a mover (its
+// value -- and, doubling, its key -- goes to its part's list in the
+// other-parity buffers, free for this group) and its position a hole of the
+// part it sits in.  Lists: movers to L / G / E at offsets 0 / nlt / nlt + ngt
+// of dv (and keys of dk; at most nlt / ngt / nlt + ngt of them); holes
+// likewise in RK's range (round 0: RK unused)
+// or, doubling, in dk after the keys (nlt + ngt < m / 2: everything fits).
+__device__ __forceinline__ uint32_t* hg_hole_list(const Ctx& c, const HgGroup& g, uint64_t* dk, uint32_t nlt,
+                                                  uint32_t ngt)
+{
+    if (c.mode) return reinterpret_cast<uint32_t*>(dk + nlt + ngt);
+    return c.scr.RK + (uint64_t)g.slot * c.scr.stride + g.s;
+}
+
+template <bool DBL>
+__device__ __forceinline__ void hg_inplace_lists(const Ctx& c, uint32_t q, const HgGroup& g, const KeySrc& ks,
+                                                 const uint32_t* sv, uint32_t* dv, uint64_t* dk, uint32_t a,
+                                                 uint32_t e, uint32_t* cnt)
+{
+    const uint32_t tid = threadIdx.x;
+    const uint32_t neq = c.L.hg_eqlt[2 * q], nlt = c.L.hg_eqlt[2 * q + 1], ngt = g.m - neq - nlt;
+    const uint32_t lo[3] = {0u, nlt + ngt, nlt};      // list offsets of the parts L, E, G (sizes <= nlt, nlt + ngt, ngt)
+    uint32_t* hl = hg_hole_list(c, g, dk, nlt, ngt);
+    const uint64_t ref = elem_key<DBL>(ks, g.s, sv[0]);
+    constexpr uint32_t U = HG_CH / 256;
+    uint32_t v[U], cl[U], rg[U], rm[U], rh[U];
+    uint64_t k[U];
+#pragma unroll
+    for (uint32_t u = 0; u < U; ++u) {
+        const uint32_t i = a + u * 256 + tid, ic = i < e ? i : a;
+        v[u] = sv[ic];
+        k[u] = elem_key<DBL>(ks, g.s + ic, v[u]);
+        cl[u] = k[u] < ref ? 0u : k[u] == ref ? 1u : 2u;
+        rg[u] = ic < nlt ? 0u : ic < nlt + neq ? 1u : 2u;
+    }
+#pragma unroll
+    for (uint32_t u = 0; u < U; ++u) {
+        const bool mis = a + u * 256 + tid < e && cl[u] != rg[u];
+        rm[u] = wave_bin_add(cnt, mis, cl[u]);
+        rh[u] = wave_bin_add(cnt + 3, mis, rg[u]);
+    }
+    __syncthreads();
+    if (tid < 6) {
+        const uint32_t x = cnt[tid];
+        cnt[8 + tid] = x ? atomicAdd(&c.L.hg_mc[6 * q + tid], x) : 0u;
+    }
+    __syncthreads();
+#pragma unroll
+    for (uint32_t u = 0; u < U; ++u) {
+        const uint32_t i = a + u * 256 + tid;
+        if (i < e && cl[u] != rg[u]) {
+            const uint32_t km = lo[cl[u]] + cnt[8 + cl[u]] + rm[u];
+            dv[km] = v[u];
+            if constexpr (DBL) if (cl[u] != 1) dk[km] = k[u];
+            hl[lo[rg[u]] + cnt[11 + rg[u]] + rh[u]] = i;
+        }
+    }
+    __syncthreads();
+}
+
+// in-place three-way groups: every mover into a hole of its part (the k-th
+// mover of a part fills its k-th hole); keys move with the values while
+// doubling (the parts L and G are sorted further by them)
+template <bool DBL>
+__global__ void __launch_bounds__(256) k3_hg_move(Ctx c)
+{
+    const uint32_t nh = hg_count(c);
+    const GridSplit gs = grid_split(nh);
+    if (gs.idle) return;
+    for (uint32_t q = gs.q0; q < nh; q += gs.gstride) {
+        if (c.L.hg_flag[q] != HG_THREE_IP) continue;
+        const HgGroup g = hg_group(c.L.hg[q]);
+        const KeySrc ks = key_src(c, g.slot, g.par);
+        const uint64_t base = (uint64_t)g.slot * c.scr.stride + g.s;
+        uint32_t* sv = c.scr.SA + base;               // par 0
+        const uint32_t* dv = c.scr.V + base;
+        uint64_t* dk = c.kB + base;
+        uint64_t* sk = c.kA + base;
+        const uint32_t neq = c.L.hg_eqlt[2 * q], nlt = c.L.hg_eqlt[2 * q + 1], ngt = g.m - neq - nlt;
+        const uint32_t* hl = hg_hole_list(c, g, dk, nlt, ngt);
+        const uint32_t n0 = c.L.hg_mc[6 * q], n1 = c.L.hg_mc[6 * q + 1], n2 = c.L.hg_mc[6 * q + 2];
+        const uint32_t lo[3] = {0u, nlt + ngt, nlt};   // as in hg_inplace_lists
+        (void)ks;
+        for (uint32_t x = gs.slice * 256u + threadIdx.x; x < n0 + n1 + n2; x += gs.per * 256u) {
+            const uint32_t part = x < n0 ? 0u : x < n0 + n2 ? 2u : 1u;   // L, G, then E
+            const uint32_t kk = part == 0 ? x : part == 2 ? x - n0 : x - n0 - n2;
+            const uint32_t j = lo[part] + kk;
+            const uint32_t pos = hl[j];
+            sv[pos] = dv[j];
+            if constexpr (DBL) if (part != 1) sk[pos] = dk[j];
+        }
+    }
+}
+
 // every chunk: its elements to their bins (one global reservation per bin
 // and chunk, then LDS cursors)
 template <bool DBL>
 __global__ void __launch_bounds__(256) k3_hg_scatter(Ctx c)
 {
     __shared__ uint32_t cnt[256];
-    __shared__ HgMap mp;
     const uint32_t tid = threadIdx.x;
-    hg_map_load(c, mp);
+    const uint32_t nh = hg_count(c);
+    if (nh == 0) return;
+    const uint32_t total = c.L.hg_pre[nh];
     constexpr uint32_t U = HG_CH / 256;
-    for (uint32_t j = blockIdx.x; j < mp.total; j += gridDim.x) {
-        const uint32_t q = hg_group_of(mp, j), ch = j - mp.pre[q];
+    for (uint32_t j = blockIdx.x; j < total; j += gridDim.x) {
+        const uint32_t q = hg_group_of(c.L.hg_pre, nh, j), ch = j - c.L.hg_pre[q];
+        const uint32_t flag = c.L.hg_flag[q];
+        if (flag && flag != HG_THREE && flag != HG_THREE_IP) continue;   // uniform: skipped at this level
         const HgGroup g = hg_group(c.L.hg[q]);
         const KeySrc ks = key_src(c, g.slot, g.par);
         const uint64_t base = (uint64_t)g.slot * c.scr.stride + g.s;
@@ -1241,14 +1470,19 @@ __global__ void __launch_bounds__(256) k3_hg_scatter(Ctx c)
         cnt[tid] = 0;
         __syncthreads();
         const uint32_t a = ch * HG_CH, e = min(g.m, a + HG_CH);
+        if (flag == HG_THREE_IP) {                    // uniform
+            hg_inplace_lists<DBL>(c, q, g, ks, sv, dv, dk, a, e, cnt);
+            continue;
+        }
         uint32_t v[U], d[U], r[U];
         uint64_t k[U];
+        const uint64_t ref = flag == HG_THREE ? elem_key<DBL>(ks, g.s, sv[0]) : 0ull;
 #pragma unroll
         for (uint32_t u = 0; u < U; ++u) {
             const uint32_t i = a + u * 256 + tid, ic = i < e ? i : a;
             v[u] = sv[ic];
             k[u] = elem_key<DBL>(ks, g.s + ic, v[u]);
-            d[u] = (uint32_t)((k[u] >> g.sh2) & g.dmask);
+            d[u] = flag == HG_THREE ? (k[u] < ref ? 0u : k[u] == ref ? 1u : 2u) : (uint32_t)((k[u] >> g.sh2) & g.dmask);
         }
 #pragma unroll
         for (uint32_t u = 0; u < U; ++u) r[u] = wave_bin_add(cnt, a + u * 256 + tid < e, d[u]);
@@ -1271,21 +1505,61 @@ __global__ void __launch_bounds__(256) k3_hg_scatter(Ctx c)
     }
 }
 
-// final sub-buckets of every huge group: SA, last column, RK, origPtr; the
-// work is the flat list of (group, final bin, 1024-element piece)
+// final sub-buckets of every huge group: SA, last column, RK, origPtr.  The
+// grid's workgroups split over the groups (several per group when there are
+// fewer groups than workgroups); a group skipped whole (HG_SKIP_ALL) is
+// written from where its elements are, as one run headed at its start.
 __global__ void __launch_bounds__(256) k3_hg_final(Ctx c)
 {
     __shared__ uint32_t fin_pre[257];
     __shared__ uint32_t scan_sh[5];
     const uint32_t tid = threadIdx.x;
-    const uint32_t nh = min(c.L.ctr[C_HG], HG_MAXN);
-    for (uint32_t q = 0; q < nh; ++q) {
+    const uint32_t nh = hg_count(c), G = gridDim.x;
+    if (nh == 0) return;
+    const uint32_t per = nh >= G ? 1u : G / nh;      // workgroups per group
+    const uint32_t gstride = G / per;                 // groups in progress at once
+    if (blockIdx.x >= per * gstride) return;
+    const uint32_t slice = blockIdx.x % per;
+    for (uint32_t q = blockIdx.x / per; q < nh; q += gstride) {
         const uint64_t item = c.L.hg[q];
         if (it_size(item) == 0) continue;
         const HgGroup g = hg_group(item);
+        const uint32_t flag = c.L.hg_flag[q];
+        if (flag == HG_SKIP_RELABEL) continue;
         const uint64_t so = (uint64_t)g.slot * c.scr.stride, base = so + g.s;
-        const uint32_t* dv = (g.par ? c.scr.SA : c.scr.V) + base;
         const KeySrc ks = key_src(c, g.slot, g.par);
+        if (flag == HG_THREE_IP) {                    // uniform: in SA already (par 0)
+            const uint32_t neq = c.L.hg_eqlt[2 * q], nlt = c.L.hg_eqlt[2 * q + 1], ngt = g.m - neq - nlt;
+            const uint32_t rk = c.L.hg_rank[q];
+            const uint32_t* sa = c.scr.SA + base;
+            if (c.mode && rk != HG_KEEP)
+                for (uint32_t p = nlt + slice * 256u + tid; p < nlt + neq; p += per * 256u) c.scr.RK[so + sa[p]] = rk;
+            if (slice == 0 && tid < 2) {              // a part of one rotation is final
+                const bool one = tid == 0 ? nlt == 1 : ngt == 1;
+                if (one) {
+                    const uint32_t p = tid == 0 ? 0u : g.m - 1u;
+                    const uint32_t v = sa[p];
+                    c.scr.LL[base + p] = last_sym(c, g.slot, v);
+                    if (c.mode) c.scr.RK[so + v] = g.s + p;
+                    if (v == 0) c.blocks[c.b0 + g.slot].orig_ptr = g.s + p;
+                }
+            }
+            continue;
+        }
+        if (flag == HG_SKIP_ALL) {                    // uniform
+            const uint32_t* sv = (g.par ? c.scr.V : c.scr.SA) + base;
+            // (a tie group: its last column is written once it resolves --
+            // every tie is re-sorted later, or its block is periodic and
+            // k_fallback_exact rebuilds that block's last column)
+            for (uint32_t p = slice * 256u + tid; p < g.m; p += per * 256u) {
+                const uint32_t v = sv[p];
+                if (g.par) c.scr.SA[base + p] = v;
+                if (c.mode) c.scr.RK[so + v] = g.s;
+                if (v == 0) c.blocks[c.b0 + g.slot].orig_ptr = g.s + p;
+            }
+            continue;
+        }
+        const uint32_t* dv = (g.par ? c.scr.SA : c.scr.V) + base;
         const uint8_t* dl = ks.l ? (g.par ? c.lA : c.lB) + base : nullptr;
         const uint32_t* info = c.L.hg_info + (uint64_t)q * 512;
         // final bins' sizes (bin end = next bin's start; the last ends at m)
@@ -1297,7 +1571,7 @@ __global__ void __launch_bounds__(256) k3_hg_final(Ctx c)
         fin_pre[tid] = fp;
         if (tid == 255) fin_pre[256] = ftot;
         __syncthreads();
-        for (uint32_t x = blockIdx.x * 256u + tid; x < ftot; x += gridDim.x * 256u) {
+        for (uint32_t x = slice * 256u + tid; x < ftot; x += per * 256u) {
             uint32_t lo = 0, hi = 255;                 // the final bin holding flat index x
             while (lo < hi) {
                 const uint32_t mid = (lo + hi + 1) >> 1;
@@ -1307,7 +1581,8 @@ __global__ void __launch_bounds__(256) k3_hg_final(Ctx c)
             const uint32_t p = b0 + (x - fin_pre[lo]);
             const uint32_t v = dv[p];
             if (!g.par) c.scr.SA[base + p] = v;
-            c.scr.LL[base + p] = dl ? dl[p] : last_sym(c, g.slot, v);
+            const uint32_t be = lo < 255 ? (info[lo + 1] & ~HG_FINAL) : g.m;
+            if (be - b0 == 1) c.scr.LL[base + p] = dl ? dl[p] : last_sym(c, g.slot, v);   // ties: once resolved
             if (c.mode) c.scr.RK[so + v] = g.s + b0;
             if (v == 0) c.blocks[c.b0 + g.slot].orig_ptr = g.s + p;
         }
@@ -2685,13 +2960,15 @@ __global__ void __launch_bounds__(256) k3_gather(Ctx c, const uint64_t* __restri
 __global__ void __launch_bounds__(256) k3_gather_big(Ctx c)
 {
     const uint32_t ng = min(c.L.ctr[C_GB], GB_MAXN);
-    const uint32_t step = gridDim.x * 256u;
-    for (uint32_t q = 0; q < ng; ++q) {
+    const GridSplit gs = grid_split(ng);
+    if (gs.idle) return;
+    const uint32_t step = gs.per * 256u;
+    for (uint32_t q = gs.q0; q < ng; q += gs.gstride) {
         const uint64_t item = c.L.gb[q];
         const uint32_t slot = it_slot(item), s = it_start(item), m = it_size(item), hm = c.L.gb_h[q];
         const uint32_t n = c.blocks[c.b0 + slot].n;
         const uint64_t so = (uint64_t)slot * c.scr.stride;
-        for (uint32_t i = blockIdx.x * 256u + threadIdx.x; i < m; i += step) {
+        for (uint32_t i = gs.slice * 256u + threadIdx.x; i < m; i += step) {
             uint32_t t = c.scr.SA[so + s + i] + hm;
             if (t >= n) t -= n;
             c.scr.K2[so + s + i] = c.scr.RK[so + t];
@@ -2739,12 +3016,14 @@ __global__ void __launch_bounds__(256) k3_rk_groups(Ctx c, const uint64_t* __res
 __global__ void __launch_bounds__(256) k3_rk_big(Ctx c)
 {
     const uint32_t ng = min(c.L.ctr[C_GB], GB_MAXN);
-    const uint32_t step = gridDim.x * 256u;
-    for (uint32_t q = 0; q < ng; ++q) {
+    const GridSplit gs = grid_split(ng);
+    if (gs.idle) return;
+    const uint32_t step = gs.per * 256u;
+    for (uint32_t q = gs.q0; q < ng; q += gs.gstride) {
         const uint64_t item = c.L.gb[q];
         const uint32_t slot = it_slot(item), s = it_start(item), m = it_size(item);
         const uint64_t so = (uint64_t)slot * c.scr.stride;
-        for (uint32_t i = blockIdx.x * 256u + threadIdx.x; i < m; i += step) c.scr.RK[so + c.scr.SA[so + s + i]] = s;
+        for (uint32_t i = gs.slice * 256u + threadIdx.x; i < m; i += step) c.scr.RK[so + c.scr.SA[so + s + i]] = s;
     }
 }
 
@@ -2861,7 +3140,8 @@ bool launch_bwt3(BlockDesc* blocks, uint32_t b0, uint32_t nb, const uint8_t* blk
     const uint64_t nwg_bin = BIN_MAXWG;
     const uint64_t nb_bins = nb < 64 ? 8ull * nb : nb;     // bins of k3_bin_* (see bin_of)
     constexpr uint32_t QSETS = 64, QSET = 8 * XQ_STRIDE + 32;   // queue heads (a line each) + segments per launch
-    const uint64_t hg_words = 2ull * HG_MAXN + (uint64_t)HG_MAXN * 512 + 3ull * GB_MAXN + 64;
+    const uint64_t hg_words = 2ull * HG_MAXN + (uint64_t)HG_MAXN * 512 + 3ull * GB_MAXN + 64 + (HG_MAXN + 1) +
+                              2ull * HG_MAXN + HG_MAXN + 2ull * HG_MAXN + 6ull * HG_MAXN + HG_MAXN + 8;
     const uint64_t words = 2 * C_N + 14ull * nb + QSETS * QSET + (nwg_bin + 2) * nb_bins +
                            2 * (cap_s + cap_s2 + cap_m0 + cap_m1 + cap_m2 + cap_m3 + 2 * cap_l) + 64 + hg_words;
     uint32_t* mw = meta.as<uint32_t>(words);
@@ -2900,7 +3180,15 @@ bool launch_bwt3(BlockDesc* blocks, uint32_t b0, uint32_t nb, const uint8_t* blk
         c.L.gb = c.L.hg + HG_MAXN;
         c.L.gb_h = reinterpret_cast<uint32_t*>(c.L.gb + GB_MAXN);
         c.L.hg_info = c.L.gb_h + GB_MAXN;
-        if (reinterpret_cast<uintptr_t>(c.L.hg_info + (uint64_t)HG_MAXN * 512) > reinterpret_cast<uintptr_t>(mw + words))
+        uintptr_t r = reinterpret_cast<uintptr_t>(c.L.hg_info + (uint64_t)HG_MAXN * 512);
+        r = (r + 7) & ~(uintptr_t)7;
+        c.L.hg_vary = reinterpret_cast<uint64_t*>(r);
+        c.L.hg_flag = reinterpret_cast<uint32_t*>(c.L.hg_vary + HG_MAXN);
+        c.L.hg_pre = c.L.hg_flag + HG_MAXN;
+        c.L.hg_eqlt = c.L.hg_pre + HG_MAXN + 1;
+        c.L.hg_mc = c.L.hg_eqlt + 2 * HG_MAXN;
+        c.L.hg_rank = c.L.hg_mc + 6 * HG_MAXN;
+        if (reinterpret_cast<uintptr_t>(c.L.hg_rank + HG_MAXN) > reinterpret_cast<uintptr_t>(mw + words))
             throw StarchError(-10, "bwt3: meta layout");
     }
     c.L.w = reinterpret_cast<uint64_t*>(scr.U);
@@ -2977,10 +3265,37 @@ bool launch_bwt3(BlockDesc* blocks, uint32_t b0, uint32_t nb, const uint8_t* blk
             if (nl == 0) break;
             if (level > 64) throw StarchError(-10, "bwt3: partition did not converge");
             const bool huge = hctr[C_LM0 + lsel] > HG_MIN;
+            static const bool ldbg = getenv("STARCH_BWT_DEBUG") != nullptr;
+            if (ldbg) {   // the L list of this level: sizes and shifts
+                std::vector<uint64_t> it(nl);
+                HIP_CHECK(hipMemcpyAsync(it.data(), c.L.l[lsel], nl * sizeof(uint64_t), hipMemcpyDeviceToHost, st));
+                HIP_CHECK(hipStreamSynchronize(st));
+                uint64_t tot = 0, big = 0, nbig = 0, mx = 0;
+                uint32_t sh[128] = {};
+                for (uint64_t v : it) {
+                    const uint64_t m = (v >> 12) & 0xFFFFFu;
+                    tot += m;
+                    mx = m > mx ? m : mx;
+                    if (m > HG_MIN) { big += m; ++nbig; }
+                    ++sh[v & 127u];
+                }
+                fprintf(stderr, "[bwt3] rtext %u mode %u level %d: L items %u elems %llu max %llu | >HG_MIN %llu items %llu elems | shifts",
+                        c.rtext, c.mode, level, nl, (unsigned long long)tot, (unsigned long long)mx,
+                        (unsigned long long)nbig, (unsigned long long)big);
+                for (int q = 0; q < 128; ++q)
+                    if (sh[q]) fprintf(stderr, " %d:%u", q, sh[q]);
+                fprintf(stderr, "\n");
+            }
             if (huge) {   // groups above HG_MIN: partitioned by the whole grid
                 zero(bit(C_HG) | bit(C_HGC));
-                HIP_CHECK(hipMemsetAsync(c.L.hg_info, 0, (uint64_t)HG_MAXN * 512 * sizeof(uint32_t), st));
+                const uint64_t nhm = std::min<uint64_t>(nl, HG_MAXN);   // huge groups: at most this many
+                HIP_CHECK(hipMemsetAsync(c.L.hg_info, 0, nhm * 512 * sizeof(uint32_t), st));
+                HIP_CHECK(hipMemsetAsync(c.L.hg_vary, 0, nhm * sizeof(uint64_t), st));
+                HIP_CHECK(hipMemsetAsync(c.L.hg_flag, 0, nhm * sizeof(uint32_t), st));
+                HIP_CHECK(hipMemsetAsync(c.L.hg_eqlt, 0, 2 * nhm * sizeof(uint32_t), st));
+                HIP_CHECK(hipMemsetAsync(c.L.hg_mc, 0, 6 * nhm * sizeof(uint32_t), st));
                 hipLaunchKernelGGL(k3_hg_pick, dim3((nl + 255) / 256), dim3(256), 0, st, c, c.L.l[lsel], nl);
+                hipLaunchKernelGGL(k3_hg_prefix, dim3(1), dim3(1024), 0, st, c);
             }
             bin(c.L.l[lsel], nl, bout);
             c.lsel = lsel ^ 1u;
@@ -2989,9 +3304,11 @@ bool launch_bwt3(BlockDesc* blocks, uint32_t b0, uint32_t nb, const uint8_t* blk
                 const dim3 gh(ncu * 4);
                 if (c.keysrc) hipLaunchKernelGGL(k3_hg_hist<true>, gh, dim3(256), 0, st, c);
                 else hipLaunchKernelGGL(k3_hg_hist<false>, gh, dim3(256), 0, st, c);
-                hipLaunchKernelGGL(k3_hg_scan, dim3(HG_MAXN), dim3(256), 0, st, c);
+                hipLaunchKernelGGL(k3_hg_scan, dim3((uint32_t)std::min<uint64_t>(nl, HG_MAXN)), dim3(256), 0, st, c);
                 if (c.keysrc) hipLaunchKernelGGL(k3_hg_scatter<true>, gh, dim3(256), 0, st, c);
                 else hipLaunchKernelGGL(k3_hg_scatter<false>, gh, dim3(256), 0, st, c);
+                if (c.keysrc) hipLaunchKernelGGL(k3_hg_move<true>, gh, dim3(256), 0, st, c);
+                else hipLaunchKernelGGL(k3_hg_move<false>, gh, dim3(256), 0, st, c);
                 hipLaunchKernelGGL(k3_hg_final, gh, dim3(256), 0, st, c);
                 HIP_CHECK(hipGetLastError());
             }

@@ -471,6 +471,35 @@ bool host_is_pinned(const void* p)
     return a.type == hipMemoryTypeHost;
 }
 
+// A large pageable input (e.g. an mmap'ed file) is registered with the HIP
+// runtime for the duration of one call, so the pipelined path's batches cross
+// PCIe by DMA straight from it: registering a page-cached 2.4 GB file took
+// ~28 ms and its copy then ran at the pinned rate (tools/probes/
+// h2d_file_probe.cpp), against ~0.2 s per GB to pin fresh memory.  Page-
+// rounded, read-only; if the runtime refuses (part of the range already
+// registered, ...) the call runs as before.
+struct HostRegistration {
+    void* base = nullptr;
+    HostRegistration(const void* p, uint64_t n)
+    {
+        if (!p || n < (256ull << 20) || host_is_pinned(p)) return;
+        static const bool off = [] { const char* e = getenv("STARCH_REGISTER"); return e && !strcmp(e, "0"); }();
+        if (off) return;
+        const uintptr_t pg = 4096, a = reinterpret_cast<uintptr_t>(p) & ~(pg - 1),
+                        e = (reinterpret_cast<uintptr_t>(p) + n + pg - 1) & ~(pg - 1);
+        if (hipHostRegister(reinterpret_cast<void*>(a), e - a, hipHostRegisterReadOnly) == hipSuccess)
+            base = reinterpret_cast<void*>(a);
+        else
+            (void)hipGetLastError();
+    }
+    ~HostRegistration()
+    {
+        if (base) (void)hipHostUnregister(base);
+    }
+    HostRegistration(const HostRegistration&) = delete;
+    HostRegistration& operator=(const HostRegistration&) = delete;
+};
+
 struct LaneBatch {
     int lane = 0;
     uint64_t coll_off = 0, bytes = 0;
@@ -935,6 +964,30 @@ void stream_reserve(starch_ctx* c, int i, uint64_t need)
     std::swap(m.dbuf[i].cap, nb.cap);
 }
 
+// pin buffer i (not the current one: nothing held) for `need` bytes, with its
+// device mirror; the session's prepin thread runs this while the first batch
+// is read
+void stream_prepin_one(starch_ctx* c, int i, uint64_t need)
+{
+    auto& m = c->sm;
+    if (need <= m.cap[i]) return;
+    const uint64_t cap = align_up(need, 1ull << 20);
+    void* p = nullptr;
+    HIP_CHECK(hipHostMalloc(&p, cap, hipHostMallocDefault));
+    if (m.buf[i]) (void)hipHostFree(m.buf[i]);
+    m.buf[i] = static_cast<uint8_t*>(p);
+    m.cap[i] = cap;
+    DevBuf nb;
+    (void)nb.as<uint8_t>(cap + 64);
+    std::swap(m.dbuf[i].p, nb.p);
+    std::swap(m.dbuf[i].cap, nb.cap);
+}
+
+void stream_prepin_join(starch_ctx* c)
+{
+    if (c->sm.prepin.joinable()) c->sm.prepin.join();
+}
+
 // Streaming inside a chromosome (bzip2): a batch may end inside a chromosome
 // (open) and the next one then starts with the last line of it (ctx bytes of
 // context).  The chromosome's stream is encoded in pieces: every batch
@@ -1347,6 +1400,7 @@ void stream_cut(starch_ctx* c)
         const uint64_t tail = m.held_n - ls;
         STRACE("stream cut inside a chromosome at %llu of %llu held", (unsigned long long)cut,
                (unsigned long long)m.held_n);
+        stream_prepin_join(c);
         const int o = stream_free_buf(c);
         stream_reserve(c, o, std::max<uint64_t>(tail + m.batch + (m.batch >> 2), 1ull << 20));
         m.pool.copy(m.buf[o], h + ls, tail);
@@ -1362,6 +1416,7 @@ void stream_cut(starch_ctx* c)
         return;
     }
     const uint64_t cut = u.back().offset, tail = m.held_n - cut;
+    stream_prepin_join(c);
     STRACE("stream cut at %llu of %llu held: wait for a free buffer", (unsigned long long)cut, (unsigned long long)m.held_n);
     const int o = stream_free_buf(c);
     STRACE("stream cut: buffer %d free", o);
@@ -1494,6 +1549,7 @@ int starch_encode_host(starch_ctx* c, const void* bed, uint64_t n, const starch_
     // large pinned inputs: PCIe copy of the next batch overlaps the encode
     // (STARCH_PIPELINE=0 turns it off; pageable memory has no async copy)
     static const bool pipe_off = [] { const char* e = getenv("STARCH_PIPELINE"); return e && !strcmp(e, "0"); }();
+    HostRegistration reg(pipe_off || o.reference_compat ? nullptr : bed, n);
     if (!pipe_off && !o.reference_compat && n >= (256ull << 20) && host_is_pinned(bed) &&
         encode_host_pipelined(c, static_cast<const uint8_t*>(bed), n, o))
         return STARCH_OK;
@@ -1527,6 +1583,7 @@ int starch_encode_host_into(starch_ctx* c, const void* bed, uint64_t n, const st
     if (o.block_size_100k < 1 || o.block_size_100k > 9 ||
         (o.compression_method != STARCH_METHOD_BZIP2 && o.compression_method != STARCH_METHOD_GZIP)) return STARCH_ERR_ARG;
     static const bool pipe_off = [] { const char* e = getenv("STARCH_PIPELINE"); return e && !strcmp(e, "0"); }();
+    HostRegistration reg(pipe_off || o.reference_compat ? nullptr : bed, n);
     if (!pipe_off && !o.reference_compat && n >= (256ull << 20) && host_is_pinned(bed) &&
         encode_host_pipelined(c, static_cast<const uint8_t*>(bed), n, o, static_cast<uint8_t*>(out), cap, out_len))
         return STARCH_OK;
@@ -1927,8 +1984,28 @@ int starch_stream_begin(starch_ctx* c, const starch_options* opt, uint64_t batch
     c->have = false;
     c->streamed = false;
     // the pinned buffers sized once for a batch plus a long held run (kept
-    // across sessions: pinning is paid on the context's first session only)
-    for (int i = 0; i < starch_ctx::Streaming::NBUF; ++i) stream_reserve(c, i, 2 * m.batch);
+    // across sessions: pinning is paid on the context's first session only):
+    // the first now, the others on the prepin thread while the first fills
+    // STARCH_PIN=eager (default): all three now; bg: the others on the prepin
+    // thread; lazy: the others at their first use (stream_cut)
+    static const int pin_mode = [] {
+        const char* e = getenv("STARCH_PIN");
+        return e && !strcmp(e, "bg") ? 1 : e && !strcmp(e, "lazy") ? 2 : 0;
+    }();
+    stream_reserve(c, 0, pin_mode ? m.batch + m.batch / 2 : 2 * m.batch);
+    bool more = false;
+    for (int i = 1; i < starch_ctx::Streaming::NBUF; ++i) more |= m.cap[i] < 2 * m.batch;
+    if (more && pin_mode == 0)
+        for (int i = 1; i < starch_ctx::Streaming::NBUF; ++i) stream_reserve(c, i, 2 * m.batch);
+    else if (more && pin_mode == 1)
+        m.prepin = std::thread([c]() {
+            (void)hipSetDevice(c->device);
+            try {
+                for (int i = 1; i < starch_ctx::Streaming::NBUF; ++i) stream_prepin_one(c, i, 2 * c->sm.batch);
+            } catch (const StarchError& e) {   // the next stream_reserve of that buffer retries and reports
+                STRACE("prepin failed: %s", e.what());
+            }
+        });
     for (int i = 0; i < starch_ctx::Streaming::NLANE; ++i) m.workers[i] = std::thread(stream_worker, c, i);
     return STARCH_OK;
     END_GUARD(c)
@@ -2000,6 +2077,7 @@ int starch_stream_end(starch_ctx* c)
     auto& m = c->sm;
     if (!m.active) return STARCH_ERR_STATE;
     try {
+        stream_prepin_join(c);
         // the rest goes to a lane as soon as one is free (the other may still
         // be encoding); an open stream's last piece waits for its predecessor
         if (m.held_n > m.ctx_len || m.last_open) stream_submit(c, m.held_n);

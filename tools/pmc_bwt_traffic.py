@@ -32,11 +32,16 @@ def is_bwt(name):
     return "k3_" in n or "k_fallback" in n or "k_last_col" in n
 
 
+KSEL = os.environ.get("PMC_KERNELS", "")     # regex over kernel names (default: the block-sort kernels)
+
+
 def sums(d, counter):
+    import re
     tot = collections.Counter()
     for f in glob.glob(os.path.join(d, "**", "run_counter_collection.csv"), recursive=True):
         for r in csv.DictReader(open(f)):
-            if r["Counter_Name"] == counter and is_bwt(r["Kernel_Name"]):
+            sel = re.search(KSEL, r["Kernel_Name"]) if KSEL else is_bwt(r["Kernel_Name"])
+            if r["Counter_Name"] == counter and sel:
                 tot[r["Kernel_Name"].replace("(anonymous namespace)::", "").split("(")[0].replace("void ", "")] += float(r["Counter_Value"])
     return tot
 
@@ -57,7 +62,8 @@ def main():
         "write_bytes": write_b,
         "method": "rocprofv3 --pmc FETCH_SIZE and WRITE_SIZE in separate passes over one bench step (kind/lines above); "
                   "FETCH_SIZE doubled (calibrated for 8/16-B gathers and 16-B streams: profiles/r04/fetch_calib.json); "
-                  "block-sort kernels k3_*, k_fallback*, k_last_col summed; Infinity-Cache hits are counted",
+                  + ("kernels matching %r summed" % KSEL if KSEL else
+                     "block-sort kernels k3_*, k_fallback*, k_last_col summed") + "; Infinity-Cache hits are counted",
         "per_kernel_fetch_bytes": {k: 2.0 * v * 1024.0 for k, v in f.most_common()},
         "per_kernel_write_bytes": {k: v * 1024.0 for k, v in w.most_common()},
     }
