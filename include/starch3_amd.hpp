@@ -49,7 +49,12 @@
 #include <cinttypes>
 #include <cstdio>
 #include <cstdlib>
+#include <condition_variable>
 #include <cstring>
+#include <deque>
+#include <map>
+#include <memory>
+#include <mutex>
 #include <string>
 #include <thread>
 #include <vector>
@@ -139,6 +144,8 @@ public:
     }
     ~Starch()
     {
+        hook_drain(true);
+        hook_stop();
         delete_bz_stream_ptr();
         delete_out_compression_stream();
         std::free(buffer.tf_buffer);
@@ -369,17 +376,19 @@ public:
     {
         const char* eb = std::getenv("STARCH_HPP_BATCH");   // tests: small batches
         if (eb && std::atoll(eb) > 0) batch = (uint64_t)std::atoll(eb);
-        std::vector<unsigned char> buf;
+        InBuf buf;
         std::vector<starch_unit> units(4096);
         int64_t is = 0, ip = 0;
         bool eof = false;
         uint64_t want = batch;
         uint64_t scanned = 0;      // bytes of buf known to hold no newline after the last complete line
+        FileReader rd(_in_stream);
         for (;;) {
             while (!eof && buf.size() < want) {
                 const size_t o = buf.size();
-                buf.resize(o + (1u << 24));
-                const size_t k = std::fread(&buf[o], 1, 1u << 24, _in_stream);
+                const size_t piece = rd.regular() ? (size_t)std::max<uint64_t>(want - o, 1u << 24) : (size_t)(1u << 24);
+                buf.resize(o + piece);
+                const size_t k = rd.read(&buf[o], piece);
                 buf.resize(o + k);
                 if (k == 0) eof = true;
             }
@@ -405,11 +414,94 @@ public:
             const starch_unit& last = units[nu - 1];
             is = last.init_start;
             ip = last.init_stop;
-            buf.erase(buf.begin(), buf.begin() + (std::ptrdiff_t)last.offset);
+            buf.erase_front(last.offset);
             scanned = 0;
             want = batch;
         }
     }
+
+    // the in stream's bytes, read with 16 pread(2) threads when it is a
+    // regular file (one fread stream from the page cache runs at a few GB/s),
+    // else with fread
+    struct FileReader {
+        FILE* f;
+        int fd;
+        bool reg;
+        uint64_t off;
+        explicit FileReader(FILE* in) : f(in), fd(-1), reg(false), off(0)
+        {
+            struct stat st;
+            fd = in ? fileno(in) : -1;
+            if (fd >= 0 && fstat(fd, &st) == 0 && S_ISREG(st.st_mode) && st.st_size > 0) {
+                const off_t o = lseek(fd, 0, SEEK_CUR);
+                if (o >= 0) {
+                    reg = true;
+                    off = (uint64_t)o;
+                }
+            }
+        }
+        ~FileReader()
+        {
+            if (reg) (void)lseek(fd, (off_t)off, SEEK_SET);   // the FILE's position where reading stopped
+        }
+        bool regular() const { return reg; }
+        size_t read(unsigned char* dst, size_t n)
+        {
+            if (!reg) return std::fread(dst, 1, n, f);
+            const int nt = 16;
+            const size_t per = (n + nt - 1) / nt;
+            std::vector<size_t> got(nt, 0);
+            std::vector<std::thread> th;
+            for (int t = 0; t < nt; ++t)
+                th.push_back(std::thread([&, t]() {
+                    const size_t b = (size_t)t * per, e = std::min(n, b + per);
+                    size_t q = b;
+                    while (q < e) {
+                        const ssize_t r = pread(fd, dst + q, e - q, (off_t)(off + q));
+                        if (r < 0 && errno == EINTR) continue;
+                        if (r <= 0) break;
+                        q += (size_t)r;
+                    }
+                    got[t] = q > b ? q - b : 0;
+                }));
+            for (size_t t = 0; t < th.size(); ++t) th[t].join();
+            size_t k = 0;                          // the bytes read contiguously from the start
+            for (int t = 0; t < nt; ++t) {
+                k += got[t];
+                const size_t b = (size_t)t * per;
+                if (b >= n || got[t] < std::min(n, b + per) - b) break;
+            }
+            off += k;
+            return k;
+        }
+    };
+
+    // a growable byte buffer that is not zero-filled (std::vector::resize
+    // zero-fills every 16 MiB piece before it is read into)
+    struct InBuf {
+        std::unique_ptr<unsigned char[]> p;
+        size_t n, cap;
+        InBuf() : n(0), cap(0) {}
+        size_t size() const { return n; }
+        unsigned char& operator[](size_t i) { return p[i]; }
+        void resize(size_t k)
+        {
+            if (k > cap) {
+                const size_t c = k + k / 2;
+                std::unique_ptr<unsigned char[]> q(new unsigned char[c]);
+                if (n) std::memcpy(q.get(), p.get(), std::min(n, k));
+                p.swap(q);
+                cap = c;
+            }
+            n = k;
+        }
+        void erase_front(size_t k)
+        {
+            if (k >= n) { n = 0; return; }
+            std::memmove(p.get(), p.get() + k, n - k);
+            n -= k;
+        }
+    };
 
     int compress_in_stream_multi(void)
     {
@@ -536,9 +628,8 @@ public:
         int rc;
         uint64_t nseg = 0, tb = 0;
         if ((rc = starch_segment_count(c, &nseg)) || (rc = starch_text_size(c, &tb))) return rc;
-        std::vector<char> text(tb + 1);
         std::vector<starch_segment> segs(nseg + 1);
-        if ((rc = starch_text_copy(c, &text[0], tb)) || (rc = starch_segments(c, &segs[0], nseg))) return rc;
+        if (nseg && (rc = starch_segments(c, &segs[0], nseg))) return rc;
         for (uint64_t s = 0; s < nseg; ++s) {
             std::string name(segs[s].name_len, '\0');
             uint64_t len = 0;
@@ -552,8 +643,10 @@ public:
             std::free(buffer.tf_buffer);
             buffer.tf_buffer_capacity = segs[s].text_bytes + 1;
             buffer.tf_buffer = static_cast<char*>(std::malloc(buffer.tf_buffer_capacity));
-            // transform-only results carry the text offset in stream_offset
-            std::memcpy(buffer.tf_buffer, &text[segs[s].stream_offset], segs[s].text_bytes);
+            if (!buffer.tf_buffer) return STARCH_ERR_MEM;
+            // the segment's text straight into its tf_buffer (transform-only
+            // results carry the text offset in stream_offset)
+            if ((rc = starch_text_read(c, segs[s].stream_offset, buffer.tf_buffer, segs[s].text_bytes))) return rc;
             buffer.tf_buffer_size = segs[s].text_bytes;
             _closing_name_len = name.size();
             process_tf_buffer(&buffer);
@@ -566,6 +659,9 @@ public:
     // initialize_out_stream wrote and the streams themselves).
     int finish_tf_buffers(void)
     {
+        hook_drain(true);
+        hook_stop();
+        if (_hook_error) return STARCH_ERR_INTERNAL;
         if (_emit_index) {
             std::vector<starch_segment> segs;
             std::vector<const char*> names;
@@ -593,6 +689,164 @@ public:
     }
 
 private:
+    // ---- process_tf_buffer's hand-off, asynchronous ---------------------------
+    // A chromosome handed to process_tf_buffer is compressed by one of four
+    // worker threads, each with its own bz_stream on the patched-libbz2 ABI
+    // (BZ2_bzCompressInit / BZ2_bzCompress(BZ_FINISH) / block_close_functor /
+    // BZ2_bzCompressEnd: the GPU encodes up to four streams at once), while the
+    // caller goes on to the next chromosome; streams are written to the out
+    // stream, and their index entries recorded, strictly in hand-off order.
+    // STARCH_HOOK_SYNC=1: each chromosome through self's own bz_stream at once.
+    struct HookJob {
+        uint64_t seq;
+        std::string chr;
+        int64_t lines;
+        char* text;
+        size_t len;
+        std::unique_ptr<char[]> out;
+        uint64_t out_bytes;
+        unsigned nb, crc;
+        bool closed;                     // block_close_functor ran (BZ_STREAM_END)
+        int rc;
+        bz_stream* z;
+    };
+    std::mutex _hmu;
+    std::condition_variable _hcv;
+    std::deque<HookJob*> _hq;            // waiting for a worker
+    std::map<uint64_t, HookJob*> _hdone; // finished, not yet written
+    std::vector<std::thread> _hworkers;
+    uint64_t _hseq = 0, _hwrite = 0;     // next hand-off / next to write
+    bool _hstop = false;
+
+    static bool hook_sync()
+    {
+        const char* e = std::getenv("STARCH_HOOK_SYNC");
+        return e && !std::strcmp(e, "1");
+    }
+    static void hook_block_close(void* h)   // the worker's stream reached BZ_STREAM_END
+    {
+        HookJob* j = static_cast<HookJob*>(h);
+        starch_bzstream_info(j->z, &j->nb, &j->crc);
+        j->out_bytes = (uint64_t)j->z->total_out_hi32 << 32 | j->z->total_out_lo32;
+        j->closed = true;
+    }
+    void hook_worker()
+    {
+        for (;;) {
+            HookJob* j = NULL;
+            {
+                std::unique_lock<std::mutex> lk(_hmu);
+                while (_hq.empty() && !_hstop) _hcv.wait(lk);
+                if (_hq.empty()) return;
+                j = _hq.front();
+                _hq.pop_front();
+            }
+            bz_stream z;
+            std::memset(&z, 0, sizeof(z));
+            j->z = &z;
+            j->rc = BZ2_bzCompressInit(&z, _block_size, 0, 30);
+            if (j->rc == BZ_OK) {
+                z.handler = j;
+                z.block_close_functor = hook_block_close;
+                // room for the whole stream: one drain (bzip2 grows incompressible text by < 1 %)
+                const size_t cap = j->len + j->len / 64 + (1u << 20);
+                j->out.reset(new char[cap]);
+                z.next_in = j->text;
+                z.avail_in = (unsigned int)j->len;
+                size_t got = 0;
+                int r;
+                do {
+                    const size_t room = std::min<size_t>(cap - got, 0xFFFFFFFFu);
+                    z.next_out = j->out.get() + got;
+                    z.avail_out = (unsigned int)room;
+                    r = BZ2_bzCompress(&z, BZ_FINISH);
+                    got += room - z.avail_out;
+                } while (r == BZ_FINISH_OK && got < cap);
+                j->rc = r == BZ_STREAM_END && j->closed ? BZ_OK : (r < 0 ? r : BZ_SEQUENCE_ERROR);
+                BZ2_bzCompressEnd(&z);
+            }
+            std::free(j->text);
+            j->text = NULL;
+            {
+                std::lock_guard<std::mutex> lk(_hmu);
+                _hdone[j->seq] = j;
+            }
+            _hcv.notify_all();
+        }
+    }
+    // write the finished streams that are next in hand-off order (all: wait
+    // for every stream handed off; else at most `keep` may stay in flight)
+    void hook_drain(bool all, size_t keep = 8)
+    {
+        for (;;) {
+            HookJob* j = NULL;
+            {
+                std::unique_lock<std::mutex> lk(_hmu);
+                const bool must = all ? _hwrite < _hseq : (_hseq - _hwrite > keep);
+                if (must)
+                    while (_hdone.find(_hwrite) == _hdone.end()) _hcv.wait(lk);
+                std::map<uint64_t, HookJob*>::iterator it = _hdone.find(_hwrite);
+                if (it == _hdone.end()) return;
+                j = it->second;
+                _hdone.erase(it);
+                ++_hwrite;
+            }
+            if (j->rc != BZ_OK) {
+                std::fprintf(stderr, "Error: bzip2 compression failed (%d)\n", j->rc);
+                _hook_error = true;
+            } else {
+                if (j->out_bytes && _out_stream) std::fwrite(j->out.get(), 1, j->out_bytes, _out_stream);
+                starch_segment sg;
+                std::memset(&sg, 0, sizeof(sg));
+                sg.line_count = (uint64_t)j->lines;
+                sg.text_bytes = j->len;
+                sg.stream_offset = _stream_end;
+                sg.stream_bytes = j->out_bytes;
+                sg.name_len = j->chr.size();
+                sg.n_blocks = j->nb;
+                sg.combined_crc = j->crc;
+                sg.unit = _closed.size();
+                _stream_end += sg.stream_bytes;
+                _closed.push_back(Closed(j->chr, sg));
+            }
+            delete j;
+        }
+    }
+    void hook_submit(const std::string& chr, int64_t lines, char* text, size_t len)
+    {
+        HookJob* j = new HookJob();
+        j->chr = chr;
+        j->lines = lines;
+        j->text = text;
+        j->len = len;
+        j->out_bytes = 0;
+        j->nb = j->crc = 0;
+        j->closed = false;
+        j->rc = BZ_OK;
+        j->z = NULL;
+        {
+            std::lock_guard<std::mutex> lk(_hmu);
+            j->seq = _hseq++;
+            _hq.push_back(j);
+            if (_hworkers.empty()) {
+                _hstop = false;
+                for (int i = 0; i < 4; ++i) _hworkers.push_back(std::thread(&Starch::hook_worker, this));
+            }
+        }
+        _hcv.notify_all();
+        hook_drain(false);
+    }
+    void hook_stop()
+    {
+        {
+            std::lock_guard<std::mutex> lk(_hmu);
+            _hstop = true;
+        }
+        _hcv.notify_all();
+        for (size_t i = 0; i < _hworkers.size(); ++i) _hworkers[i].join();
+        _hworkers.clear();
+    }
+
     struct Closed {
         std::string chr;
         starch_segment seg;
@@ -669,7 +923,13 @@ inline void Starch::process_tf_buffer(shared_buffer_t* sb)
 {
     if (!sb->tf_buffer) return;
     Starch* s = self;
-    if (s) {
+    if (s && !hook_sync()) {   // the chromosome's text to a worker's bz_stream (it owns the buffer now)
+        const char* chr = sb->tf_state && sb->tf_state->current_chr ? sb->tf_state->current_chr : "";
+        const std::string name(chr, s->_closing_name_len ? s->_closing_name_len : std::strlen(chr));
+        s->_closing_name_len = 0;
+        s->hook_submit(name, sb->tf_state ? sb->tf_state->line_count : 0, sb->tf_buffer, sb->tf_buffer_size);
+        sb->tf_buffer = NULL;
+    } else if (s) {
         if (!s->_bz_stream_ptr || s->_bz_stream_used) {   // one bzip2 stream per chromosome
             s->delete_bz_stream_ptr();
             s->initialize_bz_stream_ptr();

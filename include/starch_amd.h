@@ -267,6 +267,9 @@ int starch_transform_host_init(starch_ctx* ctx, const void* bed, uint64_t n, int
 int starch_transform_device(starch_ctx* ctx, const void* d_bed, uint64_t n);   /* BED bytes in HBM */
 int starch_text_size(starch_ctx* ctx, uint64_t* n);
 int starch_text_copy(starch_ctx* ctx, void* dst, uint64_t cap);
+/* n bytes of that text from offset off (a segment's, at its stream_offset)
+ * into dst: one chromosome's tf_buffer without a copy of the whole text. */
+int starch_text_read(starch_ctx* ctx, uint64_t off, void* dst, uint64_t n);
 
 /* One bzip2 stream (BZ_FINISH semantics) of n bytes; result to host. */
 int starch_bz2_compress_host(starch_ctx* ctx, const void* in, uint64_t n, int block_size_100k, void* out,

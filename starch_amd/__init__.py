@@ -134,6 +134,7 @@ def load():
         "starch_transform_device": ([vp, vp, u64], ctypes.c_int),
         "starch_text_size": ([vp, pu64], ctypes.c_int),
         "starch_text_copy": ([vp, vp, u64], ctypes.c_int),
+        "starch_text_read": ([vp, u64, vp, u64], ctypes.c_int),
         "starch_bz2_compress_host": ([vp, ctypes.c_char_p, u64, ctypes.c_int, vp, u64, pu64], ctypes.c_int),
         "starch_bz2_compress_many_device": ([vp, vp, pu64, pu64, u64, ctypes.c_int, vp, u64, pu64, pu64],
                                             ctypes.c_int),

@@ -25,6 +25,7 @@ struct BwtScratch {            // 40 (+18 with bwt_kmat) bytes per rotation per 
 // slower on cfg2: 25.9 vs 23.7 ms, the extra 18 B/rotation of writes cost more
 // than the gathers they save); the encoder allocates KM0..LS1 only when set
 bool bwt_kmat();
+bool bwt_kgather();
 void launch_bwt(BlockDesc* blocks, uint32_t b0, uint32_t nb, const uint8_t* blkbytes, uint64_t stride,
                 const BwtScratch& scr, unsigned long long* stats, hipStream_t st);
 // v3 (default): batch-wide segmented sort + doubling on ties (bz2_bwt3.hip).

@@ -3105,6 +3105,40 @@ __global__ void __launch_bounds__(256) k3_period(Ctx c)
     }
 }
 
+// round 0 (STARCH_KGATHER): every rotation's key window and last-column
+// symbol next to its SA entry, in SA order (KM0 / LS0), 4 per thread with
+// every gather issued before any is used
+__global__ void __launch_bounds__(256) k3_keys(Ctx c)
+{
+    const uint32_t slot = blockIdx.y;
+    const uint32_t n = c.blocks[c.b0 + slot].n;
+    const uint64_t so = (uint64_t)slot * c.scr.stride;
+    const KeySrc ks = key_src(c, slot, 0);
+    const uint32_t* SA = c.scr.SA + so;
+    uint64_t* KM = c.kA + so;
+    uint8_t* LS = c.lA + so;
+    constexpr uint32_t U = 4;
+    for (uint32_t i0 = blockIdx.x * 256u * U; i0 < n; i0 += gridDim.x * 256u * U) {
+        uint32_t v[U], ls[U];
+        uint64_t k[U];
+#pragma unroll
+        for (uint32_t u = 0; u < U; ++u) {
+            const uint32_t i = i0 + u * 256u + threadIdx.x;
+            v[u] = SA[i < n ? i : 0u];
+        }
+#pragma unroll
+        for (uint32_t u = 0; u < U; ++u) k[u] = ks.key_pss(v[u], ls[u]);
+#pragma unroll
+        for (uint32_t u = 0; u < U; ++u) {
+            const uint32_t i = i0 + u * 256u + threadIdx.x;
+            if (i < n) {
+                KM[i] = k[u];
+                LS[i] = (uint8_t)ls[u];
+            }
+        }
+    }
+}
+
 }  // namespace
 
 // zero the counters whose bits are set (one launch instead of a memset each)
@@ -3115,10 +3149,20 @@ __global__ void k3_zero(uint32_t* __restrict__ ctr, uint64_t mask)
 }
 
 // Host orchestration.  A handful of host round trips per batch (list sizes).
+// STARCH_KGATHER=1: round-0 keys gathered into a position-ordered array by
+// their own pass after the top-level scatter (k3_keys: SA read and key
+// writes coalesced, the PSS gathers at the L2's random-read rate), so the
+// sorts read keys by position; STARCH_KMAT=1: the scatter writes them
+bool bwt_kgather()
+{
+    static const bool on = [] { const char* e = getenv("STARCH_KGATHER"); return e && !strcmp(e, "1"); }();
+    return on;
+}
+
 bool bwt_kmat()
 {
     static const bool on = [] { const char* e = getenv("STARCH_KMAT"); return e && !strcmp(e, "1"); }();
-    return on;
+    return on || bwt_kgather();
 }
 
 bool launch_bwt3(BlockDesc* blocks, uint32_t b0, uint32_t nb, const uint8_t* blkbytes, uint64_t stride,
@@ -3334,9 +3378,12 @@ bool launch_bwt3(BlockDesc* blocks, uint32_t b0, uint32_t nb, const uint8_t* blk
         auto g8 = [](uint32_t x) { return dim3((x + 7) / 8 * 8); };
         // static assignment needs every workgroup resident at once: one wave of
         // workgroups, sized by the kernel's occupancy
-        auto resident = [&](const void* f, int threads = 256) {
+        auto resident = [&](const void* f, int threads = 256, const char* env = nullptr) {
             int per_cu = 0;
             HIP_CHECK(hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, f, threads, 0));
+            const char* e = env ? getenv(env) : nullptr;     // experiments: workgroups per CU
+            if (e && atoi(e) > 0) per_cu = atoi(e);
+            if (getenv("STARCH_BWT_DEBUG")) fprintf(stderr, "[bwt3] resident %s: %d per CU\n", env ? env : "-", per_cu);
             return g8((uint32_t)ncu * (uint32_t)(per_cu > 0 ? per_cu : 1));
         };
         // M classes: k3_sort_lds (MSD digit(s) + compare, LSD fallback); S: k3_sort_grp,
@@ -3366,13 +3413,13 @@ bool launch_bwt3(BlockDesc* blocks, uint32_t b0, uint32_t nb, const uint8_t* blk
 #endif
             constexpr int M2W = STARCH_M_WIDE ? 8 : 4, M2E = STARCH_M_WIDE ? 4 : 8;
             constexpr int M3W = STARCH_M_WIDE ? 16 : 4, M3E = STARCH_M_WIDE ? 4 : 16;
-            static const dim3 gm3 = resident(reinterpret_cast<const void*>(&k3_sort_lds<M3W, M3E, D>), 64 * M3W);
-            static const dim3 gm2 = resident(reinterpret_cast<const void*>(&k3_sort_lds<M2W, M2E, D>), 64 * M2W);
-            static const dim3 gm1 = resident(reinterpret_cast<const void*>(&k3_sort_lds<4, 4, D>));
-            static const dim3 gm0 = resident(reinterpret_cast<const void*>(&k3_sort_lds<4, 2, D>));
-            static const dim3 gs = resident(reinterpret_cast<const void*>(&k3_sort_grp<1, 2, D>));
-            static const dim3 gs2 = resident(reinterpret_cast<const void*>(&k3_sort_grp<1, 4, D>));
-            static const dim3 gw = resident(reinterpret_cast<const void*>(&k3_sort_w<D>));
+            static const dim3 gm3 = resident(reinterpret_cast<const void*>(&k3_sort_lds<M3W, M3E, D>), 64 * M3W, "STARCH_RES_M3");
+            static const dim3 gm2 = resident(reinterpret_cast<const void*>(&k3_sort_lds<M2W, M2E, D>), 64 * M2W, "STARCH_RES_M2");
+            static const dim3 gm1 = resident(reinterpret_cast<const void*>(&k3_sort_lds<4, 4, D>), 256, "STARCH_RES_M1");
+            static const dim3 gm0 = resident(reinterpret_cast<const void*>(&k3_sort_lds<4, 2, D>), 256, "STARCH_RES_M0");
+            static const dim3 gs = resident(reinterpret_cast<const void*>(&k3_sort_grp<1, 2, D>), 256, "STARCH_RES_S");
+            static const dim3 gs2 = resident(reinterpret_cast<const void*>(&k3_sort_grp<1, 4, D>), 256, "STARCH_RES_S2");
+            static const dim3 gw = resident(reinterpret_cast<const void*>(&k3_sort_w<D>), 256, "STARCH_RES_W");
             if (n3) {
                 bin(c.L.m3, n3, bout);
                 hipLaunchKernelGGL((k3_sort_lds<M3W, M3E, D>), gm3, dim3(64 * M3W), 0, st, c, bout, nullptr);
@@ -3437,6 +3484,7 @@ bool launch_bwt3(BlockDesc* blocks, uint32_t b0, uint32_t nb, const uint8_t* blk
     // ---- round 0: packed prefix keys gathered from the PSS by every sort, as
     // the text rounds do (bwt_kmat(): materialised next to SA by the scatter) ----
     static const bool direct = [] { const char* e = getenv("STARCH_SCATTER"); return e && !strcmp(e, "direct"); }();
+    const bool kgather = bwt_kgather() && scr.KM0 && !direct;
     if (bwt_kmat() && scr.KM0 && !direct) {   // (the direct scatter writes SA only)
         c.keysrc = 1;
         c.kA = scr.KM0;
@@ -3464,10 +3512,15 @@ bool launch_bwt3(BlockDesc* blocks, uint32_t b0, uint32_t nb, const uint8_t* blk
         const dim3 gsc((ncu + 7) / 8 * 8);
         if (direct && wide) hipLaunchKernelGGL(k3_scatter<PNB_WIDE>, gsc, dim3(SCT), 0, st, c);
         else if (direct) hipLaunchKernelGGL(k3_scatter<PNB>, gsc, dim3(SCT), 0, st, c);
-        else if (wide && c.lA) hipLaunchKernelGGL((k3_scatter_lds<PNB_WIDE, true>), gsc, dim3(SCT), 0, st, c);
+        else if (wide && c.lA && !kgather) hipLaunchKernelGGL((k3_scatter_lds<PNB_WIDE, true>), gsc, dim3(SCT), 0, st, c);
         else if (wide) hipLaunchKernelGGL((k3_scatter_lds<PNB_WIDE, false>), gsc, dim3(SCT), 0, st, c);
-        else if (c.lA) hipLaunchKernelGGL((k3_scatter_lds<PNB, true>), gsc, dim3(SCT), 0, st, c);
+        else if (c.lA && !kgather) hipLaunchKernelGGL((k3_scatter_lds<PNB, true>), gsc, dim3(SCT), 0, st, c);
         else hipLaunchKernelGGL((k3_scatter_lds<PNB, false>), gsc, dim3(SCT), 0, st, c);
+        if (kgather) {   // keys by position after the scatter (its PSS reads are the key source: keysrc 0 here)
+            Ctx ck = c;
+            ck.keysrc = 0;
+            hipLaunchKernelGGL(k3_keys, dim3(((uint32_t)(scr.stride / 1024) + 7) / 8 * 8 / 2 + 1, nb), dim3(256), 0, st, ck);
+        }
         HIP_CHECK(hipGetLastError());
     }
     sort_groups();

@@ -64,9 +64,9 @@ struct GpuStreamState {
     uint64_t consumed = 0;              // input bytes consumed (total_in)
     // blocks coded ahead
     std::deque<Coded> ahead;
-    std::vector<uint8_t> enc;           // their GPU output
+    RawBytes enc;                       // their GPU output
     // the stream's bits
-    std::vector<uint8_t> output;        // whole bytes from stream offset out_base on
+    RawBytes output;                    // whole bytes from stream offset out_base on
     uint64_t out_base = 0;              // stream offset of output[0] (drained bytes are dropped)
     uint64_t out_pos = 0;               // stream offset of the next byte to drain
     uint64_t released = 0;              // stream bytes [0, released) may be drained (the library's numZ)
@@ -172,7 +172,9 @@ void put_bits(GpuStreamState* g, uint32_t v, uint32_t n)   // n <= 24, MSB first
     g->tail_bits += n;
     while (g->tail_bits >= 8) {
         g->tail_bits -= 8;
-        g->output.push_back((uint8_t)(g->tail >> g->tail_bits));
+        const size_t o = g->output.size();
+        g->output.resize(o + 1);
+        g->output.data()[o] = (uint8_t)(g->tail >> g->tail_bits);
     }
     g->tail &= (1u << g->tail_bits) - 1u;
 }
@@ -189,19 +191,30 @@ void put_stream_bits(GpuStreamState* g, const uint8_t* src, uint64_t bit0, uint6
     }
     const uint64_t whole = (e - b) / 8;
     const uint8_t* p = src + (b >> 3);
+    const size_t o = g->output.size();
+    g->output.resize(o + whole);
+    uint8_t* q = g->output.data() + o;
     if (g->tail_bits == 0) {
-        g->output.insert(g->output.end(), p, p + whole);
-    } else {
+        if (whole) memcpy(q, p, whole);
+    } else {   // shifted by t bits: 8 bytes per step (big-endian words), then bytewise
         const uint32_t t = g->tail_bits;
-        uint32_t acc = g->tail;
-        const size_t o = g->output.size();
-        g->output.resize(o + whole);
-        for (uint64_t i = 0; i < whole; ++i) {
-            acc = (acc << 8) | p[i];
-            g->output[o + i] = (uint8_t)(acc >> t);
-            acc &= (1u << t) - 1u;
+        uint64_t acc = g->tail;                    // t pending bits, right-aligned
+        uint64_t i = 0;
+        for (; i + 8 <= whole; i += 8) {
+            uint64_t w;
+            memcpy(&w, p + i, 8);
+            w = __builtin_bswap64(w);
+            const uint64_t out = (acc << (64 - t)) | (w >> t);
+            acc = w & ((1ull << t) - 1ull);
+            const uint64_t be = __builtin_bswap64(out);
+            memcpy(q + i, &be, 8);
         }
-        g->tail = acc;
+        for (; i < whole; ++i) {
+            acc = (acc << 8) | p[i];
+            q[i] = (uint8_t)(acc >> t);
+            acc &= (1ull << t) - 1ull;
+        }
+        g->tail = (uint32_t)acc;
     }
     b += whole * 8;
     for (; b < e; ++b) put_bits(g, (src[b >> 3] >> (7 - (b & 7))) & 1u, 1);
@@ -284,11 +297,16 @@ void code_text(GpuStreamState* g, const uint8_t* a, uint64_t na, const uint8_t* 
     SlotGuard sg{acquire(dev)};
     Slot* sl = sg.s;
     if (!sl->st) HIP_CHECK(hipStreamCreateWithFlags(&sl->st, hipStreamNonBlocking));
-    uint8_t* h = static_cast<uint8_t*>(sl->stage.get(n + 64));
-    if (na) memcpy(h, a, na);
-    if (nb) memcpy(h + na, b, nb);
     uint8_t* d_in = sl->in.as<uint8_t>(n + 64);
-    HIP_CHECK(hipMemcpyAsync(d_in, h, n, hipMemcpyHostToDevice, sl->st));
+    // a large piece of the caller's input is DMA'd straight from its buffer
+    // (registered for this call); the rest goes through the slot's pinned stage
+    HostRegistration reg(b, nb, 16ull << 20);
+    const uint64_t staged = reg.ok() ? na : n;
+    uint8_t* h = static_cast<uint8_t*>(sl->stage.get(staged + 64));
+    if (na) memcpy(h, a, na);
+    if (nb && !reg.ok()) memcpy(h + na, b, nb);
+    if (staged) HIP_CHECK(hipMemcpyAsync(d_in, h, staged, hipMemcpyHostToDevice, sl->st));
+    if (reg.ok()) HIP_CHECK(hipMemcpyAsync(d_in + na, b, nb, hipMemcpyHostToDevice, sl->st));
     std::vector<bz::StreamIn> pieces(1);
     pieces[0].text_off = 0;
     pieces[0].text_len = n;
@@ -304,7 +322,7 @@ void code_text(GpuStreamState* g, const uint8_t* a, uint64_t na, const uint8_t* 
     sl->enc.block_results(res, sl->st);
     g->enc.resize(outs[0].bytes);
     if (outs[0].bytes) HIP_CHECK(hipMemcpyAsync(g->enc.data(), d_out, outs[0].bytes, hipMemcpyDeviceToHost, sl->st));
-    HIP_CHECK(hipStreamSynchronize(sl->st));
+    HIP_CHECK(hipStreamSynchronize(sl->st));     // (reg's DMA is done before it unregisters)
     for (size_t k = 0; k < res.size(); ++k) {
         const bool fl = closed && k + 1 == res.size();
         g->ahead.push_back(Coded{beg + res[k].in_beg, beg + res[k].in_end, res[k].bit_off, res[k].bits, res[k].crc,
@@ -452,8 +470,11 @@ bool drain(GpuStreamState* g)
         g->out_pos += k;
         add_out(s, k);
     }
-    if (g->out_pos - g->out_base > (1u << 20)) {   // drop the drained prefix
-        g->output.erase(g->output.begin(), g->output.begin() + (std::ptrdiff_t)(g->out_pos - g->out_base));
+    const uint64_t dr = g->out_pos - g->out_base;
+    if (dr > (1u << 20) && 2 * dr > g->output.size()) {   // drop the drained prefix (amortised: at most the kept half moves)
+        const size_t keep = g->output.size() - dr;
+        if (keep) memmove(g->output.data(), g->output.data() + dr, keep);
+        g->output.resize(keep);
         g->out_base = g->out_pos;
     }
     return k > 0;
@@ -558,7 +579,7 @@ int BZ2_bzCompress(bz_stream* strm, int action)
                     if (g->expect > 0 || !empty_rl(g) || g->out_pos < g->released) return BZ_FINISH_OK;
                     g->mode = M_IDLE;
                     g->ahead.clear();
-                    std::vector<uint8_t>().swap(g->enc);
+                    g->enc.release();
                     std::vector<uint8_t>().swap(g->blk);
                     if (strm->block_close_functor) strm->block_close_functor(strm->handler);   // bz:bzlib.c:470
                     return BZ_STREAM_END;

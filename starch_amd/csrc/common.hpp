@@ -2,6 +2,11 @@
 // (gfx950, CDNA4) Starch pipeline.  wave64 throughout; all arithmetic integer.
 #pragma once
 #include <hip/hip_runtime.h>
+
+#include <stdlib.h>
+#include <string.h>
+
+#include <memory>
 #include <stdint.h>
 #include <stdio.h>
 #include <stdlib.h>
@@ -66,6 +71,63 @@ struct PinnedBuf {
     }
     template <class T> T* as(size_t count) { return static_cast<T*>(get(count * sizeof(T))); }
     ~PinnedBuf() { if (p) (void)hipHostFree(p); }
+};
+
+// Host memory the runtime can DMA from directly for the duration of one call
+// (an mmap'ed file, a caller's buffer): registering a page-cached 2.4 GB
+// mapping took ~28 ms and its copies then ran at the pinned rate
+// (tools/probes/h2d_file_probe.cpp), against ~0.2 s per GB to pin fresh memory
+// or ~0.1 s per GB to copy through a staging buffer.  Page-rounded; read-only
+// unless `writable`.  If the runtime refuses (already pinned or registered,
+// ...) nothing happens and the copies go as before.  STARCH_REGISTER=0: off.
+struct HostRegistration {
+    void* base = nullptr;
+    HostRegistration(const void* p, uint64_t n, uint64_t min_bytes, bool writable = false)
+    {
+        if (!p || n < min_bytes) return;
+        static const bool off = [] { const char* e = getenv("STARCH_REGISTER"); return e && !strcmp(e, "0"); }();
+        if (off) return;
+        hipPointerAttribute_t a;
+        if (hipPointerGetAttributes(&a, p) == hipSuccess && a.type == hipMemoryTypeHost) return;   // pinned already
+        (void)hipGetLastError();
+        const uintptr_t pg = 4096, lo = reinterpret_cast<uintptr_t>(p) & ~(pg - 1),
+                        hi = (reinterpret_cast<uintptr_t>(p) + n + pg - 1) & ~(pg - 1);
+        if (hipHostRegister(reinterpret_cast<void*>(lo), hi - lo, writable ? hipHostRegisterDefault
+                                                                          : hipHostRegisterReadOnly) == hipSuccess)
+            base = reinterpret_cast<void*>(lo);
+        else
+            (void)hipGetLastError();
+    }
+    ~HostRegistration()
+    {
+        if (base) (void)hipHostUnregister(base);
+    }
+    bool ok() const { return base != nullptr; }
+    HostRegistration(const HostRegistration&) = delete;
+    HostRegistration& operator=(const HostRegistration&) = delete;
+};
+
+// A growable host byte buffer that is never zero-filled (std::vector's
+// resize zero-fills: ~0.1 s per GB of output that is then overwritten).
+struct RawBytes {
+    std::unique_ptr<uint8_t[]> p;
+    size_t n = 0, cap = 0;
+    void resize(size_t k)                       // contents up to min(n, k) kept
+    {
+        if (k > cap) {
+            const size_t c = k + k / 2 + 4096;
+            std::unique_ptr<uint8_t[]> q(new uint8_t[c]);
+            if (n) memcpy(q.get(), p.get(), n < k ? n : k);
+            p.swap(q);
+            cap = c;
+        }
+        n = k;
+    }
+    uint8_t* data() { return p.get(); }
+    const uint8_t* data() const { return p.get(); }
+    size_t size() const { return n; }
+    void clear() { n = 0; }
+    void release() { p.reset(); n = cap = 0; }
 };
 
 // ---------------------------------------------------------------------------

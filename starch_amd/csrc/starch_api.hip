@@ -471,35 +471,6 @@ bool host_is_pinned(const void* p)
     return a.type == hipMemoryTypeHost;
 }
 
-// A large pageable input (e.g. an mmap'ed file) is registered with the HIP
-// runtime for the duration of one call, so the pipelined path's batches cross
-// PCIe by DMA straight from it: registering a page-cached 2.4 GB file took
-// ~28 ms and its copy then ran at the pinned rate (tools/probes/
-// h2d_file_probe.cpp), against ~0.2 s per GB to pin fresh memory.  Page-
-// rounded, read-only; if the runtime refuses (part of the range already
-// registered, ...) the call runs as before.
-struct HostRegistration {
-    void* base = nullptr;
-    HostRegistration(const void* p, uint64_t n)
-    {
-        if (!p || n < (256ull << 20) || host_is_pinned(p)) return;
-        static const bool off = [] { const char* e = getenv("STARCH_REGISTER"); return e && !strcmp(e, "0"); }();
-        if (off) return;
-        const uintptr_t pg = 4096, a = reinterpret_cast<uintptr_t>(p) & ~(pg - 1),
-                        e = (reinterpret_cast<uintptr_t>(p) + n + pg - 1) & ~(pg - 1);
-        if (hipHostRegister(reinterpret_cast<void*>(a), e - a, hipHostRegisterReadOnly) == hipSuccess)
-            base = reinterpret_cast<void*>(a);
-        else
-            (void)hipGetLastError();
-    }
-    ~HostRegistration()
-    {
-        if (base) (void)hipHostUnregister(base);
-    }
-    HostRegistration(const HostRegistration&) = delete;
-    HostRegistration& operator=(const HostRegistration&) = delete;
-};
-
 struct LaneBatch {
     int lane = 0;
     uint64_t coll_off = 0, bytes = 0;
@@ -1549,7 +1520,7 @@ int starch_encode_host(starch_ctx* c, const void* bed, uint64_t n, const starch_
     // large pinned inputs: PCIe copy of the next batch overlaps the encode
     // (STARCH_PIPELINE=0 turns it off; pageable memory has no async copy)
     static const bool pipe_off = [] { const char* e = getenv("STARCH_PIPELINE"); return e && !strcmp(e, "0"); }();
-    HostRegistration reg(pipe_off || o.reference_compat ? nullptr : bed, n);
+    HostRegistration reg(pipe_off || o.reference_compat ? nullptr : bed, n, 256ull << 20);
     if (!pipe_off && !o.reference_compat && n >= (256ull << 20) && host_is_pinned(bed) &&
         encode_host_pipelined(c, static_cast<const uint8_t*>(bed), n, o))
         return STARCH_OK;
@@ -1583,7 +1554,7 @@ int starch_encode_host_into(starch_ctx* c, const void* bed, uint64_t n, const st
     if (o.block_size_100k < 1 || o.block_size_100k > 9 ||
         (o.compression_method != STARCH_METHOD_BZIP2 && o.compression_method != STARCH_METHOD_GZIP)) return STARCH_ERR_ARG;
     static const bool pipe_off = [] { const char* e = getenv("STARCH_PIPELINE"); return e && !strcmp(e, "0"); }();
-    HostRegistration reg(pipe_off || o.reference_compat ? nullptr : bed, n);
+    HostRegistration reg(pipe_off || o.reference_compat ? nullptr : bed, n, 256ull << 20);
     if (!pipe_off && !o.reference_compat && n >= (256ull << 20) && host_is_pinned(bed) &&
         encode_host_pipelined(c, static_cast<const uint8_t*>(bed), n, o, static_cast<uint8_t*>(out), cap, out_len))
         return STARCH_OK;
@@ -1882,6 +1853,17 @@ int starch_text_copy(starch_ctx* c, void* dst, uint64_t cap)
     if (!c->have) return STARCH_ERR_STATE;
     if (cap < c->text_bytes) return STARCH_ERR_MEM;
     if (c->text_bytes) HIP_CHECK(hipMemcpyAsync(dst, c->text_dev, c->text_bytes, hipMemcpyDeviceToHost, c->st));
+    HIP_CHECK(hipStreamSynchronize(c->st));
+    return STARCH_OK;
+    END_GUARD(c)
+}
+
+int starch_text_read(starch_ctx* c, uint64_t off, void* dst, uint64_t n)
+{
+    GUARD(c)
+    if (!c->have) return STARCH_ERR_STATE;
+    if (off > c->text_bytes || n > c->text_bytes - off || (n && !dst)) return STARCH_ERR_ARG;
+    if (n) HIP_CHECK(hipMemcpyAsync(dst, c->text_dev + off, n, hipMemcpyDeviceToHost, c->st));
     HIP_CHECK(hipStreamSynchronize(c->st));
     return STARCH_OK;
     END_GUARD(c)
