@@ -42,10 +42,13 @@
 #define STARCH3_AMD_HPP_
 
 #include <pthread.h>
+#include <sys/mman.h>
 #include <sys/stat.h>
 #include <unistd.h>
 
+#include <algorithm>
 #include <cerrno>
+#include <chrono>
 #include <cinttypes>
 #include <cstdio>
 #include <cstdlib>
@@ -148,6 +151,7 @@ public:
         hook_stop();
         delete_bz_stream_ptr();
         delete_out_compression_stream();
+        text_pool_clear();
         std::free(buffer.tf_buffer);
         std::free(_tf_state.current_chr);
         std::free(_tf_state.last_chr);
@@ -253,7 +257,10 @@ public:
     {
         switch (get_compression_method()) {
         case k_bzip2:
-            open_devices();
+            // the device contexts open on a thread of their own (HIP start-up,
+            // ~0.1-0.2 s) while the caller goes on to read its input; the
+            // first call that needs them waits (open_devices)
+            if (_ctx.empty() && !_opener.joinable()) _opener = std::thread([this]() { _open_rc = open_devices_now(); });
             break;
         case k_gzip:
             std::fprintf(stderr, "Error: This method is unsupported at this time\n");
@@ -265,6 +272,7 @@ public:
     }
     void delete_out_compression_stream(void)
     {
+        if (_opener.joinable()) _opener.join();
         for (size_t i = 0; i < _ctx.size(); ++i) starch_destroy(_ctx[i]);
         _ctx.clear();
     }
@@ -302,7 +310,11 @@ public:
     void set_emit_index(bool on) { _emit_index = on; }
     // per-segment base_count_unique / base_count_nonunique (hpp:61-62) in the index
     void set_base_counts(bool on) { _base_counts = on; }
-    starch_ctx* context(void) { return _ctx.empty() ? NULL : _ctx[0]; }
+    starch_ctx* context(void)
+    {
+        if (_opener.joinable()) _opener.join();
+        return _ctx.empty() ? NULL : _ctx[0];
+    }
 
     // ---- the hot path -------------------------------------------------------
     // In-memory: BED bytes -> the whole archive (magic included).  Returns a
@@ -371,18 +383,24 @@ public:
     // current before it (hpp:306-307).  A run longer than a batch is held
     // whole.  At EOF, or at a 0xFF (which reads as EOF, hpp:181), every run
     // goes.  Returns the first nonzero status of f.
+    struct FileReader;
     template <class F>
     int for_each_run_batch(uint64_t batch, F f)
     {
         const char* eb = std::getenv("STARCH_HPP_BATCH");   // tests: small batches
         if (eb && std::atoll(eb) > 0) batch = (uint64_t)std::atoll(eb);
+        FileReader rd(_in_stream);
+        {
+            bool done = false;
+            const int rc = mapped_batches(rd, batch, f, done);
+            if (rc || done) return rc;
+        }
         InBuf buf;
         std::vector<starch_unit> units(4096);
         int64_t is = 0, ip = 0;
         bool eof = false;
         uint64_t want = batch;
         uint64_t scanned = 0;      // bytes of buf known to hold no newline after the last complete line
-        FileReader rd(_in_stream);
         for (;;) {
             while (!eof && buf.size() < want) {
                 const size_t o = buf.size();
@@ -418,6 +436,46 @@ public:
             scanned = 0;
             want = batch;
         }
+    }
+
+    // for_each_run_batch over a regular file of >= 64 MiB that ends at its
+    // st_size: the file is mapped, its runs planned in one pass (the library's
+    // 0xFF scan runs on 16 threads and faults the mapping in) and handed to f
+    // in batches straight from the mapping -- no read copies, and the library
+    // DMAs each batch from the page cache.  done = false: not taken (pipe,
+    // small or growing file, STARCH_HPP_MAP=0), the caller reads instead.
+    template <class F>
+    int mapped_batches(FileReader& rd, uint64_t batch, F& f, bool& done)
+    {
+        done = false;
+        const char* e = std::getenv("STARCH_HPP_MAP");
+        if (!rd.regular() || (e && !std::strcmp(e, "0"))) return STARCH_OK;
+        struct stat st;
+        if (fstat(rd.fd, &st) != 0 || (uint64_t)st.st_size < rd.off + (64ull << 20)) return STARCH_OK;
+        unsigned char x;
+        if (pread(rd.fd, &x, 1, st.st_size) != 0) return STARCH_OK;   // more than st_size: read it instead
+        const uint64_t pg = (uint64_t)sysconf(_SC_PAGESIZE), mo = rd.off & ~(pg - 1);
+        const uint64_t len = (uint64_t)st.st_size - mo, n = (uint64_t)st.st_size - rd.off;
+        void* m = mmap(NULL, len, PROT_READ, MAP_PRIVATE, rd.fd, (off_t)mo);
+        if (m == MAP_FAILED) return STARCH_OK;
+        const unsigned char* base = static_cast<const unsigned char*>(m) + (rd.off - mo);
+        std::vector<starch_unit> units(1u << 16);
+        uint64_t nu = 0;
+        int rc = starch_plan_units_from(base, n, units.size(), 0, 0, &units[0], &nu);
+        // the whole mapping page-locked once (~12 ms per GB of page-cached
+        // file), so every batch's copy runs by DMA
+        const bool reg = !rc && starch_host_register(m, (len + pg - 1) & ~(pg - 1)) == STARCH_OK;
+        for (uint64_t k = 0; !rc && k < nu;) {   // batches of whole runs, >= batch bytes each
+            uint64_t j = k, b = 0;
+            while (j < nu && (j == k || b < batch)) b += units[j++].length;
+            rc = f(base, &units[k], j - k);
+            k = j;
+        }
+        if (reg) (void)starch_host_unregister(m);
+        munmap(m, len);
+        rd.off = (uint64_t)st.st_size;   // (a 0xFF ends the input there: nothing after it is read)
+        done = true;
+        return rc;
     }
 
     // the in stream's bytes, read with 16 pread(2) threads when it is a
@@ -611,12 +669,19 @@ public:
     // every chromosome segment is handed to process_tf_buffer in input order.
     int transform_and_flush_in_stream(void)
     {
-        int rc = open_devices();
-        if (rc) return rc;
-        starch_ctx* c = _ctx[0];
+        _tr.t0 = _tr.last = Trace::now();
+        starch_ctx* c = NULL;   // (the devices may still be opening while the first batch is read)
         return for_each_run_batch(256ull << 20, [&](const unsigned char* bed, const starch_unit* u, uint64_t n) -> int {
             const uint64_t beg = u[0].offset, len = u[n - 1].offset + u[n - 1].length - beg;
+            _tr.lap(_tr.read);
+            if (!c) {
+                const int r = open_devices();
+                if (r) return r;
+                c = _ctx[0];
+                _tr.lap(_tr.open);
+            }
             int r = starch_transform_host_init(c, bed + beg, len, u[0].init_start, u[0].init_stop);
+            _tr.lap(_tr.tf);
             if (r) return r;
             return flush_transformed(c);
         });
@@ -640,16 +705,18 @@ public:
             std::memcpy(_tf_state.current_chr, name.data(), name.size());
             _tf_state.current_chr[name.size()] = '\0';
             _tf_state.line_count = (int64_t)segs[s].line_count;
-            std::free(buffer.tf_buffer);
+            if (!text_pool_put(buffer.tf_buffer)) std::free(buffer.tf_buffer);
             buffer.tf_buffer_capacity = segs[s].text_bytes + 1;
-            buffer.tf_buffer = static_cast<char*>(std::malloc(buffer.tf_buffer_capacity));
+            buffer.tf_buffer = text_pool_get(buffer.tf_buffer_capacity);
             if (!buffer.tf_buffer) return STARCH_ERR_MEM;
             // the segment's text straight into its tf_buffer (transform-only
             // results carry the text offset in stream_offset)
             if ((rc = starch_text_read(c, segs[s].stream_offset, buffer.tf_buffer, segs[s].text_bytes))) return rc;
             buffer.tf_buffer_size = segs[s].text_bytes;
             _closing_name_len = name.size();
+            _tr.lap(_tr.text);
             process_tf_buffer(&buffer);
+            _tr.lap(_tr.hand);
             if (_hook_error) return STARCH_ERR_INTERNAL;
         }
         return STARCH_OK;
@@ -659,8 +726,11 @@ public:
     // initialize_out_stream wrote and the streams themselves).
     int finish_tf_buffers(void)
     {
+        _tr.last = Trace::now();
         hook_drain(true);
         hook_stop();
+        _tr.lap(_tr.drain);
+        _tr.report();
         if (_hook_error) return STARCH_ERR_INTERNAL;
         if (_emit_index) {
             std::vector<starch_segment> segs;
@@ -755,6 +825,7 @@ private:
                 z.avail_in = (unsigned int)j->len;
                 size_t got = 0;
                 int r;
+                const double tb = Trace::now();
                 do {
                     const size_t room = std::min<size_t>(cap - got, 0xFFFFFFFFu);
                     z.next_out = j->out.get() + got;
@@ -762,10 +833,14 @@ private:
                     r = BZ2_bzCompress(&z, BZ_FINISH);
                     got += room - z.avail_out;
                 } while (r == BZ_FINISH_OK && got < cap);
+                {
+                    std::lock_guard<std::mutex> lk(_tr.mu);
+                    _tr.bz += Trace::now() - tb;
+                }
                 j->rc = r == BZ_STREAM_END && j->closed ? BZ_OK : (r < 0 ? r : BZ_SEQUENCE_ERROR);
                 BZ2_bzCompressEnd(&z);
             }
-            std::free(j->text);
+            if (!text_pool_put(j->text)) std::free(j->text);
             j->text = NULL;
             {
                 std::lock_guard<std::mutex> lk(_hmu);
@@ -847,6 +922,30 @@ private:
         _hworkers.clear();
     }
 
+    // STARCH_HOOK_TRACE=1: where transform_and_flush_in_stream's time goes (stderr)
+    struct Trace {
+        double t0 = 0, last = 0, open = 0, read = 0, tf = 0, text = 0, hand = 0, drain = 0, bz = 0;
+        std::mutex mu;
+        static double now()
+        {
+            return std::chrono::duration<double>(std::chrono::steady_clock::now().time_since_epoch()).count();
+        }
+        void lap(double& acc)
+        {
+            const double t = now();
+            acc += t - last;
+            last = t;
+        }
+        void report()
+        {
+            const char* e = std::getenv("STARCH_HOOK_TRACE");
+            if (!e || std::strcmp(e, "1")) return;
+            std::fprintf(stderr, "hook trace: total %.1f ms  device open wait %.1f  read+plan %.1f  transform %.1f  text %.1f"
+                         "  hand-off %.1f  final drain %.1f  (workers: bzCompress %.1f)\n", (now() - t0) * 1e3, open * 1e3, read * 1e3, tf * 1e3,
+                         text * 1e3, hand * 1e3, drain * 1e3, bz * 1e3);
+        }
+    } _tr;
+
     struct Closed {
         std::string chr;
         starch_segment seg;
@@ -869,12 +968,21 @@ private:
 
     int open_devices(void)
     {
+        if (_opener.joinable()) {
+            _opener.join();
+            if (_open_rc) return _open_rc;
+        }
+        return open_devices_now();
+    }
+    int open_devices_now(void)
+    {
         if (!_ctx.empty()) return STARCH_OK;
         for (size_t i = 0; i < _devices.size(); ++i) {
             starch_ctx* c = NULL;
             int rc = starch_create(_devices[i], &c);
             if (rc) {
-                delete_out_compression_stream();
+                for (size_t k = 0; k < _ctx.size(); ++k) starch_destroy(_ctx[k]);
+                _ctx.clear();
                 return rc;
             }
             _ctx.push_back(c);
@@ -915,6 +1023,59 @@ private:
     uint64_t _closing_text = 0;
     size_t _closing_name_len = 0;
     bool _hook_error = false;
+    std::thread _opener;
+    int _open_rc = STARCH_OK;
+    // tf_buffers of flush_transformed: page-aligned, page-locked once
+    // (starch_host_register) and reused, so starch_text_read and the
+    // bz_stream's input copy run by DMA (fresh malloc'ed text ran at ~6 GB/s)
+    struct PoolBuf {
+        char* p;
+        size_t cap;
+        bool free_, reg;
+    };
+    std::mutex _pmu;
+    std::vector<PoolBuf> _pool;
+    char* text_pool_get(size_t n)
+    {
+        std::lock_guard<std::mutex> lk(_pmu);
+        size_t best = _pool.size();
+        for (size_t i = 0; i < _pool.size(); ++i)
+            if (_pool[i].free_ && _pool[i].cap >= n && (best == _pool.size() || _pool[i].cap < _pool[best].cap)) best = i;
+        if (best < _pool.size()) {
+            _pool[best].free_ = false;
+            return _pool[best].p;
+        }
+        const size_t cap = (std::max<size_t>(n, 1) + (1u << 20) - 1) & ~(size_t)((1u << 20) - 1);
+        void* q = NULL;
+        if (posix_memalign(&q, 4096, cap)) return NULL;
+        PoolBuf b;
+        b.p = static_cast<char*>(q);
+        b.cap = cap;
+        b.free_ = false;
+        b.reg = cap >= (4u << 20) && starch_host_register(q, cap) == STARCH_OK;
+        _pool.push_back(b);
+        return b.p;
+    }
+    // back to the pool (true), or not a pool buffer (false)
+    bool text_pool_put(char* p)
+    {
+        std::lock_guard<std::mutex> lk(_pmu);
+        for (size_t i = 0; i < _pool.size(); ++i)
+            if (_pool[i].p == p) {
+                _pool[i].free_ = true;
+                return true;
+            }
+        return false;
+    }
+    void text_pool_clear()
+    {
+        std::lock_guard<std::mutex> lk(_pmu);
+        for (size_t i = 0; i < _pool.size(); ++i) {
+            if (_pool[i].reg) (void)starch_host_unregister(_pool[i].p);
+            std::free(_pool[i].p);
+        }
+        _pool.clear();
+    }
 };
 
 extern Starch* self;   // hpp:921; the program defines it (cpp:10)
@@ -959,7 +1120,7 @@ inline void Starch::process_tf_buffer(shared_buffer_t* sb)
         }
     }
     reset_transformation_state(&sb->tf_state);   // hpp:396-405
-    std::free(sb->tf_buffer);
+    if (!s || !s->text_pool_put(sb->tf_buffer)) std::free(sb->tf_buffer);
     sb->tf_buffer = static_cast<char*>(std::calloc(tf_buffer_initial_length, sizeof(*sb->tf_buffer)));
     if (!sb->tf_buffer) {
         std::fprintf(stderr, "Error: Not enough memory for shared_buffer_t transformation buffer\n");

@@ -223,6 +223,16 @@ int starch_gather_host(const starch_host_comm* comm, const starch_segment* segs,
                        const uint64_t* name_lens, uint64_t nseg, const void* streams, const starch_options* opt,
                        void** archive, uint64_t* len);
 void starch_free(void* p);
+/* Page-lock [p, p + n) of caller memory (its whole pages) for the process,
+ * so copies to and from it (starch_encode_host*, starch_transform_host*,
+ * starch_text_read, the bzlib ABI's BZ2_bzCompress input) run by DMA at the
+ * PCIe rate; a buffer reused across calls pays the pinning once (~0.03 s per
+ * GB for memory already touched).  starch_host_unregister(p) with the same p
+ * before the memory is freed (a read-only mapping is registered for reads
+ * only: copies from it).  No counterpart in the reference (it has no
+ * device copies); the hpp's process_tf_buffer pool uses them. */
+int starch_host_register(const void* p, uint64_t n);
+int starch_host_unregister(const void* p);
 
 /* Streaming ingestion (replaces the reference's line-at-a-time
  * produce_line / consume_line hand-off, include/starch3api.hpp:158-345, and

@@ -2526,6 +2526,9 @@ k3_sort_lds(Ctx c, const uint64_t* __restrict__ items,
 #ifndef STARCH_HARD_Q
 #define STARCH_HARD_Q 32
 #endif
+#ifndef STARCH_GRP_EARLY
+#define STARCH_GRP_EARLY 1   // the next group's key gathers issued before this group's sort
+#endif
 constexpr uint32_t HARD_Q = STARCH_HARD_Q;
 
 
@@ -2624,6 +2627,13 @@ k3_sort_grp(Ctx c, const uint64_t* __restrict__ items,
             k[e] = ~0ull;                              // pads: max key, last in order
         }
     }
+#if STARCH_GRP_EARLY
+    // the next group's key gathers go out now, so they are in flight during
+    // this group's LDS-only sort phases (issued after the sort, the emit's
+    // returning atomics and the queue pops waited for them at once: every
+    // vmcnt wait is in issue order)
+    grp_load_keys<NW, E, DBL>(c, nxt, wid, lane);
+#endif
     diff = wave_reduce_or64(diff);
     if constexpr (NW > 1) {
         if (lane == 0) red_all[wave] = diff;
@@ -2714,8 +2724,10 @@ k3_sort_grp(Ctx c, const uint64_t* __restrict__ items,
     }
     SPROF(t3);
     SPACC(2, t1, t3);
+#if !STARCH_GRP_EARLY
     // next group's keys (its rotations were loaded one or two groups ago), a new item
     grp_load_keys<NW, E, DBL>(c, nxt, wid, lane);
+#endif
     SPROF(t4);
     SPACC(3, t3, t4);
 #if STARCH_GRP_DEEP

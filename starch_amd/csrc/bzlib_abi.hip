@@ -306,7 +306,7 @@ void code_text(GpuStreamState* g, const uint8_t* a, uint64_t na, const uint8_t* 
     if (na) memcpy(h, a, na);
     if (nb && !reg.ok()) memcpy(h + na, b, nb);
     if (staged) HIP_CHECK(hipMemcpyAsync(d_in, h, staged, hipMemcpyHostToDevice, sl->st));
-    if (reg.ok()) HIP_CHECK(hipMemcpyAsync(d_in + na, b, nb, hipMemcpyHostToDevice, sl->st));
+    if (reg.ok()) reg.h2d(d_in + na, b, nb, sl->st);
     std::vector<bz::StreamIn> pieces(1);
     pieces[0].text_off = 0;
     pieces[0].text_len = n;

@@ -77,32 +77,75 @@ struct PinnedBuf {
 // (an mmap'ed file, a caller's buffer): registering a page-cached 2.4 GB
 // mapping took ~28 ms and its copies then ran at the pinned rate
 // (tools/probes/h2d_file_probe.cpp), against ~0.2 s per GB to pin fresh memory
-// or ~0.1 s per GB to copy through a staging buffer.  Page-rounded; read-only
-// unless `writable`.  If the runtime refuses (already pinned or registered,
-// ...) nothing happens and the copies go as before.  STARCH_REGISTER=0: off.
+// or ~0.1 s per GB to copy through a staging buffer.  Only the whole pages
+// inside [p, p + n) are registered -- a page shared with a neighbouring
+// allocation (malloc'ed buffers next to each other) stays as it was, so
+// another thread's copies into that neighbour are not disturbed (a
+// page-rounded registration made them fail with "invalid argument").  Copies
+// go through h2d(): the registered middle by DMA, the partial pages around it
+// as pageable copies.  Read-only.  If the runtime refuses (already pinned or
+// registered, ...) nothing is registered.  STARCH_REGISTER=0: off.
 struct HostRegistration {
     void* base = nullptr;
-    HostRegistration(const void* p, uint64_t n, uint64_t min_bytes, bool writable = false)
+    uintptr_t lo = 0, hi = 0;                  // the registered pages [lo, hi)
+    HostRegistration(const void* p, uint64_t n, uint64_t min_bytes)
     {
         if (!p || n < min_bytes) return;
         static const bool off = [] { const char* e = getenv("STARCH_REGISTER"); return e && !strcmp(e, "0"); }();
         if (off) return;
         hipPointerAttribute_t a;
-        if (hipPointerGetAttributes(&a, p) == hipSuccess && a.type == hipMemoryTypeHost) return;   // pinned already
-        (void)hipGetLastError();
-        const uintptr_t pg = 4096, lo = reinterpret_cast<uintptr_t>(p) & ~(pg - 1),
-                        hi = (reinterpret_cast<uintptr_t>(p) + n + pg - 1) & ~(pg - 1);
-        if (hipHostRegister(reinterpret_cast<void*>(lo), hi - lo, writable ? hipHostRegisterDefault
-                                                                          : hipHostRegisterReadOnly) == hipSuccess)
-            base = reinterpret_cast<void*>(lo);
-        else
+        auto pinned = [&a](uintptr_t q) {
+            const bool y = hipPointerGetAttributes(&a, reinterpret_cast<void*>(q)) == hipSuccess &&
+                           a.type == hipMemoryTypeHost;
             (void)hipGetLastError();
+            return y;
+        };
+        const uintptr_t b0 = reinterpret_cast<uintptr_t>(p);
+        if (pinned(b0)) {   // pinned by the caller: DMA from it, up to where its pinning ends
+            uintptr_t h = b0 + n;
+            if (!pinned(h - 1)) {   // (a copy that starts in pinned memory must not run past it)
+                uintptr_t g = b0 & ~(uintptr_t)4095, e = (h - 1) & ~(uintptr_t)4095;   // page g pinned, page e not
+                while (e - g > 4096) {
+                    const uintptr_t m = g + ((e - g) / 2 & ~(uintptr_t)4095);
+                    if (pinned(m)) g = m; else e = m;
+                }
+                h = e;
+            }
+            lo = b0;
+            hi = h;
+            return;
+        }
+        (void)hipGetLastError();
+        const uintptr_t pg = 4096, b = reinterpret_cast<uintptr_t>(p);
+        const uintptr_t l = (b + pg - 1) & ~(pg - 1), h = (b + n) & ~(pg - 1);
+        if (h <= l || h - l < min_bytes / 2) return;
+        if (hipHostRegister(reinterpret_cast<void*>(l), h - l, hipHostRegisterReadOnly) == hipSuccess) {
+            base = reinterpret_cast<void*>(l);
+            lo = l;
+            hi = h;
+        } else {
+            (void)hipGetLastError();
+        }
     }
     ~HostRegistration()
     {
         if (base) (void)hipHostUnregister(base);
     }
-    bool ok() const { return base != nullptr; }
+    bool ok() const { return hi > lo; }   // (registered here, or pinned by the caller)
+    // host [src, src + n) -> dst on stream st, splitting around the registered pages
+    void h2d(void* dst, const void* src, uint64_t n, hipStream_t st) const
+    {
+        uint8_t* d = static_cast<uint8_t*>(dst);
+        const uintptr_t s = reinterpret_cast<uintptr_t>(src), e = s + n;
+        if (hi <= lo || e <= lo || s >= hi) {
+            if (n) HIP_CHECK(hipMemcpyAsync(d, src, n, hipMemcpyHostToDevice, st));
+            return;
+        }
+        const uintptr_t a = s > lo ? s : lo, b = e < hi ? e : hi;
+        if (a > s) HIP_CHECK(hipMemcpyAsync(d, src, a - s, hipMemcpyHostToDevice, st));
+        HIP_CHECK(hipMemcpyAsync(d + (a - s), reinterpret_cast<const void*>(a), b - a, hipMemcpyHostToDevice, st));
+        if (e > b) HIP_CHECK(hipMemcpyAsync(d + (b - s), reinterpret_cast<const void*>(b), e - b, hipMemcpyHostToDevice, st));
+    }
     HostRegistration(const HostRegistration&) = delete;
     HostRegistration& operator=(const HostRegistration&) = delete;
 };

@@ -22,6 +22,7 @@
 #include <string.h>
 
 #include <algorithm>
+#include <thread>
 #include <vector>
 
 #include "shard.hpp"
@@ -117,8 +118,25 @@ void parse_line(const uint8_t* b, uint64_t ls, uint64_t le, int64_t* start, bool
 
 uint64_t input_limit(const uint8_t* b, uint64_t n)
 {
-    const void* ff = memchr(b, 0xFF, n);   // 0xFF reads as EOF (hpp:181)
-    return ff ? (uint64_t)(static_cast<const uint8_t*>(ff) - b) : n;
+    // 0xFF reads as EOF (hpp:181).  Large inputs: 16 threads scan a slice each
+    // (one memchr stream runs at ~10 GB/s, and over a freshly mapped file it
+    // also takes every page fault on one core)
+    const int nt = n >= (64ull << 20) ? 16 : 1;
+    if (nt == 1) {
+        const void* ff = memchr(b, 0xFF, n);
+        return ff ? (uint64_t)(static_cast<const uint8_t*>(ff) - b) : n;
+    }
+    const uint64_t per = (n + nt - 1) / nt;
+    std::vector<uint64_t> at(nt, n);
+    std::vector<std::thread> th;
+    for (int t = 0; t < nt; ++t)
+        th.emplace_back([&, t]() {
+            const uint64_t lo = std::min(n, (uint64_t)t * per), hi = std::min(n, lo + per);
+            const void* ff = hi > lo ? memchr(b + lo, 0xFF, hi - lo) : nullptr;
+            if (ff) at[t] = (uint64_t)(static_cast<const uint8_t*>(ff) - b);
+        });
+    for (auto& x : th) x.join();
+    return *std::min_element(at.begin(), at.end());
 }
 
 void plan_units(const uint8_t* b, uint64_t n, uint64_t max_units, std::vector<Unit>& out, int64_t init_start0,

@@ -586,7 +586,8 @@ void run_lane(starch_ctx* L, const uint8_t* d_in, const std::vector<shard::Unit>
 }
 
 bool encode_host_pipelined(starch_ctx* c, const uint8_t* bed, uint64_t n, const starch_options& opt,
-                           uint8_t* hout_p = nullptr, uint64_t hout_cap = 0, uint64_t* hout_len = nullptr)
+                           const HostRegistration& reg_in, uint8_t* hout_p = nullptr, uint64_t hout_cap = 0,
+                           uint64_t* hout_len = nullptr)
 {
     using clk = std::chrono::steady_clock;
     const auto t0 = clk::now();
@@ -640,7 +641,7 @@ bool encode_host_pipelined(starch_ctx* c, const uint8_t* bed, uint64_t n, const 
         for (size_t k = 0; k < batches.size(); ++k) {
             const uint64_t o = plan[batches[k].first].offset;
             const uint64_t e = batches[k].second < plan.size() ? plan[batches[k].second].offset : n;
-            if (e > o) HIP_CHECK(hipMemcpyAsync(d_in + o, bed + o, e - o, hipMemcpyHostToDevice, c->cst));
+            if (e > o) reg_in.h2d(d_in + o, bed + o, e - o, c->cst);
             HIP_CHECK(hipEventRecord(ev[k], c->cst));
         }
     } catch (...) {
@@ -1521,11 +1522,11 @@ int starch_encode_host(starch_ctx* c, const void* bed, uint64_t n, const starch_
     // (STARCH_PIPELINE=0 turns it off; pageable memory has no async copy)
     static const bool pipe_off = [] { const char* e = getenv("STARCH_PIPELINE"); return e && !strcmp(e, "0"); }();
     HostRegistration reg(pipe_off || o.reference_compat ? nullptr : bed, n, 256ull << 20);
-    if (!pipe_off && !o.reference_compat && n >= (256ull << 20) && host_is_pinned(bed) &&
-        encode_host_pipelined(c, static_cast<const uint8_t*>(bed), n, o))
+    if (!pipe_off && !o.reference_compat && n >= (256ull << 20) && (reg.ok() || host_is_pinned(bed)) &&
+        encode_host_pipelined(c, static_cast<const uint8_t*>(bed), n, o, reg))
         return STARCH_OK;
     uint8_t* d = c->input.as<uint8_t>(n + 64);
-    if (n) HIP_CHECK(hipMemcpyAsync(d, bed, n, hipMemcpyHostToDevice, c->st));
+    reg.h2d(d, bed, n, c->st);
     HIP_CHECK(hipStreamSynchronize(c->st));
     encode_device(c, d, n, o);
     return STARCH_OK;
@@ -1555,11 +1556,11 @@ int starch_encode_host_into(starch_ctx* c, const void* bed, uint64_t n, const st
         (o.compression_method != STARCH_METHOD_BZIP2 && o.compression_method != STARCH_METHOD_GZIP)) return STARCH_ERR_ARG;
     static const bool pipe_off = [] { const char* e = getenv("STARCH_PIPELINE"); return e && !strcmp(e, "0"); }();
     HostRegistration reg(pipe_off || o.reference_compat ? nullptr : bed, n, 256ull << 20);
-    if (!pipe_off && !o.reference_compat && n >= (256ull << 20) && host_is_pinned(bed) &&
-        encode_host_pipelined(c, static_cast<const uint8_t*>(bed), n, o, static_cast<uint8_t*>(out), cap, out_len))
+    if (!pipe_off && !o.reference_compat && n >= (256ull << 20) && (reg.ok() || host_is_pinned(bed)) &&
+        encode_host_pipelined(c, static_cast<const uint8_t*>(bed), n, o, reg, static_cast<uint8_t*>(out), cap, out_len))
         return STARCH_OK;
     uint8_t* d = c->input.as<uint8_t>(n + 64);
-    if (n) HIP_CHECK(hipMemcpyAsync(d, bed, n, hipMemcpyHostToDevice, c->st));
+    reg.h2d(d, bed, n, c->st);
     HIP_CHECK(hipStreamSynchronize(c->st));
     encode_device(c, d, n, o);
     if (cap < c->archive_bytes) { *out_len = c->archive_bytes; return STARCH_ERR_MEM; }
@@ -1824,10 +1825,37 @@ int starch_transform_host_init(starch_ctx* c, const void* bed, uint64_t n, int64
     GUARD(c)
     if (n && !bed) return STARCH_ERR_ARG;
     uint8_t* d = c->input.as<uint8_t>(n + 64);
-    if (n) HIP_CHECK(hipMemcpyAsync(d, bed, n, hipMemcpyHostToDevice, c->st));
+    {
+        HostRegistration reg(bed, n, 64ull << 20);   // (a mapped file: DMA instead of staging)
+        reg.h2d(d, bed, n, c->st);
+        HIP_CHECK(hipStreamSynchronize(c->st));
+    }
     transform_only(c, d, n, init_start, init_stop);
     return STARCH_OK;
     END_GUARD(c)
+}
+
+int starch_host_register(const void* p, uint64_t n)
+{
+    const uintptr_t pg = 4096, b = reinterpret_cast<uintptr_t>(p);
+    const uintptr_t l = (b + pg - 1) & ~(pg - 1), h = (b + n) & ~(pg - 1);
+    if (!p || h <= l) return STARCH_ERR_ARG;
+    if (hipHostRegister(reinterpret_cast<void*>(l), h - l, hipHostRegisterDefault) == hipSuccess) return STARCH_OK;
+    (void)hipGetLastError();   // a read-only mapping (a mapped input file): registered for reads
+    if (hipHostRegister(reinterpret_cast<void*>(l), h - l, hipHostRegisterReadOnly) == hipSuccess) return STARCH_OK;
+    (void)hipGetLastError();
+    return STARCH_ERR_DEVICE;
+}
+
+int starch_host_unregister(const void* p)
+{
+    const uintptr_t pg = 4096, l = (reinterpret_cast<uintptr_t>(p) + pg - 1) & ~(pg - 1);
+    if (!p) return STARCH_ERR_ARG;
+    if (hipHostUnregister(reinterpret_cast<void*>(l)) != hipSuccess) {
+        (void)hipGetLastError();
+        return STARCH_ERR_DEVICE;
+    }
+    return STARCH_OK;
 }
 
 int starch_transform_device(starch_ctx* c, const void* d_bed, uint64_t n)

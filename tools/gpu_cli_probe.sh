@@ -5,6 +5,7 @@
 set -o pipefail
 O=gpurun_out/cli
 mkdir -p $O
+trap 'rm -f $O/a.starch $O/b.starch ${TMPDIR:-/tmp}/cfg2_cli.bed' EXIT
 F=${TMPDIR:-/tmp}/cfg2_cli.bed
 timeout -k 10 120 python3 -c "
 import sys; sys.path.insert(0,'.')

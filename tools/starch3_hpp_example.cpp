@@ -8,14 +8,25 @@
 // GPU-backed patched-libbz2 ABI), whose block_close_functor records the index
 // entry; finish_tf_buffers writes the index.  Both must give the same bytes as
 // the starch3 CLI.
+#include <unistd.h>
+
+#include <chrono>
 #include <cstring>
 
 #include "../include/starch3_amd.hpp"
 
 starch3::Starch* starch3::self = NULL;   // cpp:10
 
+static double now_s()
+{
+    return std::chrono::duration<double>(std::chrono::steady_clock::now().time_since_epoch()).count();
+}
+
 int main(int argc, char** argv)
 {
+    const double t0 = now_s();
+    const char* tr = std::getenv("STARCH_HOOK_TRACE");
+    const bool trace = tr && !std::strcmp(tr, "1");
     starch3::Starch starch;
     starch3::self = &starch;
     // --hook: the per-chromosome hand-off; --vdev N: N virtual devices (all on
@@ -40,14 +51,30 @@ int main(int argc, char** argv)
     } else {
         starch.initialize_bz_stream_ptr();          // hpp:773-776
         starch.setup_bz_stream_callbacks(&starch);
+        const double t1 = now_s();
         rc = starch.transform_and_flush_in_stream();
         if (!rc) rc = starch.finish_tf_buffers();
+        const double t2 = now_s();
         starch.delete_bz_stream_ptr();
+        if (trace)
+            std::fprintf(stderr, "example: setup %.1f ms  hook %.1f ms  bz stream delete %.1f ms\n", (t1 - t0) * 1e3,
+                         (t2 - t1) * 1e3, (now_s() - t2) * 1e3);
     }
     if (rc) {
-        std::fprintf(stderr, "Error: %s\n", starch_strerror(rc));
+        std::fprintf(stderr, "Error: %s (%s)\n", starch_strerror(rc),
+                     starch.context() ? starch_last_error(starch.context()) : "");
         return EINVAL;
     }
+    const double t3 = now_s();
     starch.delete_out_compression_stream();
-    return EXIT_SUCCESS;
+    if (trace) std::fprintf(stderr, "example: out stream delete %.1f ms, main %.1f ms\n", (now_s() - t3) * 1e3, (now_s() - t0) * 1e3);
+    // The archive is out (and flushed): the bzlib ABI's encoder slots, pinned
+    // stages and the HIP runtime go back with the process instead of one by
+    // one at static destruction (~0.1-0.2 s); STARCH_HPP_TEARDOWN=1 returns
+    // normally.  Same as tools/starch3_cli.cpp.
+    const char* td = std::getenv("STARCH_HPP_TEARDOWN");
+    if (td && !std::strcmp(td, "1")) return EXIT_SUCCESS;
+    std::fflush(stdout);
+    std::fflush(stderr);
+    _exit(EXIT_SUCCESS);
 }

@@ -17,13 +17,25 @@ def main():
     ap.add_argument("--lines", type=int, default=100_000_000)
     ap.add_argument("--reps", type=int, default=5)
     ap.add_argument("--sha", action="store_true")
+    ap.add_argument("--chroms", default="13,14", help="kind 2: chromosome ids (HG38 order)")
     a = ap.parse_args()
     import torch
     import starch_amd
-    n = sum(starch_amd.gen_bed_sizes(a.kind, a.lines))
-    host = torch.empty(n + 64, dtype=torch.uint8, pin_memory=True)
-    starch_amd.gen_bed(a.kind, a.lines, into=ctypes.c_void_p(host.data_ptr()))
-    dev = host.to("cuda")
+    if a.kind == 2:   # per-position (cfg5): a few whole chromosomes written by the device generator
+        chroms = [int(x) for x in a.chroms.split(",")]
+        sizes = [starch_amd.gen_perpos_device(ci) for ci in chroms]
+        n = sum(sizes)
+        dev = torch.empty(n + 64, dtype=torch.uint8, device="cuda")
+        off = 0
+        for ci, sz in zip(chroms, sizes):
+            starch_amd.gen_perpos_device(ci, dev.data_ptr() + off, n + 64 - off, stream=0)
+            off += sz
+        torch.cuda.synchronize()
+    else:
+        n = sum(starch_amd.gen_bed_sizes(a.kind, a.lines))
+        host = torch.empty(n + 64, dtype=torch.uint8, pin_memory=True)
+        starch_amd.gen_bed(a.kind, a.lines, into=ctypes.c_void_p(host.data_ptr()))
+        dev = host.to("cuda")
     c = starch_amd.Starch(0)
     ms = []
     for _ in range(a.reps):
