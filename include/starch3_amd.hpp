@@ -345,8 +345,12 @@ public:
     // the longest chromosome run, which one device must encode whole).
     int compress_in_stream(void)
     {
-        int rc = open_devices();
-        if (rc) return rc;
+        int rc;
+        if (_devices.size() == 1) {
+            bool done = false;
+            if ((rc = compress_mapped(done)) || done) return rc;
+        }
+        if ((rc = open_devices())) return rc;
         if (_ctx.size() > 1) return compress_in_stream_multi();
         starch_ctx* c = _ctx[0];
         starch_options o = options();
@@ -374,6 +378,74 @@ public:
         if ((rc = starch_stream_end(c)) || (rc = drain())) return rc;
         std::fflush(_out_stream);
         return STARCH_OK;
+    }
+
+    // smallest file the mapped paths take (tests: STARCH_HPP_MAP_MIN bytes)
+    static uint64_t map_min(uint64_t dflt)
+    {
+        const char* e = std::getenv("STARCH_HPP_MAP_MIN");
+        return e && std::atoll(e) > 0 ? (uint64_t)std::atoll(e) : dflt;
+    }
+
+    // compress_in_stream for a regular file of >= 256 MiB that ends at its
+    // st_size, on one device: the file is mapped and its pages faulted in by
+    // 16 threads while the device opens (initialize_out_compression_stream
+    // started it), then one starch_encode_host_into -- the library registers
+    // the mapping for the call and DMAs chromosome batches from it while
+    // finished ones come back -- and the archive after the magic to the out
+    // stream.  done = false: not taken (pipe, small or growing file,
+    // STARCH_HPP_MAP=0).
+    int compress_mapped(bool& done)
+    {
+        done = false;
+        const char* e = std::getenv("STARCH_HPP_MAP");
+        if (!_in_stream || (e && !std::strcmp(e, "0"))) return STARCH_OK;
+        const int fd = fileno(_in_stream);
+        struct stat st;
+        const off_t cur = lseek(fd, 0, SEEK_CUR);
+        if (fd < 0 || fstat(fd, &st) != 0 || !S_ISREG(st.st_mode) || cur < 0 ||
+            (uint64_t)st.st_size < (uint64_t)cur + map_min(256ull << 20))
+            return STARCH_OK;
+        unsigned char x;
+        if (pread(fd, &x, 1, st.st_size) != 0) return STARCH_OK;
+        const uint64_t pg = (uint64_t)sysconf(_SC_PAGESIZE), mo = (uint64_t)cur & ~(pg - 1);
+        const uint64_t len = (uint64_t)st.st_size - mo, n = (uint64_t)st.st_size - (uint64_t)cur;
+        void* m = mmap(NULL, len, PROT_READ, MAP_PRIVATE, fd, (off_t)mo);
+        if (m == MAP_FAILED) return STARCH_OK;
+        done = true;
+        {
+            (void)madvise(m, len, MADV_WILLNEED);
+            const int nt = 16;
+            const uint64_t per = ((len + nt - 1) / nt + pg - 1) & ~(pg - 1);
+            std::vector<std::thread> th;
+            std::vector<unsigned> sink(nt, 0);
+            for (int t = 0; t < nt; ++t)
+                th.push_back(std::thread([&, t]() {
+                    const volatile unsigned char* p = static_cast<const unsigned char*>(m);
+                    unsigned acc = 0;
+                    for (uint64_t o = (uint64_t)t * per; o < len && o < (uint64_t)(t + 1) * per; o += pg) acc += p[o];
+                    sink[t] = acc;
+                }));
+            for (size_t t = 0; t < th.size(); ++t) th[t].join();
+        }
+        int rc = open_devices();
+        if (!rc) {
+            starch_ctx* c = _ctx[0];
+            const starch_options o = options();
+            const unsigned char* bed = static_cast<const unsigned char*>(m) + ((uint64_t)cur - mo);
+            uint64_t cap = n / 2 + (16ull << 20), got = 0;
+            std::unique_ptr<char[]> out(new char[cap]);   // (not zero-filled: only the archive's pages are touched)
+            rc = starch_encode_host_into(c, bed, n, &o, out.get(), cap, &got);
+            if (rc == STARCH_ERR_MEM && got > cap) {      // larger than guessed: the archive is still in the context
+                out.reset(new char[got]);
+                rc = starch_archive_copy(c, out.get(), got);
+            }
+            if (!rc && got > 4) std::fwrite(out.get() + 4, 1, got - 4, _out_stream);   // (the magic is out already)
+        }
+        munmap(m, len);
+        (void)lseek(fd, st.st_size, SEEK_SET);
+        std::fflush(_out_stream);
+        return rc;
     }
 
     // The in stream in batches of whole chromosome runs (units of
@@ -451,7 +523,7 @@ public:
         const char* e = std::getenv("STARCH_HPP_MAP");
         if (!rd.regular() || (e && !std::strcmp(e, "0"))) return STARCH_OK;
         struct stat st;
-        if (fstat(rd.fd, &st) != 0 || (uint64_t)st.st_size < rd.off + (64ull << 20)) return STARCH_OK;
+        if (fstat(rd.fd, &st) != 0 || (uint64_t)st.st_size < rd.off + map_min(64ull << 20)) return STARCH_OK;
         unsigned char x;
         if (pread(rd.fd, &x, 1, st.st_size) != 0) return STARCH_OK;   // more than st_size: read it instead
         const uint64_t pg = (uint64_t)sysconf(_SC_PAGESIZE), mo = rd.off & ~(pg - 1);
