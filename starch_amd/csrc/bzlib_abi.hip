@@ -24,6 +24,8 @@
 // Otherwise one block is coded when it closes.
 #include <string.h>
 
+#include <atomic>
+#include <chrono>
 #include <condition_variable>
 #include <deque>
 #include <memory>
@@ -61,6 +63,11 @@ struct GpuStreamState {
     uint32_t in_ch = 256, in_len = 0, nblock = 0;
     std::vector<uint8_t> blk;           // the block's input bytes, the pending run included
     uint64_t blk_beg = 0;               // absolute input offset of blk[0]
+    // a coded-ahead block that arrived whole in one call is not copied: its
+    // last `virt` bytes are counted here instead of held in blk (only its
+    // closing byte, the next block's pending run, is kept: virt_last)
+    uint64_t virt = 0;
+    uint8_t virt_last = 0;
     uint64_t consumed = 0;              // input bytes consumed (total_in)
     // blocks coded ahead
     std::deque<Coded> ahead;
@@ -80,7 +87,11 @@ struct GpuStreamState {
 // Encoder slots: a stream borrows one to code blocks, so streams of different
 // threads encode concurrently (up to kSlots at once per process) on their
 // own HIP streams.  A slot belongs to one device.
-constexpr int kSlots = 4;
+int slots_per_device()
+{
+    static const int n = [] { const char* e = getenv("STARCH_BZ_SLOTS"); return e && atoi(e) > 0 ? atoi(e) : 2; }();
+    return n;
+}
 struct Slot {
     int device = 0;
     bool busy = false;
@@ -89,10 +100,12 @@ struct Slot {
     DevBuf in, out;
     PinnedBuf stage;
 };
+struct CodeReq;
 struct Pool {
     std::mutex mu;
     std::condition_variable cv;
     std::vector<std::unique_ptr<Slot>> slots;
+    std::deque<CodeReq*> queue;        // code_text requests not yet taken by a slot
 };
 Pool g_pool;
 
@@ -114,40 +127,25 @@ struct DeviceGuard {
     ~DeviceGuard() { if (prev >= 0) (void)hipSetDevice(prev); }
 };
 
-Slot* acquire(int dev)
+// a free slot of the device (made if fewer than slots_per_device exist), or
+// null; g_pool.mu held
+Slot* try_acquire_locked(int dev)
 {
-    std::unique_lock<std::mutex> lk(g_pool.mu);
-    for (;;) {
-        int n = 0;
-        for (auto& s : g_pool.slots) {
-            if (s->device != dev) continue;
-            ++n;
-            if (!s->busy) { s->busy = true; return s.get(); }
-        }
-        if (n < kSlots) {
-            g_pool.slots.emplace_back(new Slot());
-            Slot* s = g_pool.slots.back().get();
-            s->device = dev;
-            s->busy = true;
-            return s;
-        }
-        g_pool.cv.wait(lk);
+    int n = 0;
+    for (auto& s : g_pool.slots) {
+        if (s->device != dev) continue;
+        ++n;
+        if (!s->busy) { s->busy = true; return s.get(); }
     }
-}
-
-void release(Slot* s)
-{
-    {
-        std::lock_guard<std::mutex> lk(g_pool.mu);
-        s->busy = false;
+    if (n < slots_per_device()) {
+        g_pool.slots.emplace_back(new Slot());
+        Slot* s = g_pool.slots.back().get();
+        s->device = dev;
+        s->busy = true;
+        return s;
     }
-    g_pool.cv.notify_all();
+    return nullptr;
 }
-
-struct SlotGuard {
-    Slot* s;
-    ~SlotGuard() { if (s) release(s); }
-};
 
 void* default_bzalloc(void*, int items, int size) { return malloc((size_t)items * (size_t)size); }   // bz:bzlib.c:151-156
 void default_bzfree(void*, void* addr) { free(addr); }
@@ -287,47 +285,165 @@ void retrack(GpuStreamState* g)
 // Code text (host) as one piece on the GPU: closed (its last run flushed, the
 // final block included) or open (complete blocks only).  Appends one Coded
 // per block to g->ahead, with absolute offsets from `beg`.
-void code_text(GpuStreamState* g, const uint8_t* a, uint64_t na, const uint8_t* b, uint64_t nb, uint64_t beg,
-               bool closed)
+//
+// Requests of all threads go through one queue per process: a thread whose
+// request is still queued when a slot (an encoder with its own HIP stream;
+// STARCH_BZ_SLOTS, default 2 per device) is free takes every queued request
+// of that device -- up to 1 GiB of text, closed pieces in arrival order and
+// at most one open piece, last (Encoder::plan's rule) -- and codes them as the
+// pieces of ONE plan; the others wait for their results.  Streams of
+// different threads (one per chromosome in the process_tf_buffer hand-off)
+// thus share the GPU's block sort instead of each running a plan of a few
+// dozen blocks.
+// STARCH_BZ_TRACE=1: process totals of the time BZ2_bzCompress spends coding
+// on the GPU (code_text, waits for a batch included) and in all, printed at
+// every BZ2_bzCompressEnd
+std::atomic<uint64_t> g_tr_code{0}, g_tr_all{0};
+bool bz_trace()
 {
-    const uint64_t n = na + nb;
-    if (n == 0) return;
-    const int dev = target_device();
-    DeviceGuard guard(dev);
-    SlotGuard sg{acquire(dev)};
-    Slot* sl = sg.s;
+    static const bool on = [] { const char* e = getenv("STARCH_BZ_TRACE"); return e && !strcmp(e, "1"); }();
+    return on;
+}
+uint64_t now_ns()
+{
+    return (uint64_t)std::chrono::duration_cast<std::chrono::nanoseconds>(
+               std::chrono::steady_clock::now().time_since_epoch()).count();
+}
+struct TraceSpan {
+    std::atomic<uint64_t>& acc;
+    uint64_t t0;
+    explicit TraceSpan(std::atomic<uint64_t>& a) : acc(a), t0(bz_trace() ? now_ns() : 0) {}
+    ~TraceSpan() { if (t0) acc += now_ns() - t0; }
+};
+
+struct CodeReq {
+    GpuStreamState* g;
+    const uint8_t *a, *b;
+    uint64_t na, nb, beg;
+    bool closed;
+    int dev;
+    bool taken = false, done = false;
+    std::exception_ptr err;
+};
+
+void code_batch(Slot* sl, const std::vector<CodeReq*>& B)
+{
     if (!sl->st) HIP_CHECK(hipStreamCreateWithFlags(&sl->st, hipStreamNonBlocking));
-    uint8_t* d_in = sl->in.as<uint8_t>(n + 64);
-    // a large piece of the caller's input is DMA'd straight from its buffer
-    // (registered for this call); the rest goes through the slot's pinned stage
-    HostRegistration reg(b, nb, 16ull << 20);
-    const uint64_t staged = reg.ok() ? na : n;
+    const size_t nr = B.size();
+    std::vector<uint64_t> off(nr);
+    uint64_t total = 0, staged = 0;
+    std::vector<std::unique_ptr<HostRegistration>> regs(nr);
+    for (size_t i = 0; i < nr; ++i) {
+        off[i] = total;
+        total += B[i]->na + B[i]->nb;
+        // a large piece of the caller's input is DMA'd straight from its buffer
+        // (registered for this call, or page-locked by the caller); the rest
+        // goes through the slot's pinned stage
+        regs[i].reset(new HostRegistration(B[i]->b, B[i]->nb, 16ull << 20));
+        staged += B[i]->na + (regs[i]->ok() ? 0 : B[i]->nb);
+    }
+    uint8_t* d_in = sl->in.as<uint8_t>(total + 64);
     uint8_t* h = static_cast<uint8_t*>(sl->stage.get(staged + 64));
-    if (na) memcpy(h, a, na);
-    if (nb && !reg.ok()) memcpy(h + na, b, nb);
-    if (staged) HIP_CHECK(hipMemcpyAsync(d_in, h, staged, hipMemcpyHostToDevice, sl->st));
-    if (reg.ok()) reg.h2d(d_in + na, b, nb, sl->st);
-    std::vector<bz::StreamIn> pieces(1);
-    pieces[0].text_off = 0;
-    pieces[0].text_len = n;
-    pieces[0].final_run_joins = 1;   // flush_RL adds the pending run to the block, full or not
-    pieces[0].group = 0;
-    pieces[0].open = closed ? 0u : 1u;
+    uint64_t hs = 0;
+    for (size_t i = 0; i < nr; ++i) {   // one staged copy of each request's non-registered bytes
+        const CodeReq& r = *B[i];
+        const uint64_t h0 = hs;
+        if (r.na) { memcpy(h + hs, r.a, r.na); hs += r.na; }
+        if (r.nb && !regs[i]->ok()) { memcpy(h + hs, r.b, r.nb); hs += r.nb; }
+        if (hs > h0) HIP_CHECK(hipMemcpyAsync(d_in + off[i], h + h0, hs - h0, hipMemcpyHostToDevice, sl->st));
+        if (r.nb && regs[i]->ok()) regs[i]->h2d(d_in + off[i] + r.na, r.b, r.nb, sl->st);
+    }
+    std::vector<bz::StreamIn> pieces(nr);
+    for (size_t i = 0; i < nr; ++i) {
+        pieces[i] = bz::StreamIn{};
+        pieces[i].text_off = off[i];
+        pieces[i].text_len = B[i]->na + B[i]->nb;
+        pieces[i].final_run_joins = 1;   // flush_RL adds the pending run to the block, full or not
+        pieces[i].group = (uint32_t)i;
+        pieces[i].open = B[i]->closed ? 0u : 1u;
+    }
     std::vector<bz::StreamOut> outs;
-    sl->enc.plan(d_in, pieces, g->bs100k, sl->st, outs, nullptr);
-    const uint64_t cap = (outs[0].bytes + 64 + 255) / 256 * 256;
+    sl->enc.plan(d_in, pieces, B[0]->g->bs100k, sl->st, outs, nullptr);
+    uint64_t cap = 0;
+    for (const auto& o : outs) cap += o.bytes;
+    cap = (cap + 64 * nr + 255) / 256 * 256;
     uint8_t* d_out = sl->out.as<uint8_t>(cap);
     sl->enc.emit(d_out, cap, 0, outs, sl->st, nullptr);
     std::vector<bz::Encoder::BlockOut> res;
     sl->enc.block_results(res, sl->st);
-    g->enc.resize(outs[0].bytes);
-    if (outs[0].bytes) HIP_CHECK(hipMemcpyAsync(g->enc.data(), d_out, outs[0].bytes, hipMemcpyDeviceToHost, sl->st));
-    HIP_CHECK(hipStreamSynchronize(sl->st));     // (reg's DMA is done before it unregisters)
-    for (size_t k = 0; k < res.size(); ++k) {
-        const bool fl = closed && k + 1 == res.size();
-        g->ahead.push_back(Coded{beg + res[k].in_beg, beg + res[k].in_end, res[k].bit_off, res[k].bits, res[k].crc,
-                                 res[k].last_bits, fl});
+    for (size_t i = 0; i < nr; ++i) {
+        GpuStreamState* g = B[i]->g;
+        g->enc.resize(outs[i].bytes);
+        if (outs[i].bytes)
+            HIP_CHECK(hipMemcpyAsync(g->enc.data(), d_out + outs[i].out_off, outs[i].bytes, hipMemcpyDeviceToHost,
+                                     sl->st));
     }
+    HIP_CHECK(hipStreamSynchronize(sl->st));     // (the registrations' DMA is done before they unregister)
+    size_t i = 0;
+    for (size_t k = 0; k < res.size(); ++k) {    // blocks in piece order
+        while (i + 1 < nr && res[k].in_beg >= off[i + 1]) ++i;
+        const CodeReq& r = *B[i];
+        const bool last = k + 1 == res.size() || res[k + 1].in_beg >= off[i] + r.na + r.nb;
+        r.g->ahead.push_back(Coded{r.beg + (res[k].in_beg - off[i]), r.beg + (res[k].in_end - off[i]),
+                                   res[k].bit_off - 8 * outs[i].out_off, res[k].bits, res[k].crc, res[k].last_bits,
+                                   r.closed && last});
+    }
+}
+
+void code_text(GpuStreamState* g, const uint8_t* a, uint64_t na, const uint8_t* b, uint64_t nb, uint64_t beg,
+               bool closed)
+{
+    TraceSpan span(g_tr_code);
+    if (na + nb == 0) return;
+    CodeReq me;
+    me.g = g;
+    me.a = a;
+    me.na = na;
+    me.b = b;
+    me.nb = nb;
+    me.beg = beg;
+    me.closed = closed;
+    me.dev = target_device();
+    DeviceGuard guard(me.dev);
+    std::unique_lock<std::mutex> lk(g_pool.mu);
+    g_pool.queue.push_back(&me);
+    for (;;) {
+        if (me.done) break;
+        Slot* sl = me.taken ? nullptr : try_acquire_locked(me.dev);
+        if (!sl) {
+            g_pool.cv.wait(lk);
+            continue;
+        }
+        // take the device's queued requests: closed ones in order, one open one last
+        std::vector<CodeReq*> B;
+        uint64_t bytes = 0;
+        for (auto it = g_pool.queue.begin(); it != g_pool.queue.end();) {
+            CodeReq* r = *it;
+            const uint64_t n = r->na + r->nb;
+            if (r->dev != me.dev || (!B.empty() && bytes + n > (1ull << 30))) { ++it; continue; }
+            B.push_back(r);
+            bytes += n;
+            r->taken = true;
+            it = g_pool.queue.erase(it);
+            if (!r->closed) break;
+        }
+        lk.unlock();
+        std::exception_ptr err;
+        try {
+            code_batch(sl, B);
+        } catch (...) {
+            err = std::current_exception();
+        }
+        lk.lock();
+        for (CodeReq* r : B) {
+            r->err = err;
+            r->done = true;
+        }
+        sl->busy = false;
+        g_pool.cv.notify_all();
+    }
+    lk.unlock();
+    if (me.err) std::rethrow_exception(me.err);
 }
 
 // BZ2_compressBlock (bz:compress.c:602-667) at the current block: its text is
@@ -335,7 +451,8 @@ void code_text(GpuStreamState* g, const uint8_t* a, uint64_t na, const uint8_t* 
 // without the pending run (a block closed by nblockMAX)
 void compress_block(GpuStreamState* g, bool flush, bool last)
 {
-    const uint64_t text = flush ? g->blk.size() : g->blk.size() - g->in_len;
+    const uint64_t len = g->blk.size() + g->virt;
+    const uint64_t text = flush ? len : len - g->in_len;
     if (text) {
         const bool have = !g->ahead.empty() && g->ahead.front().beg == g->blk_beg &&
                           g->ahead.front().end == g->blk_beg + text && g->ahead.front().flushed == flush;
@@ -375,11 +492,17 @@ void compress_block(GpuStreamState* g, bool flush, bool last)
     // the next block starts with the pending run (none after a flush: init_RL)
     if (flush) {
         g->blk.clear();
+        g->virt = 0;
         g->blk_beg = g->consumed;
         g->in_ch = 256;
         g->in_len = 0;
     } else {
-        g->blk.erase(g->blk.begin(), g->blk.begin() + (std::ptrdiff_t)text);
+        if (g->virt) {   // (closed by nblockMAX: in_len is 1, its closing byte is the last one)
+            g->blk.assign(1, g->virt_last);
+            g->virt = 0;
+        } else {
+            g->blk.erase(g->blk.begin(), g->blk.begin() + (std::ptrdiff_t)text);
+        }
         g->blk_beg += text;
     }
     g->nblock = 0;
@@ -435,11 +558,16 @@ bool copy_input(GpuStreamState* g)
         const Coded& c = g->ahead.front();
         const uint64_t target = c.flushed ? c.end : c.end + 1;
         took = std::min<uint64_t>(lim, target - g->consumed);
-        g->blk.insert(g->blk.end(), p, p + took);
+        if (took && g->consumed + took == target) {   // the rest of the block, all in this call: counted, not copied
+            g->virt += took;
+            g->virt_last = p[took - 1];
+        } else {
+            g->blk.insert(g->blk.end(), p, p + took);
+        }
         if (g->consumed + took == target) {
             // closed by nblockMAX: full, its closing byte pending; flushed:
             // the committed input is in (the flush follows at once)
-            g->in_ch = g->blk.back();
+            g->in_ch = g->virt ? g->virt_last : g->blk.back();
             g->in_len = 1;
             g->nblock = c.flushed ? 0u : g->nblock_max;
         } else {
@@ -547,6 +675,7 @@ int BZ2_bzCompress(bz_stream* strm, int action)
 {
     GpuStreamState* g = state_of(strm);
     if (!g) return BZ_PARAM_ERROR;
+    TraceSpan span(g_tr_all);
     try {
         for (;;) {   // preswitch (bz:bzlib.c:420-471)
             switch (g->mode) {
@@ -598,6 +727,9 @@ int BZ2_bzCompressEnd(bz_stream* strm)
 {
     GpuStreamState* g = state_of(strm);
     if (!g) return BZ_PARAM_ERROR;
+    if (bz_trace())
+        fprintf(stderr, "bz trace: BZ2_bzCompress %.1f ms, of which GPU coding (code_text) %.1f ms (all threads)\n",
+                g_tr_all.load() / 1e6, g_tr_code.load() / 1e6);
     g->~GpuStreamState();
     strm->bzfree(strm->opaque, g);                                        // bz:bzlib.c:493-497
     strm->state = nullptr;
