@@ -273,6 +273,8 @@ public:
     void delete_out_compression_stream(void)
     {
         if (_opener.joinable()) _opener.join();
+        if (_ctx_aux) starch_destroy(_ctx_aux);
+        _ctx_aux = NULL;
         for (size_t i = 0; i < _ctx.size(); ++i) starch_destroy(_ctx[i]);
         _ctx.clear();
     }
@@ -742,21 +744,42 @@ public:
     int transform_and_flush_in_stream(void)
     {
         _tr.t0 = _tr.last = Trace::now();
-        starch_ctx* c = NULL;   // (the devices may still be opening while the first batch is read)
-        return for_each_run_batch(256ull << 20, [&](const unsigned char* bed, const starch_unit* u, uint64_t n) -> int {
+        // two contexts: batch k is transformed (on a helper thread) while the
+        // main thread hands batch k-1's chromosomes to process_tf_buffer; the
+        // devices may still be opening while the first batch is read
+        starch_ctx* c[2] = {NULL, NULL};
+        uint64_t k = 0;
+        int pending = -1;              // context holding a transformed batch not yet handed off
+        int rc = for_each_run_batch(512ull << 20, [&](const unsigned char* bed, const starch_unit* u, uint64_t n) -> int {
             const uint64_t beg = u[0].offset, len = u[n - 1].offset + u[n - 1].length - beg;
             _tr.lap(_tr.read);
-            if (!c) {
+            if (!c[0]) {
                 const int r = open_devices();
                 if (r) return r;
-                c = _ctx[0];
+                c[0] = _ctx[0];
+                if (!_ctx_aux && starch_create(_devices[0], &_ctx_aux) != STARCH_OK) _ctx_aux = NULL;
+                c[1] = _ctx_aux;       // (none: one context, no overlap)
                 _tr.lap(_tr.open);
             }
-            int r = starch_transform_host_init(c, bed + beg, len, u[0].init_start, u[0].init_stop);
+            const int cur = c[1] ? (int)(k & 1) : 0;
+            int tr = STARCH_OK, r = STARCH_OK;
+            if (pending >= 0 && c[1]) {
+                std::thread t([&]() {
+                    tr = starch_transform_host_init(c[cur], bed + beg, len, u[0].init_start, u[0].init_stop);
+                });
+                r = flush_transformed(c[pending]);
+                t.join();
+            } else {
+                if (pending >= 0) r = flush_transformed(c[pending]);
+                if (!r) tr = starch_transform_host_init(c[cur], bed + beg, len, u[0].init_start, u[0].init_stop);
+            }
             _tr.lap(_tr.tf);
-            if (r) return r;
-            return flush_transformed(c);
+            ++k;
+            pending = cur;
+            return r ? r : tr;
         });
+        if (!rc && pending >= 0) rc = flush_transformed(c[pending]);
+        return rc;
     }
 
     // hand every segment of the context's last transform to process_tf_buffer
@@ -1012,7 +1035,7 @@ private:
         {
             const char* e = std::getenv("STARCH_HOOK_TRACE");
             if (!e || std::strcmp(e, "1")) return;
-            std::fprintf(stderr, "hook trace: total %.1f ms  device open wait %.1f  read+plan %.1f  transform %.1f  text %.1f"
+            std::fprintf(stderr, "hook trace: total %.1f ms  device open wait %.1f  read+plan %.1f  transform (not overlapped) %.1f  text %.1f"
                          "  hand-off %.1f  final drain %.1f  (workers: bzCompress %.1f)\n", (now() - t0) * 1e3, open * 1e3, read * 1e3, tf * 1e3,
                          text * 1e3, hand * 1e3, drain * 1e3, bz * 1e3);
         }
@@ -1097,6 +1120,7 @@ private:
     bool _hook_error = false;
     std::thread _opener;
     int _open_rc = STARCH_OK;
+    starch_ctx* _ctx_aux = NULL;         // transform_and_flush_in_stream's second context
     // tf_buffers of flush_transformed: page-aligned, page-locked once
     // (starch_host_register) and reused, so starch_text_read and the
     // bz_stream's input copy run by DMA (fresh malloc'ed text ran at ~6 GB/s)
@@ -1117,14 +1141,29 @@ private:
             _pool[best].free_ = false;
             return _pool[best].p;
         }
-        const size_t cap = (std::max<size_t>(n, 1) + (1u << 20) - 1) & ~(size_t)((1u << 20) - 1);
+        const size_t cap = (std::max<size_t>(n, 1) + (2u << 20) - 1) & ~(size_t)((2u << 20) - 1);
         void* q = NULL;
-        if (posix_memalign(&q, 4096, cap)) return NULL;
+        if (posix_memalign(&q, 2u << 20, cap)) return NULL;
         PoolBuf b;
         b.p = static_cast<char*>(q);
         b.cap = cap;
         b.free_ = false;
-        b.reg = cap >= (4u << 20) && starch_host_register(q, cap) == STARCH_OK;
+        b.reg = false;
+        if (cap >= (4u << 20)) {
+            // fresh memory: 2 MiB pages where the kernel has them, first touched
+            // by 8 threads (one thread faulting and zeroing ran at ~5 GB/s),
+            // then page-locked once for all its reuses
+            (void)madvise(q, cap, MADV_HUGEPAGE);
+            std::vector<std::thread> th;
+            const size_t per = ((cap / 8) + 4095) & ~(size_t)4095;
+            for (int t = 0; t < 8; ++t)
+                th.push_back(std::thread([=]() {
+                    const size_t o = (size_t)t * per;
+                    if (o < cap) std::memset(static_cast<char*>(q) + o, 0, std::min(per, cap - o));
+                }));
+            for (size_t t = 0; t < th.size(); ++t) th[t].join();
+            b.reg = starch_host_register(q, cap) == STARCH_OK;
+        }
         _pool.push_back(b);
         return b.p;
     }
