@@ -87,6 +87,7 @@ static int env_int(const char* k, int dflt)
 // set-up: pinned buffers, lanes); -1 when the input was not streamed
 static double g_setup_s = -1.0;
 static double g_create_s = -1.0;   // ... of which: device contexts open (starch_create)
+static double g_open_s = -1.0, g_fault_s = -1.0;   // mapped path: the device open and the page faulting alone
 static double g_begin_s = -1.0;    // session begun (starch_stream_begin)
 static double g_end_s = -1.0;      // last archive byte written
 static double g_premain_s = -1.0;
@@ -125,11 +126,13 @@ static void print_stats(starch_ctx* ctx, std::chrono::steady_clock::time_point t
             "\"archive_bytes\": %llu, \"blocks\": %llu, \"ms_total\": %.3f, \"ms_transform\": %.3f, "
             "\"ms_rle\": %.3f, \"ms_bwt\": %.3f, \"ms_mtf\": %.3f, \"ms_tables\": %.3f, \"ms_emit\": %.3f, "
             "\"wall_s\": %.3f, \"e2e_mb_s\": %.1f, \"setup_s\": %.3f, \"create_s\": %.3f, \"begin_s\": %.3f, "
-            "\"end_s\": %.3f, \"premain_s\": %.3f, \"encode_s\": %.3f, \"after_setup_mb_s\": %.1f}\n",
+            "\"end_s\": %.3f, \"premain_s\": %.3f, \"encode_s\": %.3f, \"open_s\": %.3f, \"fault_s\": %.3f, "
+            "\"after_setup_mb_s\": %.1f}\n",
             (unsigned long long)input_bytes, (unsigned long long)s.n_lines, (unsigned long long)s.n_segments,
             (unsigned long long)s.text_bytes, (unsigned long long)s.archive_bytes, (unsigned long long)s.n_blocks,
             s.ms_total, s.ms_transform, s.ms_rle, s.ms_bwt, s.ms_mtf, s.ms_tables, s.ms_emit, wall,
-            wall > 0 ? input_bytes / wall / 1e6 : 0.0, g_setup_s, g_create_s, g_begin_s, g_end_s, g_premain_s, g_encode_s, run > 0 ? input_bytes / run / 1e6 : 0.0);
+            wall > 0 ? input_bytes / wall / 1e6 : 0.0, g_setup_s, g_create_s, g_begin_s, g_end_s, g_premain_s, g_encode_s, g_open_s, g_fault_s,
+            run > 0 ? input_bytes / run / 1e6 : 0.0);
 }
 
 // One rank of a multi-process run: map the file, plan units, LPT
@@ -325,7 +328,11 @@ int main(int argc, char** argv)
     void* map = MAP_FAILED;
     std::thread opener;
     int open_rc = STARCH_OK;
-    if (map_file) opener = std::thread([&]() { open_rc = starch_create(devices[0], &ctxs[0]); });
+    if (map_file)
+        opener = std::thread([&]() {
+            open_rc = starch_create(devices[0], &ctxs[0]);
+            g_open_s = std::chrono::duration<double>(std::chrono::steady_clock::now() - t0).count();
+        });
     if (map_file) {
         const uint64_t n = (uint64_t)ms.st_size;
         map = mmap(nullptr, n, PROT_READ, MAP_PRIVATE, fileno(in), 0);
@@ -343,6 +350,7 @@ int main(int argc, char** argv)
                     sink[t] = acc;
                 });
             for (auto& x : th) x.join();
+            g_fault_s = std::chrono::duration<double>(std::chrono::steady_clock::now() - t0).count();
         }
         opener.join();
         rc = open_rc;
