@@ -289,8 +289,9 @@ void retrack(GpuStreamState* g)
 // Requests of all threads go through one queue per process: a thread whose
 // request is still queued when a slot (an encoder with its own HIP stream;
 // STARCH_BZ_SLOTS, default 2 per device) is free takes every queued request
-// of that device -- up to 1 GiB of text, closed pieces in arrival order and
-// at most one open piece, last (Encoder::plan's rule) -- and codes them as the
+// of that device and block size -- up to 1 GiB of text, closed pieces in
+// arrival order and at most one open piece, last (Encoder::plan's rule) --
+// and codes them as the
 // pieces of ONE plan; the others wait for their results.  Streams of
 // different threads (one per chromosome in the process_tf_buffer hand-off)
 // thus share the GPU's block sort instead of each running a plan of a few
@@ -420,7 +421,11 @@ void code_text(GpuStreamState* g, const uint8_t* a, uint64_t na, const uint8_t* 
         for (auto it = g_pool.queue.begin(); it != g_pool.queue.end();) {
             CodeReq* r = *it;
             const uint64_t n = r->na + r->nb;
-            if (r->dev != me.dev || (!B.empty() && bytes + n > (1ull << 30))) { ++it; continue; }
+            // (one plan has one block size: streams of another level wait for a plan of their own)
+            if (r->dev != me.dev || (!B.empty() && (bytes + n > (1ull << 30) || r->g->bs100k != B[0]->g->bs100k))) {
+                ++it;
+                continue;
+            }
             B.push_back(r);
             bytes += n;
             r->taken = true;

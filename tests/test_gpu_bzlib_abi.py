@@ -229,13 +229,7 @@ def test_every_call_matches_reference_lib_small_ahead(seed, monkeypatch):
     _every_call(seed, (0, 65536))
 
 
-def _every_call(seed, chunks):
-    """libbz2's state machine call for call (bz:bzlib.c:369-471): the reference
-    library and the GPU ABI driven by the same Python loop give the same return
-    code, total_in and total_out after EVERY BZ2_bzCompress call -- BZ_RUN
-    closing blocks at nblockMAX and stopping input while output is pending,
-    FLUSH / FINISH draining in small pieces -- at levels 1 and 9, over
-    multi-block inputs (runs across block ends included)."""
+def _script(seed):
     r = random.Random(100 + seed)
     bs = 1 if seed % 2 == 0 else 9
     n = r.randint(300_000, 2_600_000) if bs == 1 else r.randint(1_000_000, 3_000_000)
@@ -253,6 +247,54 @@ def _every_call(seed, chunks):
         ops.append((act, k))
         left -= k
     ops.append((BZ_FINISH, left))
+    return data, ops, bs
+
+
+@pytest.mark.skipif(oracle_lib.ref() is None, reason="oracle/_ref not built")
+@pytest.mark.parametrize("ahead", [0, 300000])
+def test_concurrent_streams_share_plans(ahead, monkeypatch):
+    """Streams of eight threads at once, levels 1 and 9 mixed: their blocks are
+    coded in shared GPU plans (one plan per free encoder slot for every queued
+    request of the same block size; with a 300 KB coded-ahead limit some
+    pieces are open) and every call of every stream still matches the
+    reference library (return code, total_in, total_out, bytes)."""
+    import threading
+    if ahead:
+        monkeypatch.setenv("STARCH_BZ_AHEAD", str(ahead))
+    scripts = [_script(s) for s in range(8)]
+    want = []
+    for data, ops, bs in scripts:
+        calls = []
+        out, rcs = run_script(data, ops, bs=bs, lib=_ref_lib(), calls=calls)
+        want.append((out, rcs, calls))
+    got = [None] * len(scripts)
+
+    def work(i):
+        data, ops, bs = scripts[i]
+        calls = []
+        out, rcs = run_script(data, ops, bs=bs, calls=calls)
+        got[i] = (out, rcs, calls)
+
+    ths = [threading.Thread(target=work, args=(i,)) for i in range(len(scripts))]
+    for t in ths:
+        t.start()
+    for t in ths:
+        t.join()
+    for i in range(len(scripts)):
+        assert got[i] is not None, i
+        assert got[i][0] == want[i][0], i
+        assert got[i][1] == want[i][1], i
+        assert got[i][2] == want[i][2], i
+
+
+def _every_call(seed, chunks):
+    """libbz2's state machine call for call (bz:bzlib.c:369-471): the reference
+    library and the GPU ABI driven by the same Python loop give the same return
+    code, total_in and total_out after EVERY BZ2_bzCompress call -- BZ_RUN
+    closing blocks at nblockMAX and stopping input while output is pending,
+    FLUSH / FINISH draining in small pieces -- at levels 1 and 9, over
+    multi-block inputs (runs across block ends included)."""
+    data, ops, bs = _script(seed)
     for chunk in chunks:
         want_calls, got_calls = [], []
         want, wrcs = run_script(data, ops, bs=bs, out_chunk=chunk, lib=_ref_lib(), calls=want_calls)
