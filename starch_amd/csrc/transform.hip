@@ -962,7 +962,15 @@ __global__ void k_seg_info(const uint64_t* __restrict__ seg_first, uint64_t nseg
 #define STARCH_FT 8192
 #endif
 constexpr uint32_t kFT = STARCH_FT;            // tile bytes
-constexpr uint32_t kFH = 1024;                 // halo bytes before the tile
+#ifndef STARCH_FH
+#define STARCH_FH 1024
+#endif
+constexpr uint32_t kFH = STARCH_FH;            // halo bytes before the tile
+#ifndef STARCH_FTHREADS
+#define STARCH_FTHREADS 256
+#endif
+constexpr int kFThreads = STARCH_FTHREADS;     // threads of a k_tf_fused workgroup (one tile)
+static_assert(kFT <= 2u * 32u * (uint32_t)kFThreads, "two 32-byte mask chunks per thread cover the tile");
 constexpr uint32_t kFMaxLines = kFT / 4;
 constexpr uint32_t kFOut = kFT + kFT / 4;      // LDS output bytes per tile
 static_assert(kFT <= 16384, "tested tile sizes: 4, 8, 16 KiB (8 KiB measured fastest)");
@@ -1008,9 +1016,9 @@ struct FusedShared {
     uint16_t nlp[kFMaxLines];                  // LDS position of each line's '\n'
     uint32_t tabm[(kFH + kFT + 32 + kStagePad) / 32 + 8];   // tab bit masks of the staged bytes (parse_mask)
     uint32_t ob4[kFOut / 4];
-    uint64_t scan[kThreads / 64 + 1];
+    uint64_t scan[kFThreads / 64 + 1];
     FusedSeg seg[kFSeg];
-    LineKey wlast[kThreads / 64 + 1];          // [0]: carry into the chunk; [w+1]: wave w's last line
+    LineKey wlast[kFThreads / 64 + 1];         // [0]: carry into the chunk; [w+1]: wave w's last line
     uint32_t tile, ffpos, p1, p2, over, nul;
     struct { uint64_t segs; } excl;          // the tile's first record in the segment arena
 };
@@ -1031,14 +1039,14 @@ __device__ __forceinline__ LineKey shfl_up_key(const LineKey& k)
 // boundaries and chunk starts through LDS).  Returns (bytes, segments).
 // prev_ls < first_ls: the line before the tile's first one, [prev_ls, first_ls),
 // still to be parsed -- by the last thread, whose two line slots of the first
-// chunk are empty (nl <= 2 * kThreads - 2), while the others parse theirs.
+// chunk are empty (nl <= 2 * kFThreads - 2), while the others parse theirs.
 __device__ __forceinline__ void fused_lines(FusedShared& S, const uint8_t* tb, uint64_t a0, uint32_t nl,
                                             uint32_t first_ls, bool input_start, uint32_t* __restrict__ xflags,
                                             uint64_t& bytes_out, uint32_t& segs_out, uint32_t prev_ls = 0,
                                             bool parse_prev = false, bool no_write = false)
 {
     const uint32_t tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
-    if (parse_prev && tid == kThreads - 1) {      // its slots 2*tid, 2*tid+1 are past nl
+    if (parse_prev && tid == kFThreads - 1) {      // its slots 2*tid, 2*tid+1 are past nl
         LineVals pr;
         if (!parse_mask(tb, S.tabm, prev_ls, first_ls - prev_ls, a0 + prev_ls, pr)) {
             S.over = 1;                           // not the fast shape: the two-pass path takes the input
@@ -1051,7 +1059,7 @@ __device__ __forceinline__ void fused_lines(FusedShared& S, const uint8_t* tb, u
     uint8_t* ob = reinterpret_cast<uint8_t*>(S.ob4);
     uint64_t run = 0;
     uint32_t segrun = 0;
-    for (uint32_t c0 = 0; c0 < nl; c0 += 2 * kThreads) {
+    for (uint32_t c0 = 0; c0 < nl; c0 += 2 * kFThreads) {
         TfLine t[2];
         uint32_t ls[2] = {0, 0};
         LineKey key[2];
@@ -1122,7 +1130,7 @@ __device__ __forceinline__ void fused_lines(FusedShared& S, const uint8_t* tb, u
         run += tot >> 20;
         segrun += (uint32_t)(tot & 0xFFFFFu);
         // carry: the chunk's last line is the next chunk's first predecessor
-        const uint32_t last = (nl - c0 < 2 * kThreads ? nl - c0 : 2 * kThreads) - 1;
+        const uint32_t last = (nl - c0 < 2 * kFThreads ? nl - c0 : 2 * kFThreads) - 1;
         if (2 * tid == last) S.wlast[0] = key[0];
         if (2 * tid + 1 == last) S.wlast[0] = key[1];
         __syncthreads();
@@ -1144,7 +1152,7 @@ __device__ unsigned long long g_tfprof[8];
 #else
 #define TPROF(v)
 #endif
-__global__ void __launch_bounds__(kThreads) __attribute__((amdgpu_waves_per_eu(STARCH_TF_WPE)))
+__global__ void __launch_bounds__(kFThreads) __attribute__((amdgpu_waves_per_eu(STARCH_TF_WPE)))
 k_tf_fused(const uint8_t* __restrict__ bed, uint64_t n, const FusedOut fo, uint32_t* __restrict__ xflags,
            uint32_t dbg_mode)
 {
@@ -1169,7 +1177,7 @@ k_tf_fused(const uint8_t* __restrict__ bed, uint64_t n, const FusedOut fo, uint3
     const uint32_t nw = (uint32_t)((reinterpret_cast<uintptr_t>(bed + tend) - abs0 + 15) / 16);
     {
         const uint4* src = reinterpret_cast<const uint4*>(abs0);
-        for (uint32_t w = tid; w < nw; w += kThreads) S.tb4[w] = src[w];
+        for (uint32_t w = tid; w < nw; w += kFThreads) S.tb4[w] = src[w];
     }
     __syncthreads();
     TPROF(p1);
@@ -1217,7 +1225,7 @@ k_tf_fused(const uint8_t* __restrict__ bed, uint64_t n, const FusedOut fo, uint3
     }
     // tab masks and the NUL flag of the halo chunks as well (a tile's first
     // line starts in its halo)
-    for (uint32_t ch = tid; ch < cbeg; ch += kThreads) {
+    for (uint32_t ch = tid; ch < cbeg; ch += kFThreads) {
         const uint4* q = reinterpret_cast<const uint4*>(tb + ch * 32);
         const uint4 x = q[0], y = q[1];
         const uint32_t w[8] = {x.x, x.y, x.z, x.w, y.x, y.y, y.z, y.w};
@@ -1294,7 +1302,7 @@ k_tf_fused(const uint8_t* __restrict__ bed, uint64_t n, const FusedOut fo, uint3
     // the previous line: parsed inside fused_lines by an idle thread when the
     // tile's lines leave one free, else here by thread 0
     const bool need_prev = !fallback && !input_start && nl_tile > 0;
-    const bool prev_in_lines = need_prev && nl_tile <= 2 * kThreads - 2;
+    const bool prev_in_lines = need_prev && nl_tile <= 2 * kFThreads - 2;
     if (tid == 0) {
         LineKey pk{0, 0, 0, 0};
         if (need_prev && !prev_in_lines) {
@@ -1348,14 +1356,14 @@ k_tf_fused(const uint8_t* __restrict__ bed, uint64_t n, const FusedOut fo, uint3
     if (fallback || nl_tile == 0) return;
     const uint64_t ab = (uint64_t)tile * kFOut, sb = S.excl.segs;
     if (sb + segs > fo.seg_cap) return;
-    for (uint32_t q = tid; q < segs; q += kThreads) {
+    for (uint32_t q = tid; q < segs; q += kFThreads) {
         const FusedSeg f = S.seg[q];
         fo.seg_arena[sb + q] = ArenaSeg{tile, q, f.line, (uint32_t)f.name_len, a0 + f.name_ls, f.text};
     }
     const uint32_t* ob4 = S.ob4;
     uint32_t* dst = reinterpret_cast<uint32_t*>(fo.arena + ab);   // 4-byte aligned
     const uint32_t nw4 = ((uint32_t)bytes + 3u) / 4u;
-    for (uint32_t w = tid; w < nw4; w += kThreads) dst[w] = ob4[w];
+    for (uint32_t w = tid; w < nw4; w += kFThreads) dst[w] = ob4[w];
 #ifdef STARCH_TF_PROF
     TPROF(p5);
     if (lane == 0) {
@@ -1620,7 +1628,7 @@ void TransformWorkspace::run(const uint8_t* d_bed, uint64_t n, hipStream_t st, T
         // STARCH_TF_DBG (timing experiments only, wrong output): 1 parse without
         // the arena write, 2 staging + masks only, 3 parse + lengths without text
         static const uint32_t dbg_mode = getenv("STARCH_TF_DBG") ? (uint32_t)atoi(getenv("STARCH_TF_DBG")) : 0u;
-        hipLaunchKernelGGL(k_tf_fused, dim3(ntiles), dim3(kThreads), 0, st, d_bed, n, fo,
+        hipLaunchKernelGGL(k_tf_fused, dim3(ntiles), dim3(kFThreads), 0, st, d_bed, n, fo,
                            reinterpret_cast<uint32_t*>(fx + 4), dbg_mode);
         scan::excl_sum_u32_to_u64(fo.tile_bytes, fo.bytes_pre, ntiles, fo.bytes_pre + ntiles, b_tmp, st);
         scan::excl_sum_u32_to_u64(fo.tile_lines, fo.lines_pre, ntiles, fo.lines_pre + ntiles, b_tmp, st);

@@ -128,15 +128,17 @@ def test_hpp_mapped_file_input(args, tmp_path):
     transform_and_flush_in_stream (runs planned over the mapping, batches
     DMA'd from it, tf_buffers from the page-locked pool) take the mapped
     paths (STARCH_HPP_MAP_MIN lowers their size floor); same bytes as the
-    CLI, with and without a 0xFF that ends the input, and as the unmapped
-    paths (STARCH_HPP_MAP=0)."""
+    CLI, with and without a 0xFF that ends the input, as the unmapped paths
+    (STARCH_HPP_MAP=0), and in 1 MiB batches (the hook's transform of batch
+    k on its second context while batch k-1 is handed off)."""
     import starch_amd
     base = starch_amd.gen_bed(0, 400_000, chroms=[13, 14, 21]) + corpus.multi_chrom_bed(4, 500, seed=5, kind="bed6")
     for k, data in enumerate((base, base + b"chrZ\t1\t2\n\xffchrZ\t3\t4\n")):
         f = tmp_path / ("in%d.bed" % k)
         f.write_bytes(data)
         want = _run("starch3", ["--reference-compat"] if "--reference-compat" in args else [], data)
-        for env_extra in ({"STARCH_HPP_MAP_MIN": "4096"}, {"STARCH_HPP_MAP": "0"}):
+        for env_extra in ({"STARCH_HPP_MAP_MIN": "4096"}, {"STARCH_HPP_MAP": "0"},
+                          {"STARCH_HPP_MAP_MIN": "4096", "STARCH_HPP_BATCH": str(1 << 20)}):
             env = dict(os.environ, **env_extra)
             with open(f, "rb") as fh:
                 r = subprocess.run([os.path.join(BUILD, "starch3_hpp_example")] + args, stdin=fh,
