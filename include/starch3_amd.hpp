@@ -537,8 +537,9 @@ public:
         uint64_t nu = 0;
         int rc = starch_plan_units_from(base, n, units.size(), 0, 0, &units[0], &nu);
         // the whole mapping page-locked once (~12 ms per GB of page-cached
-        // file), so every batch's copy runs by DMA
-        const bool reg = !rc && starch_host_register(m, (len + pg - 1) & ~(pg - 1)) == STARCH_OK;
+        // file), so every batch's copy runs by DMA (one device: the
+        // multi-device batches copy from it as pageable memory)
+        const bool reg = !rc && _devices.size() == 1 && starch_host_register(m, (len + pg - 1) & ~(pg - 1)) == STARCH_OK;
         for (uint64_t k = 0; !rc && k < nu;) {   // batches of whole runs, >= batch bytes each
             uint64_t j = k, b = 0;
             while (j < nu && (j == k || b < batch)) b += units[j++].length;

@@ -119,7 +119,7 @@ struct HostRegistration {
         const uintptr_t pg = 4096, b = reinterpret_cast<uintptr_t>(p);
         const uintptr_t l = (b + pg - 1) & ~(pg - 1), h = (b + n) & ~(pg - 1);
         if (h <= l || h - l < min_bytes / 2) return;
-        if (hipHostRegister(reinterpret_cast<void*>(l), h - l, hipHostRegisterReadOnly) == hipSuccess) {
+        if (hipHostRegister(reinterpret_cast<void*>(l), h - l, hipHostRegisterReadOnly | hipHostRegisterPortable) == hipSuccess) {
             base = reinterpret_cast<void*>(l);
             lo = l;
             hi = h;

@@ -1840,9 +1840,9 @@ int starch_host_register(const void* p, uint64_t n)
     const uintptr_t pg = 4096, b = reinterpret_cast<uintptr_t>(p);
     const uintptr_t l = (b + pg - 1) & ~(pg - 1), h = (b + n) & ~(pg - 1);
     if (!p || h <= l) return STARCH_ERR_ARG;
-    if (hipHostRegister(reinterpret_cast<void*>(l), h - l, hipHostRegisterDefault) == hipSuccess) return STARCH_OK;
+    if (hipHostRegister(reinterpret_cast<void*>(l), h - l, hipHostRegisterPortable) == hipSuccess) return STARCH_OK;
     (void)hipGetLastError();   // a read-only mapping (a mapped input file): registered for reads
-    if (hipHostRegister(reinterpret_cast<void*>(l), h - l, hipHostRegisterReadOnly) == hipSuccess) return STARCH_OK;
+    if (hipHostRegister(reinterpret_cast<void*>(l), h - l, hipHostRegisterReadOnly | hipHostRegisterPortable) == hipSuccess) return STARCH_OK;
     (void)hipGetLastError();
     return STARCH_ERR_DEVICE;
 }
