@@ -75,14 +75,6 @@ struct FbPool {
     void init(int device);
     ~FbPool();
 };
-// a second stream of the encoder's device with a fork / join event pair:
-// independent kernels of one plan (the block CRCs beside RLE1's byte emit)
-struct SideStream {
-    hipStream_t st = nullptr;
-    hipEvent_t fork = nullptr, join = nullptr;
-    void init();
-    ~SideStream();
-};
 class Encoder {
 public:
     // Compress `streams` whose bytes live in d_text (device).  The result is
@@ -130,7 +122,6 @@ private:
         b_fallback, b_bwt3, b_crc, b_dedupe, b_rep_bytes, b_rep_blk, b_last;
     PinnedBuf h_wtot_, h_nblk_, h_blocks_, h_hr_, h_last_;
     FbPool fb_pool_;                        // periodic blocks' concurrent replays   // read-back targets (pinned)
-    SideStream side_;
     struct PinnedCtr {
         uint32_t* p = nullptr;
         uint32_t* get();

@@ -12,21 +12,6 @@
 
 namespace bz {
 
-void SideStream::init()
-{
-    if (st) return;
-    HIP_CHECK(hipStreamCreateWithFlags(&st, hipStreamNonBlocking));
-    HIP_CHECK(hipEventCreateWithFlags(&fork, hipEventDisableTiming));
-    HIP_CHECK(hipEventCreateWithFlags(&join, hipEventDisableTiming));
-}
-SideStream::~SideStream()
-{
-    if (st) (void)hipStreamSynchronize(st);
-    if (fork) (void)hipEventDestroy(fork);
-    if (join) (void)hipEventDestroy(join);
-    if (st) (void)hipStreamDestroy(st);
-}
-
 // stage timer: an event pair queued on the encoder, read by resolve_timers()
 // after the caller's synchronisation (no host wait per stage)
 struct EvTimer {
@@ -153,24 +138,11 @@ void Encoder::plan(const uint8_t* d_text, const std::vector<StreamIn>& streams, 
     uint32_t* d_tile_block = d_carry;
     rle_compact(d_btmp, d_slot0, d_nblk, d_first, nstreams_, d_blocks, d_streams, d_tile0, d_tile_block, st);
     uint8_t* d_blkbytes = b_blkbytes.as<uint8_t>(nb_max * blk_stride_ + 64);
-    // the block CRCs need only the blocks' text ranges: on the side stream,
-    // beside the byte emit (which writes the blocks' inUse words, the CRC
-    // kernels their crc fields).  STARCH_CRC_SIDE=0: both on the one stream.
-    static const bool crc_side = [] { const char* e = getenv("STARCH_CRC_SIDE"); return !(e && !strcmp(e, "0")); }();
-    uint32_t* d_creg = b_crc.as<uint32_t>(nb_max * kCrcMaxChunks);
-    if (crc_side) {
-        side_.init();
-        HIP_CHECK(hipEventRecord(side_.fork, st));
-        HIP_CHECK(hipStreamWaitEvent(side_.st, side_.fork, 0));
-        rle_crc(d_text, d_blocks, (uint32_t)nb_max, d_nb, d_creg, side_.st);
-        HIP_CHECK(hipEventRecord(side_.join, side_.st));
-    }
     if (ntiles) {
         rle_emit(d_text, d_tiles, ntiles, d_twpre, d_tile0, d_tpos, d_streams, d_first, d_nblk, d_tile_block, d_blocks,
                  d_blkbytes, blk_stride_, st);
     }
-    if (crc_side) HIP_CHECK(hipStreamWaitEvent(st, side_.join, 0));
-    else rle_crc(d_text, d_blocks, (uint32_t)nb_max, d_nb, d_creg, st);
+    rle_crc(d_text, d_blocks, (uint32_t)nb_max, d_nb, b_crc.as<uint32_t>(nb_max * kCrcMaxChunks), st);
     HIP_CHECK(hipGetLastError());
     // one read-back: per-stream block counts, the total and every block's descriptor
     uint32_t* nblk = h_nblk_.as<uint32_t>(nstreams_ + 1);
