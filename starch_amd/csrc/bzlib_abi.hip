@@ -408,6 +408,19 @@ void code_text(GpuStreamState* g, const uint8_t* a, uint64_t na, const uint8_t* 
     DeviceGuard guard(me.dev);
     std::unique_lock<std::mutex> lk(g_pool.mu);
     g_pool.queue.push_back(&me);
+    // if this thread leaves by an exception (a slot that could not be made)
+    // while its request is still queued, the request goes with it
+    struct Unqueue {
+        CodeReq* r;
+        std::unique_lock<std::mutex>& lk;
+        ~Unqueue()
+        {
+            if (r->taken) return;
+            if (!lk.owns_lock()) lk.lock();
+            for (auto it = g_pool.queue.begin(); it != g_pool.queue.end(); ++it)
+                if (*it == r) { g_pool.queue.erase(it); break; }
+        }
+    } unq{&me, lk};
     for (;;) {
         if (me.done) break;
         Slot* sl = me.taken ? nullptr : try_acquire_locked(me.dev);
@@ -417,6 +430,7 @@ void code_text(GpuStreamState* g, const uint8_t* a, uint64_t na, const uint8_t* 
         }
         // take the device's queued requests: closed ones in order, one open one last
         std::vector<CodeReq*> B;
+        B.reserve(g_pool.queue.size());   // (no allocation once requests are marked taken)
         uint64_t bytes = 0;
         for (auto it = g_pool.queue.begin(); it != g_pool.queue.end();) {
             CodeReq* r = *it;
