@@ -19,7 +19,10 @@ def main():
     n = sum(starch_amd.gen_bed_sizes(0, lines))
     host = torch.empty(n + 64, dtype=torch.uint8, pin_memory=True)
     starch_amd.gen_bed(0, lines, into=ctypes.c_void_p(host.data_ptr()))
+    t = time.perf_counter()
     c = starch_amd.Starch(0)
+    if os.environ.get("COLD"):
+        print("create: %.1f ms" % ((time.perf_counter() - t) * 1e3), flush=True)
     out = torch.empty(n // 2 + (16 << 20), dtype=torch.uint8, pin_memory=True)
     if os.environ.get("COLD"):   # first calls of a fresh context: a small input first (SMALL=lines), then the whole
         small = int(os.environ.get("SMALL", "0"))
