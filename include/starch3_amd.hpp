@@ -415,10 +415,18 @@ public:
         void* m = mmap(NULL, len, PROT_READ, MAP_PRIVATE, fd, (off_t)mo);
         if (m == MAP_FAILED) return STARCH_OK;
         done = true;
+        // the archive buffer, not zero-filled: only the archive's pages are
+        // touched, and its first n/8 (BED text compresses ~9x) are written
+        // here beside the input's faults, while the device may still be
+        // opening, so the finished batches' device-to-host copies do not
+        // fault them in one by one
+        uint64_t cap = n / 2 + (16ull << 20), got = 0;
+        std::unique_ptr<char[]> out(new char[cap]);
         {
             (void)madvise(m, len, MADV_WILLNEED);
             const int nt = 16;
             const uint64_t per = ((len + nt - 1) / nt + pg - 1) & ~(pg - 1);
+            const uint64_t pre = std::min<uint64_t>(cap, n / 8), oper = ((pre + nt - 1) / nt + pg - 1) & ~(pg - 1);
             std::vector<std::thread> th;
             std::vector<unsigned> sink(nt, 0);
             for (int t = 0; t < nt; ++t)
@@ -427,6 +435,8 @@ public:
                     unsigned acc = 0;
                     for (uint64_t o = (uint64_t)t * per; o < len && o < (uint64_t)(t + 1) * per; o += pg) acc += p[o];
                     sink[t] = acc;
+                    volatile char* q = out.get();
+                    for (uint64_t o = (uint64_t)t * oper; o < pre && o < (uint64_t)(t + 1) * oper; o += pg) q[o] = 0;
                 }));
             for (size_t t = 0; t < th.size(); ++t) th[t].join();
         }
@@ -435,8 +445,6 @@ public:
             starch_ctx* c = _ctx[0];
             const starch_options o = options();
             const unsigned char* bed = static_cast<const unsigned char*>(m) + ((uint64_t)cur - mo);
-            uint64_t cap = n / 2 + (16ull << 20), got = 0;
-            std::unique_ptr<char[]> out(new char[cap]);   // (not zero-filled: only the archive's pages are touched)
             rc = starch_encode_host_into(c, bed, n, &o, out.get(), cap, &got);
             if (rc == STARCH_ERR_MEM && got > cap) {      // larger than guessed: the archive is still in the context
                 out.reset(new char[got]);

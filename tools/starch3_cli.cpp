@@ -326,6 +326,8 @@ int main(int argc, char** argv)
                           fstat(fileno(in), &ms) == 0 && S_ISREG(ms.st_mode) && ms.st_size >= (256ll << 20) &&
                           lseek(fileno(in), 0, SEEK_CUR) == 0;
     void* map = MAP_FAILED;
+    std::unique_ptr<char[]> outp;   // the mapped path's archive buffer
+    uint64_t out_cap = 0;
     std::thread opener;
     int open_rc = STARCH_OK;
     if (map_file)
@@ -338,9 +340,20 @@ int main(int argc, char** argv)
         map = mmap(nullptr, n, PROT_READ, MAP_PRIVATE, fileno(in), 0);
         if (map != MAP_FAILED) {
             (void)madvise(map, n, MADV_WILLNEED);
+            // the output buffer is not initialised: only the pages the archive
+            // lands on are ever touched (zero-filling a 1.2 GB std::vector took
+            // ~0.25 s); its first n/8 (BED text compresses ~9x) are written
+            // once here, beside the input's faults, so the finished batches'
+            // device-to-host copies do not fault them in one by one
+            // (STARCH_CLI_OUT_PREFAULT=0: not)
+            out_cap = n / 2 + (16ull << 20);
+            outp.reset(new char[out_cap]);
+            const char* pe = getenv("STARCH_CLI_OUT_PREFAULT");
+            const uint64_t pre = (pe && !strcmp(pe, "0")) ? 0 : std::min<uint64_t>(out_cap, n / 8);
             const int nt = std::max(1, std::min(16, (int)std::thread::hardware_concurrency()));
             std::vector<std::thread> th;
             const uint64_t per = ((n + nt - 1) / nt + 4095) & ~4095ull;
+            const uint64_t oper = ((pre + nt - 1) / nt + 4095) & ~4095ull;
             std::vector<unsigned> sink(nt, 0);
             for (int t = 0; t < nt; ++t)
                 th.emplace_back([&, t]() {
@@ -348,6 +361,8 @@ int main(int argc, char** argv)
                     unsigned acc = 0;
                     for (uint64_t o = (uint64_t)t * per; o < n && o < (uint64_t)(t + 1) * per; o += 4096) acc += p[o];
                     sink[t] = acc;
+                    volatile char* q = outp.get();
+                    for (uint64_t o = (uint64_t)t * oper; o < pre && o < (uint64_t)(t + 1) * oper; o += 4096) q[o] = 0;
                 });
             for (auto& x : th) x.join();
             g_fault_s = std::chrono::duration<double>(std::chrono::steady_clock::now() - t0).count();
@@ -380,11 +395,7 @@ int main(int argc, char** argv)
         if (m != MAP_FAILED) {
             g_setup_s = std::chrono::duration<double>(std::chrono::steady_clock::now() - t0).count();
             g_begin_s = g_setup_s;
-            // the output buffer is not initialised: only the pages the
-            // archive lands on are ever touched (zero-filling a 1.2 GB
-            // std::vector took ~0.25 s)
-            uint64_t cap = n / 2 + (16ull << 20), len = 0;
-            std::unique_ptr<char[]> outp(new char[cap]);
+            uint64_t cap = out_cap, len = 0;
             rc = starch_encode_host_into(ctx, m, n, &opt, outp.get(), cap, &len);
             if (rc == STARCH_ERR_MEM && len > cap) {   // larger than guessed: the archive is still in the context
                 outp.reset(new char[len]);
