@@ -23,7 +23,7 @@ def main():
     c = starch_amd.Starch(0)
     if os.environ.get("COLD"):
         print("create: %.1f ms" % ((time.perf_counter() - t) * 1e3), flush=True)
-    out = torch.empty(n // 2 + (16 << 20), dtype=torch.uint8, pin_memory=True)
+    out = torch.empty(n // 2 + (16 << 20), dtype=torch.uint8, pin_memory=not os.environ.get("OUT_PAGEABLE"))
     if os.environ.get("COLD"):   # first calls of a fresh context: a small input first (SMALL=lines), then the whole
         small = int(os.environ.get("SMALL", "0"))
         if small:
