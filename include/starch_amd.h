@@ -229,8 +229,13 @@ void starch_free(void* p);
  * PCIe rate; a buffer reused across calls pays the pinning once (~0.03 s per
  * GB for memory already touched).  starch_host_unregister(p) with the same p
  * before the memory is freed (a read-only mapping is registered for reads
- * only: copies from it).  No counterpart in the reference (it has no
- * device copies); the hpp's process_tf_buffer pool uses them. */
+ * only: copies from it).  The library records the range and DMAs from it
+ * only within it; a range overlapping one already registered (or one a
+ * running call registered for itself) is refused with STARCH_ERR_ARG.
+ * Memory page-locked by other means (hipHostMalloc, a framework's pinned
+ * allocator) is used up to the end of its allocation.  No counterpart in the
+ * reference (it has no device copies); the hpp's process_tf_buffer pool uses
+ * them. */
 int starch_host_register(const void* p, uint64_t n);
 int starch_host_unregister(const void* p);
 

@@ -175,6 +175,7 @@ struct Ctx {
     uint32_t* qhead;        // 8 queue heads of the current persistent launch
     const uint32_t* qseg;   // 9 per-XCD segment offsets of the current binned list
     uint32_t nbins;         // top-level bins of this batch (PNB or PNB_WIDE)
+    uint32_t sdig;          // round 0, first L level: the scatter wrote the L buckets' first digits into LL
 };
 
 __device__ __forceinline__ int bits_for3(uint32_t x) { return x ? 32 - __clz(x) : 0; }
@@ -689,6 +690,11 @@ __global__ void __launch_bounds__(SCT) k3_scatter_lds(Ctx c)
     constexpr int BPT = NB / SCT;                  // bins per thread in the local scan
     __shared__ uint32_t cur[NB], tot[NB], lst[NB + 1];
     __shared__ uint32_t stage[SH_HALF];
+    // the next 8 key bits below the top-level digit, staged beside each entry:
+    // written next to the SA entries of the heavy (L-class) buckets, where
+    // k3_part_l's first partition reads them instead of gathering each
+    // rotation's key again (the plain instantiation only)
+    __shared__ uint8_t stage8[MAT ? 4 : SH_HALF];
     __shared__ uint32_t scan_sh[SCT / 64 + 1];
     __shared__ uint32_t qs[8];
     __shared__ uint32_t job_sh;
@@ -736,18 +742,22 @@ __global__ void __launch_bounds__(SCT) k3_scatter_lds(Ctx c)
             // digits of SU consecutive rotations from four PSS words; local counts
             const uint32_t q0 = tid * SU;                // SCT * SU == SH_HALF
             uint32_t d[SU], p[SU];
+            uint8_t sd[SU];
             {
                 const uint64_t bit0 = (uint64_t)(t0 + h0 + q0) * B;
                 const uint64_t qw = bit0 >> 6;
                 const uint32_t p0 = (uint32_t)(bit0 & 63u);
                 const uint64_t w[4] = {pss[qw], pss[qw + 1], pss[qw + 2], pss[qw + 3]};
+                const uint32_t sds = 64u - geo.SH - 8u;       // (the key window's bits [SH, SH + 8))
 #pragma unroll
                 for (int u = 0; u < SU; ++u) {
                     const uint32_t bit = p0 + (uint32_t)u * B;
                     const uint32_t ix = bit >> 6, pb = bit & 63u;
                     const uint64_t a = ix == 0 ? w[0] : ix == 1 ? w[1] : w[2];
                     const uint64_t nx = ix == 0 ? w[1] : ix == 1 ? w[2] : w[3];
-                    d[u] = top_digit((a << pb) | ((nx >> 1) >> (63u - pb)), geo);
+                    const uint64_t v = (a << pb) | ((nx >> 1) >> (63u - pb));
+                    d[u] = top_digit(v, geo);
+                    sd[u] = (uint8_t)(v >> sds);
                 }
             }
 #pragma unroll
@@ -766,7 +776,11 @@ __global__ void __launch_bounds__(SCT) k3_scatter_lds(Ctx c)
             __syncthreads();
 #pragma unroll
             for (int u = 0; u < SU; ++u)
-                if (q0 + u < he) stage[lst[d[u]] + p[u]] = (d[u] << 15) | (h0 + q0 + u);   // 13 + 15 bits
+                if (q0 + u < he) {
+                    const uint32_t j = lst[d[u]] + p[u];
+                    stage[j] = (d[u] << 15) | (h0 + q0 + u);   // 13 + 15 bits
+                    if constexpr (!MAT) stage8[j] = sd[u];
+                }
             __syncthreads();
             // write out in local (bucket) order: runs of a bucket land on consecutive SA slots
             for (uint32_t j = tid; j < he; j += SCT) {
@@ -791,6 +805,8 @@ __global__ void __launch_bounds__(SCT) k3_scatter_lds(Ctx c)
                 if (tot[dg] == 1u) {                   // singleton bucket: final
                     c.scr.LL[so + pos] = (uint8_t)ls;
                     if (r == 0) c.blocks[b].orig_ptr = pos;
+                } else if (!mat && tot[dg] > L_MIN) {  // L class: its first partition digit (LL is free there until then)
+                    c.scr.LL[so + pos] = stage8[j];
                 }
             }
             __syncthreads();
@@ -928,9 +944,21 @@ constexpr int LW = LT / 64;
 // PSS keys (random 8-byte loads); groups above PL_CAP recompute the keys
 constexpr uint32_t PL_CAP = 40960;
 
+#ifdef STARCH_PL_PROF   // timing experiment (dev builds): k3_part_l's phases, shader clocks summed over workgroups
+__device__ unsigned long long g_plprof[16];
+#define PLT(v) const uint64_t v = __builtin_readcyclecounter()
+#define PLA(i, a, b) plp[i] += (b) - (a)
+#else
+#define PLT(v)
+#define PLA(i, a, b)
+#endif
 template <bool DBL>
 __global__ void __launch_bounds__(LT) k3_part_l(Ctx c, const uint64_t* __restrict__ items)
 {
+#ifdef STARCH_PL_PROF
+    uint64_t plp[8] = {};
+    PLT(tk0);
+#endif
     __shared__ uint32_t wh[LW][256];
     __shared__ uint32_t st[256], cur[256], cntd[256];
     __shared__ uint32_t scan_sh[LW + 1];
@@ -949,6 +977,11 @@ __global__ void __launch_bounds__(LT) k3_part_l(Ctx c, const uint64_t* __restric
         const uint32_t slot = it_slot(item), s = it_start(item), m = it_size(item), shift = it_shift(item),
                        par = it_par(item);
         if (m == 0) continue;                          // taken by the grid-wide path (k3_hg_pick); uniform
+        PLT(t0);
+#ifdef STARCH_PL_PROF
+        plp[6] += m;
+        plp[5] += 1;
+#endif
         const uint32_t b = c.b0 + slot;
         const uint64_t so = (uint64_t)slot * c.scr.stride;
         const uint64_t base = so + s;
@@ -962,20 +995,48 @@ __global__ void __launch_bounds__(LT) k3_part_l(Ctx c, const uint64_t* __restric
         const uint32_t db = shift < 8 ? shift : 8;
         const uint32_t sh2 = shift - db;
         const uint64_t dmask = (1ull << db) - 1ull;
+        // a top-level L bucket of round 0: the scatter left each rotation's
+        // digit (its key bits [SH, SH + 8)) in LL next to it
+        const uint8_t* sdig = nullptr;
+        if (!DBL && c.sdig && c.rtext == 0 && !c.mode && par == 0 && db == 8) {
+            const Geo g = c.L.geo[slot];
+            if (shift == g.KB - g.SH) sdig = c.scr.LL + base;
+        }
         for (int i = tid; i < LW * 256; i += LT) (&wh[0][0])[i] = 0;
         if (tid == 0) big[256] = 0;
         __syncthreads();
+        PLT(t1);
+        PLA(0, t0, t1);
 #ifndef STARCH_PART_PU
-#define STARCH_PART_PU 4
+#define STARCH_PART_PU 16   // elements per thread and step (loads batched: 4 -> 16 took k3_part_l 2.5 -> 1.1 ms on cfg2)
 #endif
         constexpr int PU = STARCH_PART_PU;             // elements in flight per thread
+        // (each pass issues all PU loads of a step before using any: a load
+        // chosen per element inside the unrolled loop was waited on one by one)
         for (uint32_t i0 = 0; i0 < m; i0 += PU * LT) {
             uint32_t d[PU];
+            if (sdig) {
+#pragma unroll
+                for (int u = 0; u < PU; ++u) {
+                    const uint32_t i = i0 + u * LT + tid;
+                    d[u] = sdig[i < m ? i : 0u];
+                }
+            } else {
+                uint32_t vv[PU];
+#pragma unroll
+                for (int u = 0; u < PU; ++u) {
+                    const uint32_t i = i0 + u * LT + tid;
+                    vv[u] = ld_nt(sv + (i < m ? i : 0u));
+                }
+#pragma unroll
+                for (int u = 0; u < PU; ++u) {
+                    const uint32_t i = i0 + u * LT + tid;
+                    d[u] = (uint32_t)((elem_key<DBL>(ks, s + (i < m ? i : 0u), vv[u]) >> sh2) & dmask);
+                }
+            }
 #pragma unroll
             for (int u = 0; u < PU; ++u) {
                 const uint32_t i = i0 + u * LT + tid;
-                const uint32_t ic = i < m ? i : 0u;
-                d[u] = (uint32_t)((elem_key<DBL>(ks, s + ic, ld_nt(sv + ic)) >> sh2) & dmask);
                 if (!DBL && m <= PL_CAP && i < m) dcache[i] = (uint8_t)d[u];
             }
 #pragma unroll
@@ -983,11 +1044,15 @@ __global__ void __launch_bounds__(LT) k3_part_l(Ctx c, const uint64_t* __restric
                 if (i0 + u * LT + tid < m) atomicAdd(&wh[wid][d[u]], 1u);
         }
         __syncthreads();
+        PLT(t2);
+        PLA(1, t1, t2);
         uint32_t tcount = 0;
         if (tid < 256) for (int w = 0; w < LW; ++w) tcount += wh[w][tid];
         const uint32_t pre = block_excl_scan_add<uint32_t>(tid < 256 ? tcount : 0u, scan_sh, (uint32_t*)nullptr);
         if (tid < 256) { st[tid] = pre; cur[tid] = pre; cntd[tid] = tcount; }
         __syncthreads();
+        PLT(t3);
+        PLA(2, t2, t3);
         for (uint32_t i0 = 0; i0 < m; i0 += PU * LT) {
             uint32_t v[PU];
             uint64_t k[PU];
@@ -995,11 +1060,31 @@ __global__ void __launch_bounds__(LT) k3_part_l(Ctx c, const uint64_t* __restric
 #pragma unroll
             for (int u = 0; u < PU; ++u) {
                 const uint32_t i = i0 + u * LT + tid;
-                const uint32_t ic = i < m ? i : 0u;
-                v[u] = ld_nt(sv + ic);
-                if (!DBL && m <= PL_CAP) k[u] = (uint64_t)dcache[ic] << sh2;   // only the digit is used below
-                else k[u] = elem_key<DBL>(ks, s + ic, v[u]);
-                lsy[u] = dl ? ks.l[s + ic] : (uint8_t)0;
+                v[u] = ld_nt(sv + (i < m ? i : 0u));
+            }
+            if (!DBL && m <= PL_CAP) {                 // only the digit is used below
+#pragma unroll
+                for (int u = 0; u < PU; ++u) {
+                    const uint32_t i = i0 + u * LT + tid;
+                    k[u] = (uint64_t)dcache[i < m ? i : 0u] << sh2;
+                }
+            } else if (sdig) {
+#pragma unroll
+                for (int u = 0; u < PU; ++u) {
+                    const uint32_t i = i0 + u * LT + tid;
+                    k[u] = (uint64_t)sdig[i < m ? i : 0u] << sh2;
+                }
+            } else {
+#pragma unroll
+                for (int u = 0; u < PU; ++u) {
+                    const uint32_t i = i0 + u * LT + tid;
+                    k[u] = elem_key<DBL>(ks, s + (i < m ? i : 0u), v[u]);
+                }
+            }
+#pragma unroll
+            for (int u = 0; u < PU; ++u) {
+                const uint32_t i = i0 + u * LT + tid;
+                lsy[u] = dl ? ks.l[s + (i < m ? i : 0u)] : (uint8_t)0;
             }
 #pragma unroll
             for (int u = 0; u < PU; ++u) {
@@ -1012,6 +1097,8 @@ __global__ void __launch_bounds__(LT) k3_part_l(Ctx c, const uint64_t* __restric
             }
         }
         __syncthreads();
+        PLT(t4);
+        PLA(3, t3, t4);
         uint32_t nruns = 0;
         if (tid < 256) {
             const uint32_t cc = cntd[tid], ss = st[tid];
@@ -1037,6 +1124,8 @@ __global__ void __launch_bounds__(LT) k3_part_l(Ctx c, const uint64_t* __restric
             if (c.mode && (tid & 63) == 0 && r) atomicAdd(&c.L.runs[slot], r);
         }
         __syncthreads();
+        PLT(t5);
+        PLA(4, t4, t5);
         const uint32_t nbig = big[256];
         for (uint32_t q = 0; q < nbig; ++q) {
             const uint32_t d = big[q];
@@ -1055,7 +1144,17 @@ __global__ void __launch_bounds__(LT) k3_part_l(Ctx c, const uint64_t* __restric
             }
         }
         __syncthreads();
+        PLT(t6);
+        PLA(7, t5, t6);
     }
+#ifdef STARCH_PL_PROF
+    PLT(tk1);
+    plp[4] += 0;
+    if (tid == 0) {
+        for (int q = 0; q < 8; ++q) atomicAdd(&g_plprof[q], (unsigned long long)plp[q]);
+        atomicAdd(&g_plprof[8], (unsigned long long)(tk1 - tk0));
+    }
+#endif
 }
 
 // ---------------------------------------------------------------------------
@@ -3261,6 +3360,7 @@ bool launch_bwt3(BlockDesc* blocks, uint32_t b0, uint32_t nb, const uint8_t* blk
     c.qhead = nullptr;
     c.qseg = nullptr;
     c.nbins = wide ? PNB_WIDE : PNB;
+    c.sdig = 0;
     HIP_CHECK(hipMemsetAsync(mw, 0, (2 * C_N + 14ull * nb + QSETS * QSET + nb_bins) * sizeof(uint32_t), st));
     static const bool period_off = [] { const char* e = getenv("STARCH_PERIOD_CHECK"); return e && !strcmp(e, "0"); }();
     if (!period_off) hipLaunchKernelGGL(k3_period, dim3(nb), dim3(256), 0, st, c);
@@ -3374,6 +3474,20 @@ bool launch_bwt3(BlockDesc* blocks, uint32_t b0, uint32_t nb, const uint8_t* blk
             if (c.keysrc) hipLaunchKernelGGL(k3_part_l<true>, dim3(ncu * STARCH_PL_WG), dim3(LT), 0, st, c, bout);
             else hipLaunchKernelGGL(k3_part_l<false>, dim3(ncu * STARCH_PL_WG), dim3(LT), 0, st, c, bout);
             HIP_CHECK(hipGetLastError());
+#ifdef STARCH_PL_PROF
+            {
+                unsigned long long h[16];
+                HIP_CHECK(hipStreamSynchronize(st));
+                HIP_CHECK(hipMemcpyFromSymbol(h, HIP_SYMBOL(g_plprof), sizeof(h)));
+                static const unsigned long long z[16] = {};
+                HIP_CHECK(hipMemcpyToSymbol(HIP_SYMBOL(g_plprof), z, sizeof(z)));
+                const char* nm[9] = {"zero", "pass1", "scan", "pass2", "final+classify", "groups", "elems", "big", "kernel(all wg)"};
+                fprintf(stderr, "[plprof] level %d sdig %u:", level, c.sdig);
+                for (int q = 0; q < 9; ++q) fprintf(stderr, " %s %llu", nm[q], h[q]);
+                fprintf(stderr, "\n");
+            }
+#endif
+            c.sdig = 0;                  // (deeper levels: the sub-buckets' digits are gathered)
             zero(bit(C_L0 + lsel) | bit(C_LM0 + lsel));
             lsel ^= 1u;
         }
@@ -3393,8 +3507,10 @@ bool launch_bwt3(BlockDesc* blocks, uint32_t b0, uint32_t nb, const uint8_t* blk
         auto resident = [&](const void* f, int threads = 256, const char* env = nullptr) {
             int per_cu = 0;
             HIP_CHECK(hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, f, threads, 0));
-            const char* e = env ? getenv(env) : nullptr;     // experiments: workgroups per CU
-            if (e && atoi(e) > 0) per_cu = atoi(e);
+            // experiments: fewer workgroups per CU (never more than can be resident:
+            // the static assignment would wait on workgroups that never start)
+            const char* e = env ? getenv(env) : nullptr;
+            if (e && atoi(e) > 0 && atoi(e) < per_cu) per_cu = atoi(e);
             if (getenv("STARCH_BWT_DEBUG")) fprintf(stderr, "[bwt3] resident %s: %d per CU\n", env ? env : "-", per_cu);
             return g8((uint32_t)ncu * (uint32_t)(per_cu > 0 ? per_cu : 1));
         };
@@ -3522,6 +3638,10 @@ bool launch_bwt3(BlockDesc* blocks, uint32_t b0, uint32_t nb, const uint8_t* blk
         // about one block in flight per XCD: one 1024-thread workgroup per CU,
         // a block's MAXT tiles spread over its XCD's CUs
         const dim3 gsc((ncu + 7) / 8 * 8);
+        // (k3_scatter_lds leaves the L buckets' first partition digits in LL;
+        // STARCH_SDIG=0: k3_part_l gathers them instead)
+        static const bool sdig_off = [] { const char* e = getenv("STARCH_SDIG"); return e && !strcmp(e, "0"); }();
+        c.sdig = direct || sdig_off ? 0u : 1u;
         if (direct && wide) hipLaunchKernelGGL(k3_scatter<PNB_WIDE>, gsc, dim3(SCT), 0, st, c);
         else if (direct) hipLaunchKernelGGL(k3_scatter<PNB>, gsc, dim3(SCT), 0, st, c);
         else if (wide && c.lA && !kgather) hipLaunchKernelGGL((k3_scatter_lds<PNB_WIDE, true>), gsc, dim3(SCT), 0, st, c);
@@ -3536,6 +3656,7 @@ bool launch_bwt3(BlockDesc* blocks, uint32_t b0, uint32_t nb, const uint8_t* blk
         HIP_CHECK(hipGetLastError());
     }
     sort_groups();
+    c.sdig = 0;
     c.keysrc = 0;                    // text rounds read the PSS at an offset
     c.kA = scr.K2;
     c.kB = scr.K;

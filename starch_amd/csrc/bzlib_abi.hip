@@ -68,6 +68,10 @@ struct GpuStreamState {
     // closing byte, the next block's pending run, is kept: virt_last)
     uint64_t virt = 0;
     uint8_t virt_last = 0;
+    // where those bytes are: the caller's input of the current call (the block
+    // is compressed in the same call that counted them, copy_input ->
+    // compress_block), for a block that must be coded again after all
+    const uint8_t* virt_src = nullptr;
     uint64_t consumed = 0;              // input bytes consumed (total_in)
     // blocks coded ahead
     std::deque<Coded> ahead;
@@ -477,7 +481,16 @@ void compress_block(GpuStreamState* g, bool flush, bool last)
                           g->ahead.front().end == g->blk_beg + text && g->ahead.front().flushed == flush;
         if (!have) {   // code this block alone
             g->ahead.clear();
-            code_text(g, g->blk.data(), text, nullptr, 0, g->blk_beg, true);
+            // (a block coded ahead as closed by nblockMAX that a FLUSH / FINISH
+            // closes with its pending run instead: its counted bytes are the
+            // last ones this call consumed, still in the caller's buffer)
+            if (g->virt) {
+                if (text < g->blk.size() || text - g->blk.size() > g->virt)
+                    throw StarchError(-10, "bzlib: counted block bytes out of range");
+                code_text(g, g->blk.data(), g->blk.size(), g->virt_src, text - g->blk.size(), g->blk_beg, true);
+            } else {
+                code_text(g, g->blk.data(), text, nullptr, 0, g->blk_beg, true);
+            }
             if (g->ahead.size() != 1 || g->ahead.front().end != g->blk_beg + text)
                 throw StarchError(-10, "bzlib: block cut differs from the RLE1 bookkeeping");
         }
@@ -578,8 +591,10 @@ bool copy_input(GpuStreamState* g)
         const uint64_t target = c.flushed ? c.end : c.end + 1;
         took = std::min<uint64_t>(lim, target - g->consumed);
         if (took && g->consumed + took == target) {   // the rest of the block, all in this call: counted, not copied
-            g->virt += took;
+            if (g->virt) throw StarchError(-10, "bzlib: counted block bytes left over");
+            g->virt = took;
             g->virt_last = p[took - 1];
+            g->virt_src = p;
         } else {
             g->blk.insert(g->blk.end(), p, p + took);
         }

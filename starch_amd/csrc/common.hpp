@@ -6,7 +6,9 @@
 #include <stdlib.h>
 #include <string.h>
 
+#include <map>
 #include <memory>
+#include <mutex>
 #include <stdint.h>
 #include <stdio.h>
 #include <stdlib.h>
@@ -73,6 +75,44 @@ struct PinnedBuf {
     ~PinnedBuf() { if (p) (void)hipHostFree(p); }
 };
 
+// Process-wide record of the host ranges the library may DMA from: ranges the
+// caller page-locked through starch_host_register (permanent until
+// starch_host_unregister) and the library's own temporary registrations
+// (HostRegistration, refcounted: two threads coding from one shared input see
+// one registration, which is dropped when the last of them is done -- a
+// registration owned by one thread and merely "found pinned" by another was
+// unregistered under the other's in-flight copy).
+struct PinRegistry {
+    struct Range {
+        uintptr_t hi;
+        int refs;        // temporary registrations: users; permanent: 0
+        bool temp;
+    };
+    std::mutex mu;
+    std::map<uintptr_t, Range> m;   // lo -> range (ranges never overlap)
+    // the range holding address a (lock held), or end()
+    std::map<uintptr_t, Range>::iterator holding(uintptr_t a)
+    {
+        auto it = m.upper_bound(a);
+        if (it == m.begin()) return m.end();
+        --it;
+        return a < it->second.hi ? it : m.end();
+    }
+    bool overlaps(uintptr_t lo, uintptr_t hi)   // (lock held)
+    {
+        auto it = m.lower_bound(lo);
+        if (it != m.end() && it->first < hi) return true;
+        if (it == m.begin()) return false;
+        --it;
+        return it->second.hi > lo;
+    }
+};
+inline PinRegistry& pin_registry()
+{
+    static PinRegistry* r = new PinRegistry;   // (never destroyed: used until exit)
+    return *r;
+}
+
 // Host memory the runtime can DMA from directly for the duration of one call
 // (an mmap'ed file, a caller's buffer): registering a page-cached 2.4 GB
 // mapping took ~28 ms and its copies then ran at the pinned rate
@@ -82,45 +122,58 @@ struct PinnedBuf {
 // allocation (malloc'ed buffers next to each other) stays as it was, so
 // another thread's copies into that neighbour are not disturbed (a
 // page-rounded registration made them fail with "invalid argument").  Copies
-// go through h2d(): the registered middle by DMA, the partial pages around it
-// as pageable copies.  Read-only.  If the runtime refuses (already pinned or
-// registered, ...) nothing is registered.  STARCH_REGISTER=0: off.
+// go through h2d(): the DMA-able middle directly, the rest around it as
+// pageable copies.  Read-only.  Where the range starts:
+//   * in a range the caller registered (starch_host_register): DMA up to that
+//     range's end, never past it;
+//   * in a temporary registration of another call: shared (refcounted);
+//   * in memory pinned by other means (hipHostMalloc, a framework's pinned
+//     allocator): DMA up to the end of that allocation as the runtime reports
+//     it (hipMemGetAddressRange), else nothing is DMA'd directly;
+//   * elsewhere: its whole pages are registered for the call, unless they
+//     overlap another recorded range (then pageable copies only).
+// STARCH_REGISTER=0: off.
 struct HostRegistration {
-    void* base = nullptr;
-    uintptr_t lo = 0, hi = 0;                  // the registered pages [lo, hi)
+    uintptr_t lo = 0, hi = 0;                  // the DMA-able part [lo, hi)
+    uintptr_t temp = 0;                        // the temporary registration this call holds a reference on
     HostRegistration(const void* p, uint64_t n, uint64_t min_bytes)
     {
         if (!p || n < min_bytes) return;
         static const bool off = [] { const char* e = getenv("STARCH_REGISTER"); return e && !strcmp(e, "0"); }();
         if (off) return;
-        hipPointerAttribute_t a;
-        auto pinned = [&a](uintptr_t q) {
-            const bool y = hipPointerGetAttributes(&a, reinterpret_cast<void*>(q)) == hipSuccess &&
-                           a.type == hipMemoryTypeHost;
-            (void)hipGetLastError();
-            return y;
-        };
-        const uintptr_t b0 = reinterpret_cast<uintptr_t>(p);
-        if (pinned(b0)) {   // pinned by the caller: DMA from it, up to where its pinning ends
-            uintptr_t h = b0 + n;
-            if (!pinned(h - 1)) {   // (a copy that starts in pinned memory must not run past it)
-                uintptr_t g = b0 & ~(uintptr_t)4095, e = (h - 1) & ~(uintptr_t)4095;   // page g pinned, page e not
-                while (e - g > 4096) {
-                    const uintptr_t m = g + ((e - g) / 2 & ~(uintptr_t)4095);
-                    if (pinned(m)) g = m; else e = m;
-                }
-                h = e;
-            }
+        const uintptr_t b0 = reinterpret_cast<uintptr_t>(p), e0 = b0 + n;
+        PinRegistry& R = pin_registry();
+        std::lock_guard<std::mutex> lk(R.mu);
+        auto it = R.holding(b0);
+        if (it != R.m.end()) {                 // caller-registered, or another call's registration
             lo = b0;
-            hi = h;
+            hi = e0 < it->second.hi ? e0 : it->second.hi;
+            if (it->second.temp) { ++it->second.refs; temp = it->first; }
             return;
         }
+        hipPointerAttribute_t a;
+        const bool pinned = hipPointerGetAttributes(&a, p) == hipSuccess && a.type == hipMemoryTypeHost;
         (void)hipGetLastError();
-        const uintptr_t pg = 4096, b = reinterpret_cast<uintptr_t>(p);
-        const uintptr_t l = (b + pg - 1) & ~(pg - 1), h = (b + n) & ~(pg - 1);
+        if (pinned) {                          // pinned outside the library: its allocation bounds the DMA
+            void* base = nullptr;
+            size_t sz = 0;
+            if (hipMemGetAddressRange(&base, &sz, const_cast<void*>(p)) == hipSuccess && base && sz) {
+                const uintptr_t ah = reinterpret_cast<uintptr_t>(base) + sz;
+                if (reinterpret_cast<uintptr_t>(base) <= b0 && ah > b0) {
+                    lo = b0;
+                    hi = e0 < ah ? e0 : ah;
+                }
+            }
+            (void)hipGetLastError();
+            return;
+        }
+        const uintptr_t pg = 4096;
+        const uintptr_t l = (b0 + pg - 1) & ~(pg - 1), h = e0 & ~(pg - 1);
         if (h <= l || h - l < min_bytes / 2) return;
+        if (R.overlaps(l, h)) return;
         if (hipHostRegister(reinterpret_cast<void*>(l), h - l, hipHostRegisterReadOnly | hipHostRegisterPortable) == hipSuccess) {
-            base = reinterpret_cast<void*>(l);
+            R.m[l] = PinRegistry::Range{h, 1, true};
+            temp = l;
             lo = l;
             hi = h;
         } else {
@@ -129,10 +182,17 @@ struct HostRegistration {
     }
     ~HostRegistration()
     {
-        if (base) (void)hipHostUnregister(base);
+        if (!temp) return;
+        PinRegistry& R = pin_registry();
+        std::lock_guard<std::mutex> lk(R.mu);
+        auto it = R.m.find(temp);
+        if (it == R.m.end() || !it->second.temp || --it->second.refs > 0) return;
+        (void)hipHostUnregister(reinterpret_cast<void*>(temp));
+        (void)hipGetLastError();
+        R.m.erase(it);
     }
     bool ok() const { return hi > lo; }   // (registered here, or pinned by the caller)
-    // host [src, src + n) -> dst on stream st, splitting around the registered pages
+    // host [src, src + n) -> dst on stream st, splitting around the DMA-able part
     void h2d(void* dst, const void* src, uint64_t n, hipStream_t st) const
     {
         uint8_t* d = static_cast<uint8_t*>(dst);

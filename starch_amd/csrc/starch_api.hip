@@ -1840,17 +1840,31 @@ int starch_host_register(const void* p, uint64_t n)
     const uintptr_t pg = 4096, b = reinterpret_cast<uintptr_t>(p);
     const uintptr_t l = (b + pg - 1) & ~(pg - 1), h = (b + n) & ~(pg - 1);
     if (!p || h <= l) return STARCH_ERR_ARG;
-    if (hipHostRegister(reinterpret_cast<void*>(l), h - l, hipHostRegisterPortable) == hipSuccess) return STARCH_OK;
-    (void)hipGetLastError();   // a read-only mapping (a mapped input file): registered for reads
-    if (hipHostRegister(reinterpret_cast<void*>(l), h - l, hipHostRegisterReadOnly | hipHostRegisterPortable) == hipSuccess) return STARCH_OK;
-    (void)hipGetLastError();
-    return STARCH_ERR_DEVICE;
+    PinRegistry& R = pin_registry();
+    std::lock_guard<std::mutex> lk(R.mu);
+    if (R.overlaps(l, h)) return STARCH_ERR_ARG;            // (already registered, or in use by a call)
+    bool ok = hipHostRegister(reinterpret_cast<void*>(l), h - l, hipHostRegisterPortable) == hipSuccess;
+    if (!ok) {
+        (void)hipGetLastError();   // a read-only mapping (a mapped input file): registered for reads
+        ok = hipHostRegister(reinterpret_cast<void*>(l), h - l, hipHostRegisterReadOnly | hipHostRegisterPortable) == hipSuccess;
+    }
+    if (!ok) {
+        (void)hipGetLastError();
+        return STARCH_ERR_DEVICE;
+    }
+    R.m[l] = PinRegistry::Range{h, 0, false};               // the library DMAs from [l, h) only
+    return STARCH_OK;
 }
 
 int starch_host_unregister(const void* p)
 {
     const uintptr_t pg = 4096, l = (reinterpret_cast<uintptr_t>(p) + pg - 1) & ~(pg - 1);
     if (!p) return STARCH_ERR_ARG;
+    PinRegistry& R = pin_registry();
+    std::lock_guard<std::mutex> lk(R.mu);
+    auto it = R.m.find(l);
+    if (it == R.m.end() || it->second.temp) return STARCH_ERR_ARG;
+    R.m.erase(it);
     if (hipHostUnregister(reinterpret_cast<void*>(l)) != hipSuccess) {
         (void)hipGetLastError();
         return STARCH_ERR_DEVICE;

@@ -37,7 +37,7 @@ def _ref_lib():
     return R
 
 
-def run_script(data, ops, bs=9, out_chunk=0, trace=None, lib=None, calls=None):
+def run_script(data, ops, bs=9, out_chunk=0, trace=None, lib=None, calls=None, src=None):
     """Drive a bzlib ABI (default: the GPU one) like ref_bz2_script does
     (trace: list that gets the total output after each op; calls: list that
     gets (op, rc, total_in, total_out) after EVERY BZ2_bzCompress call)."""
@@ -48,7 +48,8 @@ def run_script(data, ops, bs=9, out_chunk=0, trace=None, lib=None, calls=None):
     CB = ctypes.CFUNCTYPE(None, ctypes.c_void_p)
     cb = CB(lambda h: called.append(h))
     s.block_close_functor = ctypes.cast(cb, ctypes.c_void_p)
-    src = ctypes.create_string_buffer(data, len(data) + 1)
+    if src is None:
+        src = ctypes.create_string_buffer(data, len(data) + 1)
     cap = len(data) + len(data) // 50 + 4096 + 64 * len(ops)
     out = ctypes.create_string_buffer(cap)
     used = produced = 0
@@ -316,3 +317,54 @@ def test_run_emits_blocks_before_finish():
     got, _ = run_script(data, ops, calls=got_calls)
     assert got == want and got_calls == want_calls
     assert got_calls[len(ops) // 2][3] > 0          # bytes out halfway through the RUN calls
+
+
+def test_threads_share_one_large_input_buffer():
+    """two streams coding from ONE shared caller buffer of >= 16 MiB
+    at once (the bzlib ABI DMAs such input from a registration made for the
+    call): the registration is shared and refcounted, so neither thread's copy
+    runs after the other unregistered it.  Repeated, with the threads started
+    together, and checked against system libbz2."""
+    import bz2
+    import threading
+    import starch_amd
+    data = bytes(starch_amd.gen_bed(0, 2_000_000)[:40_000_000])
+    want = bz2.compress(data, 9)
+    src = ctypes.create_string_buffer(data, len(data) + 1)
+    for rep in range(3):
+        got = [None, None]
+        go = threading.Barrier(2)
+
+        def work(i):
+            go.wait()
+            got[i] = run_script(data, [(BZ_FINISH, len(data))], src=src)[0]
+
+        ths = [threading.Thread(target=work, args=(i,)) for i in range(2)]
+        for t in ths:
+            t.start()
+        for t in ths:
+            t.join()
+        assert got[0] == want and got[1] == want, rep
+
+
+@pytest.mark.skipif(oracle_lib.ref() is None, reason="oracle/_ref not built")
+def test_finish_closes_block_coded_ahead_on_its_closing_byte():
+    """a block coded ahead as closed by nblockMAX whose closing byte
+    is the last byte of a FLUSH / FINISH (so libbz2 flushes the pending run
+    into it instead): coded again from the bytes the call just consumed.
+    Level 1, text without runs, the FLUSH / FINISH ending around each of the
+    first block ends."""
+    r = random.Random(31)
+    data = bytes(r.choice(b"0123456789\np-") for _ in range(420_000))
+    m = 99981
+    for end in (m, m + 1, 2 * m, 2 * m + 1, 2 * m + 2, 3 * m + 1):
+        for first in (BZ_RUN, BZ_FLUSH):
+            ops = [(first, 50_000), (BZ_RUN, 250_000), (BZ_FINISH, end + 1 - 300_000 if end + 1 > 300_000 else 0)]
+            if end + 1 <= 300_000:
+                ops = [(first, 50_000), (BZ_RUN, end - 50_000), (BZ_FINISH, 1)]
+            n = sum(k for _, k in ops)
+            d = data[:n]
+            want_calls, got_calls = [], []
+            want, _ = run_script(d, ops, bs=1, lib=_ref_lib(), calls=want_calls)
+            got, _ = run_script(d, ops, bs=1, calls=got_calls)
+            assert got == want and got_calls == want_calls, (end, first)

@@ -115,6 +115,18 @@ static double since_process_start()
     return ts.tv_sec + ts.tv_nsec * 1e-9 - (double)start / hz;
 }
 
+// the archive reached stdout: flushed, and no write failed on the way (ENOSPC,
+// EPIPE, ...); otherwise the process must not exit 0 with a truncated archive
+static bool stdout_ok()
+{
+    if (fflush(stdout) != 0 || ferror(stdout)) {
+        fprintf(stderr, "Error: writing the archive failed (%s)\n", strerror(errno ? errno : EIO));
+        fflush(stderr);
+        return false;
+    }
+    return true;
+}
+
 static void print_stats(starch_ctx* ctx, std::chrono::steady_clock::time_point t0, uint64_t input_bytes)
 {
     const double wall = std::chrono::duration<double>(std::chrono::steady_clock::now() - t0).count();
@@ -417,7 +429,7 @@ int main(int argc, char** argv)
                 fprintf(stderr, "Error: encode failed (%s: %s)\n", starch_strerror(rc), starch_last_error(ctx));
                 return rc == STARCH_ERR_MEM ? ENOMEM : EINVAL;
             }
-            fflush(stdout);
+            if (!stdout_ok()) _exit(EIO);
             if (stats) {
                 starch_stats s;
                 starch_get_stats(ctx, &s);
@@ -544,7 +556,10 @@ int main(int argc, char** argv)
         for (auto* c : ctxs) starch_destroy(c);
         return rc == STARCH_ERR_MEM ? ENOMEM : EINVAL;
     }
-    fflush(stdout);
+    if (!stdout_ok()) {
+        if (getenv("STARCH_CLI_TEARDOWN")) for (auto* c : ctxs) starch_destroy(c);
+        _exit(EIO);
+    }
     if (stats) {
         starch_stats s;
         starch_get_stats(ctx, &s);

@@ -74,7 +74,11 @@ int main(int argc, char** argv)
     // normally.  Same as tools/starch3_cli.cpp.
     const char* td = std::getenv("STARCH_HPP_TEARDOWN");
     if (td && !std::strcmp(td, "1")) return EXIT_SUCCESS;
-    std::fflush(stdout);
+    if (std::fflush(stdout) != 0 || std::ferror(stdout)) {
+        std::fprintf(stderr, "Error: writing the archive failed\n");
+        std::fflush(stderr);
+        _exit(EIO);
+    }
     std::fflush(stderr);
     _exit(EXIT_SUCCESS);
 }
