@@ -1008,7 +1008,7 @@ __global__ void __launch_bounds__(LT) k3_part_l(Ctx c, const uint64_t* __restric
         PLT(t1);
         PLA(0, t0, t1);
 #ifndef STARCH_PART_PU
-#define STARCH_PART_PU 16   // elements per thread and step (loads batched: 4 -> 16 took k3_part_l 2.5 -> 1.1 ms on cfg2)
+#define STARCH_PART_PU 24   // elements per thread and step, loads batched (cfg2 block sort: 4 -> 16 -> 24 -> 32: 21.3, 20.6, 20.4, 20.7 ms)
 #endif
         constexpr int PU = STARCH_PART_PU;             // elements in flight per thread
         // (each pass issues all PU loads of a step before using any: a load

@@ -145,3 +145,21 @@ def test_hpp_mapped_file_input(args, tmp_path):
                                    capture_output=True, timeout=300, env=env)
             assert r.returncode == 0, r.stderr[-2000:]
             assert r.stdout == want, (args, k, env_extra)
+
+
+@pytest.mark.parametrize("pipe_reader", ["1", "0"])
+def test_cli_pipe_larger_than_reader_pool(pipe_reader):
+    """A pipe on stdin larger than the reader's buffer pool (8 x 32 MiB): the
+    early-start reader thread (F_SETPIPE_SZ, pooled buffers fed to the
+    session) and the plain read(2)-into-window loop (STARCH_CLI_PIPE=0) both
+    give the one-call archive."""
+    import starch_amd
+    data = bytes(starch_amd.gen_bed(0, 14_000_000))
+    assert len(data) > 300 << 20
+    c = starch_amd.Starch(0)
+    want = c.compress(data)
+    c.close()
+    env = dict(os.environ, STARCH_CLI_PIPE=pipe_reader)
+    r = subprocess.run([os.path.join(BUILD, "starch3")], input=data, capture_output=True, timeout=300, env=env)
+    assert r.returncode == 0, r.stderr[-2000:]
+    assert r.stdout == want

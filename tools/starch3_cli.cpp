@@ -11,7 +11,8 @@
 // --reference-compat (stdout exactly as the reference: the 4 magic bytes),
 // --device N, --gpus N (shard chromosomes over devices 0..N-1 in one process),
 // --devices LIST (explicit device list, e.g. 0,1 or 0,0 for virtual shards),
-// --stats, --batch-mb N, --slurp, --distributed.
+// --stats, --batch-mb N (streamed batches: 256 MiB, 32 MiB from a pipe), --slurp,
+// --distributed.
 //
 // --distributed: one process per GPU (e.g. `torchrun --no-python
 // --nproc-per-node 8 starch3 --distributed in.bed > out`): RANK / WORLD_SIZE /
@@ -20,6 +21,15 @@
 // maps the input file, plans the chromosome units, encodes its LPT share on
 // its GPU, and the library's RCCL gather (starch_gather_archive) assembles the
 // archive on rank 0, which writes it to stdout.
+//
+// A pipe on stdin (`sort-bed ... | starch3`, `cat f | starch3`, hpp:158-199's
+// documented use): a reader thread starts at once, before the device opens,
+// with the pipe's buffer raised (F_SETPIPE_SZ) so each read(2) takes up to
+// that much; it fills a small pool of reused 32 MiB buffers that the main
+// thread hands to the session (starch_stream_feed: a multi-threaded copy into
+// the pinned buffers) as they fill, so reading overlaps the device open, the
+// session set-up and the encode.  STARCH_CLI_PIPE=0: read(2) into the pinned
+// window after set-up, as for any other stream.
 //
 // One device (the default): streaming ingestion -- the input
 // is read(2) in 64 MiB pieces straight into the session's pinned buffer
@@ -40,7 +50,10 @@
 #include <unistd.h>
 
 #include <chrono>
+#include <condition_variable>
+#include <deque>
 #include <memory>
+#include <mutex>
 #include <string>
 #include <thread>
 #include <vector>
@@ -117,6 +130,93 @@ static double since_process_start()
 
 // the archive reached stdout: flushed, and no write failed on the way (ENOSPC,
 // EPIPE, ...); otherwise the process must not exit 0 with a truncated archive
+// stdin as a pipe: read(2) on a thread of its own into pooled buffers (see the
+// header comment); the consumer takes filled buffers in order and gives them
+// back once fed
+struct PipeReader {
+    static constexpr size_t kChunk = 32ull << 20;
+    static constexpr int kPool = 8;          // buffers in flight (256 MiB)
+    int fd = -1;
+    std::thread th;
+    std::mutex mu;
+    std::condition_variable cv;
+    std::deque<std::pair<char*, size_t>> full;
+    std::vector<char*> free_;
+    bool eof = false;
+    int err = 0;
+    size_t pipe_sz = 0;
+    void start(int f)
+    {
+        fd = f;
+        for (int i = 0; i < kPool; ++i) free_.push_back(static_cast<char*>(malloc(kChunk)));
+        for (char* b : free_)
+            if (!b) { err = ENOMEM; return; }
+        th = std::thread([this]() { run(); });
+    }
+    void run()
+    {
+        // the largest pipe buffer allowed (/proc/sys/fs/pipe-max-size, 1 MiB by default)
+        for (size_t sz = 64ull << 20; sz >= (64u << 10); sz >>= 1) {
+            const int r = fcntl(fd, F_SETPIPE_SZ, (int)sz);
+            if (r >= 0) { pipe_sz = (size_t)r; break; }
+        }
+        for (;;) {
+            char* b;
+            {
+                std::unique_lock<std::mutex> lk(mu);
+                cv.wait(lk, [&]() { return !free_.empty(); });
+                b = free_.back();
+                free_.pop_back();
+            }
+            size_t got = 0;
+            int e = 0;
+            bool end = false;
+            while (got < kChunk) {
+                const ssize_t r = read(fd, b + got, kChunk - got);
+                if (r < 0 && errno == EINTR) continue;
+                if (r < 0) { e = errno ? errno : EIO; break; }
+                if (r == 0) { end = true; break; }
+                got += (size_t)r;
+            }
+            std::lock_guard<std::mutex> lk(mu);
+            if (got) full.emplace_back(b, got);
+            else free_.push_back(b);
+            if (e) err = e;
+            if (e || end) eof = true;
+            cv.notify_all();
+            if (e || end) return;
+        }
+    }
+    // the next filled buffer, or {nullptr, 0} at the end of input
+    std::pair<char*, size_t> next()
+    {
+        std::unique_lock<std::mutex> lk(mu);
+        cv.wait(lk, [&]() { return !full.empty() || eof; });
+        if (full.empty()) return {nullptr, 0};
+        auto x = full.front();
+        full.pop_front();
+        return x;
+    }
+    void give_back(char* b)
+    {
+        std::lock_guard<std::mutex> lk(mu);
+        free_.push_back(b);
+        cv.notify_all();
+    }
+    ~PipeReader()
+    {
+        if (th.joinable()) th.detach();   // (an early error exit: the process ends with it)
+    }
+    void join()
+    {
+        if (th.joinable()) th.join();
+        for (char* b : free_) free(b);
+        for (auto& x : full) free(x.first);
+        free_.clear();
+        full.clear();
+    }
+};
+
 static bool stdout_ok()
 {
     if (fflush(stdout) != 0 || ferror(stdout)) {
@@ -229,7 +329,7 @@ int main(int argc, char** argv)
     std::string note, input;
     int methods = 0, gzip = 0, level = 9, emit_index = 1, compat = 0, device = 0, stats = 0, slurp = 0, bases = 0;
     int distributed = 0;
-    uint64_t batch_mb = 256;
+    uint64_t batch_mb = 0;          // 0: 256 MiB, or 32 MiB for a pipe (see below)
     std::vector<int> devices;
     static struct option longs[] = {
         {"note", required_argument, nullptr, 'n'}, {"bzip2", no_argument, nullptr, 'b'},
@@ -386,6 +486,22 @@ int main(int argc, char** argv)
             return EINVAL;
         }
     }
+    // stdin from a pipe: start reading before the device opens
+    PipeReader pipe;
+    bool piped = false;
+    {
+        struct stat ps;
+        const char* pe = getenv("STARCH_CLI_PIPE");
+        piped = !map_file && devices.size() == 1 && !slurp && !(pe && !strcmp(pe, "0")) &&
+                fstat(fileno(in), &ps) == 0 && (S_ISFIFO(ps.st_mode) || S_ISSOCK(ps.st_mode));
+        if (piped) {
+            pipe.start(fileno(in));
+            if (pipe.err) {
+                fprintf(stderr, "Error: out of memory for the input buffers\n");
+                return ENOMEM;
+            }
+        }
+    }
     for (size_t i = 0; i < devices.size() && !map_file; ++i) {
         rc = starch_create(devices[i], &ctxs[i]);
         if (rc != STARCH_OK) {
@@ -465,11 +581,30 @@ int main(int argc, char** argv)
         const uint64_t fsize = par ? (uint64_t)fs.st_size : 0;
         const int nthr = std::max(1, std::min(16, (int)std::thread::hardware_concurrency()));
         bool read_err = false;
+        // a pipe delivers a few GB/s at most: small batches keep the pinned
+        // buffers small (pinning them, and unpinning at exit, cost ~0.15 s per
+        // GB; cfg2 through `cat | starch3`: 256 / 128 / 64 / 32 MiB batches
+        // 1.19 / 1.08-1.20 / 0.82-0.93 / 0.78 s whole process)
+        if (!batch_mb) batch_mb = piped ? 32 : 256;
         rc = starch_stream_begin(ctx, &opt, batch_mb << 20);
         g_begin_s = std::chrono::duration<double>(std::chrono::steady_clock::now() - t0).count();
         drain();
         g_setup_s = std::chrono::duration<double>(std::chrono::steady_clock::now() - t0).count();
-        while (rc == STARCH_OK) {
+        while (piped && rc == STARCH_OK) {       // the pipe reader's buffers, in order
+            const auto x = pipe.next();
+            if (!x.first) break;
+            rc = starch_stream_feed(ctx, x.first, x.second);
+            pipe.give_back(x.first);
+            drain();
+        }
+        if (piped) {
+            if (rc != STARCH_OK) {   // (the reader may be blocked on a full pool: let it finish the pipe)
+                for (auto x = pipe.next(); x.first; x = pipe.next()) pipe.give_back(x.first);
+            }
+            pipe.join();
+            if (pipe.err) read_err = true, errno = pipe.err;
+        }
+        while (!piped && rc == STARCH_OK) {
             void* w = nullptr;
             uint64_t cap = 0;
             rc = starch_stream_window(ctx, kPiece, &w, &cap);
@@ -570,7 +705,11 @@ int main(int argc, char** argv)
     // (STARCH_CLI_TEARDOWN=1: destroy them first)
     const char* td = getenv("STARCH_CLI_TEARDOWN");
     if (td && !strcmp(td, "1")) {
+        const auto d0 = std::chrono::steady_clock::now();
         for (auto* c : ctxs) starch_destroy(c);
+        if (stats)
+            fprintf(stderr, "teardown %.1f ms\n",
+                    std::chrono::duration<double>(std::chrono::steady_clock::now() - d0).count() * 1e3);
         return 0;
     }
     fflush(stderr);
