@@ -2666,7 +2666,7 @@ k3_sort_grp(Ctx c, const uint64_t* __restrict__ items,
     uint32_t* bcur = bcur_all[g];
     const int tg = wid * 64 + lane;
 #ifndef STARCH_GRP_CHUNK
-#define STARCH_GRP_CHUNK 16
+#define STARCH_GRP_CHUNK 32   // groups per queue pop (cfg2 block sort: 8 / 16 / 32 / 64 / 128: 25.0, 20.5, 19.7, 20.0, 21.8 ms)
 #endif
     // dynamic assignment (NW == 1): each wave pops groups, STARCH_GRP_CHUNK at a time,
     // from its XCD's queue, so the XCD's waves stay on neighbouring groups (one block's
@@ -2676,7 +2676,10 @@ k3_sort_grp(Ctx c, const uint64_t* __restrict__ items,
     __shared__ uint32_t qs[8];
     const uint32_t xs = xcc_id();
     load_qsizes_binned(c, qs);
-    WaveQueue<STARCH_GRP_CHUNK> wq;
+#ifndef STARCH_GRP_CHUNK_S2
+#define STARCH_GRP_CHUNK_S2 STARCH_GRP_CHUNK
+#endif
+    WaveQueue<E == 4 ? STARCH_GRP_CHUNK_S2 : STARCH_GRP_CHUNK> wq;
     constexpr uint32_t NONE = 0xFFFFFFFFu;
     // software pipeline, three groups deep: while group n sorts, the keys of
     // n + 1 are issued (its rotations arrived an iteration ago) and the
