@@ -943,6 +943,10 @@ constexpr int LW = LT / 64;
 // so the scatter pass re-reads only the (coalesced) rotations, not their
 // PSS keys (random 8-byte loads); groups above PL_CAP recompute the keys
 constexpr uint32_t PL_CAP = 40960;
+#ifndef STARCH_PL_STG
+#define STARCH_PL_STG 24576
+#endif
+constexpr uint32_t PL_STG = STARCH_PL_STG;
 
 #ifdef STARCH_PL_PROF   // timing experiment (dev builds): k3_part_l's phases, shader clocks summed over workgroups
 __device__ unsigned long long g_plprof[16];
@@ -967,6 +971,10 @@ __global__ void __launch_bounds__(LT) k3_part_l(Ctx c, const uint64_t* __restric
     __shared__ uint32_t job_sh;
     __shared__ uint32_t cls_sh[16];
     __shared__ uint8_t dcache[DBL ? 4 : PL_CAP];
+    // round 0 / text rounds: the partitioned rotations of a group up to
+    // PL_STG are assembled here and stored in one coalesced pass (the scatter
+    // into 256 sub-buckets wrote one lone 4-byte word per rotation)
+    __shared__ uint32_t stg[DBL ? 1 : PL_STG];
     const int tid = threadIdx.x, wid = tid >> 6;
     const uint32_t x = xcc_id();
     load_qsizes_binned(c, qs);
@@ -1053,6 +1061,7 @@ __global__ void __launch_bounds__(LT) k3_part_l(Ctx c, const uint64_t* __restric
         __syncthreads();
         PLT(t3);
         PLA(2, t2, t3);
+        const bool staged = !DBL && m <= PL_STG && !(STARCH_PL_STG == 0);
         for (uint32_t i0 = 0; i0 < m; i0 += PU * LT) {
             uint32_t v[PU];
             uint64_t k[PU];
@@ -1090,13 +1099,18 @@ __global__ void __launch_bounds__(LT) k3_part_l(Ctx c, const uint64_t* __restric
             for (int u = 0; u < PU; ++u) {
                 if (i0 + u * LT + tid < m) {
                     const uint32_t p = atomicAdd(&cur[(uint32_t)((k[u] >> sh2) & dmask)], 1u);
-                    st_nt(dv + p, v[u]);
+                    if (!DBL && staged) stg[p] = v[u];
+                    else st_nt(dv + p, v[u]);
                     if constexpr (DBL) dk[p] = k[u];
                     if (dl) dl[p] = lsy[u];
                 }
             }
         }
         __syncthreads();
+        if (!DBL && staged) {
+            for (uint32_t i = tid; i < m; i += LT) st_nt(dv + i, stg[i]);
+            __syncthreads();
+        }
         PLT(t4);
         PLA(3, t3, t4);
         uint32_t nruns = 0;
