@@ -159,7 +159,10 @@ struct NibP {
     static constexpr uint32_t IXB = 4;                // bits per stored MTF index (k_mtf_runs -> k_mtf_emit)
     // nibble MTF is cheap: k_mtf_emit re-runs it from the last column (storing
     // the indices measured slower: the stores queue behind the chunk's loads)
-    static constexpr bool SIX = false;
+#ifndef STARCH_NIB_SIX
+#define STARCH_NIB_SIX 0
+#endif
+    static constexpr bool SIX = STARCH_NIB_SIX != 0;
     __device__ static State empty() { State r; r.list = 0; r.set = 0; r.cnt = 0; return r; }
     __device__ static void add(State& st, uint32_t s)
     {

@@ -1,11 +1,12 @@
 #!/usr/bin/env bash
-# GPU box, end-of-round measurement package at the current sources (round 5),
+# GPU box, end-of-round measurement package at the current sources (round 6),
 # one PHASE per gpurun call:
 #   PHASE=tests  every GPU test and smoke()
 #   PHASE=pmc    stamped counters (FETCH/WRITE_SIZE traffic, SQ wait/issue
 #                split) of the block sort for cfg2 and cfg4, of the transform
 #                kernels (k_tf_*) for cfg2, and of every kernel (SQ) for cfg2
 #   PHASE=pmc5   the same for cfg5 (block sort, transform, every kernel)
+#   PHASE=pmc5nd the same for cfg5 with block reuse off (STARCH_DEDUPE=0)
 #                (copy pmc_k_*.json to profiles/ before PHASE=bench: the bench
 #                line attaches them only when their stamp matches)
 #   PHASE=bench  the cfg2 bench line (CPU baseline, e2e, streamed, CLI, hpp,
@@ -44,6 +45,11 @@ pmc)
   ;;
 pmc5)
   TP=300 pmc cfg5 _cfg5 2 0 || exit 1
+  ls $O
+  ;;
+pmc5nd)   # cfg5 with block reuse off: every block's doubling rounds
+  export STARCH_DEDUPE=0
+  TP=600 pmc cfg5nd _cfg5_nodedupe 2 0 || exit 1
   ls $O
   ;;
 bench)

@@ -73,6 +73,7 @@ def main():
     stage = derive(total)
     res = {"src_stamp": src_stamp(), "lines": int(os.environ.get("LINES", "100000000")),
            "kind": int(os.environ.get("KIND", "0")),
+        "block_reuse": os.environ.get("STARCH_DEDUPE") != "0",
            "method": "rocprofv3 --kernel-trace --pmc, passes sq1 (SQ_WAVES SQ_INSTS_VALU SQ_INSTS_SALU SQ_INSTS_LDS "
                      "SQ_INSTS_VMEM_RD SQ_INSTS_VMEM_WR SQ_WAIT_INST_ANY SQ_WAVE_CYCLES) and sq2 (SQ_BUSY_CYCLES "
                      "SQ_WAIT_ANY SQ_ACTIVE_INST_ANY SQ_LDS_BANK_CONFLICT SQ_INSTS_BRANCH SQ_ACTIVE_INST_VALU "

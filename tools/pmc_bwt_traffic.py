@@ -57,6 +57,7 @@ def main():
         "src_stamp": src_stamp(),
         "lines": int(os.environ.get("LINES", "100000000")),
         "kind": int(os.environ.get("KIND", "0")),
+        "block_reuse": os.environ.get("STARCH_DEDUPE") != "0",
         "hbm_bytes_per_launch": fetch_b + write_b,
         "fetch_bytes": fetch_b,
         "write_bytes": write_b,
