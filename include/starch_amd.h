@@ -119,6 +119,16 @@ int starch_set_stream(starch_ctx* ctx, void* hip_stream);
 /* Back to the context's own non-blocking stream (the default after
  * starch_create; not ordered with the null stream). */
 int starch_use_own_stream(starch_ctx* ctx);
+/* Encoder lanes of this context's device-path encodes (starch_encode_device,
+ * starch_encode_host below its pipelined size, starch_encode_units_device):
+ * after the one transform, the segments split into `lanes` contiguous runs of
+ * about equal text, each encoded (RLE1 .. Huffman tables) by its own encoder
+ * on its own stream and host thread, then emitted in order -- the archive
+ * bytes do not depend on it.  1: one encoder; 2..8; 0: the default (the
+ * STARCH_DEV_LANES environment variable, else 2).  Inputs under 16 MB of text
+ * (STARCH_DEV_LANES_MIN) always take one.  Stage times in starch_stats are then
+ * wall time during which any lane ran the stage. */
+int starch_set_lanes(starch_ctx* ctx, int lanes);
 void starch_options_init(starch_options* opt);
 
 /* Whole pipeline.  Input BED bytes already in HBM (d_bed, n bytes).  The

@@ -118,6 +118,7 @@ def load():
         "starch_destroy": ([vp], None),
         "starch_set_stream": ([vp, vp], ctypes.c_int),
         "starch_use_own_stream": ([vp], ctypes.c_int),
+        "starch_set_lanes": ([vp, ctypes.c_int], ctypes.c_int),
         "starch_options_init": ([ctypes.POINTER(Options)], None),
         "starch_encode_device": ([vp, vp, u64, ctypes.POINTER(Options)], ctypes.c_int),
         "starch_encode_host": ([vp, ctypes.c_char_p, u64, ctypes.POINTER(Options)], ctypes.c_int),
@@ -253,6 +254,10 @@ class Starch:
     def set_stream(self, hip_stream_ptr):
         """Run on an external HIP stream; 0 is the HIP null stream (torch's default stream)."""
         _check(self._L.starch_set_stream(self._h, ctypes.c_void_p(hip_stream_ptr)), self._h)
+
+    def set_lanes(self, lanes):
+        """Encoder lanes of the device-path encodes (1..8; 0: the default, STARCH_DEV_LANES or 2)."""
+        _check(self._L.starch_set_lanes(self._h, int(lanes)), self._h)
 
     def use_own_stream(self):
         """Back to the context's own non-blocking stream (the default)."""

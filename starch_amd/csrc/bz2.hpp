@@ -108,6 +108,14 @@ public:
     // waiting on them; once the stream has synchronised, this adds them to
     // *stats (null: drops them).  plan() drops any left from an earlier call.
     void resolve_timers(Stats* stats);
+    // the same timers as intervals, in ms after `ref` (an event recorded on a
+    // stream before any of them), for a caller that merges several encoders'
+    // stages; drops them
+    struct Interval {
+        int stage;
+        float a, b;
+    };
+    void take_intervals(hipEvent_t ref, std::vector<Interval>& out);
     // text offset (in the plan's d_text) where an open last piece's unencoded
     // rest starts; its end is the piece's end
     uint64_t open_rest() const { return open_rest_; }

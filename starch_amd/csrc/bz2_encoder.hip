@@ -53,6 +53,20 @@ void Encoder::resolve_timers(Stats* stats)
     pend_.clear();
 }
 
+void Encoder::take_intervals(hipEvent_t ref, std::vector<Interval>& out)
+{
+    for (auto& t : pend_) {
+        float a = 0, b = 0;
+        HIP_CHECK(hipEventSynchronize(t.b));
+        HIP_CHECK(hipEventElapsedTime(&a, ref, t.a));
+        HIP_CHECK(hipEventElapsedTime(&b, ref, t.b));
+        out.push_back(Interval{t.stage, a, b});
+        (void)hipEventDestroy(t.a);
+        (void)hipEventDestroy(t.b);
+    }
+    pend_.clear();
+}
+
 static uint64_t round_up(uint64_t x, uint64_t m) { return (x + m - 1) / m * m; }
 
 uint32_t* Encoder::PinnedCtr::get()

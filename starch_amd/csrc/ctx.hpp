@@ -9,6 +9,7 @@
 #include <algorithm>
 #include <atomic>
 #include <condition_variable>
+#include <functional>
 #include <memory>
 #include <map>
 #include <mutex>
@@ -126,6 +127,56 @@ struct CopyPool {
     }
 };
 
+// One persistent host thread that runs jobs one at a time (an extra encoder
+// lane's plan in the device path: no thread start per encode).
+struct LaneWorker {
+    std::thread th;
+    std::mutex mu;
+    std::condition_variable cv;
+    std::function<void()> job;
+    bool pending = false, stop = false;
+    void start(std::function<void()> f)
+    {
+        {
+            std::lock_guard<std::mutex> lk(mu);
+            job = std::move(f);
+            pending = true;
+        }
+        if (!th.joinable()) th = std::thread([this] { loop(); });
+        cv.notify_all();
+    }
+    void wait()
+    {
+        std::unique_lock<std::mutex> lk(mu);
+        cv.wait(lk, [&] { return !pending; });
+    }
+    void loop()
+    {
+        std::unique_lock<std::mutex> lk(mu);
+        for (;;) {
+            cv.wait(lk, [&] { return pending || stop; });
+            if (!pending) return;
+            std::function<void()> f = std::move(job);
+            lk.unlock();
+            f();                      // (catches its own errors)
+            lk.lock();
+            pending = false;
+            cv.notify_all();
+        }
+    }
+    void shutdown()
+    {
+        if (!th.joinable()) return;
+        {
+            std::lock_guard<std::mutex> lk(mu);
+            stop = true;
+        }
+        cv.notify_all();
+        th.join();
+    }
+    ~LaneWorker() { shutdown(); }
+};
+
 struct starch_ctx {
     int device = 0;
     hipStream_t own = nullptr;
@@ -134,6 +185,8 @@ struct starch_ctx {
     DevBuf pin_in[2];                // the pipelined path's two device input slots
     DevBuf collect;                  // the pipelined path: this lane's finished streams, batch after batch
     std::vector<std::unique_ptr<starch_ctx>> lanes;   // the pipelined path's extra lanes (same device)
+    LaneWorker worker;               // an extra lane's host thread (device-path encoder lanes)
+    int dev_lanes = 0;               // device-path encoder lanes (starch_set_lanes; 0: default)
     TransformWorkspace tf;
     bz::Encoder enc;
     gz::Encoder genc;            // the gzip method (-g)
@@ -267,6 +320,8 @@ struct starch_ctx {
     ~starch_ctx()
     {
         stream_shutdown();
+        for (auto& l : lanes) l->worker.shutdown();
+        worker.shutdown();
         lanes.clear();
         if (is_lane) {
             (void)hipSetDevice(device);

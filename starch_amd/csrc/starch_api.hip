@@ -315,8 +315,76 @@ enum Layout { L_ARCHIVE, L_STREAMS };
 // transform + bzip2 over units.  L_ARCHIVE: magic + streams + index in
 // c->archive (the whole-input result); L_STREAMS: the streams alone, back to
 // back from offset 0 of c->part (one shard of a multi-GPU run).
+// Encoder lanes of a one-transform encode (STARCH_DEV_LANES, default 2): the
+// segments split into contiguous runs of about equal text, each planned
+// (RLE1 .. tables) by its own encoder on its own stream and host thread, so
+// one lane's host round trips and the drain of its persistent kernels are
+// filled by the other lanes' kernels.  Returns the first segment of every
+// lane (empty: one lane).  Streams keep their order; the archive is the same
+// bytes.
+starch_ctx* lane_ctx(starch_ctx* c, int i);
+
+std::vector<uint64_t> lane_cuts(const std::vector<SegInfo>& si, uint64_t tbytes, int want)
+{
+    static const int nl_env = [] { const char* e = getenv("STARCH_DEV_LANES"); return e ? atoi(e) : 2; }();
+    const int nl_req = want > 0 ? want : nl_env;
+    static const uint64_t min_b = [] {
+        const char* e = getenv("STARCH_DEV_LANES_MIN");
+        return e ? (uint64_t)atoll(e) : (uint64_t)(16ull << 20);
+    }();
+    const uint64_t nseg = si.size();
+    const uint64_t nl = std::min<uint64_t>({(uint64_t)std::max(nl_req, 1), nseg, 8});
+    std::vector<uint64_t> cuts;
+    if (nl < 2 || tbytes < min_b) return cuts;
+    cuts.push_back(0);
+    uint64_t acc = 0, k = 0;
+    for (uint64_t i = 1; i < nl; ++i) {
+        const uint64_t target = tbytes * i / nl;   // lane i starts at the segment whose middle passes it
+        while (k < nseg && 2 * acc + si[k].text_len < 2 * target) acc += si[k++].text_len;
+        if (k <= cuts.back()) acc += si[k++].text_len;
+        if (k >= nseg) break;
+        cuts.push_back(k);
+    }
+    if (cuts.size() < 2) cuts.clear();
+    return cuts;
+}
+
+void merge_counters(bz::Stats& a, const bz::Stats& b)
+{
+    a.n_blocks += b.n_blocks;
+    a.rle_bytes += b.rle_bytes;
+    a.bwt_rounds += b.bwt_rounds;
+    a.periodic_blocks += b.periodic_blocks;
+    a.bwt_tied += b.bwt_tied;
+    a.dedup_blocks += b.dedup_blocks;
+}
+
+// per stage, the wall time during which any lane ran it (union of intervals)
+void stage_union(const std::vector<bz::Encoder::Interval>& iv, bz::Stats& st)
+{
+    float* f[5] = {&st.rle, &st.bwt, &st.mtf, &st.tables, &st.emit};
+    for (int k = 0; k < 5; ++k) {
+        std::vector<std::pair<float, float>> x;
+        for (auto& v : iv)
+            if (v.stage == k) x.emplace_back(v.a, v.b);
+        std::sort(x.begin(), x.end());
+        float tot = 0, ca = 0, cb = -1e30f;
+        for (auto& p : x) {
+            if (p.first > cb) {
+                if (cb > ca) tot += cb - ca;
+                ca = p.first;
+                cb = p.second;
+            } else if (p.second > cb) {
+                cb = p.second;
+            }
+        }
+        if (cb > ca) tot += cb - ca;
+        *f[k] = tot;
+    }
+}
+
 void encode_units(starch_ctx* c, const uint8_t* d_base, const std::vector<UnitIn>& units, const starch_options& opt,
-                  Layout lay, bool planned = false)
+                  Layout lay, bool planned = false, bool split_ok = false)
 {
     hipEvent_t* tv = c->timers();   // owned by the context: nothing to release on a throw
     hipEvent_t e0 = tv[0], e1 = tv[1], e2 = tv[2];
@@ -381,8 +449,61 @@ void encode_units(starch_ctx* c, const uint8_t* d_base, const std::vector<UnitIn
     std::vector<bz::StreamOut> outs;
     bz::Stats bst;
     const bool gzip = opt.compression_method == STARCH_METHOD_GZIP;
-    if (gzip) c->genc.plan(text, sin, c->st, outs, &bst);
-    else c->enc.plan(text, sin, opt.block_size_100k, c->st, outs, &bst);
+    const std::vector<uint64_t> cuts = !gzip && split_ok ? lane_cuts(si, tbytes, c->dev_lanes) : std::vector<uint64_t>();
+    const size_t nl = cuts.size();
+    std::vector<starch_ctx*> ln(nl);
+    std::vector<std::vector<bz::StreamOut>> lo(nl);   // each lane's streams (offsets from its own base)
+    std::vector<bz::Stats> lst(nl);
+    std::vector<uint64_t> lbase(nl, 0);                // lane i's first byte after `base`
+    if (gzip) {
+        c->genc.plan(text, sin, c->st, outs, &bst);
+    } else if (nl) {
+        std::vector<int> code(nl, 0);
+        std::vector<std::string> msg(nl);
+        std::vector<std::vector<bz::StreamIn>> li(nl);
+        for (size_t i = 0; i < nl; ++i) {
+            ln[i] = lane_ctx(c, (int)i);
+            const uint64_t s0 = cuts[i], s1 = i + 1 < nl ? cuts[i + 1] : nseg;
+            li[i].assign(sin.begin() + s0, sin.begin() + s1);
+            for (auto& x : li[i]) x.group -= (uint32_t)s0;
+        }
+        auto plan_lane = [&](size_t i) {
+            try {
+                Ctx g(ln[i]);
+                ln[i]->enc.plan(text, li[i], opt.block_size_100k, ln[i]->st, lo[i], &lst[i]);
+            } catch (const StarchError& e) {
+                code[i] = e.code;
+                msg[i] = e.what();
+            } catch (const std::exception& e) {
+                code[i] = STARCH_ERR_INTERNAL;
+                msg[i] = e.what();
+            }
+        };
+        for (size_t i = 1; i < nl; ++i) HIP_CHECK(hipStreamWaitEvent(ln[i]->st, e1, 0));   // the text is written
+        for (size_t i = 1; i < nl; ++i) ln[i]->worker.start([&plan_lane, i] { plan_lane(i); });
+        plan_lane(0);
+        for (size_t i = 1; i < nl; ++i) ln[i]->worker.wait();
+        for (size_t i = 0; i < nl; ++i)
+            if (code[i]) {
+                for (size_t j = 1; j < nl; ++j) (void)hipStreamSynchronize(ln[j]->st);
+                throw StarchError(code[i], msg[i]);
+            }
+        uint64_t end = 0;
+        for (size_t i = 0; i < nl; ++i) {
+            lbase[i] = end;
+            uint64_t b = 0;
+            for (auto o : lo[i]) {
+                b = std::max(b, o.out_off + o.bytes);
+                o.out_off += end;
+                outs.push_back(o);
+            }
+            end += b;
+            if (i) merge_counters(lst[0], lst[i]);
+        }
+        bst = lst[0];
+    } else {
+        c->enc.plan(text, sin, opt.block_size_100k, c->st, outs, &bst);
+    }
     finish_names(c, pnames);
     uint64_t streams_bytes = 0;
     for (auto& o : outs) streams_bytes = std::max(streams_bytes, o.out_off + o.bytes);
@@ -400,8 +521,17 @@ void encode_units(starch_ctx* c, const uint8_t* d_base, const std::vector<UnitIn
                                   256);
     uint8_t* out = (lay == L_ARCHIVE ? c->archive : c->part).as<uint8_t>(cap);
     if (lay == L_ARCHIVE) HIP_CHECK(hipMemcpyAsync(out, kMagic, 4, hipMemcpyHostToDevice, c->st));
-    if (gzip) c->genc.emit(out, cap, base, outs, c->st, &bst);
-    else c->enc.emit(out, cap, base, outs, c->st, &bst);
+    if (gzip) {
+        c->genc.emit(out, cap, base, outs, c->st, &bst);
+    } else if (nl) {   // (plan left the lanes' streams idle: every lane's emit goes on this one, in order)
+        uint64_t s = 0;
+        for (size_t i = 0; i < nl; ++i) {
+            ln[i]->enc.emit(out, cap, base + lbase[i], lo[i], c->st, &lst[i]);
+            for (auto& o : lo[i]) outs[s++].combined_crc = o.combined_crc;
+        }
+    } else {
+        c->enc.emit(out, cap, base, outs, c->st, &bst);
+    }
     for (uint64_t s = 0; s < nseg; ++s) c->segs[s].combined_crc = outs[s].combined_crc;
     uint64_t total = index_off;
     std::string idx;
@@ -417,7 +547,13 @@ void encode_units(starch_ctx* c, const uint8_t* d_base, const std::vector<UnitIn
     }
     HIP_CHECK(hipEventRecord(e2, c->st));
     HIP_CHECK(hipStreamSynchronize(c->st));
-    if (!gzip) c->enc.resolve_timers(&bst);
+    if (nl) {
+        std::vector<bz::Encoder::Interval> iv;
+        for (size_t i = 0; i < nl; ++i) ln[i]->enc.take_intervals(e1, iv);
+        stage_union(iv, bst);
+    } else if (!gzip) {
+        c->enc.resolve_timers(&bst);
+    }
     float ms_t = 0, ms_all = 0;
     HIP_CHECK(hipEventElapsedTime(&ms_t, e0, e1));
     HIP_CHECK(hipEventElapsedTime(&ms_all, e0, e2));
@@ -444,7 +580,7 @@ void encode_units(starch_ctx* c, const uint8_t* d_base, const std::vector<UnitIn
 void encode_device(starch_ctx* c, const uint8_t* d_bed, uint64_t n, const starch_options& opt)
 {
     std::vector<UnitIn> u(1, UnitIn{0, n, 0, 0, 0});
-    encode_units(c, d_bed, u, opt, L_ARCHIVE);
+    encode_units(c, d_bed, u, opt, L_ARCHIVE, false, true);
 }
 
 // Pipelined encode of pinned host bytes (the one-call host path).  The input
@@ -1477,6 +1613,13 @@ int starch_set_stream(starch_ctx* c, void* s)
     return STARCH_OK;
 }
 
+int starch_set_lanes(starch_ctx* c, int lanes)
+{
+    if (!c || lanes < 0 || lanes > 8) return STARCH_ERR_ARG;
+    c->dev_lanes = lanes;
+    return STARCH_OK;
+}
+
 int starch_use_own_stream(starch_ctx* c)
 {
     if (!c) return STARCH_ERR_ARG;
@@ -1583,7 +1726,7 @@ int starch_encode_units_device(starch_ctx* c, const void* d_base, const starch_u
     std::vector<UnitIn> u;
     int rc = units_in(units, unit_ids, nunits, u);
     if (rc) return rc;
-    encode_units(c, static_cast<const uint8_t*>(d_base), u, o, L_STREAMS);
+    encode_units(c, static_cast<const uint8_t*>(d_base), u, o, L_STREAMS, false, true);
     return STARCH_OK;
     END_GUARD(c)
 }

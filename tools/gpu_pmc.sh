@@ -7,6 +7,10 @@ set -o pipefail
 mkdir -p gpurun_out/pmc
 ROOT=${GRAFT_REPO_ROOT:-$(pwd)}
 cd /tmp && export TMPDIR=/tmp
+# one encoder lane (starch_set_lanes): per-kernel durations and counters not
+# shared with a concurrent lane, and bench.py then runs no extra one-lane steps
+# (the steps traced are exactly the ones asked for)
+export STARCH_DEV_LANES=${STARCH_DEV_LANES:-1}
 LINES=${LINES:-20000000}
 PASSES=${PASSES:-sq1 sq2 fetch write}
 run() {   # name, counters...

@@ -6,6 +6,10 @@ set -o pipefail
 ROOT=${GRAFT_REPO_ROOT:-$(pwd)}
 mkdir -p $ROOT/gpurun_out/prof $ROOT/gpurun_out/pmc
 cd /tmp && export TMPDIR=/tmp
+# one encoder lane (starch_set_lanes): per-kernel durations and counters not
+# shared with a concurrent lane, and bench.py then runs no extra one-lane steps
+# (the steps traced are exactly the ones asked for)
+export STARCH_DEV_LANES=${STARCH_DEV_LANES:-1}
 BA=${BENCH_ARGS:---steps 2 --warmup 1}
 timeout -k 10 ${TP:-300} rocprofv3 --kernel-trace --stats -d $ROOT/gpurun_out/prof -o run --output-format csv -- \
     python3 $ROOT/bench.py $BA --no-cpu-baseline --no-verify --no-e2e > $ROOT/gpurun_out/prof.log 2>&1 \

@@ -30,7 +30,7 @@ fi
 for v in ${VARIANTS:-}; do
   name=${v//=/_}
   rm -rf $O/prof_$name
-  ( cd /tmp && export TMPDIR=/tmp && if [ "$v" != base ]; then export STARCH_$v; fi
+  ( cd /tmp && export TMPDIR=/tmp && export STARCH_DEV_LANES=${STARCH_DEV_LANES:-1} && if [ "$v" != base ]; then export STARCH_$v; fi
     timeout -k 10 ${TP:-300} rocprofv3 --kernel-trace --stats -d $O/prof_$name -o run --output-format csv -- \
       python3 $ROOT/bench.py --steps 2 --warmup 1 ${PROF_ARGS:-} --no-cpu-baseline --no-e2e > $O/prof_$name.log 2>&1 ) \
       || { tail -20 $O/prof_$name.log; exit 1; }
