@@ -120,14 +120,12 @@ void Encoder::plan(const uint8_t* d_text, const std::vector<StreamIn>& streams, 
     uint32_t* d_carry = b_tile_carry.as<uint32_t>(ntiles + 1);
     uint32_t* d_tw = b_tile_w.as<uint32_t>(ntiles + 1);
     uint64_t* d_twpre = b_tile_wpre.as<uint64_t>(ntiles + 1);
-    uint8_t* d_tpos = b_tpos.as<uint8_t>(ntiles * kTB + 16);            // tile-aligned
     uint64_t* d_scal = b_scal.as<uint64_t>(nstreams_ + 16);
     HIP_CHECK(hipMemsetAsync(d_twpre, 0, (ntiles + 1) * sizeof(uint64_t), st));
     if (ntiles) {
         rle_tiles(d_tile0, d_streams, nstreams_, ntiles, d_tiles, st);
         rle_sum(d_text, d_tiles, ntiles, d_sums, st);
-        rle_carry(d_tile0, nstreams_, d_sums, d_carry, st);
-        rle_pos(d_text, d_tiles, ntiles, d_carry, d_tpos, d_tw, st);
+        rle_carry(d_tile0, nstreams_, d_sums, d_carry, d_tw, st);
         scan::excl_sum_u32_to_u64(d_tw, d_twpre, ntiles, d_twpre + ntiles, b_tmp, st);
     }
     // block-descriptor slots per stream from an upper bound on its RLE1 size
@@ -141,19 +139,19 @@ void Encoder::plan(const uint8_t* d_text, const std::vector<StreamIn>& streams, 
     uint32_t* d_nblk = reinterpret_cast<uint32_t*>(d_slot0 + nstreams_ + 1);
     HIP_CHECK(hipMemcpyAsync(d_slot0, slot0.data(), (nstreams_ + 1) * sizeof(uint64_t), hipMemcpyHostToDevice, st));
     BlockDesc* d_btmp = b_blk_tmp.as<BlockDesc>(nb_max + 1);
-    rle_cut(d_streams, d_tile0, d_twpre, d_tpos, nstreams_, nblock_max, d_slot0, d_btmp, d_nblk, st);
+    rle_cut(d_streams, d_tile0, d_twpre, d_text, d_carry, nstreams_, nblock_max, d_slot0, d_btmp, d_nblk, st);
     // first block of every stream and the block count, on the device; the
     // block arrays are sized by the bound, the counts read back once below
     uint32_t* d_first = reinterpret_cast<uint32_t*>(b_souts.as<uint64_t>(nstreams_ + 2));
     uint32_t* d_nb = d_first + nstreams_;
     rle_block_first(d_nblk, nstreams_, d_first, d_nb, st);
     BlockDesc* d_blocks = b_blk.as<BlockDesc>(nb_max + 1);
-    // tile -> block of its first byte, in the (dead after rle_pos) carry array
-    uint32_t* d_tile_block = d_carry;
+    // tile -> block of its first byte
+    uint32_t* d_tile_block = b_tile_block.as<uint32_t>(ntiles + 1);
     rle_compact(d_btmp, d_slot0, d_nblk, d_first, nstreams_, d_blocks, d_streams, d_tile0, d_tile_block, st);
     uint8_t* d_blkbytes = b_blkbytes.as<uint8_t>(nb_max * blk_stride_ + 64);
     if (ntiles) {
-        rle_emit(d_text, d_tiles, ntiles, d_twpre, d_tile0, d_tpos, d_streams, d_first, d_nblk, d_tile_block, d_blocks,
+        rle_emit(d_text, d_tiles, ntiles, d_twpre, d_tile0, d_carry, d_streams, d_first, d_nblk, d_tile_block, d_blocks,
                  d_blkbytes, blk_stride_, st);
     }
     rle_crc(d_text, d_blocks, (uint32_t)nb_max, d_nb, b_crc.as<uint32_t>(nb_max * kCrcMaxChunks), st);

@@ -17,6 +17,8 @@ struct TileDesc {                     // a <= 4 KiB slice of one stream
 struct TileSum {                      // run summary of a tile
     uint32_t len, trail;
     uint8_t first, last, uni, pad;
+    uint32_t lead;                    // bytes before its first change (the run it continues)
+    uint32_t wrest;                   // RLE1 size of the bytes from its first change on
 };
 
 struct Tables {                       // per-block Huffman state (bz:compress.c:238-598)
@@ -156,16 +158,16 @@ void upload_crc_constants();
 void rle_tiles(const uint64_t* tile0, const StreamIn* streams, uint32_t ns, uint64_t ntiles, TileDesc* tiles,
                hipStream_t st);
 void rle_sum(const uint8_t* text, const TileDesc* tiles, uint64_t ntiles, TileSum* sums, hipStream_t st);
-void rle_carry(const uint64_t* tile0, uint32_t ns, const TileSum* sums, uint32_t* carry, hipStream_t st);
-void rle_pos(const uint8_t* text, const TileDesc* tiles, uint64_t ntiles, const uint32_t* carry, uint8_t* tpos,
-             uint32_t* tile_w, hipStream_t st);
+void rle_carry(const uint64_t* tile0, uint32_t ns, const TileSum* sums, uint32_t* carry, uint32_t* tile_w,
+               hipStream_t st);
 void rle_stream_w(const uint64_t* tile0, const uint64_t* wpre, uint32_t ns, uint64_t* out, hipStream_t st);
-void rle_cut(const StreamIn* streams, const uint64_t* tile0, const uint64_t* wpre, const uint8_t* tpos, uint32_t ns,
-             uint32_t nblock_max, const uint64_t* slot0, BlockDesc* tmp, uint32_t* nblk, hipStream_t st);
+void rle_cut(const StreamIn* streams, const uint64_t* tile0, const uint64_t* wpre, const uint8_t* text,
+             const uint32_t* carry, uint32_t ns, uint32_t nblock_max, const uint64_t* slot0, BlockDesc* tmp,
+             uint32_t* nblk, hipStream_t st);
 void rle_compact(const BlockDesc* tmp, const uint64_t* slot0, const uint32_t* nblk, const uint32_t* first, uint32_t ns,
                  BlockDesc* out, const StreamIn* streams, const uint64_t* tile0, uint32_t* tile_block, hipStream_t st);
 void rle_emit(const uint8_t* text, const TileDesc* tiles, uint64_t ntiles, const uint64_t* wpre, const uint64_t* tile0,
-              const uint8_t* tpos, const StreamIn* streams, const uint32_t* first, const uint32_t* nblk,
+              const uint32_t* carry, const StreamIn* streams, const uint32_t* first, const uint32_t* nblk,
               const uint32_t* tile_block, BlockDesc* blocks, uint8_t* blk, uint64_t stride, hipStream_t st);
 constexpr uint32_t kCrcMaxChunks = 128;       // per block (k_crc_chunks)
 void rle_block_first(const uint32_t* nblk, uint32_t ns, uint32_t* first, uint32_t* total, hipStream_t st);

@@ -1,23 +1,30 @@
 // starch_amd/csrc/bz2_rle.hip -- RLE1, block cut and block CRC on MI355X.
 //
 // Restates bzip2-1.0.6's input side (bz:bzlib.c:224-338, 369-412) as
-// data-parallel passes over 4 KiB tiles of a stream's bytes:
-//   1. k_rle_sum    per-tile run summary (first/last byte, uniform, trailing run)
-//   2. k_rle_carry  per-stream sequential fold -> run length entering each tile
-//   3. k_rle_pos    per-byte RLE1 chunk position t = (position in run) mod 255
-//                   and per-tile RLE1 output size (a chunk of L bytes emits
-//                   min(L,4) copies + one count byte when L >= 4)
-//   4. k_cut        per-stream greedy block cut over the RLE1 size prefix:
+// data-parallel passes over 4 KiB tiles of a stream's bytes.  A byte's RLE1
+// chunk position t = (position in its run) mod 255 decides its output: a
+// chunk of L bytes emits min(L,4) copies + one count byte when L >= 4, so t < 3
+// weighs 1, t == 3 weighs 2 (its copy + the count), t > 3 nothing.
+//   1. k_rle_sum    per-tile run summary (first/last byte, uniform, trailing
+//                   run, the leading run's length) and the RLE1 size of the
+//                   bytes from the tile's first change on (their run positions
+//                   are known inside the tile)
+//   2. k_rle_carry  per-stream fold -> run position entering each tile, and
+//                   the tile's RLE1 size (its leading run's weight in closed
+//                   form from that position)
+//   3. k_cut        per-stream greedy block cut over the RLE1 size prefix:
 //                   chunk k joins the block iff the block holds < nblockMAX
 //                   bytes before it (bz:bzlib.c:307,399-402); the final chunk
 //                   joins a full block only when it is a single byte supplied
 //                   with the finishing call (bz:bzlib.c:393-397)
-//   5. k_rle_emit   materialise each block's RLE1 bytes + inUse map
-//   6. k_crc_chunks + k_crc_final
+//   4. k_rle_emit   materialise each block's RLE1 bytes + inUse map
+//   5. k_crc_chunks + k_crc_final
 //                   CRC-32/BZIP2 of each block's input bytes: slice-by-4 CRC of
 //                   16-byte strips, GF(2) combine of strips -> chunks -> block
-// Every lane handles one 16-byte strip, loaded with one or two aligned 16-B
-// loads (any text alignment); tpos is stored tile-aligned (tile t at t*4096).
+// The per-byte chunk positions are never stored: k_cut (one tile per block)
+// and k_rle_emit recompute them from the text and the tile's entering run
+// position.  Every lane handles one 16-byte strip, loaded with one or two
+// aligned 16-B loads (any text alignment).
 #include "bz2_int.hpp"
 #include <atomic>
 
@@ -181,12 +188,68 @@ __device__ __forceinline__ void load_strip(const uint8_t* text, const TileDesc& 
     pb = off > 0 && cnt > 0 ? (uint32_t)text[d.beg + off - 1] : (v.x & 0xffu);
 }
 
+__device__ __forceinline__ int first_change(const uint32_t (&m)[4])   // index (0..15) of the first changed byte, or -1
+{
+    return m[0] ? ((__builtin_ctz(m[0]) - 7) >> 3)
+         : m[1] ? 4 + ((__builtin_ctz(m[1]) - 7) >> 3)
+         : m[2] ? 8 + ((__builtin_ctz(m[2]) - 7) >> 3)
+         : m[3] ? 12 + ((__builtin_ctz(m[3]) - 7) >> 3) : -1;
+}
+
+__device__ __forceinline__ uint32_t rle_w(uint32_t t) { return t < 3 ? 1u : (t == 3 ? 2u : 0u); }
+
+// Chunk positions t of a lane's strip (bytes off .. off + cnt - 1 of a tile),
+// packed 4 per word into tw; returns the strip's RLE1 weight.  ex = the
+// tile's last change before the strip + 1 (0: none); the bytes before the
+// tile's first change continue the run entering the tile at position c
+// (KNOWN), or (!KNOWN) are left out of the weight.  One modulo per strip,
+// then t steps by one (wrapping at 255) or restarts at a change.
+template <bool KNOWN>
+__device__ __forceinline__ uint32_t strip_t(const uint32_t (&m)[4], uint32_t off, int cnt, uint32_t ex, uint32_t c,
+                                            uint32_t (&tw)[4])
+{
+    uint32_t tp = ex ? (off - ex) % 255u : (KNOWN ? (c + off + 254u) % 255u : 0u);   // t of byte off - 1
+    bool lead = ex == 0;
+    uint32_t w = 0;
+#pragma unroll
+    for (int q = 0; q < 4; ++q) tw[q] = 0;
+#pragma unroll
+    for (int k = 0; k < 16; ++k) {
+        if (k < cnt) {
+            const bool chg = ((m[k >> 2] >> (8 * (k & 3) + 7)) & 1u) != 0;
+            lead = lead && !chg;
+            const uint32_t t = chg ? 0u : (tp == 254u ? 0u : tp + 1u);
+            tw[k >> 2] |= t << (8 * (k & 3));
+            if (KNOWN || !lead) w += rle_w(t);
+            tp = t;
+        }
+    }
+    return w;
+}
+
+// the tile's last change before this lane's strip + 1 (0: none), from every
+// lane's last change (x = position + 1, 0: none); msh: 4 words of LDS.  Ends
+// with a barrier.
+__device__ __forceinline__ uint32_t tile_ex(uint32_t x, uint32_t* msh)
+{
+    const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
+    const uint32_t incl = wave_incl_scan_max<uint32_t>(x);
+    uint32_t ex = (uint32_t)__shfl_up((int)incl, 1, 64);
+    if (lane == 0) ex = 0;
+    if (lane == 63) msh[wid] = incl;
+    __syncthreads();
+    for (int w = 0; w < wid; ++w) ex = msh[w] > ex ? msh[w] : ex;
+    return ex;
+}
+
 __global__ void __launch_bounds__(256) k_rle_sum(const uint8_t* __restrict__ text, const TileDesc* __restrict__ tiles,
                                                   TileSum* __restrict__ sums)
 {
-    __shared__ int wsh[4];
+    __shared__ uint32_t msh[4], fsh[4];
+    __shared__ uint32_t wsh[5];
     const TileDesc d = tiles[blockIdx.x];
     const int off = threadIdx.x * 16;
+    const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
     int cnt = (int)d.len - off;
     cnt = cnt < 0 ? 0 : (cnt > 16 ? 16 : cnt);
     uint4 v;
@@ -194,15 +257,26 @@ __global__ void __launch_bounds__(256) k_rle_sum(const uint8_t* __restrict__ tex
     load_strip(text, d, off, cnt, v, pb);
     uint32_t m[4];
     chg_mask(v, pb, cnt, m);
-    const int lc = last_change(m);
-    // tile's last change: max over the workgroup (+1 so "none" is 0)
-    uint32_t x = lc >= 0 ? (uint32_t)(off + lc + 1) : 0u;
-    x = (uint32_t)__builtin_amdgcn_readlane((int)wave_incl_scan_max<uint32_t>(x), 63);
-    if ((threadIdx.x & 63) == 0) wsh[threadIdx.x >> 6] = (int)x;
-    __syncthreads();
+    const int lc = last_change(m), fc = first_change(m);
+    // the tile's first change (its leading run's length), a wave minimum per wave
+    uint32_t f = fc >= 0 ? (uint32_t)(off + fc) : 0xFFFFFFFFu;
+#pragma unroll
+    for (int dd = 32; dd >= 1; dd >>= 1) {
+        const uint32_t o = (uint32_t)__shfl_xor((int)f, dd, 64);
+        f = o < f ? o : f;
+    }
+    if (lane == 0) fsh[wid] = f;
+    const uint32_t ex = tile_ex(lc >= 0 ? (uint32_t)(off + lc + 1) : 0u, msh);
+    uint32_t tw[4];
+    const uint32_t w = strip_t<false>(m, (uint32_t)off, cnt, ex, 0u, tw);
+    uint32_t tot = 0;
+    (void)block_excl_scan_add<uint32_t>(w, wsh, &tot);   // (barriers: fsh, msh complete)
     if (threadIdx.x == 0) {
-        uint32_t p = 0;
-        for (int w = 0; w < 4; ++w) p = (uint32_t)wsh[w] > p ? (uint32_t)wsh[w] : p;
+        uint32_t p = 0, fl = 0xFFFFFFFFu;
+        for (int q = 0; q < 4; ++q) {
+            p = msh[q] > p ? msh[q] : p;
+            fl = fsh[q] < fl ? fsh[q] : fl;
+        }
         TileSum o;
         o.len = d.len;
         o.first = d.len ? text[d.beg] : (uint8_t)0xff;
@@ -210,8 +284,24 @@ __global__ void __launch_bounds__(256) k_rle_sum(const uint8_t* __restrict__ tex
         o.uni = p == 0 ? 1 : 0;
         o.trail = p == 0 ? d.len : d.len - (p - 1);
         o.pad = 0;
+        o.lead = fl == 0xFFFFFFFFu ? d.len : fl;
+        o.wrest = tot;
         sums[blockIdx.x] = o;
     }
+}
+
+// RLE1 size of a run's L bytes starting at chunk position c: how many of
+// them sit at positions 0, 1, 2 (weight 1) and 3 (weight 2) mod 255
+__device__ __forceinline__ uint32_t lead_w(uint32_t c, uint32_t L)
+{
+    const uint32_t q = L / 255u, r = L % 255u;
+    uint32_t w = 5u * q;
+#pragma unroll
+    for (uint32_t v = 0; v < 4; ++v) {
+        const uint32_t dv = (v + 255u - c) % 255u;   // offset of the first byte at position v
+        if (dv < r) w += v == 3 ? 2u : 1u;
+    }
+    return w;
 }
 
 // one 256-thread workgroup per stream: run length entering each tile, via an
@@ -240,7 +330,8 @@ __device__ __forceinline__ RunSum64 rs64_combine(const RunSum64& A, const RunSum
 // summaries instead of a barrier-bound scan per 256 tiles
 constexpr int CT = 1024;
 __global__ void __launch_bounds__(CT) k_rle_carry(const uint64_t* __restrict__ seg_tile0, uint32_t nstreams,
-                                                   const TileSum* __restrict__ sums, uint32_t* __restrict__ carry)
+                                                   const TileSum* __restrict__ sums, uint32_t* __restrict__ carry,
+                                                   uint32_t* __restrict__ tile_w)
 {
     __shared__ RunSum64 sh[CT];
     const uint32_t s = blockIdx.x;
@@ -270,69 +361,12 @@ __global__ void __launch_bounds__(CT) k_rle_carry(const uint64_t* __restrict__ s
     else { P.len = 0; P.trail = 0; P.first = P.last = -1; P.uni = 1; P.pad = 0; }
     for (uint64_t t = a; t < e; ++t) {
         const RunSum64 S = load(t);
-        carry[t] = (t > t0 && P.len > 0 && P.last == S.first) ? (uint32_t)(P.trail % 255u) : 0u;
+        const uint32_t c = (t > t0 && P.len > 0 && P.last == S.first) ? (uint32_t)(P.trail % 255u) : 0u;
+        carry[t] = c;
+        tile_w[t] = sums[t].wrest + lead_w(c, sums[t].lead);
         P = rs64_combine(P, S);
     }
 }
-
-__device__ __forceinline__ uint32_t rle_w(uint32_t t) { return t < 3 ? 1u : (t == 3 ? 2u : 0u); }
-
-__global__ void __launch_bounds__(256) k_rle_pos(const uint8_t* __restrict__ text, const TileDesc* __restrict__ tiles,
-                                                  const uint32_t* __restrict__ carry, uint8_t* __restrict__ tpos,
-                                                  uint32_t* __restrict__ tile_w)
-{
-    __shared__ uint32_t msh[4];
-    __shared__ uint32_t wsh[5];
-    const TileDesc d = tiles[blockIdx.x];
-    const int off = threadIdx.x * 16;
-    const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
-    int cnt = (int)d.len - off;
-    cnt = cnt < 0 ? 0 : (cnt > 16 ? 16 : cnt);
-    uint4 v;
-    uint32_t pb;
-    load_strip(text, d, off, cnt, v, pb);
-    uint32_t m[4];
-    chg_mask(v, pb, cnt, m);
-    const int lc = last_change(m);
-    // last change before this strip: exclusive prefix max over the workgroup
-    // (positions + 1, 0 = none)
-    const uint32_t x = lc >= 0 ? (uint32_t)(off + lc + 1) : 0u;
-    const uint32_t incl = wave_incl_scan_max<uint32_t>(x);
-    uint32_t ex = (uint32_t)__shfl_up((int)incl, 1, 64);
-    if (lane == 0) ex = 0;
-    if (lane == 63) msh[wid] = incl;
-    __syncthreads();
-    for (int w = 0; w < wid; ++w) ex = msh[w] > ex ? msh[w] : ex;
-    // run position of each byte: since the last change, or from the run
-    // carried into the tile when there is none
-    const uint32_t c = carry[blockIdx.x];
-    uint32_t w = 0;
-    uint32_t tw[4] = {0, 0, 0, 0};
-    uint32_t last = ex;                                   // last change + 1 (0 = none)
-#pragma unroll
-    for (int k = 0; k < 16; ++k) {
-        if (k < cnt) {
-            if ((m[k >> 2] >> (8 * (k & 3) + 7)) & 1u) last = (uint32_t)(off + k + 1);
-            const uint32_t y = (uint32_t)(off + k);
-            const uint32_t run = last ? y + 1 - last : c + y;
-            const uint32_t t = run % 255u;
-            tw[k >> 2] |= t << (8 * (k & 3));
-            w += rle_w(t);
-        }
-    }
-    *reinterpret_cast<uint4*>(tpos + (uint64_t)blockIdx.x * kTB + off) = make_uint4(tw[0], tw[1], tw[2], tw[3]);
-    uint32_t tot;
-    (void)block_excl_scan_add<uint32_t>(w, wsh, &tot);
-    if (threadIdx.x == 0) tile_w[blockIdx.x] = tot;
-}
-
-// RLE1 size prefix (stream-relative) at text position x of stream s
-struct WView {
-    const uint64_t* tile_wpre;
-    const uint8_t* tpos;
-    uint64_t beg, end, t0, w0;
-    __device__ uint64_t tile_w_at(uint64_t t) const { return tile_wpre[t] - w0; }
-};
 
 __global__ void k_stream_w(const uint64_t* __restrict__ seg_tile0, const uint64_t* __restrict__ tile_wpre,
                            uint32_t nstreams, uint64_t* __restrict__ out)
@@ -341,21 +375,76 @@ __global__ void k_stream_w(const uint64_t* __restrict__ seg_tile0, const uint64_
     if (s < nstreams) out[s] = tile_wpre[seg_tile0[s + 1]] - tile_wpre[seg_tile0[s]];
 }
 
+// Chunk positions t of K consecutive bytes per lane (lane l: bytes p0 + K*l +
+// k, packed 4 per word), one wave: tin = t of byte p0 - 1 and bin its value
+// (p0 starting a stream: tin 254, bin = text[p0]).  Bytes at or past lim get
+// t = 1 (no chunk starts there; the callers give them no weight).
+template <int K>
+__device__ __forceinline__ void run_t(const uint8_t* __restrict__ text, uint64_t p0, uint64_t lim, uint32_t tin,
+                                      uint32_t bin, uint32_t (&tw)[K / 4])
+{
+    const int lane = threadIdx.x & 63;
+    const uint64_t a = p0 + (uint64_t)K * (uint64_t)lane;
+    uint32_t w[K / 4];
+    if constexpr (K >= 16) {
+#pragma unroll
+        for (int i = 0; i < K / 16; ++i) {
+            const uint64_t p = a + 16u * (uint64_t)i;
+            const uint4 v = p < lim ? load16u(text + p, text + lim) : make_uint4(0, 0, 0, 0);
+            w[4 * i] = v.x; w[4 * i + 1] = v.y; w[4 * i + 2] = v.z; w[4 * i + 3] = v.w;
+        }
+    } else {
+        static_assert(K == 4, "run_t: K = 4 or a multiple of 16");
+        w[0] = 0;
+#pragma unroll
+        for (int k = 0; k < 4; ++k)
+            if (a + k < lim) w[0] |= (uint32_t)text[a + k] << (8 * k);
+    }
+    uint32_t carry = (uint32_t)__shfl_up((int)(w[K / 4 - 1] >> 24), 1, 64);
+    if (lane == 0) carry = bin & 0xffu;
+    uint32_t m[K / 4];
+    int lc = -1;
+#pragma unroll
+    for (int i = 0; i < K / 4; ++i) {
+        const uint32_t sh = (w[i] << 8) | carry;
+        carry = w[i] >> 24;
+        const uint64_t pi = a + 4u * (uint64_t)i;
+        const int lim_i = pi >= lim ? 0 : (lim - pi >= 4 ? 4 : (int)(lim - pi));
+        const uint32_t keep = lim_i >= 4 ? 0x80808080u : (lim_i <= 0 ? 0u : (0x80808080u >> (8 * (4 - lim_i))));
+        m[i] = nonzero_bytes(w[i] ^ sh) & keep;
+        if (m[i]) lc = 4 * i + ((31 - __clz((int)m[i])) >> 3);
+    }
+    const uint32_t x = lc >= 0 ? (uint32_t)(K * lane + lc + 1) : 0u;   // last change + 1, relative to p0
+    const uint32_t incl = wave_incl_scan_max<uint32_t>(x);
+    uint32_t ex = (uint32_t)__shfl_up((int)incl, 1, 64);
+    if (lane == 0) ex = 0;
+    uint32_t tp = ex ? ((uint32_t)(K * lane) - ex) % 255u : (tin + (uint32_t)(K * lane)) % 255u;   // t of byte a - 1
+#pragma unroll
+    for (int q = 0; q < K / 4; ++q) tw[q] = 0;
+#pragma unroll
+    for (int k = 0; k < K; ++k) {
+        const bool chg = ((m[k >> 2] >> (8 * (k & 3) + 7)) & 1u) != 0;
+        const uint32_t t = chg ? 0u : (tp == 254u ? 0u : tp + 1u);
+        tw[k >> 2] |= (a + k < lim ? t : 1u) << (8 * (k & 3));
+        tp = t;
+    }
+}
+
 // one wave per stream: greedy cut (see file header).  Per block: binary search
-// of the tile where the RLE1 size crosses nblockMAX, a 64-lane scan of that
-// tile's byte weights for the crossing byte q, then a ballot over the next 256
+// of the tile where the RLE1 size crosses nblockMAX, the chunk positions of
+// that tile (run_t, from its entering run position) and a 64-lane scan of
+// their weights for the crossing byte q, then a ballot over the next 256
 // bytes for the first chunk start p >= q (chunks are at most 255 bytes).
 __global__ void __launch_bounds__(64) k_cut(const StreamIn* __restrict__ streams, const uint64_t* __restrict__ seg_tile0,
-                                             const uint64_t* __restrict__ tile_wpre, const uint8_t* __restrict__ tpos_t,
-                                             uint32_t nstreams, uint32_t nblock_max, const uint64_t* __restrict__ slot0,
-                                             BlockDesc* __restrict__ tmp, uint32_t* __restrict__ nblk)
+                                             const uint64_t* __restrict__ tile_wpre, const uint8_t* __restrict__ text,
+                                             const uint32_t* __restrict__ carry, uint32_t nstreams, uint32_t nblock_max,
+                                             const uint64_t* __restrict__ slot0, BlockDesc* __restrict__ tmp,
+                                             uint32_t* __restrict__ nblk)
 {
     const uint32_t s = blockIdx.x;
     const int lane = threadIdx.x;
     const uint64_t beg = streams[s].text_off, end = beg + streams[s].text_len;
     const uint64_t t0 = seg_tile0[s], t1 = seg_tile0[s + 1];
-    // tile-aligned tpos: text position y of this stream -> tile t0 + (y-beg)/kTB
-    const uint8_t* tpos = tpos_t + t0 * kTB - beg;
     const uint64_t w0 = tile_wpre[t0], wend = tile_wpre[t1] - w0;
     const bool frj = streams[s].final_run_joins != 0;
     uint64_t bs = beg, wbs = 0;
@@ -392,25 +481,18 @@ __global__ void __launch_bounds__(64) k_cut(const StreamIn* __restrict__ streams
                 if (tile_wpre[mid] - w0 < target) lo = mid; else hi = mid;
             }
             uint64_t q = 0, Wq = 0;
+            uint32_t tq = 0;                 // chunk position of byte q - 1
             for (;;) {   // normally one iteration
                 const uint64_t tstart = beg + (lo - t0) * kTB;
                 uint64_t tend = tstart + kTB;
                 if (tend > end) tend = end;
                 const uint64_t y0 = tstart < bs ? bs : tstart;
                 const uint64_t W0 = tstart < bs ? wbs : tile_wpre[lo] - w0;
-                // each lane: one 64-byte aligned stretch of the tile's tpos, in
-                // registers (four 16-B loads); bytes outside [y0, tend) weigh 0
-                const uint64_t a = beg + ((y0 - beg) & ~63ull) + (uint64_t)lane * 64;
+                // each lane: 64 bytes of the tile and their chunk positions in
+                // registers; bytes outside [y0, tend) weigh 0
+                const uint64_t a = tstart + (uint64_t)lane * 64;
                 uint32_t tw[16];
-                {
-                    const uint4* p4 = reinterpret_cast<const uint4*>(tpos + a);
-                    const bool in = a < tend;
-#pragma unroll
-                    for (int k = 0; k < 4; ++k) {
-                        const uint4 v = in ? p4[k] : make_uint4(0, 0, 0, 0);
-                        tw[4 * k] = v.x; tw[4 * k + 1] = v.y; tw[4 * k + 2] = v.z; tw[4 * k + 3] = v.w;
-                    }
-                }
+                run_t<64>(text, tstart, tend, (carry[lo] + 254u) % 255u, text[tstart], tw);
                 uint32_t ssum = 0;
 #pragma unroll
                 for (int k = 0; k < 64; ++k) {
@@ -422,6 +504,7 @@ __global__ void __launch_bounds__(64) k_cut(const StreamIn* __restrict__ streams
                 if (ball) {
                     const int L = __ffsll((unsigned long long)ball) - 1;
                     uint64_t x = a < y0 ? y0 : a, Wx = W0 + incl - ssum;
+                    uint32_t tx = 0;
                     {   // the crossing byte, from the registers: per-word weights
                         // by SWAR (rle_w = [t <= 3] + [t == 3]), then a walk over
                         // 16 words and 4 bytes instead of 64 bytes
@@ -452,34 +535,36 @@ __global__ void __launch_bounds__(64) k_cut(const StreamIn* __restrict__ streams
                             const uint32_t cj = (uint32_t)(__popc(le & upto(jsel + 1)) + __popc(eq & upto(jsel + 1)));
                             x = a + (uint64_t)(4 * wsel + jsel) + 1;
                             Wx = target - need + cj;
+                            tx = (tw[wsel] >> (8 * jsel)) & 0xffu;
                         }
                     }
                     q = __shfl(x, L, 64);
                     Wq = __shfl(Wx, L, 64);
+                    tq = (uint32_t)__shfl((int)tx, L, 64);
                     break;
                 }
                 ++lo;   // cannot happen when the tile search is exact; stay safe
                 if (lo >= t1) { q = end; Wq = wend; break; }
             }
             // the first chunk start p >= q (within 255 bytes) and the weight of
-            // [q, p): the 256 bytes after q in one round of loads
-            uint32_t tv[4];
-#pragma unroll
-            for (int r = 0; r < 4; ++r) {
-                const uint64_t pos = q + (uint64_t)r * 64 + lane;
-                tv[r] = pos < end ? tpos[pos] : 1u;
-            }
+            // [q, p): the chunk positions of the 256 bytes after q, four per lane
             uint64_t p = end;
-#pragma unroll
-            for (int r = 0; r < 4; ++r) {
-                const uint64_t hit = __ballot(tv[r] == 0);
-                if (hit) { p = q + (uint64_t)r * 64 + (__ffsll((unsigned long long)hit) - 1); break; }
-            }
             uint32_t part = 0;
+            if (q < end) {
+                uint32_t tv[1];
+                run_t<4>(text, q, end, tq, text[q - 1], tv);
+                const uint32_t zb = ~nonzero_bytes(tv[0]) & 0x80808080u;   // bytes with t == 0
+                const uint64_t hit = __ballot(zb != 0);
+                if (hit) {
+                    const int L = __ffsll((unsigned long long)hit) - 1;
+                    const uint32_t zl = (uint32_t)__shfl((int)zb, L, 64);
+                    p = q + 4u * (uint64_t)L + (uint64_t)((__builtin_ctz(zl) - 7) >> 3);
+                }
 #pragma unroll
-            for (int r = 0; r < 4; ++r) {
-                const uint64_t pos = q + (uint64_t)r * 64 + lane;
-                if (pos < p) part += rle_w(tv[r]);
+                for (int k = 0; k < 4; ++k) {
+                    const uint64_t pos = q + 4u * (uint64_t)lane + k;
+                    if (pos < p) part += rle_w((tv[0] >> (8 * k)) & 0xffu);
+                }
             }
             const uint64_t Wp = Wq + wave_reduce_add(part);
             if (p < end && !(frj && p == end - 1)) { block_end = p; wblock_end = Wp; }
@@ -555,13 +640,13 @@ __device__ __forceinline__ void copy_out(uint8_t* dst, const uint8_t* src, uint3
 __global__ void __launch_bounds__(256) k_rle_emit(const uint8_t* __restrict__ text, const TileDesc* __restrict__ tiles,
                                                    const uint64_t* __restrict__ tile_wpre,
                                                    const uint64_t* __restrict__ seg_tile0,
-                                                   const uint8_t* __restrict__ tpos, const StreamIn* __restrict__ streams,
+                                                   const uint32_t* __restrict__ carry, const StreamIn* __restrict__ streams,
                                                    const uint32_t* __restrict__ sfirst, const uint32_t* __restrict__ snblk,
                                                    const uint32_t* __restrict__ tile_block,
                                                    BlockDesc* __restrict__ blocks, uint8_t* __restrict__ blk,
                                                    uint64_t stride)
 {
-    __shared__ uint32_t wsh[5];
+    __shared__ uint32_t wsh[5], msh[4];
     __shared__ uint8_t ob[kTB + kTB / 4 + 16];      // the tile's RLE1 output (<= 5/4 of its bytes)
     // inUse bits per lane ([slot][word][lane]: no two lanes share a word, so no
     // serialised LDS atomics on the few words a text's bytes fall in)
@@ -575,13 +660,17 @@ __global__ void __launch_bounds__(256) k_rle_emit(const uint8_t* __restrict__ te
     int off = threadIdx.x * 16;
     int cnt = (int)d.len - off;
     cnt = cnt < 0 ? 0 : (cnt > 16 ? 16 : cnt);
-    // tpos of this stream, indexed by text position (tiles of a stream are consecutive)
-    const uint8_t* tp = tpos + (uint64_t)blockIdx.x * kTB - d.beg;
-    const uint4 tv = *reinterpret_cast<const uint4*>(tpos + (uint64_t)blockIdx.x * kTB + off);
-    const uint4 xv = cnt > 0 ? load16u(text + d.beg + off, text + d.beg + d.len) : make_uint4(0, 0, 0, 0);
-    uint32_t w = 0;
-#pragma unroll
-    for (int k = 0; k < 16; ++k) if (k < cnt) w += rle_w(byte16(tv, k));
+    // the strip's chunk positions, from the tile's changes and its entering run position
+    uint4 xv;
+    uint32_t pb;
+    load_strip(text, d, off, cnt, xv, pb);
+    uint32_t m[4];
+    chg_mask(xv, pb, cnt, m);
+    const int lc = last_change(m);
+    const uint32_t ex = tile_ex(lc >= 0 ? (uint32_t)(off + lc + 1) : 0u, msh);
+    uint32_t twd[4];
+    const uint32_t w = strip_t<true>(m, (uint32_t)off, cnt, ex, carry[blockIdx.x], twd);
+    const uint4 tv = make_uint4(twd[0], twd[1], twd[2], twd[3]);
     uint32_t tot = 0;
     const uint32_t pre = block_excl_scan_add<uint32_t>(w, wsh, &tot);   // contains __syncthreads
     const uint32_t b0 = bsel;
@@ -604,9 +693,12 @@ __global__ void __launch_bounds__(256) k_rle_emit(const uint8_t* __restrict__ te
             // through the byte loop
             if (t == 0) atomicOr(&ul[slot][c >> 5][threadIdx.x], 1u << (c & 31));
         } else if (t == 3) {
+            // the chunk's length: its bytes go on while they equal c, up to 255
+            // (its start i - 3 plus 254)
             const uint64_t i = d.beg + off + k;
+            const uint64_t jl = i + 252 < send ? i + 252 : send;
             uint64_t j = i + 1;
-            while (j < send && tp[j] != 0) ++j;
+            while (j < jl && text[j] == c) ++j;
             const uint32_t L = (uint32_t)(j - i) + 3;
             const uint8_t cnt_byte = (uint8_t)(L - 4);
             ob[o] = c;
@@ -748,23 +840,20 @@ void rle_sum(const uint8_t* text, const TileDesc* tiles, uint64_t ntiles, TileSu
 {
     hipLaunchKernelGGL(k_rle_sum, dim3((unsigned)ntiles), dim3(256), 0, st, text, tiles, sums);
 }
-void rle_carry(const uint64_t* tile0, uint32_t ns, const TileSum* sums, uint32_t* carry, hipStream_t st)
+void rle_carry(const uint64_t* tile0, uint32_t ns, const TileSum* sums, uint32_t* carry, uint32_t* tile_w,
+               hipStream_t st)
 {
-    hipLaunchKernelGGL(k_rle_carry, dim3(ns), dim3(CT), 0, st, tile0, ns, sums, carry);
-}
-void rle_pos(const uint8_t* text, const TileDesc* tiles, uint64_t ntiles, const uint32_t* carry, uint8_t* tpos,
-             uint32_t* tile_w, hipStream_t st)
-{
-    hipLaunchKernelGGL(k_rle_pos, dim3((unsigned)ntiles), dim3(256), 0, st, text, tiles, carry, tpos, tile_w);
+    hipLaunchKernelGGL(k_rle_carry, dim3(ns), dim3(CT), 0, st, tile0, ns, sums, carry, tile_w);
 }
 void rle_stream_w(const uint64_t* tile0, const uint64_t* wpre, uint32_t ns, uint64_t* out, hipStream_t st)
 {
     hipLaunchKernelGGL(k_stream_w, dim3(g1(ns, 64)), dim3(64), 0, st, tile0, wpre, ns, out);
 }
-void rle_cut(const StreamIn* streams, const uint64_t* tile0, const uint64_t* wpre, const uint8_t* tpos, uint32_t ns,
-             uint32_t nblock_max, const uint64_t* slot0, BlockDesc* tmp, uint32_t* nblk, hipStream_t st)
+void rle_cut(const StreamIn* streams, const uint64_t* tile0, const uint64_t* wpre, const uint8_t* text,
+             const uint32_t* carry, uint32_t ns, uint32_t nblock_max, const uint64_t* slot0, BlockDesc* tmp,
+             uint32_t* nblk, hipStream_t st)
 {
-    hipLaunchKernelGGL(k_cut, dim3(ns), dim3(64), 0, st, streams, tile0, wpre, tpos, ns, nblock_max, slot0, tmp,
+    hipLaunchKernelGGL(k_cut, dim3(ns), dim3(64), 0, st, streams, tile0, wpre, text, carry, ns, nblock_max, slot0, tmp,
                        nblk);
 }
 void rle_compact(const BlockDesc* tmp, const uint64_t* slot0, const uint32_t* nblk, const uint32_t* first, uint32_t ns,
@@ -774,10 +863,10 @@ void rle_compact(const BlockDesc* tmp, const uint64_t* slot0, const uint32_t* nb
                        tile_block);
 }
 void rle_emit(const uint8_t* text, const TileDesc* tiles, uint64_t ntiles, const uint64_t* wpre, const uint64_t* tile0,
-              const uint8_t* tpos, const StreamIn* streams, const uint32_t* first, const uint32_t* nblk,
+              const uint32_t* carry, const StreamIn* streams, const uint32_t* first, const uint32_t* nblk,
               const uint32_t* tile_block, BlockDesc* blocks, uint8_t* blk, uint64_t stride, hipStream_t st)
 {
-    hipLaunchKernelGGL(k_rle_emit, dim3((unsigned)ntiles), dim3(256), 0, st, text, tiles, wpre, tile0, tpos, streams,
+    hipLaunchKernelGGL(k_rle_emit, dim3((unsigned)ntiles), dim3(256), 0, st, text, tiles, wpre, tile0, carry, streams,
                        first, nblk, tile_block, blocks, blk, stride);
 }
 void rle_block_first(const uint32_t* nblk, uint32_t ns, uint32_t* first, uint32_t* total, hipStream_t st)
