@@ -125,7 +125,7 @@ public:
     };
 
 private:
-    DevBuf b_streams, b_tiles, b_tile_sum, b_tile_carry, b_tile_w, b_tile_wpre, b_tile_block, b_seg_tile0, b_seg_nblk,
+    DevBuf b_streams, b_tiles, b_tile_sum, b_tile_carry, b_tile_w, b_tile_wpre, b_tile_block, b_cut_tab, b_seg_tile0, b_seg_nblk,
         b_blk_tmp, b_blk, b_blkbytes, b_scal, b_tmp, b_bwt, b_mtfv, b_freq, b_sel, b_tabs, b_gbits, b_souts,
         b_fallback, b_bwt3, b_crc, b_dedupe, b_rep_bytes, b_rep_blk, b_last;
     PinnedBuf h_wtot_, h_nblk_, h_blocks_, h_hr_, h_last_;

@@ -139,7 +139,10 @@ void Encoder::plan(const uint8_t* d_text, const std::vector<StreamIn>& streams, 
     uint32_t* d_nblk = reinterpret_cast<uint32_t*>(d_slot0 + nstreams_ + 1);
     HIP_CHECK(hipMemcpyAsync(d_slot0, slot0.data(), (nstreams_ + 1) * sizeof(uint64_t), hipMemcpyHostToDevice, st));
     BlockDesc* d_btmp = b_blk_tmp.as<BlockDesc>(nb_max + 1);
-    rle_cut(d_streams, d_tile0, d_twpre, d_text, d_carry, nstreams_, nblock_max, d_slot0, d_btmp, d_nblk, st);
+    uint64_t max_slots = 0;
+    for (uint32_t s = 0; s < nstreams_; ++s) max_slots = std::max<uint64_t>(max_slots, slot0[s + 1] - slot0[s]);
+    rle_cut(d_streams, d_tile0, d_twpre, d_text, d_carry, nstreams_, nblock_max, d_slot0, nb_max, max_slots,
+            b_cut_tab.get(rle_cut_tab_bytes(nb_max)), d_btmp, d_nblk, st);
     // first block of every stream and the block count, on the device; the
     // block arrays are sized by the bound, the counts read back once below
     uint32_t* d_first = reinterpret_cast<uint32_t*>(b_souts.as<uint64_t>(nstreams_ + 2));

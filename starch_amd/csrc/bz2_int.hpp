@@ -161,9 +161,12 @@ void rle_sum(const uint8_t* text, const TileDesc* tiles, uint64_t ntiles, TileSu
 void rle_carry(const uint64_t* tile0, uint32_t ns, const TileSum* sums, uint32_t* carry, uint32_t* tile_w,
                hipStream_t st);
 void rle_stream_w(const uint64_t* tile0, const uint64_t* wpre, uint32_t ns, uint64_t* out, hipStream_t st);
+// tab: rle_cut_tab_bytes(nslots) of scratch for the cut tables (k_cut_tab);
+// max_slots: the most block slots of one stream
+uint64_t rle_cut_tab_bytes(uint64_t nslots);
 void rle_cut(const StreamIn* streams, const uint64_t* tile0, const uint64_t* wpre, const uint8_t* text,
-             const uint32_t* carry, uint32_t ns, uint32_t nblock_max, const uint64_t* slot0, BlockDesc* tmp,
-             uint32_t* nblk, hipStream_t st);
+             const uint32_t* carry, uint32_t ns, uint32_t nblock_max, const uint64_t* slot0, uint64_t nslots,
+             uint64_t max_slots, void* tab, BlockDesc* tmp, uint32_t* nblk, hipStream_t st);
 void rle_compact(const BlockDesc* tmp, const uint64_t* slot0, const uint32_t* nblk, const uint32_t* first, uint32_t ns,
                  BlockDesc* out, const StreamIn* streams, const uint64_t* tile0, uint32_t* tile_block, hipStream_t st);
 void rle_emit(const uint8_t* text, const TileDesc* tiles, uint64_t ntiles, const uint64_t* wpre, const uint64_t* tile0,

@@ -27,6 +27,7 @@
 // aligned 16-B loads (any text alignment).
 #include "bz2_int.hpp"
 #include <atomic>
+#include <string.h>
 
 namespace bz {
 
@@ -242,51 +243,79 @@ __device__ __forceinline__ uint32_t tile_ex(uint32_t x, uint32_t* msh)
     return ex;
 }
 
-__global__ void __launch_bounds__(256) k_rle_sum(const uint8_t* __restrict__ text, const TileDesc* __restrict__ tiles,
-                                                  TileSum* __restrict__ sums)
+// One wave per tile, 64 bytes per lane: the lane's change masks, the tile's
+// last change before the lane (a wave max-scan), its first change (the
+// leading run) and the chunk positions of the bytes from the first change on
+// -- wave scans only, no workgroup barriers.
+constexpr int SUM_WPG = 4;                       // tiles (waves) per workgroup
+
+__global__ void __launch_bounds__(64 * SUM_WPG) k_rle_sum(const uint8_t* __restrict__ text,
+                                                         const TileDesc* __restrict__ tiles, uint64_t ntiles,
+                                                         TileSum* __restrict__ sums)
 {
-    __shared__ uint32_t msh[4], fsh[4];
-    __shared__ uint32_t wsh[5];
-    const TileDesc d = tiles[blockIdx.x];
-    const int off = threadIdx.x * 16;
-    const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
-    int cnt = (int)d.len - off;
-    cnt = cnt < 0 ? 0 : (cnt > 16 ? 16 : cnt);
-    uint4 v;
-    uint32_t pb;
-    load_strip(text, d, off, cnt, v, pb);
-    uint32_t m[4];
-    chg_mask(v, pb, cnt, m);
-    const int lc = last_change(m), fc = first_change(m);
-    // the tile's first change (its leading run's length), a wave minimum per wave
-    uint32_t f = fc >= 0 ? (uint32_t)(off + fc) : 0xFFFFFFFFu;
+    const uint64_t tile = (uint64_t)blockIdx.x * SUM_WPG + (threadIdx.x >> 6);
+    if (tile >= ntiles) return;                  // wave-uniform
+    const int lane = threadIdx.x & 63;
+    const TileDesc d = tiles[tile];
+    const uint32_t a = 64u * (uint32_t)lane;     // the lane's first byte, tile offset
+    const int cnt = d.len > a ? (d.len - a < 64u ? (int)(d.len - a) : 64) : 0;
+    uint32_t w[16];
 #pragma unroll
-    for (int dd = 32; dd >= 1; dd >>= 1) {
-        const uint32_t o = (uint32_t)__shfl_xor((int)f, dd, 64);
-        f = o < f ? o : f;
+    for (int i = 0; i < 4; ++i) {
+        const uint32_t p = a + 16u * i;
+        const uint4 v = p < d.len ? load16u(text + d.beg + p, text + d.beg + d.len) : make_uint4(0, 0, 0, 0);
+        w[4 * i] = v.x; w[4 * i + 1] = v.y; w[4 * i + 2] = v.z; w[4 * i + 3] = v.w;
     }
-    if (lane == 0) fsh[wid] = f;
-    const uint32_t ex = tile_ex(lc >= 0 ? (uint32_t)(off + lc + 1) : 0u, msh);
-    uint32_t tw[4];
-    const uint32_t w = strip_t<false>(m, (uint32_t)off, cnt, ex, 0u, tw);
-    uint32_t tot = 0;
-    (void)block_excl_scan_add<uint32_t>(w, wsh, &tot);   // (barriers: fsh, msh complete)
-    if (threadIdx.x == 0) {
-        uint32_t p = 0, fl = 0xFFFFFFFFu;
-        for (int q = 0; q < 4; ++q) {
-            p = msh[q] > p ? msh[q] : p;
-            fl = fsh[q] < fl ? fsh[q] : fl;
+    uint32_t carry = (uint32_t)__shfl_up((int)(w[15] >> 24), 1, 64);
+    if (lane == 0) carry = w[0] & 0xffu;         // the tile's first byte is never a change
+    uint32_t m[16];
+    int lc = -1, fc = -1;
+#pragma unroll
+    for (int i = 0; i < 16; ++i) {
+        const uint32_t sh = (w[i] << 8) | carry;
+        carry = w[i] >> 24;
+        const int lim = cnt - 4 * i;
+        const uint32_t keep = lim >= 4 ? 0x80808080u : (lim <= 0 ? 0u : (0x80808080u >> (8 * (4 - lim))));
+        m[i] = nonzero_bytes(w[i] ^ sh) & keep;
+    }
+#pragma unroll
+    for (int i = 15; i >= 0; --i)
+        if (lc < 0 && m[i]) lc = 4 * i + ((31 - __clz((int)m[i])) >> 3);
+#pragma unroll
+    for (int i = 0; i < 16; ++i)
+        if (fc < 0 && m[i]) fc = 4 * i + ((__builtin_ctz(m[i]) - 7) >> 3);
+    const uint32_t incl = wave_incl_scan_max<uint32_t>(lc >= 0 ? a + (uint32_t)lc + 1u : 0u);
+    uint32_t ex = (uint32_t)__shfl_up((int)incl, 1, 64);
+    if (lane == 0) ex = 0;
+    const uint32_t plast = (uint32_t)__builtin_amdgcn_readlane((int)incl, 63);   // last change + 1 (0: none)
+    const uint32_t finv = wave_incl_scan_max<uint32_t>(fc >= 0 ? ~(a + (uint32_t)fc) : 0u);
+    const uint32_t ffirst = ~(uint32_t)__builtin_amdgcn_readlane((int)finv, 63);  // first change (~0: none)
+    // chunk positions of the bytes from the tile's first change on, and their weight
+    uint32_t tp = ex ? (a - ex) % 255u : 0u;     // t of the byte before the lane's first
+    bool lead = ex == 0;
+    uint32_t wt = 0;
+#pragma unroll
+    for (int k = 0; k < 64; ++k) {
+        if (k < cnt) {
+            const bool chg = ((m[k >> 2] >> (8 * (k & 3) + 7)) & 1u) != 0;
+            lead = lead && !chg;
+            const uint32_t t = chg ? 0u : (tp == 254u ? 0u : tp + 1u);
+            if (!lead) wt += rle_w(t);
+            tp = t;
         }
+    }
+    const uint32_t wsum = (uint32_t)__builtin_amdgcn_readlane((int)wave_incl_scan_add<uint32_t>(wt), 63);
+    if (lane == 0) {
         TileSum o;
         o.len = d.len;
-        o.first = d.len ? text[d.beg] : (uint8_t)0xff;
+        o.first = d.len ? (uint8_t)(w[0] & 0xffu) : (uint8_t)0xff;
         o.last = d.len ? text[d.beg + d.len - 1] : (uint8_t)0xff;
-        o.uni = p == 0 ? 1 : 0;
-        o.trail = p == 0 ? d.len : d.len - (p - 1);
+        o.uni = plast == 0 ? 1 : 0;
+        o.trail = plast == 0 ? d.len : d.len - (plast - 1);
         o.pad = 0;
-        o.lead = fl == 0xFFFFFFFFu ? d.len : fl;
-        o.wrest = tot;
-        sums[blockIdx.x] = o;
+        o.lead = ffirst == 0xFFFFFFFFu ? d.len : ffirst;
+        o.wrest = wsum;
+        sums[tile] = o;
     }
 }
 
@@ -430,6 +459,123 @@ __device__ __forceinline__ void run_t(const uint8_t* __restrict__ text, uint64_t
     }
 }
 
+// Block-cut tables.  The cut is a chain -- block k + 1 starts at the first
+// chunk start whose RLE1 offset W reaches W_k + nblockMAX -- so one wave per
+// stream walks it; walking it by searching the text per block left the GPU
+// idle for ~8 us per block.  Since W_{k+1} - W_k - nblockMAX is 0..4 (a chunk
+// weighs at most 5), W_k = k * nblockMAX + e_k with a slowly growing e_k, and
+// every block's end can be tabulated in parallel beforehand for e in
+// [0, CUT_E): one wave per (stream, k) finds the chunk starts c whose W(c) -
+// T0 lies in [0, CUT_E), T0 = (k + 1) * nblockMAX, in the tile where W
+// crosses T0 and the next one, and stores for every e the first of them at or
+// past T0 + e (its offset in dtab, its text position in ptab).  254: none
+// before the stream ends; 255: not within the two tiles (the walk then
+// searches the text as before).  The walk itself becomes one table read per
+// block, the next row already loaded.
+constexpr int CUT_E = 128;
+constexpr int CUT_WPG = 4;                       // (stream, k) waves per workgroup
+
+__global__ void __launch_bounds__(64 * CUT_WPG) k_cut_tab(const StreamIn* __restrict__ streams,
+                                                         const uint64_t* __restrict__ seg_tile0,
+                                                         const uint64_t* __restrict__ tile_wpre,
+                                                         const uint8_t* __restrict__ text,
+                                                         const uint32_t* __restrict__ carry, uint32_t nblock_max,
+                                                         const uint64_t* __restrict__ slot0, uint8_t* __restrict__ dtab,
+                                                         uint64_t* __restrict__ ptab)
+{
+    __shared__ uint64_t pos_sh[CUT_WPG][CUT_E];
+    const uint32_t s = blockIdx.y;
+    const int wv = threadIdx.x >> 6, lane = threadIdx.x & 63;
+    const uint64_t k = (uint64_t)blockIdx.x * CUT_WPG + (uint64_t)wv;
+    if (k >= slot0[s + 1] - slot0[s]) return;                  // wave-uniform from here on
+    const uint64_t beg = streams[s].text_off, end = beg + streams[s].text_len;
+    const uint64_t t0 = seg_tile0[s], t1 = seg_tile0[s + 1];
+    if (t1 == t0) return;
+    const uint64_t w0 = tile_wpre[t0], wend = tile_wpre[t1] - w0;
+    const uint64_t T0 = (k + 1) * (uint64_t)nblock_max;
+    if (T0 > wend) return;                                      // the walk reads no such row
+    // tile lo with W(lo) < T0 <= W(lo + 1) (tile starts; W(t1) = wend): a
+    // 64-tile window around T0 / kTB (a byte weighs about one), bisection otherwise
+    uint64_t lo = t0, hi = t1;
+    {
+        const uint64_t g = t0 + T0 / kTB;
+        uint64_t a = g > t0 + 32 ? g - 32 : t0;
+        if (a + 64 > hi) a = hi > t0 + 64 ? hi - 64 : t0;
+        const uint64_t t = a + (uint64_t)lane;
+        const uint64_t ball = __ballot(t <= hi && tile_wpre[t] - w0 >= T0);
+        const bool below_all = (tile_wpre[a] - w0) < T0;
+        if (ball && below_all) {
+            hi = a + (uint64_t)(__ffsll((unsigned long long)ball) - 1);
+            lo = hi - 1;
+        } else if (ball) {
+            hi = a;
+        } else if (a + 63 < hi) {
+            lo = a + 63;
+        }
+    }
+    while (hi - lo > 1) {
+        const uint64_t mid = (lo + hi) >> 1;
+        if (tile_wpre[mid] - w0 < T0) lo = mid; else hi = mid;
+    }
+    // chunk starts of tiles lo and lo + 1 with W - T0 in [0, CUT_E): a bit each
+    uint32_t mk[CUT_E / 32];
+#pragma unroll
+    for (int i = 0; i < CUT_E / 32; ++i) mk[i] = 0;
+    bool to_end = false;                                        // the two tiles reach the stream's end
+#pragma unroll
+    for (int j = 0; j < 2; ++j) {
+        const uint64_t tj = lo + (uint64_t)j;
+        if (tj >= t1) { to_end = true; break; }                 // (uniform)
+        const uint64_t tstart = beg + (tj - t0) * kTB;
+        const uint64_t tend = tstart + kTB < end ? tstart + kTB : end;
+        if (tend == end) to_end = true;
+        uint32_t tw[16];
+        run_t<64>(text, tstart, tend, (carry[tj] + 254u) % 255u, text[tstart], tw);
+        uint32_t ls = 0;
+#pragma unroll
+        for (int q = 0; q < 16; ++q) {
+            const uint32_t l3 = ~nonzero_bytes(tw[q] & 0xFCFCFCFCu) & 0x80808080u;   // t <= 3
+            const uint32_t e3 = ~nonzero_bytes(tw[q] ^ 0x03030303u) & 0x80808080u;  // t == 3
+            ls += (uint32_t)(__popc(l3) + __popc(e3));
+        }
+        // (bytes past tend carry t = 1: weight 1, after every real byte of the lane)
+        uint64_t W = tile_wpre[tj] - w0 + (wave_incl_scan_add<uint32_t>(ls) - ls);
+        const uint64_t a = tstart + 64u * (uint64_t)lane;
+#pragma unroll
+        for (int b = 0; b < 64; ++b) {
+            const uint32_t t = (tw[b >> 2] >> (8 * (b & 3))) & 0xffu;
+            if (t == 0 && a + b < tend && W >= T0 && W - T0 < (uint64_t)CUT_E) {
+                const uint32_t o = (uint32_t)(W - T0);
+#pragma unroll
+                for (int i = 0; i < CUT_E / 32; ++i)
+                    if ((o >> 5) == (uint32_t)i) mk[i] |= 1u << (o & 31u);
+                pos_sh[wv][o] = a + (uint64_t)b;
+            }
+            W += rle_w(t);
+        }
+    }
+#pragma unroll
+    for (int i = 0; i < CUT_E / 32; ++i)
+        mk[i] = (uint32_t)__builtin_amdgcn_readlane((int)wave_incl_scan_or(mk[i]), 63);
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+    const uint64_t row = (slot0[s] + k) * (uint64_t)CUT_E;
+#pragma unroll
+    for (int h = 0; h < CUT_E / 64; ++h) {
+        const uint32_t e = (uint32_t)lane + 64u * h;
+        int b = -1;                                             // first bit >= e
+#pragma unroll
+        for (int i = 0; i < CUT_E / 32; ++i) {
+            const uint32_t lo_bit = (uint32_t)i * 32u;
+            const uint32_t mm = e <= lo_bit ? mk[i] : (e < lo_bit + 32u ? mk[i] & (~0u << (e - lo_bit)) : 0u);
+            if (b < 0 && mm) b = (int)lo_bit + __builtin_ctz(mm);
+        }
+        dtab[row + e] = b >= 0 ? (uint8_t)b : (to_end ? (uint8_t)254 : (uint8_t)255);
+        ptab[row + e] = b >= 0 ? pos_sh[wv][b] : end;
+    }
+}
+
 // one wave per stream: greedy cut (see file header).  Per block: binary search
 // of the tile where the RLE1 size crosses nblockMAX, the chunk positions of
 // that tile (run_t, from its entering run position) and a 64-lane scan of
@@ -438,7 +584,8 @@ __device__ __forceinline__ void run_t(const uint8_t* __restrict__ text, uint64_t
 __global__ void __launch_bounds__(64) k_cut(const StreamIn* __restrict__ streams, const uint64_t* __restrict__ seg_tile0,
                                              const uint64_t* __restrict__ tile_wpre, const uint8_t* __restrict__ text,
                                              const uint32_t* __restrict__ carry, uint32_t nstreams, uint32_t nblock_max,
-                                             const uint64_t* __restrict__ slot0, BlockDesc* __restrict__ tmp,
+                                             const uint64_t* __restrict__ slot0, const uint8_t* __restrict__ dtab,
+                                             const uint64_t* __restrict__ ptab, BlockDesc* __restrict__ tmp,
                                              uint32_t* __restrict__ nblk)
 {
     const uint32_t s = blockIdx.x;
@@ -447,12 +594,44 @@ __global__ void __launch_bounds__(64) k_cut(const StreamIn* __restrict__ streams
     const uint64_t t0 = seg_tile0[s], t1 = seg_tile0[s + 1];
     const uint64_t w0 = tile_wpre[t0], wend = tile_wpre[t1] - w0;
     const bool frj = streams[s].final_run_joins != 0;
+    const uint64_t nrow = slot0[s + 1] - slot0[s];
     uint64_t bs = beg, wbs = 0;
     uint32_t k = 0;
+    // table rows (k_cut_tab): lane l holds entries l and l + 64, the next row in flight
+    uint32_t da = 255u, db = 255u;
+    uint64_t pa = 0, pb = 0;
+    auto row = [&](uint32_t kk, uint32_t& xa, uint32_t& xb, uint64_t& ya, uint64_t& yb) {
+        xa = xb = 255u;
+        ya = yb = 0;
+        if (dtab && kk < nrow) {
+            const uint64_t r = (slot0[s] + kk) * (uint64_t)CUT_E;
+            xa = dtab[r + lane];
+            xb = dtab[r + 64 + lane];
+            ya = ptab[r + lane];
+            yb = ptab[r + 64 + lane];
+        }
+    };
+    row(0, da, db, pa, pb);
     while (bs < end) {
         const uint64_t target = wbs + nblock_max;
         uint64_t block_end = end, wblock_end = wend;
+        uint32_t na, nb2;
+        uint64_t qa, qb;
+        row(k + 1, na, nb2, qa, qb);
         if (wend >= target) {
+          // this block's end from its table row when W_k - k * nblockMAX is tabulated
+          const uint64_t e = wbs - (uint64_t)k * nblock_max;
+          uint32_t d = 255u;
+          if (e < (uint64_t)CUT_E)
+              d = (uint32_t)__builtin_amdgcn_readlane((int)(e < 64 ? da : db), (int)(e & 63u));
+          uint64_t p = end, Wp = wend;
+          if (d < 254u) {
+              const uint64_t pp = e < 64 ? pa : pb;
+              const uint32_t plo = (uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)pp, (int)(e & 63u));
+              const uint32_t phi = (uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)(pp >> 32), (int)(e & 63u));
+              p = ((uint64_t)phi << 32) | plo;
+              Wp = (uint64_t)(k + 1) * nblock_max + d;
+          } else if (d == 255u) {   // not tabulated: search the text
             uint64_t lo = t0 + (bs - beg) / kTB, hi = t1;   // Wstart(lo) <= wbs < target <= Wstart(hi)
             // RLE1 sizes run close to text sizes (a byte weighs 0..2), so the
             // crossing tile sits near lo + (target - W(lo)) / kTB: one window of
@@ -548,7 +727,6 @@ __global__ void __launch_bounds__(64) k_cut(const StreamIn* __restrict__ streams
             }
             // the first chunk start p >= q (within 255 bytes) and the weight of
             // [q, p): the chunk positions of the 256 bytes after q, four per lane
-            uint64_t p = end;
             uint32_t part = 0;
             if (q < end) {
                 uint32_t tv[1];
@@ -566,8 +744,9 @@ __global__ void __launch_bounds__(64) k_cut(const StreamIn* __restrict__ streams
                     if (pos < p) part += rle_w((tv[0] >> (8 * k)) & 0xffu);
                 }
             }
-            const uint64_t Wp = Wq + wave_reduce_add(part);
-            if (p < end && !(frj && p == end - 1)) { block_end = p; wblock_end = Wp; }
+            Wp = Wq + wave_reduce_add(part);
+          }
+          if (p < end && !(frj && p == end - 1)) { block_end = p; wblock_end = Wp; }
         }
         if (lane == 0) {
             BlockDesc b;
@@ -577,6 +756,7 @@ __global__ void __launch_bounds__(64) k_cut(const StreamIn* __restrict__ streams
         ++k;
         bs = block_end;
         wbs = wblock_end;
+        da = na; db = nb2; pa = qa; pb = qb;
     }
     if (lane == 0) nblk[s] = k;
 }
@@ -838,7 +1018,8 @@ void rle_tiles(const uint64_t* tile0, const StreamIn* streams, uint32_t ns, uint
 }
 void rle_sum(const uint8_t* text, const TileDesc* tiles, uint64_t ntiles, TileSum* sums, hipStream_t st)
 {
-    hipLaunchKernelGGL(k_rle_sum, dim3((unsigned)ntiles), dim3(256), 0, st, text, tiles, sums);
+    hipLaunchKernelGGL(k_rle_sum, dim3((unsigned)((ntiles + SUM_WPG - 1) / SUM_WPG)), dim3(64 * SUM_WPG), 0, st, text,
+                       tiles, ntiles, sums);
 }
 void rle_carry(const uint64_t* tile0, uint32_t ns, const TileSum* sums, uint32_t* carry, uint32_t* tile_w,
                hipStream_t st)
@@ -849,12 +1030,24 @@ void rle_stream_w(const uint64_t* tile0, const uint64_t* wpre, uint32_t ns, uint
 {
     hipLaunchKernelGGL(k_stream_w, dim3(g1(ns, 64)), dim3(64), 0, st, tile0, wpre, ns, out);
 }
+uint64_t rle_cut_tab_bytes(uint64_t nslots) { return nslots * CUT_E * (1 + sizeof(uint64_t)) + 64; }
+
 void rle_cut(const StreamIn* streams, const uint64_t* tile0, const uint64_t* wpre, const uint8_t* text,
-             const uint32_t* carry, uint32_t ns, uint32_t nblock_max, const uint64_t* slot0, BlockDesc* tmp,
-             uint32_t* nblk, hipStream_t st)
+             const uint32_t* carry, uint32_t ns, uint32_t nblock_max, const uint64_t* slot0, uint64_t nslots,
+             uint64_t max_slots, void* tab, BlockDesc* tmp, uint32_t* nblk, hipStream_t st)
 {
-    hipLaunchKernelGGL(k_cut, dim3(ns), dim3(64), 0, st, streams, tile0, wpre, text, carry, ns, nblock_max, slot0, tmp,
-                       nblk);
+    // STARCH_CUT_TAB=0: the walk searches the text for every block
+    static const bool tab_off = [] { const char* e = getenv("STARCH_CUT_TAB"); return e && !strcmp(e, "0"); }();
+    uint64_t* ptab = nullptr;
+    uint8_t* dtab = nullptr;
+    if (!tab_off && tab && max_slots) {
+        ptab = static_cast<uint64_t*>(tab);
+        dtab = reinterpret_cast<uint8_t*>(ptab + nslots * CUT_E);
+        hipLaunchKernelGGL(k_cut_tab, dim3((unsigned)((max_slots + CUT_WPG - 1) / CUT_WPG), ns), dim3(64 * CUT_WPG), 0, st,
+                           streams, tile0, wpre, text, carry, nblock_max, slot0, dtab, ptab);
+    }
+    hipLaunchKernelGGL(k_cut, dim3(ns), dim3(64), 0, st, streams, tile0, wpre, text, carry, ns, nblock_max, slot0,
+                       dtab, ptab, tmp, nblk);
 }
 void rle_compact(const BlockDesc* tmp, const uint64_t* slot0, const uint32_t* nblk, const uint32_t* first, uint32_t ns,
                  BlockDesc* out, const StreamIn* streams, const uint64_t* tile0, uint32_t* tile_block, hipStream_t st)
