@@ -416,8 +416,32 @@ __global__ void __launch_bounds__(MCT) k_mtf_runs(const BlockDesc* __restrict__ 
     if (!mtf_mine<P>(nin) || a >= n) return;
     const uint32_t e = a + cs < n ? a + cs : n;
     const MtfScr<P> ms = mtf_scr<P>(K, kstride, slot, C);
-    typename P::List L = ms.l0()[ch];
     uint32_t z = 0, nz = 0, lz = 0, inner = 0;
+    if constexpr (!P::SIX) {
+        // An MTF index is 0 exactly when the symbol equals the one before it
+        // (the list's front is the last symbol coded; the block's first symbol
+        // meets the initial list, whose front is symbol 0), so the zero runs --
+        // all the run summary needs -- come from comparing neighbours, without
+        // the move-to-front chain (k_mtf_emit runs that once)
+        const uint8_t* ll = LL + (uint64_t)slot * ll_stride;
+        uint32_t prev = a ? ll[a - 1] : 0u;
+        visit_chunk_lines(ll, a, e, [&](uint32_t s) {
+            const uint32_t nzf = s != prev ? 1u : 0u;
+            prev = s;
+            inner += (nzf & nz) ? 1u + (31u - __clz(z + 1u)) : 0u;
+            lz = (nzf & (nz ^ 1u)) ? z : lz;
+            nz |= nzf;
+            z = nzf ? 0u : z + 1u;
+        });
+        RunSum r;
+        r.nz = nz;
+        r.lz = nz ? lz : z;
+        r.tz = nz ? z : 0u;
+        r.inner = inner;
+        ms.rs()[ch] = r;
+        return;
+    }
+    typename P::List L = ms.l0()[ch];
     uint8_t* ixp = ms.ix() + (uint64_t)a * P::IXB / 8;     // 16 symbols = 8 (IXB 4) or 16 (IXB 8) bytes
     // indices enter at the top of a 64-bit (IXB 4) / 128-bit (IXB 8) shift
     // register; after 16 symbols the first sits in the lowest bits
