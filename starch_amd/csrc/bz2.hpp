@@ -116,6 +116,9 @@ public:
         float a, b;
     };
     void take_intervals(hipEvent_t ref, std::vector<Interval>& out);
+    // free the device buffers (they grow again on the next plan); the caller
+    // has synchronised the stream they were used on
+    void release_device();
     // text offset (in the plan's d_text) where an open last piece's unencoded
     // rest starts; its end is the piece's end
     uint64_t open_rest() const { return open_rest_; }

@@ -67,6 +67,12 @@ void Encoder::take_intervals(hipEvent_t ref, std::vector<Interval>& out)
     pend_.clear();
 }
 
+void Encoder::release_device()
+{
+    for (DevBuf* b : {&b_streams, &b_tiles, &b_tile_sum, &b_tile_carry, &b_tile_w, &b_tile_wpre, &b_tile_block, &b_cut_tab, &b_seg_tile0, &b_seg_nblk, &b_blk_tmp, &b_blk, &b_blkbytes, &b_scal, &b_tmp, &b_bwt, &b_mtfv, &b_freq, &b_sel, &b_tabs, &b_gbits, &b_souts, &b_fallback, &b_bwt3, &b_crc, &b_dedupe, &b_rep_bytes, &b_rep_blk, &b_last})
+        b->release();
+}
+
 static uint64_t round_up(uint64_t x, uint64_t m) { return (x + m - 1) / m * m; }
 
 uint32_t* Encoder::PinnedCtr::get()

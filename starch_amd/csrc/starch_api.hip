@@ -1616,8 +1616,15 @@ int starch_set_stream(starch_ctx* c, void* s)
 int starch_set_lanes(starch_ctx* c, int lanes)
 {
     if (!c || lanes < 0 || lanes > 8) return STARCH_ERR_ARG;
+    GUARD(c)
     c->dev_lanes = lanes;
+    if (lanes == 1)   // the extra lanes' encoders give their HBM back (one encoder now holds every block)
+        for (auto& l : c->lanes) {
+            HIP_CHECK(hipStreamSynchronize(l->st));
+            l->enc.release_device();
+        }
     return STARCH_OK;
+    END_GUARD(c)
 }
 
 int starch_use_own_stream(starch_ctx* c)
