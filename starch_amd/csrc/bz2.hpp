@@ -119,6 +119,9 @@ public:
     // free the device buffers (they grow again on the next plan); the caller
     // has synchronised the stream they were used on
     void release_device();
+    // the part of the device's free memory plan() sizes its sort batches by
+    // (1: all; encoder lanes planning concurrently take 1 / lanes each)
+    void set_mem_share(double f) { mem_share_ = f > 0 && f <= 1 ? f : 1.0; }
     // text offset (in the plan's d_text) where an open last piece's unencoded
     // rest starts; its end is the piece's end
     uint64_t open_rest() const { return open_rest_; }
@@ -149,6 +152,7 @@ private:
     std::vector<BlockDesc> host_blocks_;
     std::vector<PendTimer> pend_;
     uint64_t open_rest_ = 0;
+    double mem_share_ = 1.0;
 };
 
 }  // namespace bz

@@ -308,7 +308,9 @@ void Encoder::plan(const uint8_t* d_text, const std::vector<StreamIn>& streams, 
     HIP_CHECK(hipMemGetInfo(&free_b, &total_b));
     const bool kmat = bwt_kmat();
     const uint64_t per_slot = blk_stride_ * (kmat ? 59ull : 41ull);   // sort scratch + 1 B last column
-    uint64_t max_batch = std::max<uint64_t>(1, (uint64_t)(free_b * 0.45) / per_slot);
+    // (mem_share_: the part of the free HBM this encoder may take -- encoder
+    // lanes planning at once all see the same free memory)
+    uint64_t max_batch = std::max<uint64_t>(1, (uint64_t)(free_b * 0.45 * mem_share_) / per_slot);
 #ifndef STARCH_BATCH_MAX
 #define STARCH_BATCH_MAX 2048
 #endif

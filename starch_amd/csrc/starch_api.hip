@@ -463,6 +463,7 @@ void encode_units(starch_ctx* c, const uint8_t* d_base, const std::vector<UnitIn
         std::vector<std::vector<bz::StreamIn>> li(nl);
         for (size_t i = 0; i < nl; ++i) {
             ln[i] = lane_ctx(c, (int)i);
+            ln[i]->enc.set_mem_share(1.0 / (double)nl);
             const uint64_t s0 = cuts[i], s1 = i + 1 < nl ? cuts[i + 1] : nseg;
             li[i].assign(sin.begin() + s0, sin.begin() + s1);
             for (auto& x : li[i]) x.group -= (uint32_t)s0;
@@ -502,6 +503,7 @@ void encode_units(starch_ctx* c, const uint8_t* d_base, const std::vector<UnitIn
         }
         bst = lst[0];
     } else {
+        c->enc.set_mem_share(1.0);
         c->enc.plan(text, sin, opt.block_size_100k, c->st, outs, &bst);
     }
     finish_names(c, pnames);
