@@ -220,8 +220,11 @@ __global__ void __launch_bounds__(DT) k_emit_data(const BlockDesc* __restrict__ 
     const uint32_t n_mtf = blocks[b].n_mtf;
     const uint32_t s0 = g0 * 50;
     const uint32_t s1 = (g0 + gcnt) * 50 < n_mtf ? (g0 + gcnt) * 50 : n_mtf;
-    const uint32_t nwi = (s1 - s0 + 1) / 2;
-    const uint32_t* src = reinterpret_cast<const uint32_t*>(mtfv_all + (uint64_t)d * mtf_stride + s0);
+    // alphabets <= 32 store their MTF values as bytes (bz2_mtf.hip Out8), larger ones as u16
+    const bool v8 = alpha <= 32;                            // uniform
+    const uint32_t nwi = v8 ? (s1 - s0 + 3) / 4 : (s1 - s0 + 1) / 2;
+    const uint32_t* src = v8 ? reinterpret_cast<const uint32_t*>(reinterpret_cast<const uint8_t*>(mtfv_all + (uint64_t)d * mtf_stride) + s0)
+                             : reinterpret_cast<const uint32_t*>(mtfv_all + (uint64_t)d * mtf_stride + s0);
     for (uint32_t i = tid; i < nwi; i += DT) mv[i] = src[i];
     const uint32_t* gpre = gpre_all + (uint64_t)b * kMaxSelectors;
     const uint64_t base = blocks[b].bit_off + blocks[b].hdr_bits;
@@ -238,13 +241,35 @@ __global__ void __launch_bounds__(DT) k_emit_data(const BlockDesc* __restrict__ 
         const uint32_t* row = lc[sel_all[(uint64_t)d * (2 * kMaxSelectors) + g]];
         const uint32_t* m = mv + (gs - s0) / 2;                // gs, s0 even
         auto code_group = [&](auto& o) {
-            for (uint32_t i = gs; i < ge; i += 2) {
-                const uint32_t w = m[(i - gs) >> 1];
-                const uint32_t c0 = row[w & 0xffffu];
-                o.put((int)(c0 >> 24), c0 & 0xFFFFFFu);
-                if (i + 1 < ge) {
-                    const uint32_t c1 = row[w >> 16];
-                    o.put((int)(c1 >> 24), c1 & 0xFFFFFFu);
+            if (v8) {   // bytes: the group starts at an even byte (50 g); 4 per LDS word after the first 2
+                uint32_t i = gs, off = gs - s0;
+                auto sym = [&](uint32_t v) {
+                    const uint32_t c = row[v];
+                    o.put((int)(c >> 24), c & 0xFFFFFFu);
+                };
+                if (off & 2u) {
+                    const uint32_t w = mv[off >> 2] >> 16;
+                    sym(w & 0xffu);
+                    if (i + 1 < ge) sym(w >> 8);
+                    i += 2;
+                    off += 2;
+                }
+                for (; i < ge; i += 4, off += 4) {
+                    const uint32_t w = mv[off >> 2];
+                    sym(w & 0xffu);
+                    if (i + 1 < ge) sym((w >> 8) & 0xffu);
+                    if (i + 2 < ge) sym((w >> 16) & 0xffu);
+                    if (i + 3 < ge) sym(w >> 24);
+                }
+            } else {
+                for (uint32_t i = gs; i < ge; i += 2) {
+                    const uint32_t w = m[(i - gs) >> 1];
+                    const uint32_t c0 = row[w & 0xffffu];
+                    o.put((int)(c0 >> 24), c0 & 0xFFFFFFu);
+                    if (i + 1 < ge) {
+                        const uint32_t c1 = row[w >> 16];
+                        o.put((int)(c1 >> 24), c1 & 0xFFFFFFu);
+                    }
                 }
             }
             o.finish();

@@ -89,44 +89,62 @@ __device__ __forceinline__ void visit_line(const uint8_t* p, F&& f)
     }
 }
 
-// u16 output through a 128-bit shift register: whole 16-byte stores once the
-// write position is 8-aligned, scalar stores at the two ends of the chunk.
-struct Out16 {
-    uint16_t* base;
+// MTF values of alphabets <= 32 are stored as u8 (every value <= nInUse + 1
+// <= 31; k_tables32 and k_emit_data read bytes for those blocks, k_mtf_big's
+// larger alphabets stay u16), through a 128-bit shift register: one 16-byte
+// store per 16 symbols once a window is wholly the chunk's; the partial
+// windows at the chunk's two ends are written as 8/4/2/1-byte pieces
+// (neighbouring chunks own the other bytes).  (u16 values took twice the
+// stores: MTF stage 2.57 -> 2.40 ms on cfg2.  OR-ing a run's RUNA/RUNB
+// symbols and the index into the window as one branch-free insertion
+// measured slower, 2.80 ms.)
+struct Out8 {
+    uint8_t* base;
     uint32_t o;       // next index
-    uint32_t o_al;    // first 8-aligned index at or after the chunk's first output
-    uint64_t lo, hi;
-    __device__ __forceinline__ void init(uint16_t* b, uint32_t start)
+    uint32_t s;       // the chunk's first output index
+    uint64_t lo, hi;  // window byte j at register byte j once the window is complete
+    __device__ __forceinline__ void init(uint8_t* b, uint32_t start)
     {
-        base = b; o = start; o_al = (start + 7u) & ~7u; lo = 0; hi = 0;
+        base = b; o = start; s = start; lo = 0; hi = 0;
+    }
+    // store register bytes [p, q) of the window at w (register byte j = window byte j)
+    __device__ __forceinline__ void store_range(uint32_t w, uint32_t p, uint32_t q, uint64_t rl, uint64_t rh)
+    {
+#pragma unroll 1
+        while (p < q) {
+            const uint64_t x = p >= 8 ? rh >> (8 * (p - 8)) : ((rl >> (8 * p)) | (p ? rh << (64 - 8 * p) : 0ull));
+            uint8_t* d = base + w + p;
+            if ((p & 7u) == 0 && p + 8 <= q) { *reinterpret_cast<uint64_t*>(d) = x; p += 8; }
+            else if ((p & 3u) == 0 && p + 4 <= q) { *reinterpret_cast<uint32_t*>(d) = (uint32_t)x; p += 4; }
+            else if ((p & 1u) == 0 && p + 2 <= q) { *reinterpret_cast<uint16_t*>(d) = (uint16_t)x; p += 2; }
+            else { *d = (uint8_t)x; p += 1; }
+        }
     }
     __device__ __forceinline__ void put(uint32_t sym)
     {
-        if (o < o_al) {
-            base[o] = (uint16_t)sym;
-        } else {
-            lo = (lo >> 16) | (hi << 48);
-            hi = (hi >> 16) | ((uint64_t)sym << 48);
-            if ((o & 7u) == 7u) {
-                *reinterpret_cast<uint4*>(base + (o - 7u)) =
-                    make_uint4((uint32_t)lo, (uint32_t)(lo >> 32), (uint32_t)hi, (uint32_t)(hi >> 32));
-            }
+        lo = (lo >> 8) | (hi << 56);
+        hi = (hi >> 8) | ((uint64_t)sym << 56);
+        if ((o & 15u) == 15u) {
+            const uint32_t w = o - 15u;
+            if (w >= s) *reinterpret_cast<uint4*>(base + w) =
+                make_uint4((uint32_t)lo, (uint32_t)(lo >> 32), (uint32_t)hi, (uint32_t)(hi >> 32));
+            else store_range(w, s - w, 16u, lo, hi);
         }
         ++o;
     }
     __device__ __forceinline__ void flush()
     {
-        if (o <= o_al) return;
-        const uint32_t k = o & 7u;               // symbols held: the top k of the register
-        for (uint32_t i = 0; i < k; ++i) {
-            const uint32_t bit = 128u - 16u * k + 16u * i;
-            const uint32_t v = bit >= 64 ? (uint32_t)(hi >> (bit - 64)) : (uint32_t)((lo >> bit) | (bit ? (hi << (64 - bit)) : 0));
-            base[(o & ~7u) + i] = (uint16_t)v;
-        }
+        const uint32_t k = o & 15u;               // bytes of the open window: the top k of the register
+        if (!k) return;
+        const uint32_t w = o - k, p = s > w ? s - w : 0u;
+        const uint32_t sh = 8u * (16u - k);       // align window byte 0 to register byte 0
+        const uint64_t rl = sh >= 64 ? hi >> (sh - 64) : ((lo >> sh) | (sh ? hi << (64 - sh) : 0ull));
+        const uint64_t rh = sh >= 64 ? 0ull : hi >> sh;
+        store_range(w, p, k, rl, rh);
     }
 };
 
-__device__ __forceinline__ void put_run(Out16& out, uint32_t z)   // bijective base 2: RUNA = 0, RUNB = 1
+__device__ __forceinline__ void put_run(Out8& out, uint32_t z)   // bijective base 2: RUNA = 0, RUNB = 1
 {
     while (z) {
         const uint32_t d = ((z - 1) & 1u) ? 1u : 0u;
@@ -527,15 +545,15 @@ __global__ void __launch_bounds__(MST) k_mtf_scan_runs(BlockDesc* __restrict__ b
     }
     if (tid == MST - 1) {
         const RunSum T = sh[MST - 1];
-        uint16_t* mtfv = mtfv_all + (uint64_t)b * mtf_stride;
+        uint8_t* mtfv = reinterpret_cast<uint8_t*>(mtfv_all + (uint64_t)b * mtf_stride);   // u8 values
         uint32_t z = T.nz ? T.tz : T.lz;
         uint32_t o = T.nz ? nsym_run(T.lz) + 1 + T.inner : 0;
         while (z) {
             const uint32_t d = ((z - 1) & 1u) ? 1u : 0u;
-            mtfv[o++] = (uint16_t)d;
+            mtfv[o++] = (uint8_t)d;
             z = (z - (d + 1)) >> 1;
         }
-        mtfv[o++] = (uint16_t)(nin + 1);       // EOB
+        mtfv[o++] = (uint8_t)(nin + 1);        // EOB
         blocks[b].n_mtf = o;
     }
 }
@@ -556,8 +574,8 @@ __global__ void __launch_bounds__(MCT) k_mtf_emit(const BlockDesc* __restrict__ 
     const uint32_t e = a + cs < n ? a + cs : n;
     const MtfScr<P> ms = mtf_scr<P>(const_cast<uint64_t*>(K), kstride, slot, C);
     const uint2 zo = ms.zo()[ch];
-    Out16 out;
-    out.init(mtfv_all + (uint64_t)b * mtf_stride, zo.y);
+    Out8 out;
+    out.init(reinterpret_cast<uint8_t*>(mtfv_all + (uint64_t)b * mtf_stride), zo.y);
     uint32_t z = zo.x;
     auto f = [&](uint32_t x) {
         if (x == 0) {

@@ -446,7 +446,8 @@ __global__ void __launch_bounds__(T32) __attribute__((amdgpu_waves_per_eu(STARCH
     const uint32_t b = b0 + blockIdx.x;
     const int32_t alpha = (int32_t)blocks[b].n_in_use + 2;
     if (alpha > 32) return;                        // uniform: k_tables handles it
-    const uint16_t* mtfv = mtfv_all + (uint64_t)b * mtf_stride;
+    // alphabets <= 32: the MTF values are bytes (k_mtf_emit / k_mtf_scan_runs)
+    const uint8_t* mtfv = reinterpret_cast<const uint8_t*>(mtfv_all + (uint64_t)b * mtf_stride);
     uint8_t* sel = sel_all + (uint64_t)b * (2 * kMaxSelectors);
     uint8_t* selmtf = sel + kMaxSelectors;
     uint32_t* gbits = gbits_all + (uint64_t)b * kMaxSelectors;
@@ -470,25 +471,23 @@ __global__ void __launch_bounds__(T32) __attribute__((amdgpu_waves_per_eu(STARCH
             for (int q = 0; q < 8; ++q) hl[q][tid] = 0;
             const uint32_t gs = g * 50;
             const uint32_t cnt = gs + 50 < n_mtf ? 50u : n_mtf - gs;
-            // the group's 100 bytes (4-B aligned: gs even) by seven aligned
-            // 16-B loads over its 112-byte window -- a lane per group strides
-            // 100 B, so 16-B loads touch the same lines in a quarter of the
-            // instructions 4-B loads took; o = the group's first word in it
+            // the group's 50 bytes by four aligned 16-B loads over its 64-byte
+            // window (the block's base is 32-B aligned and gs = 50 g is even,
+            // so the group starts at byte o <= 14 of the window)
             const uintptr_t ga = reinterpret_cast<uintptr_t>(mtfv + gs);
             const uint4* w4 = reinterpret_cast<const uint4*>(ga & ~(uintptr_t)15);
-            const uint32_t o = (uint32_t)(ga & 15u) >> 2, wend = o + (cnt + 1) / 2;   // words [o, wend)
-            uint32_t wv[28];
+            const uint32_t o = (uint32_t)(ga & 15u), bend = o + cnt;          // bytes [o, bend)
+            uint32_t wv[16];
 #pragma unroll
-            for (int k = 0; k < 7; ++k) {
-                const uint4 x = 4u * k < wend ? w4[k] : make_uint4(0, 0, 0, 0);   // all loads in flight
+            for (int k = 0; k < 4; ++k) {
+                const uint4 x = 16u * k < bend ? w4[k] : make_uint4(0, 0, 0, 0);   // all loads in flight
                 wv[4 * k] = x.x; wv[4 * k + 1] = x.y; wv[4 * k + 2] = x.z; wv[4 * k + 3] = x.w;
             }
 #pragma unroll
-            for (int k = 0; k < 28; ++k) {
-                const uint32_t j = (uint32_t)k - o;                          // word of the group (wraps if k < o)
-                const uint32_t v0 = wv[k] & 0xffffu, v1 = wv[k] >> 16;
-                if (j < 25u && 2u * j < cnt) atomicAdd(&hl[v0 >> 2][tid], 1u << (8 * (v0 & 3)));
-                if (j < 25u && 2u * j + 1 < cnt) atomicAdd(&hl[v1 >> 2][tid], 1u << (8 * (v1 & 3)));
+            for (int k = 0; k < 64; ++k) {
+                const uint32_t j = (uint32_t)k - o;                          // byte of the group (wraps if k < o)
+                const uint32_t v = (wv[k >> 2] >> (8 * (k & 3))) & 0xffu;
+                if (j < cnt) atomicAdd(&hl[v >> 2][tid], 1u << (8 * (v & 3)));
             }
 #pragma unroll
             for (int q = 0; q < 8; ++q) h[q] = hl[q][tid];
