@@ -862,6 +862,15 @@ __global__ void __launch_bounds__(256) k_rle_emit(const uint8_t* __restrict__ te
     const uint64_t Wt = tile_wpre[blockIdx.x] - tile_wpre[seg_tile0[s]];   // stream W of the tile's first byte
     const uint64_t wb0 = blocks[b0].w_beg;
     const uint64_t wnext = b0 + 1 < bl ? blocks[b0 + 1].w_beg : ~0ull;
+    // the strip's changes as 16 bits (bit p: byte p differs from the one before),
+    // the bytes past the strip counted as changes: a chunk length (t == 3) whose
+    // run ends inside the strip is read off the mask, without loading the text
+    uint32_t cm = cnt < 16 ? (0xffffu << cnt) & 0xffffu : 0u;
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+        const uint32_t x = m[i] >> 7;
+        cm |= ((x | (x >> 7) | (x >> 14) | (x >> 21)) & 0xfu) << (4 * i);
+    }
     uint32_t o = pre;
     for (int k = 0; k < cnt; ++k) {
         const uint32_t t = byte16(tv, k);
@@ -876,9 +885,14 @@ __global__ void __launch_bounds__(256) k_rle_emit(const uint8_t* __restrict__ te
             // the chunk's length: its bytes go on while they equal c, up to 255
             // (its start i - 3 plus 254)
             const uint64_t i = d.beg + off + k;
-            const uint64_t jl = i + 252 < send ? i + 252 : send;
-            uint64_t j = i + 1;
-            while (j < jl && text[j] == c) ++j;
+            const uint32_t rest = (cm >> (k + 1)) | 0x10000u;   // bit 16 - k - 1: past the strip
+            const uint32_t p = (uint32_t)k + 1u + (uint32_t)__builtin_ctz(rest);   // first change after k
+            uint64_t j = i + (p - (uint32_t)k);
+            if (p >= (uint32_t)cnt) {                          // the run reaches the strip's end
+                const uint64_t jl = i + 252 < send ? i + 252 : send;
+                j = d.beg + off + cnt;
+                while (j < jl && text[j] == c) ++j;
+            }
             const uint32_t L = (uint32_t)(j - i) + 3;
             const uint8_t cnt_byte = (uint8_t)(L - 4);
             ob[o] = c;

@@ -705,8 +705,14 @@ void launch_tables(BlockDesc* blocks, uint32_t b0, uint32_t nb, const uint16_t* 
 #ifndef STARCH_TABLES_WIDE_NB
 #define STARCH_TABLES_WIDE_NB 512
 #endif
-    if (nb < STARCH_TABLES_WIDE_NB)
+    // STARCH_TABLES_T=256 / 512 / 1024 forces the workgroup size (experiments)
+    static const int t_force = [] { const char* e = getenv("STARCH_TABLES_T"); return e ? atoi(e) : 0; }();
+    const int t32 = t_force == 256 || t_force == 512 || t_force == 1024 ? t_force : (nb < STARCH_TABLES_WIDE_NB ? 1024 : 256);
+    if (t32 == 1024)
         hipLaunchKernelGGL(k_tables32<1024>, dim3(nb), dim3(1024), 0, st, blocks, b0, mtfv, mtf_stride, tabs, sel, gbits,
+                           reinterpret_cast<uint4*>(scr.K), hist_stride / sizeof(uint4));
+    else if (t32 == 512)
+        hipLaunchKernelGGL(k_tables32<512>, dim3(nb), dim3(512), 0, st, blocks, b0, mtfv, mtf_stride, tabs, sel, gbits,
                            reinterpret_cast<uint4*>(scr.K), hist_stride / sizeof(uint4));
     else
         hipLaunchKernelGGL(k_tables32<256>, dim3(nb), dim3(256), 0, st, blocks, b0, mtfv, mtf_stride, tabs, sel, gbits,

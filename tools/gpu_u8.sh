@@ -1,4 +1,4 @@
-# GPU box: parity subset, then cfg2 A/B (variant libraries via STARCH_AMD_LIB) and cfg4
+# GPU box: parity subset, then cfg2 (one and two lanes) and cfg4
 mkdir -p gpurun_out/u8
 timeout -k 10 600 python -u -m pytest tests/test_gpu_mtf.py tests/test_gpu_parity.py tests/test_gpu_bwt.py tests/test_gpu_dedupe.py tests/test_gpu_decode.py tests/test_gpu_fullsize.py -x -q --timeout 200 --timeout-method thread > gpurun_out/u8/t.log 2>&1
 rc=$?; tail -4 gpurun_out/u8/t.log; [ $rc -eq 0 ] || exit $rc
@@ -8,9 +8,8 @@ run() {  # name lib lanes args...
   python3 -c "import json;d=json.load(open('gpurun_out/u8/$name.json'));print('$name', d['ms_per_step'], d['value'], d['verify']['all'], d['stage_ms'])"
 }
 B=starch_amd/_build
+for v in ${VARIANTS:-}; do run cfg2_l1_$v $B/$v/libstarch_amd.so 1; done
 run cfg2_l1 $B/libstarch_amd.so 1
-run cfg2_l1_crc7 $B/v_crc7/libstarch_amd.so 1
-run cfg2_l1_ul1 $B/v_ul1/libstarch_amd.so 1
-run cfg2_l1_b $B/libstarch_amd.so 1
 run cfg2_l2 $B/libstarch_amd.so 2
-run cfg4 $B/libstarch_amd.so 2 --kind 1 --lines 50000000 --steps 5 --warmup 2
+[ "${CFG4:-1}" = 1 ] && run cfg4 $B/libstarch_amd.so 2 --kind 1 --lines 50000000 --steps 5 --warmup 2
+true
