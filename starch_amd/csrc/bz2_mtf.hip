@@ -215,7 +215,13 @@ struct ByteP {
     static constexpr uint32_t LO = 17, HI = 30;
     static constexpr uint32_t SW = 5, LW = 4;
     static constexpr uint32_t IXB = 8;
-    static constexpr bool SIX = true;                 // byte-list MTF: store the indices, emit reads them
+    // the zero runs from neighbour compares (k_mtf_runs) and the byte-list MTF
+    // run once, in k_mtf_emit (STARCH_BYTE_SIX=1: k_mtf_runs runs the MTF and
+    // stores the indices, k_mtf_emit reads them)
+#ifndef STARCH_BYTE_SIX
+#define STARCH_BYTE_SIX 0
+#endif
+    static constexpr bool SIX = STARCH_BYTE_SIX != 0;
     __device__ static void put(uint64_t* w, uint32_t i, uint32_t s)
     {
         const uint32_t j = i >> 3, sh = 8 * (i & 7);
