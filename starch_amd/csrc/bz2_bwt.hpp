@@ -43,10 +43,18 @@ void launch_fallback(BlockDesc* blocks, uint32_t b0, const uint32_t* which_host,
 // last column for blocks whose SA was produced elsewhere (fallback / LSD path)
 void launch_last_col(const BlockDesc* blocks, uint32_t b0, const uint32_t* which, uint32_t nwhich,
                      const uint8_t* blkbytes, uint64_t stride, const BwtScratch& scr, hipStream_t st);
+// alphabet classes of a batch (nInUse 1..16 / 17..24 / 25..30 / > 30): the
+// MTF and table kernels of a class are launched only when a block needs them
+constexpr uint32_t kMtfNib = 1, kMtfByte3 = 2, kMtfByte4 = 4, kMtfBig = 8, kMtfAll = 15;
+inline uint32_t mtf_class(uint32_t nin)
+{
+    return nin <= 16 ? kMtfNib : nin <= 24 ? kMtfByte3 : nin <= 30 ? kMtfByte4 : kMtfBig;
+}
 void launch_mtf(BlockDesc* blocks, uint32_t b0, uint32_t nb, const uint8_t* blkbytes, uint64_t stride,
-                const BwtScratch& scr, uint16_t* mtfv, uint64_t mtf_stride, Tables* tabs, hipStream_t st);
+                const BwtScratch& scr, uint16_t* mtfv, uint64_t mtf_stride, Tables* tabs, hipStream_t st,
+                uint32_t need = kMtfAll);
 void launch_tables(BlockDesc* blocks, uint32_t b0, uint32_t nb, const uint16_t* mtfv, uint64_t mtf_stride,
-                   Tables* tabs, uint8_t* sel, uint32_t* gbits, const BwtScratch& scr, hipStream_t st);
+                   Tables* tabs, uint8_t* sel, uint32_t* gbits, const BwtScratch& scr, hipStream_t st, uint32_t need = kMtfAll);
 // src_of (nullable): block b's MTF values / tables / selectors / group sizes
 // live at data index src_of[b] (exact block reuse, bz2_dedupe.hip); gpre has
 // one kMaxSelectors row per block.

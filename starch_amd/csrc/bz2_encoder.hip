@@ -353,6 +353,7 @@ void Encoder::plan(const uint8_t* d_text, const std::vector<StreamIn>& streams, 
     uint32_t* d_which = reinterpret_cast<uint32_t*>(b_fallback.as<uint32_t>(batch + 1));
     for (uint32_t b0 = 0; b0 < nr; b0 += batch) {
         uint32_t cnt = std::min(batch, nr - b0);
+        uint32_t mtf_need = kMtfAll;
         {
             EvTimer tb(st, stats, &pend_, 1);
             // STARCH_BWT=lsd selects the one-workgroup-per-block prefix-doubling sort of
@@ -362,11 +363,13 @@ void Encoder::plan(const uint8_t* d_text, const std::vector<StreamIn>& streams, 
             // (STARCH_WIDE=0: binary 12-bit digit everywhere; tests compare the two)
             static const bool wide_off = [] { const char* e = getenv("STARCH_WIDE"); return e && !strcmp(e, "0"); }();
             bool wide = false;
-            for (uint32_t k = 0; k < cnt && !wide && !wide_off; ++k) {
+            mtf_need = 0;                  // alphabet classes of the batch (launch_mtf / launch_tables)
+            for (uint32_t k = 0; k < cnt; ++k) {
                 const BlockDesc& bd = hb[reuse ? reps[b0 + k] : b0 + k];
                 uint32_t nin = 0;
                 for (int j = 0; j < 8; ++j) nin += (uint32_t)__builtin_popcount(bd.in_use[j]);
-                wide = nin >= 17 && nin <= 20;
+                wide = wide || (!wide_off && nin >= 17 && nin <= 20);
+                mtf_need |= mtf_class(nin);
             }
             bool doubled = true;
             if (lsd) launch_bwt(d_bl, b0, cnt, d_bytes, blk_stride_, scr, d_stats, st);
@@ -393,11 +396,11 @@ void Encoder::plan(const uint8_t* d_text, const std::vector<StreamIn>& streams, 
         }
         {
             EvTimer tm(st, stats, &pend_, 2);
-            launch_mtf(d_bl, b0, cnt, d_bytes, blk_stride_, scr, d_mtfv, mtf_stride, d_tabs, st);
+            launch_mtf(d_bl, b0, cnt, d_bytes, blk_stride_, scr, d_mtfv, mtf_stride, d_tabs, st, mtf_need);
         }
         {
             EvTimer tt(st, stats, &pend_, 3);
-            launch_tables(d_bl, b0, cnt, d_mtfv, mtf_stride, d_tabs, d_sel, d_gbits, scr, st);
+            launch_tables(d_bl, b0, cnt, d_mtfv, mtf_stride, d_tabs, d_sel, d_gbits, scr, st, mtf_need);
         }
     }
     HIP_CHECK(hipMemcpyAsync(hr, d_bl, nr * sizeof(BlockDesc), hipMemcpyDeviceToHost, st));

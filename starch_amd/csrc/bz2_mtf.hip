@@ -162,7 +162,7 @@ __device__ __forceinline__ void put_run(Out8& out, uint32_t z)   // bijective ba
 // so every CU has work whatever the block count; the two scans are one
 // workgroup per block over <= 2 chunks per thread.  The list lives in
 // registers: 16 nibbles of a u64 for <= 16 symbols (NibP, BED3 text), 32
-// bytes in four u64 for 17..32 symbols (ByteP, narrowPeak and other BED6+
+// bytes in three / four u64 for 17..24 / 25..30 symbols (ByteP<3> / ByteP<4>, narrowPeak and other BED6+
 // text); both do the move-to-front branch-free with SWAR compares.
 constexpr uint32_t MCS = 512;                 // symbols per chunk (4 lines); batches of few blocks
                                               // use shorter chunks (mtf_chunk)
@@ -207,12 +207,15 @@ struct ByteState {        // transform L -> list ++ (L \ set); list byte i = i-t
 };
 struct ByteList { uint64_t w[4]; };
 
+// NW list words: 3 for 17..24 symbols (narrowPeak's 17..20), 4 for 25..30
+template <int NW>
 struct ByteP {
+    static_assert(NW == 3 || NW == 4, "ByteP: 3 or 4 list words");
     using State = ByteState;
     using List = ByteList;
     // <= 30 symbols: the alphabet (nInUse + 2) stays within k_tables32, which
     // counts mtfFreq itself (k_tables reads the counts k_mtf_big leaves)
-    static constexpr uint32_t LO = 17, HI = 30;
+    static constexpr uint32_t LO = NW == 3 ? 17 : 25, HI = NW == 3 ? 24 : 30;
     static constexpr uint32_t SW = 5, LW = 4;
     static constexpr uint32_t IXB = 8;
     // the zero runs from neighbour compares (k_mtf_runs) and the byte-list MTF
@@ -276,21 +279,21 @@ struct ByteP {
     __device__ static uint32_t mtf(List& L, uint32_t s)
     {
         const uint64_t pat = (uint64_t)s * 0x0101010101010101ull;
-        uint64_t z[4];
+        uint64_t z[4] = {0, 0, 0, 0};
 #pragma unroll
-        for (int j = 0; j < 4; ++j) {
+        for (int j = 0; j < NW; ++j) {
             const uint64_t x = L.w[j] ^ pat;
             z[j] = (x - 0x0101010101010101ull) & ~x & 0x8080808080808080ull;
         }
         const uint32_t k = z[0] ? ((uint32_t)__builtin_ctzll(z[0]) >> 3)
                          : z[1] ? 8u + ((uint32_t)__builtin_ctzll(z[1]) >> 3)
-                         : z[2] ? 16u + ((uint32_t)__builtin_ctzll(z[2]) >> 3)
+                         : (NW == 3 || z[2]) ? 16u + ((uint32_t)__builtin_ctzll(z[2]) >> 3)
                                 : 24u + ((uint32_t)__builtin_ctzll(z[3]) >> 3);
         const uint32_t jk = k >> 3, kb = k & 7u;
         const uint64_t m = kb == 7u ? ~0ull : ((1ull << (8u * kb + 8u)) - 1ull);   // bytes [0, kb]
         uint64_t carry = s;
 #pragma unroll
-        for (uint32_t j = 0; j < 4; ++j) {
+        for (uint32_t j = 0; j < (uint32_t)NW; ++j) {
             const uint64_t nv = (L.w[j] << 8) | carry;
             carry = L.w[j] >> 56;
             L.w[j] = j < jk ? nv : (j == jk ? ((nv & m) | (L.w[j] & ~m)) : L.w[j]);
@@ -646,7 +649,7 @@ __global__ void __launch_bounds__(MT) k_mtf_big(BlockDesc* __restrict__ blocks, 
     const uint32_t b = b0 + slot;
     const uint32_t n = blocks[b].n;
     const uint32_t nin = blocks[b].n_in_use;
-    if (nin <= ByteP::HI) return;                    // <= 30 symbols: the register-list kernels
+    if (nin <= ByteP<4>::HI) return;                 // <= 30 symbols: the register-list kernels
     for (int i = tid; i < NF * 258; i += MT) (&freq[0][0])[i] = 0;
     const uint8_t* ll = LL + (uint64_t)slot * ll_stride;
     uint8_t* idx = scratch + (uint64_t)slot * scratch_stride;            // MTF indices
@@ -830,7 +833,8 @@ void launch_last_col(const BlockDesc* blocks, uint32_t b0, const uint32_t* which
 }
 
 void launch_mtf(BlockDesc* blocks, uint32_t b0, uint32_t nb, const uint8_t* blkbytes, uint64_t stride,
-                const BwtScratch& scr, uint16_t* mtfv, uint64_t mtf_stride, Tables* tabs, hipStream_t st)
+                const BwtScratch& scr, uint16_t* mtfv, uint64_t mtf_stride, Tables* tabs, hipStream_t st,
+                uint32_t need)
 {
     (void)blkbytes;
     (void)stride;
@@ -852,11 +856,15 @@ void launch_mtf(BlockDesc* blocks, uint32_t b0, uint32_t nb, const uint8_t* blkb
         hipLaunchKernelGGL(k_mtf_emit<P>, gch, dim3(MCT), 0, st, blocks, b0, scr.LL, scr.stride, scr.K, kstride, C,
                            cs, mtfv, mtf_stride);
     };
-    run(NibP{});
-    run(ByteP{});
+    // need (mtf_need): the alphabet classes present in the batch; the other
+    // classes' kernels are not launched
+    if (need & kMtfNib) run(NibP{});
+    if (need & kMtfByte3) run(ByteP<3>{});
+    if (need & kMtfByte4) run(ByteP<4>{});
     // large alphabets: index bytes + per-chunk lists in the (free) key scratch
-    hipLaunchKernelGGL(k_mtf_big, dim3(nb), dim3(MT), 0, st, blocks, b0, scr.LL, scr.stride,
-                       reinterpret_cast<uint8_t*>(scr.K), scr.stride * sizeof(uint64_t), mtfv, mtf_stride, tabs);
+    if (need & kMtfBig)
+        hipLaunchKernelGGL(k_mtf_big, dim3(nb), dim3(MT), 0, st, blocks, b0, scr.LL, scr.stride,
+                           reinterpret_cast<uint8_t*>(scr.K), scr.stride * sizeof(uint64_t), mtfv, mtf_stride, tabs);
     HIP_CHECK(hipGetLastError());
 }
 

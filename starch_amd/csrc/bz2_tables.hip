@@ -697,7 +697,7 @@ __global__ void __launch_bounds__(T32) __attribute__((amdgpu_waves_per_eu(STARCH
 }
 
 void launch_tables(BlockDesc* blocks, uint32_t b0, uint32_t nb, const uint16_t* mtfv, uint64_t mtf_stride,
-                   Tables* tabs, uint8_t* sel, uint32_t* gbits, const BwtScratch& scr, hipStream_t st)
+                   Tables* tabs, uint8_t* sel, uint32_t* gbits, const BwtScratch& scr, hipStream_t st, uint32_t need)
 {
     // per-group histograms live in the (now free) block-sort key scratch
     uint8_t* hist = reinterpret_cast<uint8_t*>(scr.K);
@@ -708,7 +708,9 @@ void launch_tables(BlockDesc* blocks, uint32_t b0, uint32_t nb, const uint16_t* 
     // STARCH_TABLES_T=256 / 512 / 1024 forces the workgroup size (experiments)
     static const int t_force = [] { const char* e = getenv("STARCH_TABLES_T"); return e ? atoi(e) : 0; }();
     const int t32 = t_force == 256 || t_force == 512 || t_force == 1024 ? t_force : (nb < STARCH_TABLES_WIDE_NB ? 1024 : 256);
-    if (t32 == 1024)
+    if (!(need & (kMtfNib | kMtfByte3 | kMtfByte4))) {
+        // no block of <= 30 symbols in the batch: k_tables32 has nothing to do
+    } else if (t32 == 1024)
         hipLaunchKernelGGL(k_tables32<1024>, dim3(nb), dim3(1024), 0, st, blocks, b0, mtfv, mtf_stride, tabs, sel, gbits,
                            reinterpret_cast<uint4*>(scr.K), hist_stride / sizeof(uint4));
     else if (t32 == 512)
@@ -717,8 +719,9 @@ void launch_tables(BlockDesc* blocks, uint32_t b0, uint32_t nb, const uint16_t* 
     else
         hipLaunchKernelGGL(k_tables32<256>, dim3(nb), dim3(256), 0, st, blocks, b0, mtfv, mtf_stride, tabs, sel, gbits,
                            reinterpret_cast<uint4*>(scr.K), hist_stride / sizeof(uint4));
-    hipLaunchKernelGGL(k_tables, dim3(nb), dim3(TT), 0, st, blocks, b0, mtfv, mtf_stride, tabs, sel, gbits, hist,
-                       hist_stride);
+    if (need & kMtfBig)
+        hipLaunchKernelGGL(k_tables, dim3(nb), dim3(TT), 0, st, blocks, b0, mtfv, mtf_stride, tabs, sel, gbits, hist,
+                           hist_stride);
     HIP_CHECK(hipGetLastError());
 #ifdef STARCH_TABLES_PROF
     {

@@ -42,10 +42,11 @@ def test_alphabet_sizes(ctx, nsym):
     assert ctx.bz2_compress(data[:150_000], 1) == _ref(data[:150_000], 1)
 
 
-@pytest.mark.parametrize("nsym", [29, 30, 31, 32])
+@pytest.mark.parametrize("nsym", [16, 17, 23, 24, 25, 26, 29, 30, 31, 32])
 def test_alphabet_edges_without_runs(ctx, nsym):
     """No run of 4 (no RLE1 count bytes): nInUse is exactly nsym, at the
-    boundary between the register-list path (<= 30) and the LDS path."""
+    boundaries between the nibble lists (<= 16), the three- and four-word
+    byte lists (<= 24, <= 30) and the LDS path."""
     r = random.Random(100 + nsym)
     alpha = list(range(65, 65 + nsym))
     out, prev = [], None
@@ -64,3 +65,24 @@ def test_narrowpeak_text_multiblock(ctx):
     data = starch_amd.gen_bed(1, 300_000, chroms=[13])
     text, segs = ctx.transform(data)
     assert ctx.bz2_compress(segs[0][2], 9) == _ref(segs[0][2], 9)
+
+
+def test_mixed_alphabet_classes_in_one_batch(ctx):
+    """Blocks of every alphabet class in one stream (one sort / MTF batch):
+    the batch launches each class's kernels once, every block takes its own."""
+    r = random.Random(7)
+    out = bytearray()
+    for nsym in (10, 22, 28, 45, 12, 20):
+        alpha = list(range(40, 40 + nsym))
+        prev = None
+        part = []
+        while len(part) < 120_000:
+            c = r.choice(alpha)
+            if c == prev:
+                continue
+            part.append(c)
+            prev = c
+        out += bytes(part)
+    data = bytes(out)
+    assert ctx.bz2_compress(data, 1) == _ref(data, 1)       # 100 KB blocks: one class each, mostly
+    assert ctx.bz2_compress(data, 9) == _ref(data, 9)
