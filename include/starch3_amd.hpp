@@ -871,6 +871,12 @@ private:
     // caller goes on to the next chromosome; streams are written to the out
     // stream, and their index entries recorded, strictly in hand-off order.
     // STARCH_HOOK_SYNC=1: each chromosome through self's own bz_stream at once.
+    // The workers' streams carry their own block-close callbacks (they record
+    // the index entries in hand-off order), so a block_close_functor a caller
+    // installs on self's stream is not called on this path; STARCH_HOOK_SYNC=1
+    // codes through self's stream (re-initialised per chromosome by
+    // initialize_bz_stream_ptr / setup_bz_stream_callbacks, as the reference's
+    // hand-off does).
     struct HookJob {
         uint64_t seq;
         std::string chr;
@@ -1176,12 +1182,29 @@ private:
         _pool.push_back(b);
         return b.p;
     }
-    // back to the pool (true), or not a pool buffer (false)
+    // back to the pool (true), or not a pool buffer (false).  The pool keeps at
+    // most STARCH_HOOK_POOL_MAX bytes (default 4 GiB) of buffers: a buffer
+    // returned while the pool holds more is unregistered and freed (per-base
+    // BED runs to GBs of text per chromosome; the buffers in flight are bounded
+    // by the hook's job count, the idle ones by this cap)
+    static size_t text_pool_max()
+    {
+        const char* e = std::getenv("STARCH_HOOK_POOL_MAX");
+        return e ? (size_t)std::strtoull(e, NULL, 10) : ((size_t)4 << 30);
+    }
     bool text_pool_put(char* p)
     {
         std::lock_guard<std::mutex> lk(_pmu);
+        size_t total = 0;
+        for (size_t i = 0; i < _pool.size(); ++i) total += _pool[i].cap;
         for (size_t i = 0; i < _pool.size(); ++i)
             if (_pool[i].p == p) {
+                if (total > text_pool_max()) {
+                    if (_pool[i].reg) (void)starch_host_unregister(_pool[i].p);
+                    std::free(_pool[i].p);
+                    _pool.erase(_pool.begin() + (std::ptrdiff_t)i);
+                    return true;            // released: the caller must not free it
+                }
                 _pool[i].free_ = true;
                 return true;
             }

@@ -119,6 +119,13 @@ def test_hpp_hook_large_chromosomes():
                        timeout=300, env=env)
     assert r.returncode == 0, r.stderr[-2000:]
     assert r.stdout == want
+    # the text pool capped at nothing: every page-locked buffer is released
+    # when its chromosome is done (no reuse), the archive is the same
+    env = dict(os.environ, STARCH_HOOK_POOL_MAX="0")
+    r = subprocess.run([os.path.join(BUILD, "starch3_hpp_example"), "--hook"], input=data, capture_output=True,
+                       timeout=300, env=env)
+    assert r.returncode == 0, r.stderr[-2000:]
+    assert r.stdout == want
 
 
 @pytest.mark.parametrize("args", [[], ["--hook"], ["--reference-compat"]])
